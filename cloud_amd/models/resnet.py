@@ -1,0 +1,82 @@
+"""ResNet-50 (v1.5) in NHWC on cloud_amd ops -- the north-star workload.
+
+Reference workload: ``tf.keras.applications.ResNet50`` trained on images in
+``TFC/core/tests/examples/call_run_within_script_with_keras_fit.py:80-107``; the
+BASELINE.json config is ResNet-50 on synthetic ImageNet (224x224x3, 1000
+classes).  Layout is NHWC end to end: every 1x1 convolution runs as a GEMM on
+the activation memory as it lies, BatchNorm + residual + ReLU are one fused
+HIP kernel pair, pooling and the loss are HIP kernels.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .layers import BatchNormAct, Conv2d, GlobalAvgPool, Linear, MaxPool2d
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride=1, dtype=torch.bfloat16, device=None, zero_init_residual=True):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = Conv2d(cin, width, 1, dtype=dtype, device=device)
+        self.bn1 = BatchNormAct(width, relu=True, device=device)
+        self.conv2 = Conv2d(width, width, 3, stride=stride, padding=1, dtype=dtype, device=device)
+        self.bn2 = BatchNormAct(width, relu=True, device=device)
+        self.conv3 = Conv2d(width, cout, 1, dtype=dtype, device=device)
+        self.bn3 = BatchNormAct(cout, relu=True, zero_init=zero_init_residual, device=device)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.ModuleDict({
+                "conv": Conv2d(cin, cout, 1, stride=stride, dtype=dtype, device=device),
+                "bn": BatchNormAct(cout, relu=False, device=device),
+            })
+
+    def forward(self, x):
+        identity = x
+        if self.downsample is not None:
+            identity = self.downsample["bn"](self.downsample["conv"](x))
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), residual=identity)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, in_channels=3, stem_channels_pad=0,
+                 dtype=torch.bfloat16, device=None, zero_init_residual=True):
+        super().__init__()
+        self.in_channels = in_channels
+        self.stem_cin = in_channels + stem_channels_pad
+        self.conv1 = Conv2d(self.stem_cin, 64, 7, stride=2, padding=3, dtype=dtype, device=device)
+        self.bn1 = BatchNormAct(64, relu=True, device=device)
+        self.maxpool = MaxPool2d(3, 2, 1)
+        blocks = []
+        cin = 64
+        for i, (n, width) in enumerate(zip(layers, (64, 128, 256, 512))):
+            for j in range(n):
+                stride = 2 if (j == 0 and i > 0) else 1
+                blocks.append(Bottleneck(cin, width, stride, dtype=dtype, device=device,
+                                         zero_init_residual=zero_init_residual))
+                cin = width * Bottleneck.expansion
+        self.layers = nn.Sequential(*blocks)
+        self.pool = GlobalAvgPool()
+        self.fc = Linear(cin, num_classes, dtype=dtype, device=device)
+
+    def forward(self, x):
+        """x: NHWC [N, H, W, in_channels] in the compute dtype -> logits [N, classes]."""
+        if self.stem_cin != self.in_channels:
+            x = torch.nn.functional.pad(x, (0, self.stem_cin - self.in_channels))
+        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.layers(x)
+        return self.fc(self.pool(x))
+
+
+def resnet50(**kw):
+    return ResNet((3, 4, 6, 3), **kw)
+
+
+def resnet18_like_small(**kw):
+    """Tiny bottleneck ResNet for CPU tests (same code path, few blocks)."""
+    return ResNet((1, 1, 1, 1), **kw)

@@ -1,0 +1,65 @@
+"""Process-group bootstrap for one-process-per-GPU jobs.
+
+Reads the torchrun / cloud_amd-launcher environment (``RANK``, ``LOCAL_RANK``,
+``WORLD_SIZE``, ``MASTER_ADDR``, ``MASTER_PORT``) and initialises
+``torch.distributed`` with RCCL (backend ``"nccl"`` on ROCm) when a GPU is
+present, gloo otherwise.  ``MASTER_ADDR`` defaults to 127.0.0.1 (container
+hostnames may not resolve).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_int(name, default):
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def rank():
+    return env_int("RANK", 0)
+
+
+def local_rank():
+    return env_int("LOCAL_RANK", 0)
+
+
+def world_size():
+    return env_int("WORLD_SIZE", 1)
+
+
+def init_distributed(backend=None, timeout_s=None, device=None):
+    """Initialise the default process group if WORLD_SIZE > 1. Returns (rank, world, device)."""
+    r, w, lr = rank(), world_size(), local_rank()
+    if device is None:
+        device = torch.device("cuda", lr) if torch.cuda.is_available() else torch.device("cpu")
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    if w > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        backend = backend or ("nccl" if device.type == "cuda" else "gloo")
+        timeout = datetime.timedelta(seconds=timeout_s or env_int("CLOUD_AMD_PG_TIMEOUT_S", 600))
+        kw = {"device_id": device} if (backend == "nccl" and device.type == "cuda") else {}
+        try:
+            dist.init_process_group(backend, rank=r, world_size=w, timeout=timeout, **kw)
+        except TypeError:
+            dist.init_process_group(backend, rank=r, world_size=w, timeout=timeout)
+    return r, w, device
+
+
+def barrier():
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def all_reduce_max(x: float, device) -> float:
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

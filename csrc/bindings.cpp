@@ -1,0 +1,108 @@
+// pybind11 face of the gfx950 kernels.  Every entry point takes raw device
+// pointers (uintptr_t from torch.Tensor.data_ptr()) and the HIP stream handle
+// (torch.cuda.current_stream().cuda_stream); shape/dtype validation happens in
+// the Python layer (cloud_amd/ops/*).  A non-zero HIP status raises.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <stdint.h>
+
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+typedef uint16_t bf16_t;
+
+extern "C" {
+int ca_sgd_step(float*, const void*, int, float*, bf16_t*, const float*, long, int, hipStream_t);
+int ca_adam_step(float*, const void*, int, float*, float*, bf16_t*, const float*, long, int, hipStream_t);
+int ca_rmsprop_step(float*, const void*, int, float*, float*, bf16_t*, const float*, long, hipStream_t);
+int ca_sumsq(const void*, int, long, float*, hipStream_t);
+int ca_scale(void*, int, long, const float*, hipStream_t);
+long ca_bn_workspace_floats(long, int);
+int ca_bn_fwd(const bf16_t*, const bf16_t*, bf16_t*, long, int, const float*, const float*, float, float,
+              float*, float*, float*, float*, float*, float*, int, hipStream_t);
+int ca_bn_apply(const bf16_t*, const bf16_t*, bf16_t*, long, int, const float*, int, hipStream_t);
+int ca_bn_bwd(const bf16_t*, const bf16_t*, const bf16_t*, long, int, const float*, const float*, const float*,
+              bf16_t*, bf16_t*, float*, float*, float*, float*, int, hipStream_t);
+int ca_softmax_xent(const void*, int, const int64_t*, int, int, float, float, float*, float*, void*, hipStream_t);
+int ca_maxpool_fwd(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ca_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int ca_gap_fwd(const bf16_t*, void*, int, int, int, int, hipStream_t);
+int ca_gap_bwd(const void*, int, bf16_t*, int, int, int, hipStream_t);
+}
+
+#define P(T, x) reinterpret_cast<T>(static_cast<uintptr_t>(x))
+#define S(x) reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(x))
+
+static void check(int rc, const char* what) {
+  if (rc != 0) {
+    std::string msg = std::string(what) + " failed: ";
+    if (rc > 0) msg += hipGetErrorString(static_cast<hipError_t>(rc));
+    else msg += "invalid arguments (code " + std::to_string(rc) + ")";
+    throw std::runtime_error(msg);
+  }
+}
+
+typedef unsigned long long u64;
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "cloud_amd gfx950 HIP kernels";
+  m.attr("ARCH") = "gfx950";
+
+  m.def("sgd_step", [](u64 p, u64 g, int gbf, u64 mom, u64 p16, u64 hp, long n, int nesterov, u64 s) {
+    check(ca_sgd_step(P(float*, p), P(const void*, g), gbf, P(float*, mom), P(bf16_t*, p16), P(const float*, hp), n,
+                      nesterov, S(s)), "sgd_step");
+  });
+  m.def("adam_step", [](u64 p, u64 g, int gbf, u64 mm, u64 vv, u64 p16, u64 hp, long n, int decoupled, u64 s) {
+    check(ca_adam_step(P(float*, p), P(const void*, g), gbf, P(float*, mm), P(float*, vv), P(bf16_t*, p16),
+                       P(const float*, hp), n, decoupled, S(s)), "adam_step");
+  });
+  m.def("rmsprop_step", [](u64 p, u64 g, int gbf, u64 ms, u64 buf, u64 p16, u64 hp, long n, u64 s) {
+    check(ca_rmsprop_step(P(float*, p), P(const void*, g), gbf, P(float*, ms), P(float*, buf), P(bf16_t*, p16),
+                          P(const float*, hp), n, S(s)), "rmsprop_step");
+  });
+  m.def("sumsq", [](u64 g, int gbf, long n, u64 out, u64 s) {
+    check(ca_sumsq(P(const void*, g), gbf, n, P(float*, out), S(s)), "sumsq");
+  });
+  m.def("scale", [](u64 g, int gbf, long n, u64 sc, u64 s) {
+    check(ca_scale(P(void*, g), gbf, n, P(const float*, sc), S(s)), "scale");
+  });
+  m.def("bn_workspace_floats", [](long M, int C) { return ca_bn_workspace_floats(M, C); });
+  m.def("bn_fwd", [](u64 x, u64 res, u64 y, long M, int C, u64 gamma, u64 beta, float eps, float momentum,
+                     u64 rm, u64 rv, u64 sm, u64 sr, u64 ss, u64 ws, int relu, u64 s) {
+    check(ca_bn_fwd(P(const bf16_t*, x), P(const bf16_t*, res), P(bf16_t*, y), M, C, P(const float*, gamma),
+                    P(const float*, beta), eps, momentum, P(float*, rm), P(float*, rv), P(float*, sm), P(float*, sr),
+                    P(float*, ss), P(float*, ws), relu, S(s)), "bn_fwd");
+  });
+  m.def("bn_apply", [](u64 x, u64 res, u64 y, long M, int C, u64 ss, int relu, u64 s) {
+    check(ca_bn_apply(P(const bf16_t*, x), P(const bf16_t*, res), P(bf16_t*, y), M, C, P(const float*, ss), relu,
+                      S(s)), "bn_apply");
+  });
+  m.def("bn_bwd", [](u64 dy, u64 y, u64 x, long M, int C, u64 gamma, u64 sm, u64 sr, u64 dx, u64 dres, u64 dg,
+                     u64 db, u64 coef, u64 ws, int relu, u64 s) {
+    check(ca_bn_bwd(P(const bf16_t*, dy), P(const bf16_t*, y), P(const bf16_t*, x), M, C, P(const float*, gamma),
+                    P(const float*, sm), P(const float*, sr), P(bf16_t*, dx), P(bf16_t*, dres), P(float*, dg),
+                    P(float*, db), P(float*, coef), P(float*, ws), relu, S(s)), "bn_bwd");
+  });
+  m.def("softmax_xent", [](u64 z, int zbf, u64 labels, int B, int C, float gscale, float ls, u64 loss, u64 correct,
+                           u64 dz, u64 s) {
+    check(ca_softmax_xent(P(const void*, z), zbf, P(const int64_t*, labels), B, C, gscale, ls, P(float*, loss),
+                          P(float*, correct), P(void*, dz), S(s)), "softmax_xent");
+  });
+  m.def("maxpool_fwd", [](u64 x, u64 y, u64 idx, int N, int H, int W, int C, int OH, int OW, int k, int st, int p,
+                          u64 s) {
+    check(ca_maxpool_fwd(P(const bf16_t*, x), P(bf16_t*, y), P(uint8_t*, idx), N, H, W, C, OH, OW, k, st, p, S(s)),
+          "maxpool_fwd");
+  });
+  m.def("maxpool_bwd", [](u64 dy, u64 idx, u64 dx, int N, int H, int W, int C, int OH, int OW, int k, int st, int p,
+                          u64 s) {
+    check(ca_maxpool_bwd(P(const bf16_t*, dy), P(const uint8_t*, idx), P(bf16_t*, dx), N, H, W, C, OH, OW, k, st, p,
+                         S(s)), "maxpool_bwd");
+  });
+  m.def("gap_fwd", [](u64 x, u64 y, int ybf, int N, int HW, int C, u64 s) {
+    check(ca_gap_fwd(P(const bf16_t*, x), P(void*, y), ybf, N, HW, C, S(s)), "gap_fwd");
+  });
+  m.def("gap_bwd", [](u64 dy, int dybf, u64 dx, int N, int HW, int C, u64 s) {
+    check(ca_gap_bwd(P(const void*, dy), dybf, P(bf16_t*, dx), N, HW, C, S(s)), "gap_bwd");
+  });
+}

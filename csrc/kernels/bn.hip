@@ -1,0 +1,365 @@
+// Training-mode BatchNorm (+ residual add + ReLU) for NHWC bf16 activations
+// viewed as a row-major [M = N*H*W, C] matrix (K10 in SURVEY.md section 2.7).
+//
+// Forward  : stats (1 read)  -> finalize (per-channel, tiny) -> apply (1 read + 1 write
+//            [+1 read residual]).
+// Backward : reduce (3 reads: dy, y, x) -> finalize -> apply (3 reads, 1-2 writes),
+//            ReLU mask recomputed from the saved output y, residual gradient emitted
+//            by the same pass.
+//
+// Tiling: a block is 256 threads = TW column-vectors (8 channels, 16 B each) x RP
+// rows; each thread owns ONE column vector for the whole launch (so per-channel
+// coefficients live in registers) and walks rows with stride RP.  Partial sums
+// go to a [nchunks][C] fp32 workspace (deterministic, no atomics) and are
+// combined in double precision by the finalize kernel.
+#include "ca_common.h"
+
+namespace {
+
+constexpr int BLK = 256;
+
+struct Tiling {
+  int CT, TW, RP, ncol, nchunks;
+  long rows_per_chunk;
+};
+
+__host__ __device__ inline Tiling make_tiling(long M, int C) {
+  Tiling t;
+  t.CT = C / 8;
+  t.TW = t.CT < 64 ? t.CT : 64;
+  t.RP = BLK / t.TW;
+  t.ncol = (t.CT + t.TW - 1) / t.TW;
+  long maxchunks = (M + t.RP - 1) / t.RP;
+  long want = 2048 / t.ncol;
+  if (want < 1) want = 1;
+  if (want > maxchunks) want = maxchunks;
+  if (want > 1024) want = 1024;
+  t.nchunks = (int)want;
+  long rpc = (M + t.nchunks - 1) / t.nchunks;
+  rpc = ((rpc + t.RP - 1) / t.RP) * t.RP;
+  t.rows_per_chunk = rpc;
+  t.nchunks = (int)((M + rpc - 1) / rpc);
+  return t;
+}
+
+__device__ __forceinline__ void ld8bf(const bf16_t* p, float (&o)[8]) {
+  us8 v = *reinterpret_cast<const us8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = bf2f(v[j]);
+}
+__device__ __forceinline__ void st8bf(bf16_t* p, const float (&o)[8]) {
+  us8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = f2bf(o[j]);
+  *reinterpret_cast<us8*>(p) = v;
+}
+
+// Reduce two per-thread 8-vectors over the RP threads sharing a column, write
+// the block's partial to ws[chunk][C] (a) and ws[nchunks + chunk][C] (b).
+__device__ __forceinline__ void block_col_reduce(float (&a)[8], float (&b)[8], const Tiling& t,
+                                                 int tx, int ty, int vc, int chunk, int C,
+                                                 float* __restrict__ ws) {
+  __shared__ float sa[BLK * 8];
+  __shared__ float sb[BLK * 8];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sa[j * BLK + tid] = a[j]; sb[j * BLK + tid] = b[j]; }
+  __syncthreads();
+  // thread (tx, ty<8) sums channel j=ty of column tx over the RP rows
+  if (ty < 8 && vc < t.CT) {
+    float ra = 0.f, rb = 0.f;
+    const int j = ty;
+    for (int r = 0; r < t.RP; ++r) {
+      ra += sa[j * BLK + r * t.TW + tx];
+      rb += sb[j * BLK + r * t.TW + tx];
+    }
+    const int c = vc * 8 + j;
+    ws[(long)chunk * C + c] = ra;
+    ws[(long)(t.nchunks + chunk) * C + c] = rb;
+  }
+}
+
+__global__ void __launch_bounds__(BLK) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
+                                                      float* __restrict__ ws) {
+  const Tiling t = make_tiling(M, C);
+  const int tx = threadIdx.x % t.TW, ty = threadIdx.x / t.TW;
+  const int vc = blockIdx.x * t.TW + tx;
+  const int chunk = blockIdx.y;
+  float s[8] = {0}, q[8] = {0};
+  if (vc < t.CT) {
+    const long r0 = (long)chunk * t.rows_per_chunk;
+    long r1 = r0 + t.rows_per_chunk;
+    if (r1 > M) r1 = M;
+    const bf16_t* base = x + (long)vc * 8;
+    long r = r0 + ty;
+    for (; r + 3 * t.RP < r1; r += 4 * t.RP) {
+      float v0[8], v1[8], v2[8], v3[8];
+      ld8bf(base + r * C, v0);
+      ld8bf(base + (r + t.RP) * C, v1);
+      ld8bf(base + (r + 2 * t.RP) * C, v2);
+      ld8bf(base + (r + 3 * t.RP) * C, v3);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += (v0[j] + v1[j]) + (v2[j] + v3[j]);
+        q[j] += (v0[j] * v0[j] + v1[j] * v1[j]) + (v2[j] * v2[j] + v3[j] * v3[j]);
+      }
+    }
+    for (; r < r1; r += t.RP) {
+      float v0[8];
+      ld8bf(base + r * C, v0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s[j] += v0[j]; q[j] += v0[j] * v0[j]; }
+    }
+  }
+  block_col_reduce(s, q, t, tx, ty, vc, chunk, C, ws);
+}
+
+// Per-channel finalize of the forward statistics.
+//   save_mean/save_rstd : fp32 [C] (needed by backward)
+//   scale/shift         : fp32 [C], y = x*scale + shift
+//   running stats updated in place when non-null (unbiased variance).
+__global__ void bn_fwd_finalize_kernel(const float* __restrict__ ws, int nchunks, long M, int C,
+                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                       float eps, float momentum,
+                                       float* __restrict__ run_mean, float* __restrict__ run_var,
+                                       float* __restrict__ save_mean, float* __restrict__ save_rstd,
+                                       float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < nchunks; ++k) {
+    s += ws[(long)k * C + c];
+    q += ws[(long)(nchunks + k) * C + c];
+  }
+  const double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  save_mean[c] = (float)mean;
+  save_rstd[c] = rstd;
+  scale[c] = g * rstd;
+  shift[c] = b - (float)mean * g * rstd;
+  if (run_mean) {
+    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+  }
+}
+
+// y = act(x*scale + shift [+ res])
+template <bool RELU, bool RES>
+__global__ void __launch_bounds__(BLK) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                      const float* __restrict__ scale, const float* __restrict__ shift,
+                                                      bf16_t* __restrict__ y, long M, int C) {
+  const Tiling t = make_tiling(M, C);
+  const int tx = threadIdx.x % t.TW, ty = threadIdx.x / t.TW;
+  const int vc = blockIdx.x * t.TW + tx;
+  if (vc >= t.CT) return;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = scale[vc * 8 + j]; sh[j] = shift[vc * 8 + j]; }
+  const long r0 = (long)blockIdx.y * t.rows_per_chunk;
+  long r1 = r0 + t.rows_per_chunk;
+  if (r1 > M) r1 = M;
+  const long off0 = (long)vc * 8;
+  for (long r = r0 + ty; r < r1; r += t.RP) {
+    const long o = r * C + off0;
+    float v[8];
+    ld8bf(x + o, v);
+    float rv[8];
+    if (RES) ld8bf(res + o, rv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float z = v[j] * sc[j] + sh[j];
+      if (RES) z += rv[j];
+      if (RELU) z = fmaxf(z, 0.f);
+      v[j] = z;
+    }
+    st8bf(y + o, v);
+  }
+}
+
+// Backward reduce: dz = dy * (y > 0 if RELU); partial sums of dz and dz*xhat.
+template <bool RELU>
+__global__ void __launch_bounds__(BLK) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                           const bf16_t* __restrict__ x,
+                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                           long M, int C, float* __restrict__ ws) {
+  const Tiling t = make_tiling(M, C);
+  const int tx = threadIdx.x % t.TW, ty = threadIdx.x / t.TW;
+  const int vc = blockIdx.x * t.TW + tx;
+  const int chunk = blockIdx.y;
+  float sd[8] = {0}, sdx[8] = {0};
+  if (vc < t.CT) {
+    float mu[8], rs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mu[j] = mean[vc * 8 + j]; rs[j] = rstd[vc * 8 + j]; }
+    const long r0 = (long)chunk * t.rows_per_chunk;
+    long r1 = r0 + t.rows_per_chunk;
+    if (r1 > M) r1 = M;
+    const long off0 = (long)vc * 8;
+    long r = r0 + ty;
+    for (; r + t.RP < r1; r += 2 * t.RP) {
+      const long o0 = r * C + off0, o1 = (r + t.RP) * C + off0;
+      float d0[8], x0[8], d1[8], x1[8], y0[8], y1[8];
+      ld8bf(dy + o0, d0);
+      ld8bf(x + o0, x0);
+      ld8bf(dy + o1, d1);
+      ld8bf(x + o1, x1);
+      if (RELU) { ld8bf(y + o0, y0); ld8bf(y + o1, y1); }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = d0[j], b = d1[j];
+        if (RELU) { a = y0[j] > 0.f ? a : 0.f; b = y1[j] > 0.f ? b : 0.f; }
+        sd[j] += a + b;
+        sdx[j] += a * (x0[j] - mu[j]) * rs[j] + b * (x1[j] - mu[j]) * rs[j];
+      }
+    }
+    for (; r < r1; r += t.RP) {
+      const long o0 = r * C + off0;
+      float d0[8], x0[8], y0[8];
+      ld8bf(dy + o0, d0);
+      ld8bf(x + o0, x0);
+      if (RELU) ld8bf(y + o0, y0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = d0[j];
+        if (RELU) a = y0[j] > 0.f ? a : 0.f;
+        sd[j] += a;
+        sdx[j] += a * (x0[j] - mu[j]) * rs[j];
+      }
+    }
+  }
+  block_col_reduce(sd, sdx, t, tx, ty, vc, chunk, C, ws);
+}
+
+// dgamma = sum(dz*xhat), dbeta = sum(dz); coefficients so that
+// dx = A*dz + B*x + D.
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ ws, int nchunks, long M, int C,
+                                       const float* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ rstd, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sd = 0.0, sdx = 0.0;
+  for (int k = 0; k < nchunks; ++k) {
+    sd += ws[(long)k * C + c];
+    sdx += ws[(long)(nchunks + k) * C + c];
+  }
+  if (dgamma) dgamma[c] = (float)sdx;
+  if (dbeta) dbeta[c] = (float)sd;
+  const double g = gamma ? gamma[c] : 1.0;
+  const double rs = rstd[c], mu = mean[c];
+  const double k1 = g * rs;
+  const double a = sd / (double)M, b = sdx / (double)M;
+  coef[c] = (float)k1;                               // A
+  coef[C + c] = (float)(-k1 * b * rs);               // B
+  coef[2 * C + c] = (float)(-k1 * a + k1 * b * rs * mu);  // D
+}
+
+template <bool RELU, bool DRES>
+__global__ void __launch_bounds__(BLK) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                          const bf16_t* __restrict__ x, const float* __restrict__ coef,
+                                                          bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
+                                                          long M, int C) {
+  const Tiling t = make_tiling(M, C);
+  const int tx = threadIdx.x % t.TW, ty = threadIdx.x / t.TW;
+  const int vc = blockIdx.x * t.TW + tx;
+  if (vc >= t.CT) return;
+  float A[8], B[8], D[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    A[j] = coef[vc * 8 + j];
+    B[j] = coef[C + vc * 8 + j];
+    D[j] = coef[2 * C + vc * 8 + j];
+  }
+  const long r0 = (long)blockIdx.y * t.rows_per_chunk;
+  long r1 = r0 + t.rows_per_chunk;
+  if (r1 > M) r1 = M;
+  const long off0 = (long)vc * 8;
+  for (long r = r0 + ty; r < r1; r += t.RP) {
+    const long o = r * C + off0;
+    float d[8], xv[8], yv[8];
+    ld8bf(dy + o, d);
+    ld8bf(x + o, xv);
+    if (RELU) ld8bf(y + o, yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (RELU) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+    }
+    if (DRES) st8bf(dres + o, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = A[j] * d[j] + B[j] * xv[j] + D[j];
+    st8bf(dx + o, xv);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Workspace floats needed by the stats / bwd-reduce kernels: 2 * nchunks * C.
+long ca_bn_workspace_floats(long M, int C) {
+  Tiling t = make_tiling(M, C);
+  return 2L * t.nchunks * C;
+}
+
+int ca_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
+              const float* gamma, const float* beta, float eps, float momentum,
+              float* run_mean, float* run_var, float* save_mean, float* save_rstd,
+              float* scale_shift /* [2C] */, float* ws, int relu, hipStream_t s) {
+  if (C % 8 != 0) return -1;
+  Tiling t = make_tiling(M, C);
+  dim3 grid(t.ncol, t.nchunks);
+  bn_stats_kernel<<<grid, BLK, 0, s>>>(x, M, C, ws);
+  CA_LAUNCH_CHECK();
+  bn_fwd_finalize_kernel<<<ca_cdiv(C, 256), 256, 0, s>>>(ws, t.nchunks, M, C, gamma, beta, eps, momentum,
+                                                         run_mean, run_var, save_mean, save_rstd,
+                                                         scale_shift, scale_shift + C);
+  CA_LAUNCH_CHECK();
+  if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+// Inference / frozen-stat apply with precomputed scale/shift.
+int ca_bn_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
+                const float* scale_shift, int relu, hipStream_t s) {
+  if (C % 8 != 0) return -1;
+  Tiling t = make_tiling(M, C);
+  dim3 grid(t.ncol, t.nchunks);
+  if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+int ca_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, long M, int C,
+              const float* gamma, const float* save_mean, const float* save_rstd,
+              bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta,
+              float* coef /* [3C] */, float* ws, int relu, hipStream_t s) {
+  if (C % 8 != 0) return -1;
+  Tiling t = make_tiling(M, C);
+  dim3 grid(t.ncol, t.nchunks);
+  if (relu) bn_bwd_reduce_kernel<true><<<grid, BLK, 0, s>>>(dy, y, x, save_mean, save_rstd, M, C, ws);
+  else bn_bwd_reduce_kernel<false><<<grid, BLK, 0, s>>>(dy, y, x, save_mean, save_rstd, M, C, ws);
+  CA_LAUNCH_CHECK();
+  bn_bwd_finalize_kernel<<<ca_cdiv(C, 256), 256, 0, s>>>(ws, t.nchunks, M, C, gamma, save_mean, save_rstd,
+                                                         dgamma, dbeta, coef);
+  CA_LAUNCH_CHECK();
+  if (relu && dres) bn_bwd_apply_kernel<true, true><<<grid, BLK, 0, s>>>(dy, y, x, coef, dx, dres, M, C);
+  else if (relu) bn_bwd_apply_kernel<true, false><<<grid, BLK, 0, s>>>(dy, y, x, coef, dx, dres, M, C);
+  else if (dres) bn_bwd_apply_kernel<false, true><<<grid, BLK, 0, s>>>(dy, y, x, coef, dx, dres, M, C);
+  else bn_bwd_apply_kernel<false, false><<<grid, BLK, 0, s>>>(dy, y, x, coef, dx, dres, M, C);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,162 @@
+"""Numerics of the gfx950 HIP kernels vs plain PyTorch fp32 references.
+
+Each test runs the HIP path (CUDA tensors, CLOUD_AMD_OPS=native) and compares
+against the same op computed in fp32 with stock PyTorch on the same inputs.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ext_loaded():
+    from cloud_amd.ops import _ext
+
+    assert _ext.load(required=True) is not None
+
+
+def test_extension_loads():
+    _ext_loaded()
+    import cloud_amd._C as C
+
+    assert C.ARCH == "gfx950"
+
+
+@pytest.mark.parametrize("shape", [(8, 14, 14, 64), (4, 7, 7, 2048), (2, 56, 56, 256), (3, 5, 5, 24)])
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+def test_bn_act_fwd_bwd(shape, relu, res):
+    from cloud_amd.ops import bn_act
+
+    torch.manual_seed(0)
+    C = shape[-1]
+    x = (torch.randn(shape, device=DEV) * 2 + 0.5).to(torch.bfloat16).requires_grad_()
+    r = torch.randn(shape, device=DEV).to(torch.bfloat16).requires_grad_() if res else None
+    g = (torch.rand(C, device=DEV) + 0.5).requires_grad_()
+    b = torch.randn(C, device=DEV).requires_grad_()
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    y = bn_act(x, g, b, rm, rv, residual=r, relu=relu)
+    dy = torch.randn(shape, device=DEV).to(torch.bfloat16)
+    y.backward(dy)
+
+    # fp32 reference
+    xr = x.detach().float().requires_grad_()
+    rr = r.detach().float().requires_grad_() if res else None
+    gr, br = g.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    rm2, rv2 = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    yr = F.batch_norm(xr.reshape(-1, C), rm2, rv2, gr, br, training=True, momentum=0.1, eps=1e-5).reshape(shape)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    yr.backward(dy.float())
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=5e-2, rtol=5e-2)
+    torch.testing.assert_close(g.grad, gr.grad, atol=5e-2 * (x.numel() / C) ** 0.5, rtol=2e-2)
+    torch.testing.assert_close(b.grad, br.grad, atol=5e-2 * (x.numel() / C) ** 0.5, rtol=2e-2)
+    if res:
+        torch.testing.assert_close(r.grad.float(), rr.grad, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(rm, rm2, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(rv, rv2, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("B,C", [(256, 1000), (64, 10), (7, 130)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_softmax_xent(B, C, dtype):
+    from cloud_amd.ops import softmax_cross_entropy
+
+    torch.manual_seed(1)
+    z = (torch.randn(B, C, device=DEV) * 3).to(dtype).requires_grad_()
+    y = torch.randint(0, C, (B,), device=DEV)
+    loss, correct = softmax_cross_entropy(z, y, denom=B)
+    loss.backward()
+    zr = z.detach().float().requires_grad_()
+    lr = F.cross_entropy(zr, y)
+    lr.backward()
+    torch.testing.assert_close(loss.float(), lr, atol=1e-3, rtol=1e-3)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(z.grad.float(), zr.grad, atol=tol / B, rtol=tol)
+    assert torch.equal(correct.bool(), zr.argmax(-1) == y)
+
+
+def test_maxpool_and_gap():
+    from cloud_amd.ops import global_avg_pool_nhwc, max_pool2d_nhwc
+
+    torch.manual_seed(2)
+    x = torch.randn(4, 17, 18, 64, device=DEV).to(torch.bfloat16).requires_grad_()
+    y = max_pool2d_nhwc(x, 3, 2, 1)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    torch.testing.assert_close(y.float(), yr.permute(0, 2, 3, 1), atol=0, rtol=0)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    torch.testing.assert_close(x.grad.float(), xr.grad.permute(0, 2, 3, 1), atol=2e-2, rtol=2e-2)
+
+    x2 = torch.randn(5, 7, 7, 256, device=DEV).to(torch.bfloat16).requires_grad_()
+    g = global_avg_pool_nhwc(x2)
+    g2 = x2.detach().float().mean(dim=(1, 2))
+    torch.testing.assert_close(g.float(), g2, atol=1e-2, rtol=1e-2)
+    dg = torch.randn_like(g)
+    g.backward(dg)
+    torch.testing.assert_close(x2.grad.float(), (dg.float() / 49)[:, None, None, :].expand_as(x2), atol=1e-3, rtol=1e-2)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "sgd_nesterov", "adam", "adamw", "rmsprop"])
+def test_fused_optimizers_match_cpu_reference(kind):
+    from cloud_amd import optim
+
+    torch.manual_seed(3)
+
+    def make(device):
+        torch.manual_seed(3)
+        m = torch.nn.Sequential(torch.nn.Linear(33, 65), torch.nn.Linear(65, 7)).to(device)
+        m[0].weight.data = m[0].weight.data.to(torch.bfloat16)
+        return m
+
+    def opt_for(m):
+        if kind == "sgd":
+            return optim.SGD(m, learning_rate=0.1, momentum=0.9, weight_decay=1e-2)
+        if kind == "sgd_nesterov":
+            return optim.SGD(m, learning_rate=0.1, momentum=0.9, nesterov=True)
+        if kind == "adam":
+            return optim.Adam(m, learning_rate=1e-2, weight_decay=1e-3)
+        if kind == "adamw":
+            return optim.AdamW(m, learning_rate=1e-2, weight_decay=1e-2)
+        return optim.RMSprop(m, learning_rate=1e-2, momentum=0.5)
+
+    mg, mc = make(DEV), make("cpu")
+    og, oc = opt_for(mg), opt_for(mc)
+    for step in range(4):
+        for o in (og, oc):
+            for a in o.arenas:
+                torch.manual_seed(100 + step)
+                a.grad.copy_(torch.randn(a.n).to(a.grad.dtype))
+        og.step()
+        oc.step()
+    for ag, ac in zip(og.arenas, oc.arenas):
+        torch.testing.assert_close(ag.master.cpu(), ac.master, atol=1e-5, rtol=1e-5)
+        if ag.model is not None:
+            torch.testing.assert_close(ag.model.cpu().float(), ac.model.float(), atol=1e-2, rtol=1e-2)
+
+
+def test_resnet_small_trains_on_gpu():
+    from cloud_amd.models.resnet import ResNet
+    from cloud_amd.ops import softmax_cross_entropy
+    from cloud_amd.optim import SGD
+
+    torch.manual_seed(4)
+    m = ResNet((1, 1, 1, 1), num_classes=10, dtype=torch.bfloat16, device=DEV)
+    opt = SGD(m, learning_rate=0.05, momentum=0.9)
+    x = torch.randn(8, 64, 64, 3, device=DEV).to(torch.bfloat16)
+    y = torch.randint(0, 10, (8,), device=DEV)
+    losses = []
+    for _ in range(15):
+        opt.zero_grad()
+        loss, _ = softmax_cross_entropy(m(x), y)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    assert losses[-1] < losses[0] * 0.5, losses
