@@ -1,0 +1,229 @@
+"""On-node job launcher: one process per MI355X (replaces reference ``TFC/core/deploy.py``).
+
+``deploy_job`` keeps the reference's contract -- generate a job id, "submit",
+print the same three info lines, optionally stream logs, return the job id --
+but the "cluster" is the local node:
+
+* world size = chief GPUs + worker_count x worker GPUs (CPU machines: one
+  process each, gloo);
+* every rank gets ``RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE /
+  MASTER_ADDR=127.0.0.1 / MASTER_PORT`` (torch.distributed rendezvous, RCCL
+  over xGMI on GPU), ``TF_CONFIG``-shaped cluster JSON with ``chief`` /
+  ``worker`` roles (``use_chief_in_tf_config`` semantics of reference
+  ``deploy.py:159-161``), the remote markers, and per-rank log files
+  ``logs/<role>-<index>[-gpu<k>].log``;
+* a watchdog: if any rank exits non-zero the rest of the group is terminated,
+  exit codes go to ``job.json`` and the job is marked FAILED;
+* ``stream_logs=True`` tails the chief log (rank 0) to stdout until the job ends.
+
+The launcher process never initialises the GPU (it only counts devices), so
+spawning ranks is safe on the MI355X pool.
+"""
+from __future__ import annotations
+
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+import uuid
+
+from . import topology
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def generate_job_id(prefix="cloud_amd_train"):
+    return "{}_{}".format(prefix, str(uuid.uuid4()).replace("-", "_"))
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def plan_ranks(chief_config, worker_count, worker_config):
+    """List of dicts: one per process, with role/index/local device."""
+    ranks = []
+    machines = [("chief", 0, chief_config)] + [("worker", i, worker_config) for i in range(worker_count)]
+    gpu = 0
+    for role, idx, cfg in machines:
+        n = cfg.num_processes
+        for k in range(n):
+            ranks.append({"role": role, "index": idx, "proc_in_machine": k,
+                          "gpu": gpu if cfg.is_gpu else None})
+            if cfg.is_gpu:
+                gpu += 1
+    for r, info in enumerate(ranks):
+        info["rank"] = r
+    return ranks
+
+
+def tf_config_for(ranks, rank, port):
+    chief = ["127.0.0.1:{}".format(port)]
+    workers = sorted({r["index"] for r in ranks if r["role"] == "worker"})
+    cluster = {"chief": chief}
+    if workers:
+        cluster["worker"] = ["127.0.0.1:{}".format(port + 1 + i) for i in workers]
+    me = ranks[rank]
+    return {"cluster": cluster, "task": {"type": me["role"], "index": me["index"]}}
+
+
+def log_name(info):
+    name = "{}-{}".format(info["role"], info["index"])
+    if info["gpu"] is not None and info["proc_in_machine"] > 0:
+        name += "-gpu{}".format(info["proc_in_machine"])
+    return name + ".log"
+
+
+def _print_logs_info(job_id, job_dir):
+    print("Job submitted successfully.")
+    print("Your job ID is: ", job_id)
+    print("Please access your job logs at the following URL:")
+    print("file://{}".format(os.path.join(job_dir, "logs")))
+
+
+class Job:
+    """A running local job (all rank processes + watchdog)."""
+
+    def __init__(self, job_id, job_dir, procs, ranks, meta):
+        self.job_id, self.job_dir, self.procs, self.ranks, self.meta = job_id, job_dir, procs, ranks, meta
+        self._done = threading.Event()
+        self.returncode = None
+        self._watch = threading.Thread(target=self._watchdog, daemon=True)
+        self._watch.start()
+
+    def _write_meta(self):
+        with open(os.path.join(self.job_dir, "job.json"), "w") as f:
+            json.dump(self.meta, f, indent=2)
+
+    def _watchdog(self):
+        failed_at = None
+        while True:
+            codes = [p.poll() for p in self.procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad and failed_at is None:
+                failed_at = time.time()
+                for p in self.procs:
+                    if p.poll() is None:
+                        try:
+                            os.killpg(p.pid, signal.SIGTERM)
+                        except (ProcessLookupError, PermissionError):
+                            pass
+            if failed_at is not None and time.time() - failed_at > 15:
+                for p in self.procs:
+                    if p.poll() is None:
+                        try:
+                            os.killpg(p.pid, signal.SIGKILL)
+                        except (ProcessLookupError, PermissionError):
+                            pass
+            if all(c is not None for c in codes):
+                break
+            time.sleep(0.2)
+        codes = [p.returncode for p in self.procs]
+        self.meta["exit_codes"] = codes
+        self.meta["end_time"] = time.time()
+        self.returncode = next((c for c in codes if c != 0), 0)
+        self.meta["state"] = "SUCCEEDED" if self.returncode == 0 else "FAILED"
+        self._write_meta()
+        self._done.set()
+
+    def wait(self, timeout=None):
+        self._done.wait(timeout)
+        return self.returncode
+
+    def done(self):
+        return self._done.is_set()
+
+    def log_path(self, rank=0):
+        return os.path.join(self.job_dir, "logs", log_name(self.ranks[rank]))
+
+    def stream(self, rank=0, out=None):
+        """Tail one rank's log to ``out`` until the job finishes."""
+        out = out or sys.stdout
+        path = self.log_path(rank)
+        while not os.path.exists(path) and not self.done():
+            time.sleep(0.05)
+        with open(path, "r", errors="replace") as f:
+            while True:
+                line = f.readline()
+                if line:
+                    out.write(line.replace("\x08", ""))
+                    out.flush()
+                    continue
+                if self.done():
+                    rest = f.read()
+                    if rest:
+                        out.write(rest)
+                        out.flush()
+                    break
+                time.sleep(0.05)
+
+
+def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, entry_point_args=None,
+           job_labels=None, extra_env=None, profile=False, python=None):
+    """Spawn all ranks of a staged job; returns a :class:`Job`."""
+    ranks = plan_ranks(chief_config, worker_count, worker_config)
+    world = len(ranks)
+    port = free_port()
+    app_dir = os.path.dirname(target)
+    python = python or sys.executable
+    any_gpu = any(r["gpu"] is not None for r in ranks)
+    meta = {
+        "job_id": job_id, "state": "RUNNING", "start_time": time.time(), "world_size": world,
+        "chief_config": chief_config.to_dict(), "worker_count": worker_count,
+        "worker_config": worker_config.to_dict() if worker_config is not None and worker_count > 0 else None,
+        "labels": dict(job_labels or {}), "args": list(entry_point_args or []),
+        "backend": "nccl(rccl)" if any_gpu else "gloo", "master_port": port,
+        "ranks": ranks, "node": {"gpus_visible": topology.visible_gpu_count()},
+    }
+    procs = []
+    for info in ranks:
+        env = dict(os.environ)
+        env.update(extra_env or {})
+        env.update({
+            "RANK": str(info["rank"]), "WORLD_SIZE": str(world),
+            "LOCAL_RANK": str(info["gpu"] if info["gpu"] is not None else info["rank"]),
+            "LOCAL_WORLD_SIZE": str(world),
+            "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+            "TF_CONFIG": json.dumps(tf_config_for(ranks, info["rank"], port)),
+            "TF_KERAS_RUNNING_REMOTELY": "1", "CLOUD_AMD_RUNNING_REMOTELY": "1",
+            "CLOUD_AMD_JOB_ID": job_id, "CLOUD_AMD_JOB_DIR": job_dir,
+            "CLOUD_AMD_LAUNCH_TIME": str(meta["start_time"]),
+            "PYTHONPATH": PKG_ROOT + os.pathsep + env.get("PYTHONPATH", ""),
+            "PYTHONUNBUFFERED": "1",
+        })
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if not any_gpu:
+            env["CLOUD_AMD_DEVICE"] = "cpu"
+        cmd = [python, target] + list(entry_point_args or [])
+        if profile and info["rank"] == 0:
+            prof_dir = os.path.join(job_dir, "profile")
+            cmd = ["rocprofv3", "--kernel-trace", "--stats", "-d", prof_dir, "-o", "rank0",
+                   "--output-format", "csv", "--"] + cmd
+        logf = open(os.path.join(job_dir, "logs", log_name(info)), "w")
+        p = subprocess.Popen(cmd, cwd=app_dir, env=env, stdout=logf, stderr=subprocess.STDOUT,
+                             start_new_session=True)
+        logf.close()
+        procs.append(p)
+    job = Job(job_id, job_dir, procs, ranks, meta)
+    job._write_meta()
+    return job
+
+
+def deploy_job(job_id, job_dir, target, chief_config, worker_count, worker_config, entry_point_args,
+               enable_stream_logs, job_labels=None, wait=None, extra_env=None, profile=False):
+    """Submit (spawn) the job, print the info lines, optionally stream/wait. Returns the Job."""
+    job = launch(job_id, job_dir, target, chief_config, worker_count, worker_config, entry_point_args,
+                 job_labels=job_labels, extra_env=extra_env, profile=profile)
+    _print_logs_info(job_id, job_dir)
+    if enable_stream_logs:
+        print("Streaming job logs: ")
+        job.stream(0)
+    if wait or (wait is None and enable_stream_logs):
+        job.wait()
+    return job

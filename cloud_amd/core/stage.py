@@ -1,0 +1,108 @@
+"""Job staging: the local replacement for Docker image build + push.
+
+Reference ``TFC/core/containerize.py`` tarred the entry-point directory,
+generated a Dockerfile and built/pushed an image.  On an MI355X node the
+"image" is a job directory::
+
+    <jobs_root>/<job_id>/
+        app/                 <- entry-point directory tree (same file map as the reference:
+                                entry dir -> app/, wrapper -> app/<wrapper>, requirements -> app/)
+        manifest.json        <- the Dockerfile equivalent: python, entry, env, requirements,
+                                framework/ROCm/arch stamp
+        logs/                <- per-rank logs (filled by the launcher)
+        job.json             <- job metadata + exit codes (launcher)
+
+Requirements are installed best-effort with ``pip install --user`` only when
+``CLOUD_AMD_PIP_INSTALL=1`` (GPU boxes have no package index).
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import subprocess
+import sys
+import time
+
+from ..version import ARCH, __version__
+
+IGNORE = shutil.ignore_patterns("__pycache__", "*.pyc", ".git", "jobs", ".ipynb_checkpoints", "gpurun_out")
+
+
+def _ignore(root):
+    root = os.path.abspath(root)
+
+    def ign(d, names):
+        out = set(IGNORE(d, names))
+        out.update(n for n in names if os.path.abspath(os.path.join(d, n)) == root)
+        return out
+
+    return ign
+
+
+def jobs_root():
+    return os.path.abspath(os.environ.get("CLOUD_AMD_JOBS_DIR", os.path.join(os.getcwd(), "jobs")))
+
+
+def file_path_map(entry_point, preprocessed_entry_point, requirements_txt=None, destination_dir="app"):
+    """source path -> path relative to the job dir (reference containerize.py:235-277)."""
+    if entry_point is None:
+        entry_point = sys.argv[0]
+    entry_dir = os.path.dirname(os.path.abspath(entry_point)) if entry_point else os.getcwd()
+    m = {entry_dir: destination_dir}
+    if preprocessed_entry_point is not None:
+        m[preprocessed_entry_point] = os.path.join(destination_dir, os.path.basename(preprocessed_entry_point))
+    if requirements_txt is not None:
+        m[os.path.abspath(requirements_txt)] = os.path.join(destination_dir, os.path.basename(requirements_txt))
+    return m
+
+
+def _framework_stamp():
+    stamp = {"cloud_amd": __version__, "arch": ARCH, "python": sys.version.split()[0]}
+    try:
+        import torch
+
+        stamp["torch"] = torch.__version__
+        stamp["hip"] = getattr(torch.version, "hip", None)
+    except Exception:  # pragma: no cover
+        pass
+    return stamp
+
+
+def stage_job(job_id, entry_point, preprocessed_entry_point, requirements_txt=None, entry_point_args=None,
+              env=None, root=None):
+    """Create the job directory; return (job_dir, run_target) where run_target is the script to exec."""
+    root = root or jobs_root()
+    job_dir = os.path.join(root, job_id)
+    app = os.path.join(job_dir, "app")
+    os.makedirs(os.path.join(job_dir, "logs"), exist_ok=True)
+    fmap = file_path_map(entry_point, preprocessed_entry_point, requirements_txt)
+    for src, rel in fmap.items():
+        dst = os.path.join(job_dir, rel)
+        if os.path.isdir(src):
+            if os.path.abspath(src).startswith(os.path.abspath(job_dir)):
+                raise ValueError("entry-point directory is inside the job directory")
+            shutil.copytree(src, dst, ignore=_ignore(root), dirs_exist_ok=True, symlinks=False)
+        else:
+            os.makedirs(os.path.dirname(dst), exist_ok=True)
+            shutil.copy2(src, dst)
+    if preprocessed_entry_point is not None:
+        target = os.path.join(app, os.path.basename(preprocessed_entry_point))
+    else:
+        target = os.path.join(app, os.path.basename(entry_point or sys.argv[0]))
+    manifest = {
+        "job_id": job_id,
+        "created": time.time(),
+        "entrypoint": ["python", os.path.relpath(target, job_dir)] + list(entry_point_args or []),
+        "workdir": "app",
+        "requirements": os.path.basename(requirements_txt) if requirements_txt else None,
+        "env": dict(env or {}),
+        "framework": _framework_stamp(),
+        "file_map": {k: v for k, v in fmap.items()},
+    }
+    with open(os.path.join(job_dir, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=2)
+    if requirements_txt and os.environ.get("CLOUD_AMD_PIP_INSTALL") == "1":
+        subprocess.run([sys.executable, "-m", "pip", "install", "--user", "-r",
+                        os.path.join(app, os.path.basename(requirements_txt))], check=False)
+    return job_dir, target

@@ -30,7 +30,7 @@ def conv2d_nhwc(x, w, bias=None, stride=1, padding=0):
         if stride != 1:
             x = x[:, ::stride, ::stride, :]
         N, OH, OW, _ = x.shape
-        y = gemm.linear(x.reshape(N * OH * OW, Cin), w.reshape(Cout, Cin), bias)
+        y = gemm.linear(x.reshape(N * OH * OW, Cin), w.reshape(Cout, Cin), bias, param=w)
         return y.view(N, OH, OW, Cout)
     xc = x.permute(0, 3, 1, 2)          # NCHW view with channels-last strides
     wc = w.permute(0, 3, 1, 2)          # OIHW view with channels-last strides

@@ -97,6 +97,7 @@ def build_arenas(named_params, decay_fn=default_decay):
                     a.model[s.offset:s.offset + s.numel].copy_(src.reshape(-1))
                 s.param.data = flat[s.offset:s.offset + s.numel].view_as(src)
                 s.param.grad = a.grad[s.offset:s.offset + s.numel].view_as(src)
+                s.param._ca_arena = True
         arenas.append(a)
     return arenas
 

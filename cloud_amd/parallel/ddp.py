@@ -28,9 +28,19 @@ keeps the first bucket ready early in backward; tune with
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 import torch.distributed as dist
+
+_ACTIVE = weakref.WeakSet()
+
+
+def notify_grad_ready(param):
+    """Called by ops that write a parameter's gradient straight into its arena
+    slice (bypassing autograd's AccumulateGrad, hence its hooks)."""
+    for r in list(_ACTIVE):
+        r._on_grad(param)
 
 
 class Bucket:
@@ -62,6 +72,7 @@ class GradAllReducer:
         self._build()
         if self.world > 1 and overlap:
             self._install_hooks()
+            _ACTIVE.add(self)
 
     def _build(self):
         for a in self.arenas:

@@ -29,6 +29,10 @@ int ca_maxpool_fwd(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, in
 int ca_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ca_gap_fwd(const bf16_t*, void*, int, int, int, int, hipStream_t);
 int ca_gap_bwd(const void*, int, bf16_t*, int, int, int, hipStream_t);
+int ca_gemm_bf16(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float*, hipStream_t);
+int ca_gemm_splitk(int, const bf16_t*, long, const bf16_t*, long, void*, int, float, int, int, int, int, float*,
+                   hipStream_t);
+int ca_gemm_splitk_effective(int, int);
 }
 
 #define P(T, x) reinterpret_cast<T>(static_cast<uintptr_t>(x))
@@ -102,6 +106,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("gap_fwd", [](u64 x, u64 y, int ybf, int N, int HW, int C, u64 s) {
     check(ca_gap_fwd(P(const bf16_t*, x), P(void*, y), ybf, N, HW, C, S(s)), "gap_fwd");
   });
+  m.def("gemm_bf16", [](int layout, u64 A, long lda, u64 B, long ldb, u64 C, long ldc, int M, int N, int K,
+                        u64 stats, u64 s) {
+    check(ca_gemm_bf16(layout, P(const bf16_t*, A), lda, P(const bf16_t*, B), ldb, P(bf16_t*, C), ldc, M, N, K,
+                       P(float*, stats), S(s)), "gemm_bf16");
+  });
+  m.def("gemm_splitk", [](int layout, u64 A, long lda, u64 B, long ldb, u64 out, int out_bf16, float beta, int M,
+                          int N, int K, int splits, u64 ws, u64 s) {
+    check(ca_gemm_splitk(layout, P(const bf16_t*, A), lda, P(const bf16_t*, B), ldb, P(void*, out), out_bf16, beta,
+                         M, N, K, splits, P(float*, ws), S(s)), "gemm_splitk");
+  });
+  m.def("gemm_splitk_effective", [](int K, int splits) { return ca_gemm_splitk_effective(K, splits); });
   m.def("gap_bwd", [](u64 dy, int dybf, u64 dx, int N, int HW, int C, u64 s) {
     check(ca_gap_bwd(P(const void*, dy), dybf, P(bf16_t*, dx), N, HW, C, S(s)), "gap_bwd");
   });

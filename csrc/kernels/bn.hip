@@ -65,18 +65,38 @@ __device__ __forceinline__ void block_col_reduce(float (&a)[8], float (&b)[8], c
 #pragma unroll
   for (int j = 0; j < 8; ++j) { sa[j * BLK + tid] = a[j]; sb[j * BLK + tid] = b[j]; }
   __syncthreads();
-  // thread (tx, ty<8) sums channel j=ty of column tx over the RP rows
-  if (ty < 8 && vc < t.CT) {
-    float ra = 0.f, rb = 0.f;
-    const int j = ty;
-    for (int r = 0; r < t.RP; ++r) {
-      ra += sa[j * BLK + r * t.TW + tx];
-      rb += sb[j * BLK + r * t.TW + tx];
+  // threads (tx, ty) sum channels j = ty, ty+RP, ... of column tx over the RP rows
+  if (vc < t.CT) {
+    for (int j = ty; j < 8; j += t.RP) {
+      float ra = 0.f, rb = 0.f;
+      for (int r = 0; r < t.RP; ++r) {
+        ra += sa[j * BLK + r * t.TW + tx];
+        rb += sb[j * BLK + r * t.TW + tx];
+      }
+      const int c = vc * 8 + j;
+      ws[(long)chunk * C + c] = ra;
+      ws[(long)(t.nchunks + chunk) * C + c] = rb;
     }
-    const int c = vc * 8 + j;
-    ws[(long)chunk * C + c] = ra;
-    ws[(long)(t.nchunks + chunk) * C + c] = rb;
   }
+}
+
+// Sum the [nchunks][C] partials of channel c with one WAVE (lanes stride over
+// chunks, fp64 accumulation, shuffle reduction).  Returns the totals in every lane.
+__device__ __forceinline__ void wave_chunk_sum(const float* __restrict__ ws, int nchunks, int C, int c,
+                                               double& a, double& b) {
+  const int lane = threadIdx.x & 63;
+  double sa = 0.0, sb = 0.0;
+  for (int k = lane; k < nchunks; k += 64) {
+    sa += ws[(long)k * C + c];
+    sb += ws[(long)(nchunks + k) * C + c];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sa += __shfl_xor(sa, o, 64);
+    sb += __shfl_xor(sb, o, 64);
+  }
+  a = sa;
+  b = sb;
 }
 
 __global__ void __launch_bounds__(BLK) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
@@ -124,13 +144,11 @@ __global__ void bn_fwd_finalize_kernel(const float* __restrict__ ws, int nchunks
                                        float* __restrict__ run_mean, float* __restrict__ run_var,
                                        float* __restrict__ save_mean, float* __restrict__ save_rstd,
                                        float* __restrict__ scale, float* __restrict__ shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int k = 0; k < nchunks; ++k) {
-    s += ws[(long)k * C + c];
-    q += ws[(long)(nchunks + k) * C + c];
-  }
+  double s, q;
+  wave_chunk_sum(ws, nchunks, C, c, s, q);
+  if ((threadIdx.x & 63) != 0) return;
   const double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -241,13 +259,11 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ ws, int nchunks
                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ rstd, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
-  double sd = 0.0, sdx = 0.0;
-  for (int k = 0; k < nchunks; ++k) {
-    sd += ws[(long)k * C + c];
-    sdx += ws[(long)(nchunks + k) * C + c];
-  }
+  double sd, sdx;
+  wave_chunk_sum(ws, nchunks, C, c, sd, sdx);
+  if ((threadIdx.x & 63) != 0) return;
   if (dgamma) dgamma[c] = (float)sdx;
   if (dbeta) dbeta[c] = (float)sd;
   const double g = gamma ? gamma[c] : 1.0;
@@ -315,7 +331,7 @@ int ca_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
   dim3 grid(t.ncol, t.nchunks);
   bn_stats_kernel<<<grid, BLK, 0, s>>>(x, M, C, ws);
   CA_LAUNCH_CHECK();
-  bn_fwd_finalize_kernel<<<ca_cdiv(C, 256), 256, 0, s>>>(ws, t.nchunks, M, C, gamma, beta, eps, momentum,
+  bn_fwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(ws, t.nchunks, M, C, gamma, beta, eps, momentum,
                                                          run_mean, run_var, save_mean, save_rstd,
                                                          scale_shift, scale_shift + C);
   CA_LAUNCH_CHECK();
@@ -351,7 +367,7 @@ int ca_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, long M, int C,
   if (relu) bn_bwd_reduce_kernel<true><<<grid, BLK, 0, s>>>(dy, y, x, save_mean, save_rstd, M, C, ws);
   else bn_bwd_reduce_kernel<false><<<grid, BLK, 0, s>>>(dy, y, x, save_mean, save_rstd, M, C, ws);
   CA_LAUNCH_CHECK();
-  bn_bwd_finalize_kernel<<<ca_cdiv(C, 256), 256, 0, s>>>(ws, t.nchunks, M, C, gamma, save_mean, save_rstd,
+  bn_bwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(ws, t.nchunks, M, C, gamma, save_mean, save_rstd,
                                                          dgamma, dbeta, coef);
   CA_LAUNCH_CHECK();
   if (relu && dres) bn_bwd_apply_kernel<true, true><<<grid, BLK, 0, s>>>(dy, y, x, coef, dx, dres, M, C);

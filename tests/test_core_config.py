@@ -1,0 +1,127 @@
+"""Machine configs, validation and job labels (parity: reference
+core/tests/unit/{validate,gcp}_test.py expectations, adapted to a local MI355X node)."""
+import os
+
+import pytest
+
+from cloud_amd.core import machine_config as mc
+from cloud_amd.core import topology, validate
+
+
+def test_accelerator_enum_and_auto():
+    assert mc.AcceleratorType.AMD_INSTINCT_MI355X.value == "MI355X"
+    assert mc.AcceleratorType.NO_ACCELERATOR in mc.AcceleratorType.all()
+    with pytest.raises(ValueError, match="Invalid accelerator key"):
+        mc.AcceleratorType.validate("H100")
+    cfg = mc.MachineConfig()
+    assert cfg.accelerator_type == mc.AcceleratorType.AMD_INSTINCT_MI355X
+    assert cfg.accelerator_count == 1 and cfg.is_gpu and cfg.num_processes == 1
+
+
+def test_common_configs():
+    c = mc.COMMON_MACHINE_CONFIGS
+    for k in ("CPU", "MI355X_1X", "MI355X_2X", "MI355X_4X", "MI355X_8X", "T4_1X", "V100_4X", "TPU"):
+        assert k in c
+    assert c["MI355X_8X"].accelerator_count == 8 and c["MI355X_8X"].num_processes == 8
+    assert c["CPU"].accelerator_count == 0 and not c["CPU"].is_gpu and c["CPU"].num_processes == 1
+    assert mc.is_tpu_config(c["TPU"]) and not mc.is_tpu_config(c["MI355X_1X"])
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(accelerator_type=mc.AcceleratorType.NO_ACCELERATOR, accelerator_count=2), "CPU machine"),
+    (dict(accelerator_type="MI355X", accelerator_count=9), r"\[1, 8\]"),
+    (dict(accelerator_type="MI355X", accelerator_count=0), r"\[1, 8\]"),
+    (dict(cpu_cores=-1), "cpu_cores"),
+])
+def test_invalid_machine_configs(kw, msg):
+    with pytest.raises(ValueError, match=msg):
+        mc.MachineConfig(**kw)
+
+
+def _ok_kwargs(tmp_path, **over):
+    kw = dict(entry_point=None, requirements_txt=None, distribution_strategy="auto",
+              chief_config=mc.COMMON_MACHINE_CONFIGS["MI355X_1X"], worker_config=mc.COMMON_MACHINE_CONFIGS["MI355X_1X"],
+              worker_count=0, region="local", entry_point_args=None, stream_logs=False,
+              docker_image_bucket_name=None, called_from_notebook=False)
+    kw.update(over)
+    return kw
+
+
+def test_validate_ok(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    (tmp_path / "train.py").write_text("print(1)\n")
+    (tmp_path / "req.txt").write_text("numpy\n")
+    validate.validate(**_ok_kwargs(tmp_path, entry_point="train.py", requirements_txt="req.txt"))
+    validate.validate(**_ok_kwargs(tmp_path, distribution_strategy=None))
+
+
+@pytest.mark.parametrize("over,err", [
+    (dict(entry_point="missing.py"), r"Invalid `entry_point`"),
+    (dict(requirements_txt="nope.txt"), r"Invalid `requirements_txt`"),
+    (dict(distribution_strategy="Mirrored"), r"Invalid `distribution_strategy`"),
+    (dict(chief_config="gpu"), r"Invalid `chief_config`"),
+    (dict(worker_count=-1), r"Invalid `worker_count`"),
+    (dict(worker_count=1, worker_config=None), r"Invalid `worker_config`"),
+    (dict(chief_config=mc.COMMON_MACHINE_CONFIGS["TPU"]), r"Invalid `chief_config`"),
+    (dict(region=3), r"Invalid `region`"),
+    (dict(entry_point_args="--x"), r"Invalid `entry_point_args`"),
+    (dict(stream_logs="yes"), r"Invalid `stream_logs`"),
+])
+def test_validate_errors(tmp_path, monkeypatch, over, err):
+    monkeypatch.chdir(tmp_path)
+    with pytest.raises(ValueError, match=err):
+        validate.validate(**_ok_kwargs(tmp_path, **over))
+
+
+def test_validate_bad_suffix(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    (tmp_path / "train.txt").write_text("x")
+    with pytest.raises(ValueError, match="Expected a python file or an iPython notebook"):
+        validate.validate(**_ok_kwargs(tmp_path, entry_point="train.txt"))
+
+
+def test_tpu_worker_rejected(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    with pytest.raises(ValueError, match="Expected worker_count=1"):
+        validate.validate(**_ok_kwargs(tmp_path, worker_count=2, worker_config=mc.COMMON_MACHINE_CONFIGS["TPU"]))
+    with pytest.raises(NotImplementedError):
+        validate.validate(**_ok_kwargs(tmp_path, worker_count=1, worker_config=mc.COMMON_MACHINE_CONFIGS["TPU"]))
+
+
+def test_node_capacity():
+    c8 = mc.COMMON_MACHINE_CONFIGS["MI355X_8X"]
+    validate.validate_node_capacity(c8, None, 0, available=8)
+    with pytest.raises(ValueError, match="needs 16 GPUs"):
+        validate.validate_node_capacity(c8, c8, 1, available=8)
+    validate.validate_node_capacity(mc.COMMON_MACHINE_CONFIGS["CPU"], mc.COMMON_MACHINE_CONFIGS["CPU"], 3,
+                                    available=0)
+
+
+@pytest.mark.parametrize("labels,err", [
+    ({"Key": "v"}, "Label key must start with lowercase"),
+    ({"k": "V"}, "Label value must start with lowercase"),
+    ({"k" * 64: "v"}, "Label key is too long"),
+    ({"k": "v" * 64}, "Label value is too long"),
+    ({"k.x": "v"}, "Label key can only contain"),
+    ({"k": "v!"}, "Label value can only contain"),
+    ({f"k{i}": "v" for i in range(65)}, "too many labels"),
+])
+def test_job_label_errors(labels, err):
+    with pytest.raises(ValueError, match=err):
+        topology.validate_job_labels(labels)
+
+
+def test_job_labels_ok(capsys):
+    topology.validate_job_labels({"team": "vision", "run_1": "a-b"})
+    topology.validate_job_labels({})
+    assert "No labels provided" in capsys.readouterr().out
+
+
+def test_topology_counts(monkeypatch):
+    monkeypatch.setenv("CLOUD_AMD_NUM_GPUS", "8")
+    assert topology.visible_gpu_count() == 8
+    monkeypatch.delenv("CLOUD_AMD_NUM_GPUS")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,3")
+    assert topology.visible_gpu_count() == 2
+    assert topology.xgmi_links_per_gpu(8) == 7
+    assert topology.get_region() == os.environ.get("CLOUD_AMD_REGION", "local")

