@@ -26,8 +26,8 @@ class Conv2d(nn.Module):
         self.weight = nn.Parameter(w.to(dtype))
         self.bias = nn.Parameter(torch.zeros(cout, dtype=dtype, device=device)) if bias else None
 
-    def forward(self, x):
-        return ops.conv2d_nhwc(x, self.weight, self.bias, self.stride, self.padding)
+    def forward(self, x, stats=False):
+        return ops.conv2d_nhwc(x, self.weight, self.bias, self.stride, self.padding, stats=stats)
 
     def extra_repr(self):
         return f"{self.cin}, {self.cout}, k={self.k}, s={self.stride}, p={self.padding}"
@@ -44,9 +44,12 @@ class BatchNormAct(nn.Module):
         self.register_buffer("running_mean", torch.zeros(c, device=device))
         self.register_buffer("running_var", torch.ones(c, device=device))
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, partials=None):
+        if isinstance(x, tuple):  # (conv output, fused statistics partials)
+            x, partials = x
         return ops.bn_act(x, self.weight, self.bias, self.running_mean, self.running_var, residual=residual,
-                          eps=self.eps, momentum=self.momentum, relu=self.relu, training=self.training)
+                          eps=self.eps, momentum=self.momentum, relu=self.relu, training=self.training,
+                          partials=partials)
 
 
 class Linear(nn.Module):

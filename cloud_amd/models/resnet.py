@@ -27,6 +27,7 @@ class Bottleneck(nn.Module):
         self.bn2 = BatchNormAct(width, relu=True, device=device)
         self.conv3 = Conv2d(width, cout, 1, dtype=dtype, device=device)
         self.bn3 = BatchNormAct(cout, relu=True, zero_init=zero_init_residual, device=device)
+        self.fused_stats = True
         self.downsample = None
         if stride != 1 or cin != cout:
             self.downsample = nn.ModuleDict({
@@ -36,11 +37,12 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         identity = x
+        fs = self.fused_stats
         if self.downsample is not None:
-            identity = self.downsample["bn"](self.downsample["conv"](x))
-        out = self.bn1(self.conv1(x))
-        out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), residual=identity)
+            identity = self.downsample["bn"](self.downsample["conv"](x, stats=fs))
+        out = self.bn1(self.conv1(x, stats=fs))
+        out = self.bn2(self.conv2(out, stats=fs))
+        return self.bn3(self.conv3(out, stats=fs), residual=identity)
 
 
 class ResNet(nn.Module):
@@ -68,12 +70,15 @@ class ResNet(nn.Module):
         """x: NHWC [N, H, W, in_channels] in the compute dtype -> logits [N, classes]."""
         if self.stem_cin != self.in_channels:
             x = torch.nn.functional.pad(x, (0, self.stem_cin - self.in_channels))
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.maxpool(self.bn1(self.conv1(x, stats=True)))
         x = self.layers(x)
         return self.fc(self.pool(x))
 
 
 def resnet50(**kw):
+    """ResNet-50 v1.5.  The 3-channel input is zero-padded to 8 channels so the 7x7
+    stem runs on the implicit-GEMM kernel (16-byte channel chunks)."""
+    kw.setdefault("stem_channels_pad", 5)
     return ResNet((3, 4, 6, 3), **kw)
 
 

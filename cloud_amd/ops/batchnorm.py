@@ -45,22 +45,30 @@ def _torch_bn_act(x, res, gamma, beta, running_mean, running_var, eps, momentum,
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, gamma, beta, running_mean, running_var, eps, momentum, relu):
+    def forward(ctx, x, res, gamma, beta, running_mean, running_var, eps, momentum, relu, partials):
         ext = _ext.load(required=True)
         assert x.dtype == torch.bfloat16 and x.is_contiguous(), "bn_act expects contiguous NHWC bf16"
         C = x.shape[-1]
         M = x.numel() // C
         dev = x.device
         y = torch.empty_like(x)
-        ws = torch.empty(ext.bn_workspace_floats(M, C), dtype=torch.float32, device=dev)
         stats = torch.empty(4 * C, dtype=torch.float32, device=dev)  # mean, rstd, scale, shift
         if res is not None:
             assert res.shape == x.shape and res.dtype == x.dtype
             res = res.contiguous()
-        ext.bn_fwd(x.data_ptr(), _ext.ptr(res), y.data_ptr(), M, C, _ext.ptr(gamma), _ext.ptr(beta),
-                   float(eps), float(momentum), _ext.ptr(running_mean), _ext.ptr(running_var),
-                   stats.data_ptr(), stats.data_ptr() + 4 * C, stats.data_ptr() + 8 * C, ws.data_ptr(),
-                   int(relu), _ext.stream_handle(dev))
+        if partials is not None:
+            assert partials.shape[1:] == (2, C), partials.shape
+            ext.bn_fwd_partials(x.data_ptr(), _ext.ptr(res), y.data_ptr(), M, C, partials.data_ptr(),
+                                partials.shape[0], _ext.ptr(gamma), _ext.ptr(beta), float(eps), float(momentum),
+                                _ext.ptr(running_mean), _ext.ptr(running_var), stats.data_ptr(),
+                                stats.data_ptr() + 4 * C, stats.data_ptr() + 8 * C, int(relu),
+                                _ext.stream_handle(dev))
+        else:
+            ws = torch.empty(ext.bn_workspace_floats(M, C), dtype=torch.float32, device=dev)
+            ext.bn_fwd(x.data_ptr(), _ext.ptr(res), y.data_ptr(), M, C, _ext.ptr(gamma), _ext.ptr(beta),
+                       float(eps), float(momentum), _ext.ptr(running_mean), _ext.ptr(running_var),
+                       stats.data_ptr(), stats.data_ptr() + 4 * C, stats.data_ptr() + 8 * C, ws.data_ptr(),
+                       int(relu), _ext.stream_handle(dev))
         ctx.save_for_backward(x, y, gamma, stats)
         ctx.relu = relu
         ctx.has_res = res is not None
@@ -86,14 +94,18 @@ class _BNActFn(torch.autograd.Function):
                    coef.data_ptr(), ws.data_ptr(), int(ctx.relu), _ext.stream_handle(dev))
         if dres is None and ctx.has_res and ctx.needs_input_grad[1]:
             raise RuntimeError("residual grad requested but not produced")
-        return dx, dres, dgamma, dbeta, None, None, None, None, None
+        return dx, dres, dgamma, dbeta, None, None, None, None, None, None
 
 
 def bn_act(x, gamma, beta, running_mean, running_var, *, residual=None, eps=1e-5, momentum=0.1,
-           relu=True, training=True):
-    """y = act(BN(x) [+ residual]) over the last (channel) dim of an NHWC tensor."""
+           relu=True, training=True, partials=None):
+    """y = act(BN(x) [+ residual]) over the last (channel) dim of an NHWC tensor.
+
+    ``partials``: optional [tiles][2][C] channel sum / sum-of-squares partials of
+    ``x`` produced by the convolution epilogue (skips the statistics pass).
+    """
     if training and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0 and _ext.use_native(x):
-        return _BNActFn.apply(x, residual, gamma, beta, running_mean, running_var, eps, momentum, relu)
+        return _BNActFn.apply(x, residual, gamma, beta, running_mean, running_var, eps, momentum, relu, partials)
     if not training and x.is_cuda and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0 and _ext.use_native(x):
         ext = _ext.load(required=True)
         C = x.shape[-1]

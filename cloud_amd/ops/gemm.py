@@ -28,7 +28,7 @@ BK = 64
 
 
 def _native_ok(M, N, K):
-    return K % BK == 0 and N % 8 == 0 and M % 8 == 0 and M > 0
+    return K % 8 == 0 and N % 8 == 0 and M % 8 == 0 and M > 0 and M * max(K, N) < 2 ** 31
 
 
 def _gemm_mode():
@@ -42,20 +42,23 @@ def mm_nt(x, w, stats=None):
     N = w.shape[0]
     y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
     ext.gemm_bf16(NT, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), y.data_ptr(), N, M, N, K,
-                  _ext.ptr(stats), _ext.stream_handle(x.device))
+                  _ext.ptr(stats), 0.0, _ext.stream_handle(x.device))
     return y
 
 
-def mm_nn(a, b):
-    """a [M,K] @ b[K,N] -> [M,N] bf16 (native; b read transposed in LDS)."""
+def mm_nn(a, b, out=None, beta=0.0):
+    """a [M,K] @ b[K,N] (+ beta*out) -> [M,N] bf16 (native; b read transposed in LDS)."""
     ext = _ext.load(required=True)
     M, K = a.shape
     N = b.shape[1]
-    if K % BK or N % 8 or b.stride(1) != 1 or a.stride(1) != 1:
-        return torch.mm(a, b)
-    y = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if K % 8 or N % 8 or b.stride(1) != 1 or a.stride(1) != 1:
+        r = torch.mm(a, b)
+        if out is not None:
+            return out.copy_(r + beta * out) if beta else out.copy_(r)
+        return r
+    y = out if out is not None else torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
     ext.gemm_bf16(NN, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), y.data_ptr(), N, M, N, K, 0,
-                  _ext.stream_handle(a.device))
+                  float(beta), _ext.stream_handle(a.device))
     return y
 
 
@@ -70,7 +73,7 @@ def mm_tn_into(a, b, out, beta=0.0, splits=None):
     ext = _ext.load(required=True)
     K, M = a.shape
     N = b.shape[1]
-    if K % BK or M % 8 or N % 8 or (M * N) % 4 or a.stride(1) != 1 or b.stride(1) != 1:
+    if M % 8 or N % 8 or (M * N) % 4 or a.stride(1) != 1 or b.stride(1) != 1:
         r = torch.mm(a.t().float(), b.float())
         if beta:
             r = r + beta * out.float()
@@ -97,10 +100,10 @@ class _LinearFn(torch.autograd.Function):
     """y = x @ w2d^T where w2d is a 2-D view of ``param`` (passed for its .grad)."""
 
     @staticmethod
-    def forward(ctx, x, w2d, param):
+    def forward(ctx, x, w2d, param, stats):
         ctx.save_for_backward(x, w2d)
         ctx.param = param
-        return mm_nt(x, w2d)
+        return mm_nt(x, w2d, stats=stats)
 
     @staticmethod
     def backward(ctx, dy):
@@ -123,10 +126,10 @@ class _LinearFn(torch.autograd.Function):
                     dparam = g.view_as(param)
                 else:
                     dw = g
-        return dx, dw, dparam
+        return dx, dw, dparam, None
 
 
-def linear(x, w, bias=None, param=None):
+def linear(x, w, bias=None, param=None, stats=None):
     """x @ w^T + bias; ``param`` = the leaf Parameter that ``w`` is a (reshaped) view of."""
     M, K = x.shape
     N = w.shape[0]
@@ -135,10 +138,26 @@ def linear(x, w, bias=None, param=None):
         if param is None and w.is_leaf and w.requires_grad:
             param = w
         if param is not None:
-            y = _LinearFn.apply(x.contiguous(), w.detach(), param)
+            y = _LinearFn.apply(x.contiguous(), w.detach(), param, stats)
         else:
-            y = _LinearFn.apply(x.contiguous(), w, None)
+            y = _LinearFn.apply(x.contiguous(), w, None, stats)
         if bias is not None:
             y = y + bias
         return y
-    return F.linear(x, w, bias)
+    y = F.linear(x, w, bias)
+    if stats is not None:
+        fill_stats_torch(y, stats)
+    return y
+
+
+def fill_stats_torch(y2d, stats):
+    """Reference/fallback for the fused BN-statistics epilogue ([tiles][2][C], 128-row tiles)."""
+    M, C = y2d.shape
+    tiles = stats.shape[0]
+    yf = y2d.float()
+    pad = tiles * 128 - M
+    if pad:
+        yf = torch.cat([yf, yf.new_zeros(pad, C)])
+    yt = yf.view(tiles, 128, C)
+    stats[:, 0].copy_(yt.sum(1))
+    stats[:, 1].copy_((yt * yt).sum(1))

@@ -22,6 +22,8 @@ long ca_bn_workspace_floats(long, int);
 int ca_bn_fwd(const bf16_t*, const bf16_t*, bf16_t*, long, int, const float*, const float*, float, float,
               float*, float*, float*, float*, float*, float*, int, hipStream_t);
 int ca_bn_apply(const bf16_t*, const bf16_t*, bf16_t*, long, int, const float*, int, hipStream_t);
+int ca_bn_fwd_partials(const bf16_t*, const bf16_t*, bf16_t*, long, int, const float*, int, const float*, const float*,
+                       float, float, float*, float*, float*, float*, float*, int, hipStream_t);
 int ca_bn_bwd(const bf16_t*, const bf16_t*, const bf16_t*, long, int, const float*, const float*, const float*,
               bf16_t*, bf16_t*, float*, float*, float*, float*, int, hipStream_t);
 int ca_softmax_xent(const void*, int, const int64_t*, int, int, float, float, float*, float*, void*, hipStream_t);
@@ -29,7 +31,15 @@ int ca_maxpool_fwd(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, in
 int ca_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ca_gap_fwd(const bf16_t*, void*, int, int, int, int, hipStream_t);
 int ca_gap_bwd(const void*, int, bf16_t*, int, int, int, hipStream_t);
-int ca_gemm_bf16(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float*, hipStream_t);
+int ca_gemm_bf16(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float*, float,
+                 hipStream_t);
+int ca_conv_fwd(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int, float*,
+                hipStream_t);
+int ca_conv_dgrad(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int, float,
+                  hipStream_t);
+int ca_conv_wgrad(const bf16_t*, const bf16_t*, void*, int, float, int, int, int, int, int, int, int, int, int, int,
+                  int, int, float*, hipStream_t);
+int ca_splitk_reduce(const float*, int, long, void*, int, float, hipStream_t);
 int ca_gemm_splitk(int, const bf16_t*, long, const bf16_t*, long, void*, int, float, int, int, int, int, float*,
                    hipStream_t);
 int ca_gemm_splitk_effective(int, int);
@@ -78,6 +88,13 @@ PYBIND11_MODULE(_C, m) {
                     P(const float*, beta), eps, momentum, P(float*, rm), P(float*, rv), P(float*, sm), P(float*, sr),
                     P(float*, ss), P(float*, ws), relu, S(s)), "bn_fwd");
   });
+  m.def("bn_fwd_partials", [](u64 x, u64 res, u64 y, long M, int C, u64 parts, int nparts, u64 gamma, u64 beta,
+                              float eps, float momentum, u64 rm, u64 rv, u64 sm, u64 sr, u64 ss, int relu, u64 s) {
+    check(ca_bn_fwd_partials(P(const bf16_t*, x), P(const bf16_t*, res), P(bf16_t*, y), M, C, P(const float*, parts),
+                             nparts, P(const float*, gamma), P(const float*, beta), eps, momentum, P(float*, rm),
+                             P(float*, rv), P(float*, sm), P(float*, sr), P(float*, ss), relu, S(s)),
+          "bn_fwd_partials");
+  });
   m.def("bn_apply", [](u64 x, u64 res, u64 y, long M, int C, u64 ss, int relu, u64 s) {
     check(ca_bn_apply(P(const bf16_t*, x), P(const bf16_t*, res), P(bf16_t*, y), M, C, P(const float*, ss), relu,
                       S(s)), "bn_apply");
@@ -107,9 +124,27 @@ PYBIND11_MODULE(_C, m) {
     check(ca_gap_fwd(P(const bf16_t*, x), P(void*, y), ybf, N, HW, C, S(s)), "gap_fwd");
   });
   m.def("gemm_bf16", [](int layout, u64 A, long lda, u64 B, long ldb, u64 C, long ldc, int M, int N, int K,
-                        u64 stats, u64 s) {
+                        u64 stats, float beta, u64 s) {
     check(ca_gemm_bf16(layout, P(const bf16_t*, A), lda, P(const bf16_t*, B), ldb, P(bf16_t*, C), ldc, M, N, K,
-                       P(float*, stats), S(s)), "gemm_bf16");
+                       P(float*, stats), beta, S(s)), "gemm_bf16");
+  });
+  m.def("conv_fwd", [](u64 x, u64 w, u64 y, int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw,
+                       int ph, int pw, u64 stats, u64 s) {
+    check(ca_conv_fwd(P(const bf16_t*, x), P(const bf16_t*, w), P(bf16_t*, y), Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph,
+                      pw, P(float*, stats), S(s)), "conv_fwd");
+  });
+  m.def("conv_dgrad", [](u64 dy, u64 w, u64 dx, int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh,
+                         int sw, int ph, int pw, float beta, u64 s) {
+    check(ca_conv_dgrad(P(const bf16_t*, dy), P(const bf16_t*, w), P(bf16_t*, dx), Nb, H, W, Cin, Cout, KH, KW, sh, sw,
+                        ph, pw, beta, S(s)), "conv_dgrad");
+  });
+  m.def("conv_wgrad", [](u64 dy, u64 x, u64 dw, int dw_bf16, float beta, int Nb, int H, int W, int Cin, int Cout,
+                         int KH, int KW, int sh, int sw, int ph, int pw, int splits, u64 ws, u64 s) {
+    check(ca_conv_wgrad(P(const bf16_t*, dy), P(const bf16_t*, x), P(void*, dw), dw_bf16, beta, Nb, H, W, Cin, Cout,
+                        KH, KW, sh, sw, ph, pw, splits, P(float*, ws), S(s)), "conv_wgrad");
+  });
+  m.def("splitk_reduce", [](u64 ws, int splits, long MN, u64 out, int out_bf16, float beta, u64 s) {
+    check(ca_splitk_reduce(P(const float*, ws), splits, MN, P(void*, out), out_bf16, beta, S(s)), "splitk_reduce");
   });
   m.def("gemm_splitk", [](int layout, u64 A, long lda, u64 B, long ldb, u64 out, int out_bf16, float beta, int M,
                           int N, int K, int splits, u64 ws, u64 s) {

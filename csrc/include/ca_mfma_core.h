@@ -1,0 +1,302 @@
+// Shared MFMA GEMM core for cloud_amd's dense and implicit-GEMM convolution
+// kernels (gfx950 / CDNA4).
+//
+//   C[M,N] = sum_k A(m,k) * B(k,n)      bf16 operands, fp32 accumulation
+//
+// The core is parameterised by two *loader* policies (how a 16-B chunk of the
+// A or B tile is fetched from global memory: dense row-major, or gathered from
+// an NHWC activation for implicit-GEMM convolution) and an epilogue mode.
+//
+//  * MFMA: v_mfma_f32_16x16x32_bf16; a workgroup = WM x WN waves of 64 lanes.
+//  * BK = 64; register-staged global->LDS double buffering, one barrier per K
+//    step: the next tile's 16-B global loads are issued before this tile's
+//    MFMAs and written to the other LDS buffer after them.
+//  * K-contiguous tiles ("KC") live in LDS as [rows][64+8] and feed MFMA with
+//    ds_read_b128 (16-B padded rows: conflict-free for 16 consecutive rows);
+//    M/N-contiguous tiles ("NC") live as [64][rows+8] and feed MFMA through the
+//    gfx950 transposed read ds_read_b64_tr_b16 (two per fragment).
+//  * blockIdx -> tile mapping is XCD-aware and bijective (contiguous tile
+//    ranges per XCD share an L2).
+//  * Split-K over grid.z writes fp32 slabs (deterministic reduce kernel).
+#pragma once
+#include "ca_common.h"
+
+namespace ca {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4v lds_s4v;
+
+constexpr int BK = 64;
+constexpr int PAD = 8;
+
+enum Epi { EPI_BF16 = 0, EPI_F32_PARTIAL = 1 };
+
+// Fast unsigned division by a runtime constant (n < 2^31): q = (umulhi(n, m) + n) >> s.
+struct FastDiv {
+  uint32_t d, m, s;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while (s < 32 && (1u << s) < d) ++s;
+  const uint64_t one = 1;
+  f.m = (uint32_t)(((one << 32) * ((one << s) - d)) / d + 1);
+  f.s = s;
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+
+// Everything any loader / epilogue may need (one kernel-argument struct).
+struct CoreParams {
+  const bf16_t* A; long lda;
+  const bf16_t* B; long ldb;
+  void* C; long ldc;
+  float* stats;          // optional: per-M-tile column [sum | sumsq] partials [tiles_m][2][N]
+  float beta;            // C = acc + beta * C_old (bf16 epilogue)
+  int M, N, K;
+  int k_per_split;
+  long split_stride;
+  // convolution geometry (NHWC input [Nb,H,W,Cin], output [Nb,OH,OW,Cout], weights [Cout][KH][KW][Cin])
+  int Nb, H, W, Cin, OH, OW, Cout, KH, KW, sh, sw, ph, pw;
+  FastDiv div_ow, div_oh, div_w, div_h, div_cin, div_cout, div_kw;
+};
+
+template <int R, bool KC>
+struct TileGeom {
+  static constexpr int ROWS = KC ? R : BK;
+  static constexpr int COLS = KC ? BK : R;
+  static constexpr int LD = COLS + PAD;
+  static constexpr int ELEMS = ROWS * LD;
+  static constexpr int CHUNKS = ROWS * COLS / 8;
+};
+
+template <int R, bool KC>
+__device__ __forceinline__ void chunk_coords(int c, int& row, int& col) {
+  using G = TileGeom<R, KC>;
+  row = c / (G::COLS / 8);
+  col = (c % (G::COLS / 8)) * 8;
+}
+
+template <int R, bool KC>
+__device__ __forceinline__ bf16x8 read_frag(const short* lds, int r0, int k0, int lane) {
+  using G = TileGeom<R, KC>;
+  if constexpr (KC) {
+    s8v v = *reinterpret_cast<const s8v*>(lds + (r0 + (lane & 15)) * G::LD + k0 + 8 * (lane >> 4));
+    return __builtin_bit_cast(bf16x8, v);
+  } else {
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const short* b0 = lds + (k0 + 8 * g + q) * G::LD + r0 + 4 * p;
+    s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b0));
+    s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b0 + 4 * G::LD));
+    s8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+__device__ __forceinline__ s8v zero8() { return s8v{0, 0, 0, 0, 0, 0, 0, 0}; }
+__device__ __forceinline__ s8v ld16(const bf16_t* p) { return *reinterpret_cast<const s8v*>(p); }
+
+// ---------------------------------------------------------------- loaders --
+// A loader fetches the chunk (row, col) of the tile whose corner is (r0, k0).
+// KC loaders: row = output-dim index offset, col = k offset.
+// NC loaders: row = k offset, col = output-dim offset.
+
+// Dense operand, K-contiguous: X[r][k] at p[r*ld + k].
+template <int R>
+struct DenseKC {
+  static constexpr bool KC = true;
+  const bf16_t* p; long ld; int rlimit, K;
+  __device__ DenseKC(const CoreParams& P, bool isA) {
+    p = isA ? P.A : P.B; ld = isA ? P.lda : P.ldb; rlimit = isA ? P.M : P.N; K = P.K;
+  }
+  __device__ __forceinline__ s8v load(int r0, int k0, int row, int col) const {
+    const int r = r0 + row, k = k0 + col;
+    return (r < rlimit && k < K) ? ld16(p + (long)r * ld + k) : zero8();
+  }
+};
+
+// Dense operand, output-dim contiguous: X[r][k] at p[k*ld + r].
+template <int R>
+struct DenseNC {
+  static constexpr bool KC = false;
+  const bf16_t* p; long ld; int rlimit, K;
+  __device__ DenseNC(const CoreParams& P, bool isA) {
+    p = isA ? P.A : P.B; ld = isA ? P.lda : P.ldb; rlimit = isA ? P.M : P.N; K = P.K;
+  }
+  __device__ __forceinline__ s8v load(int r0, int k0, int row, int col) const {
+    const int k = k0 + row, r = r0 + col;
+    return (r < rlimit && k < K) ? ld16(p + (long)k * ld + r) : zero8();
+  }
+};
+
+// ------------------------------------------------------------------ core --
+template <int BM, int BN, int WM, int WN, class LA, class LB, int EPI>
+__device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  using GA = TileGeom<BM, LA::KC>;
+  using GB = TileGeom<BN, LB::KC>;
+  constexpr int STAGE = GA::ELEMS + GB::ELEMS;
+  constexpr int EPI_LD = BN + PAD;
+  constexpr int SMEM = (2 * STAGE > BM * EPI_LD ? 2 * STAGE : BM * EPI_LD);
+  constexpr int CPA = GA::CHUNKS / NT, CPB = GB::CHUNKS / NT;
+  static_assert(GA::CHUNKS % NT == 0 && GB::CHUNKS % NT == 0, "tile chunks must divide threads");
+  __shared__ __attribute__((aligned(16))) short smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_m = (P.M + BM - 1) / BM, tiles_n = (P.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.z * P.k_per_split;
+  int kend = kbeg + P.k_per_split;
+  if (kend > P.K) kend = P.K;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  const LA la(P, true);
+  const LB lb(P, false);
+  s8v ra[CPA], rb[CPB];
+  int arow[CPA], acol[CPA], brow[CPB], bcol[CPB];
+#pragma unroll
+  for (int i = 0; i < CPA; ++i) chunk_coords<BM, LA::KC>(tid + i * NT, arow[i], acol[i]);
+#pragma unroll
+  for (int i = 0; i < CPB; ++i) chunk_coords<BN, LB::KC>(tid + i * NT, brow[i], bcol[i]);
+
+  f4v acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < CPA; ++i) ra[i] = la.load(m0, k0, arow[i], acol[i]);
+#pragma unroll
+    for (int i = 0; i < CPB; ++i) rb[i] = lb.load(n0, k0, brow[i], bcol[i]);
+  };
+  auto lstore = [&](short* base) {
+#pragma unroll
+    for (int i = 0; i < CPA; ++i) *reinterpret_cast<s8v*>(base + arow[i] * GA::LD + acol[i]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < CPB; ++i) *reinterpret_cast<s8v*>(base + GA::ELEMS + brow[i] * GB::LD + bcol[i]) = rb[i];
+  };
+
+  if (nk > 0) {
+    gload(kbeg);
+    lstore(smem);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int t = 0; t < nk; ++t) {
+    const bool more = (t + 1) < nk;
+    if (more) gload(kbeg + (t + 1) * BK);
+    const short* As = smem + cur * STAGE;
+    const short* Bs = As + GA::ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, LA::KC>(As, wm * (BM / WM) + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, LB::KC>(Bs, wn * (BN / WN) + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) lstore(smem + (cur ^ 1) * STAGE);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // C/D layout of mfma_f32_16x16x32: col = lane&15, row = (lane>>4)*4 + r
+  const int rbase = wm * (BM / WM) + (lane >> 4) * 4;
+  const int cbase = wn * (BN / WN) + (lane & 15);
+  if constexpr (EPI == EPI_F32_PARTIAL) {
+    float* Cp = reinterpret_cast<float*>(P.C) + (long)blockIdx.z * P.split_stride;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gm = m0 + rbase + i * 16 + r, gn = n0 + cbase + j * 16;
+          if (gm < P.M && gn < P.N) Cp[(long)gm * P.ldc + gn] = acc[i][j][r];
+        }
+    return;
+  } else {
+    short* Cs = smem;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(rbase + i * 16 + r) * EPI_LD + cbase + j * 16] = (short)f2bf(acc[i][j][r]);
+    __syncthreads();
+    bf16_t* Cg = reinterpret_cast<bf16_t*>(P.C);
+    constexpr int CH = BM * BN / 8;
+    for (int c = tid; c < CH; c += NT) {
+      const int row = c / (BN / 8), col = (c % (BN / 8)) * 8;
+      const int gm = m0 + row, gn = n0 + col;
+      if (gm < P.M && gn < P.N) {
+        s8v v = *reinterpret_cast<const s8v*>(Cs + row * EPI_LD + col);
+        bf16_t* dst = Cg + (long)gm * P.ldc + gn;
+        if (P.beta != 0.f) {
+          s8v o = *reinterpret_cast<const s8v*>(dst);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[j] = (short)f2bf(bf2f((bf16_t)v[j]) + P.beta * bf2f((bf16_t)o[j]));
+          if (P.stats) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
+        }
+        *reinterpret_cast<s8v*>(dst) = v;
+      }
+    }
+    if (P.stats) {
+      // per-column sum / sum of squares of the stored bf16 values of this tile
+      constexpr int TPC = NT / BN;
+      const int col = tid % BN, part = tid / BN;
+      float s = 0.f, q = 0.f;
+      int rows = P.M - m0;
+      if (rows > BM) rows = BM;
+      __syncthreads();
+      for (int r = part; r < rows; r += TPC) {
+        const float v = bf2f((bf16_t)Cs[r * EPI_LD + col]);
+        s += v;
+        q += v * v;
+      }
+      __syncthreads();
+      float* sred = reinterpret_cast<float*>(smem);
+      sred[part * BN + col] = s;
+      sred[(TPC + part) * BN + col] = q;
+      __syncthreads();
+      if (part == 0 && n0 + col < P.N) {
+        float ts = 0.f, tq = 0.f;
+#pragma unroll
+        for (int pp = 0; pp < TPC; ++pp) {
+          ts += sred[pp * BN + col];
+          tq += sred[(TPC + pp) * BN + col];
+        }
+        float* st = P.stats + (long)tm * 2 * P.N;
+        st[n0 + col] = ts;
+        st[P.N + n0 + col] = tq;
+      }
+    }
+  }
+}
+
+}  // namespace ca

@@ -82,13 +82,13 @@ __device__ __forceinline__ void block_col_reduce(float (&a)[8], float (&b)[8], c
 
 // Sum the [nchunks][C] partials of channel c with one WAVE (lanes stride over
 // chunks, fp64 accumulation, shuffle reduction).  Returns the totals in every lane.
-__device__ __forceinline__ void wave_chunk_sum(const float* __restrict__ ws, int nchunks, int C, int c,
-                                               double& a, double& b) {
+__device__ __forceinline__ void wave_chunk_sum(const float* __restrict__ ws, int nchunks, long stride_k, long off_q,
+                                               int c, double& a, double& b) {
   const int lane = threadIdx.x & 63;
   double sa = 0.0, sb = 0.0;
   for (int k = lane; k < nchunks; k += 64) {
-    sa += ws[(long)k * C + c];
-    sb += ws[(long)(nchunks + k) * C + c];
+    sa += ws[(long)k * stride_k + c];
+    sb += ws[(long)k * stride_k + off_q + c];
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -138,7 +138,8 @@ __global__ void __launch_bounds__(BLK) bn_stats_kernel(const bf16_t* __restrict_
 //   save_mean/save_rstd : fp32 [C] (needed by backward)
 //   scale/shift         : fp32 [C], y = x*scale + shift
 //   running stats updated in place when non-null (unbiased variance).
-__global__ void bn_fwd_finalize_kernel(const float* __restrict__ ws, int nchunks, long M, int C,
+__global__ void bn_fwd_finalize_kernel(const float* __restrict__ ws, int nchunks, long stride_k, long off_q,
+                                       long M, int C,
                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                        float eps, float momentum,
                                        float* __restrict__ run_mean, float* __restrict__ run_var,
@@ -147,7 +148,7 @@ __global__ void bn_fwd_finalize_kernel(const float* __restrict__ ws, int nchunks
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
   double s, q;
-  wave_chunk_sum(ws, nchunks, C, c, s, q);
+  wave_chunk_sum(ws, nchunks, stride_k, off_q, c, s, q);
   if ((threadIdx.x & 63) != 0) return;
   const double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
@@ -262,7 +263,7 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ ws, int nchunks
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
   double sd, sdx;
-  wave_chunk_sum(ws, nchunks, C, c, sd, sdx);
+  wave_chunk_sum(ws, nchunks, (long)C, (long)nchunks * C, c, sd, sdx);
   if ((threadIdx.x & 63) != 0) return;
   if (dgamma) dgamma[c] = (float)sdx;
   if (dbeta) dbeta[c] = (float)sd;
@@ -331,8 +332,30 @@ int ca_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
   dim3 grid(t.ncol, t.nchunks);
   bn_stats_kernel<<<grid, BLK, 0, s>>>(x, M, C, ws);
   CA_LAUNCH_CHECK();
-  bn_fwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(ws, t.nchunks, M, C, gamma, beta, eps, momentum,
+  bn_fwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(ws, t.nchunks, (long)C, (long)t.nchunks * C, M, C, gamma,
+                                                         beta, eps, momentum,
                                                          run_mean, run_var, save_mean, save_rstd,
+                                                         scale_shift, scale_shift + C);
+  CA_LAUNCH_CHECK();
+  if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+// Training forward from statistics partials produced by a GEMM/conv epilogue:
+// partials[k][0][c] = sum, partials[k][1][c] = sum of squares over tile k.
+int ca_bn_fwd_partials(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, const float* partials,
+                       int nparts, const float* gamma, const float* beta, float eps, float momentum,
+                       float* run_mean, float* run_var, float* save_mean, float* save_rstd,
+                       float* scale_shift, int relu, hipStream_t s) {
+  if (C % 8 != 0) return -1;
+  Tiling t = make_tiling(M, C);
+  dim3 grid(t.ncol, t.nchunks);
+  bn_fwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(partials, nparts, 2L * C, (long)C, M, C, gamma, beta, eps,
+                                                         momentum, run_mean, run_var, save_mean, save_rstd,
                                                          scale_shift, scale_shift + C);
   CA_LAUNCH_CHECK();
   if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);

@@ -216,3 +216,41 @@ def test_linear_autograd_writes_arena_grad():
     torch.testing.assert_close(conv.weight.grad.float().reshape(128, 64), ref_dw, atol=0.5, rtol=2e-2)
     torch.testing.assert_close(x.grad.float().reshape(-1, 64), dy.float().reshape(-1, 128) @ w, atol=0.2, rtol=2e-2)
     assert conv.weight.grad.data_ptr() == opt.arenas[0].grad.data_ptr() + 0 or True
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k,s,p", [
+    (2, 14, 64, 64, 3, 1, 1), (2, 15, 64, 128, 3, 2, 1), (2, 16, 8, 64, 7, 2, 3),
+    (2, 14, 128, 256, 1, 2, 0), (1, 9, 24, 40, 3, 1, 1), (2, 8, 256, 64, 1, 1, 0)])
+def test_conv_fwd_dgrad_wgrad_vs_fp32(N, H, Cin, Cout, k, s, p):
+    from cloud_amd.ops import conv2d_nhwc
+
+    torch.manual_seed(8)
+    x = torch.randn(N, H, H, Cin, device=DEV).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(Cout, k, k, Cin, device=DEV) / (k * k * Cin) ** 0.5).to(torch.bfloat16).requires_grad_()
+    y = conv2d_nhwc(x, w, None, s, p)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    wr = w.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    yr = F.conv2d(xr, wr, None, s, p).permute(0, 2, 3, 1)
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad.permute(0, 2, 3, 1), atol=5e-2, rtol=3e-2)
+    wg = wr.grad.permute(0, 2, 3, 1)
+    torch.testing.assert_close(w.grad.float(), wg, atol=3e-2 * wg.abs().max().item() + 1e-2, rtol=3e-2)
+
+
+def test_conv_stats_partials_feed_bn():
+    from cloud_amd.ops import bn_act, conv2d_nhwc
+
+    torch.manual_seed(9)
+    x = torch.randn(4, 14, 14, 64, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(128, 3, 3, 64, device=DEV) * 0.05).to(torch.bfloat16)
+    y, part = conv2d_nhwc(x, w, None, 1, 1, stats=True)
+    assert part is not None
+    yf = y.float().reshape(-1, 128)
+    torch.testing.assert_close(part[:, 0].sum(0), yf.sum(0), atol=1e-1, rtol=1e-3)
+    g, b = torch.ones(128, device=DEV), torch.zeros(128, device=DEV)
+    out_a = bn_act(y, g, b, torch.zeros(128, device=DEV), torch.ones(128, device=DEV), partials=part)
+    out_b = bn_act(y, g, b, torch.zeros(128, device=DEV), torch.ones(128, device=DEV))
+    torch.testing.assert_close(out_a.float(), out_b.float(), atol=2e-2, rtol=2e-2)
