@@ -1,0 +1,564 @@
+"""Keras ``Model`` / ``Sequential`` with a data-parallel ``fit`` on MI355X.
+
+Functional (``Model(inputs, outputs)``), sequential and subclassed models are
+supported.  ``fit``/``evaluate``/``predict`` run under the current
+distribution strategy (:mod:`cloud_amd.parallel.strategy`, installed by the
+``run()`` wrapper or by ``strategy.scope()``):
+
+* one process per GPU; the model is broadcast from rank 0 at the first fit;
+* ``batch_size`` is the GLOBAL batch -- each replica trains on its
+  1/num_replicas slice of every global batch (MirroredStrategy semantics);
+* gradients live in the fused optimizer's flat arena and are all-reduced in
+  buckets overlapped with backward (:mod:`cloud_amd.parallel.ddp`); the
+  1/num_replicas mean is folded into the fused update kernel;
+* metric states are all-reduced once per epoch (not per step);
+* a final softmax + ``SparseCategoricalCrossentropy`` is trained through the
+  fused softmax-xent HIP kernel on the pre-softmax logits;
+* checkpoints are written by the chief only and load under any strategy
+  (reference ``core/tests/testdata/save_and_load.py:89-125``).
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+from ..parallel import strategy as strat
+from . import callbacks as cbks
+from . import losses as losses_mod
+from . import metrics as metrics_mod
+from . import optimizers as opt_mod
+from .data import Dataset
+from .engine import KerasTensor, Layer, global_policy
+
+FORMAT = "cloud_amd.keras/1"
+
+
+def _to_torch(x, device, dtype=None):
+    if isinstance(x, dict):
+        return {k: _to_torch(v, device, dtype) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_torch(v, device, dtype) for v in x)
+    t = x if isinstance(x, torch.Tensor) else torch.as_tensor(np.asarray(x))
+    if dtype is not None and t.is_floating_point():
+        t = t.to(dtype)
+    return t.to(device, non_blocking=True)
+
+
+def _first(x):
+    while isinstance(x, (list, tuple)):
+        x = x[0]
+    if isinstance(x, dict):
+        return next(iter(x.values()))
+    return x
+
+
+def _slice(x, idx):
+    if isinstance(x, dict):
+        return {k: _slice(v, idx) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_slice(v, idx) for v in x)
+    return x[idx]
+
+
+def _length(x):
+    return len(_first(x))
+
+
+class Model(Layer):
+    def __init__(self, inputs=None, outputs=None, name=None, **kw):
+        super().__init__(name=name, **kw)
+        self.stop_training = False
+        self.optimizer = None
+        self.loss = None
+        self.compiled_metrics = []
+        self.history = None
+        self._strategy = None
+        self._reducer = None
+        self._fused_xent = False
+        self._graph = None
+        if inputs is not None and outputs is not None:
+            self._init_graph(inputs, outputs)
+
+    # ------------------------------------------------------------ functional API
+    def _init_graph(self, inputs, outputs):
+        ins = list(inputs) if isinstance(inputs, (list, tuple)) else [inputs]
+        outs = list(outputs) if isinstance(outputs, (list, tuple)) else [outputs]
+        order, seen = [], set()
+
+        def visit(kt):
+            if kt.id in seen:
+                return
+            seen.add(kt.id)
+            for p in kt.inputs:
+                visit(p)
+            order.append(kt)
+
+        for o in outs:
+            visit(o)
+        layers, lids = [], set()
+        for kt in order:
+            if kt.layer is not None and not getattr(kt, "is_input", False) and id(kt.layer) not in lids:
+                lids.add(id(kt.layer))
+                layers.append(kt.layer)
+        self._layer_list = torch.nn.ModuleList(layers)
+        self._graph = (ins, outs, order)
+        self._multi_out = isinstance(outputs, (list, tuple))
+        self.built = True
+
+    @property
+    def layers(self):
+        if self._graph is not None:
+            return list(self._layer_list)
+        return [m for m in self.children() if isinstance(m, Layer)]
+
+    def get_layer(self, name=None, index=None):
+        if index is not None:
+            return self.layers[index]
+        for layer in self.layers:
+            if layer.name == name:
+                return layer
+        raise ValueError(f"No such layer: {name}")
+
+    def call(self, inputs, training=None):
+        if self._graph is None:
+            raise NotImplementedError("subclassed models must implement call()")
+        ins, outs, order = self._graph
+        vals = {}
+        xs = inputs if isinstance(inputs, (list, tuple)) else [inputs]
+        for kt, x in zip(ins, xs):
+            vals[kt.id] = x
+        for kt in order:
+            if kt.id in vals:
+                continue
+            args = [vals[p.id] for p in kt.inputs]
+            vals[kt.id] = kt.layer(args if len(args) > 1 else args[0], training=training)
+        res = [vals[o.id] for o in outs]
+        return res if self._multi_out else res[0]
+
+    def __call__(self, inputs, *args, **kwargs):
+        out = super().__call__(inputs, *args, **kwargs)
+        if isinstance(out, torch.Tensor) and global_policy().name != "float32" and out.is_floating_point():
+            out = out.float()
+        return out
+
+    def build(self, input_shape):
+        self.built = True
+
+    def _dry_build(self, sample_x):
+        """Create lazily-built weights with one CPU forward on a single example."""
+        if all(getattr(m, "built", True) for m in self.modules() if isinstance(m, Layer)) and \
+                any(True for _ in self.parameters()):
+            return
+        x = _slice(sample_x, slice(0, 1))
+        x = _to_torch(x, "cpu", torch.float32)
+        was = self.training
+        self.eval()
+        with torch.no_grad():
+            self(x)
+        self.train(was)
+
+    # ------------------------------------------------------------------- compile
+    def compile(self, optimizer="rmsprop", loss=None, metrics=None, loss_weights=None, run_eagerly=None,
+                steps_per_execution=None, **kwargs):
+        self.optimizer = opt_mod.get(optimizer)
+        self.loss = losses_mod.get(loss) if loss is not None else None
+        self.compiled_metrics = [metrics_mod.get(m, self.loss) for m in (metrics or [])]
+        self._compiled = True
+
+    def _final_softmax_layer(self):
+        from .layers import Activation, Dense
+
+        last = None
+        if self._graph is not None:
+            last = self._graph[1][0].layer
+        elif self.layers:
+            last = self.layers[-1]
+        if isinstance(last, (Dense, Activation)) and getattr(last.activation, "__name__", "") == "softmax":
+            return last
+        return None
+
+    # ----------------------------------------------------------------- training
+    def _setup(self, sample_x):
+        s = strat.get_strategy()
+        if self._strategy is s and self.optimizer is not None and self.optimizer.impl is not None:
+            return s
+        self._strategy = s
+        self._dry_build(sample_x)
+        self.to(s.device)
+        if self.optimizer is None:
+            raise RuntimeError("You must compile your model before training/testing.")
+        world = s.num_replicas_in_sync
+        impl = self.optimizer.bind(self, grad_scale=1.0 / world)
+        pend = getattr(self, "_pending_optimizer_state", None)
+        if pend and os.path.exists(pend):
+            impl.load_state_dict(torch.load(pend, map_location="cpu", weights_only=True))
+            self._pending_optimizer_state = None
+        from ..parallel.ddp import GradAllReducer
+
+        self._reducer = GradAllReducer(impl.arenas) if world > 1 else None
+        if self._reducer is not None:
+            self._reducer.broadcast_parameters()
+            self._broadcast_buffers()
+        sm = self._final_softmax_layer()
+        self._fused_xent = (isinstance(self.loss, losses_mod.SparseCategoricalCrossentropy)
+                            and (self.loss.from_logits or sm is not None) and not self._multi_output())
+        return s
+
+    def _multi_output(self):
+        return self._graph is not None and self._multi_out
+
+    def _broadcast_buffers(self):
+        import torch.distributed as dist
+
+        for b in self.buffers():
+            t = b.data if b.device.type == "cuda" or dist.get_backend() == "gloo" else b.data.cpu()
+            dist.broadcast(t, 0)
+            if t is not b.data:
+                b.data.copy_(t)
+
+    def _forward_train(self, x):
+        sm = self._final_softmax_layer() if (self._fused_xent and not self.loss.from_logits) else None
+        if sm is not None:
+            sm._emit_logits = True
+        try:
+            return self(x, training=True)
+        finally:
+            if sm is not None:
+                sm._emit_logits = False
+
+    def train_step(self, xb, yb, sample_weight=None):
+        dev = self._strategy.device
+        x = _to_torch(xb, dev, self._input_dtype())
+        y = _to_torch(yb, dev) if yb is not None else None
+        impl = self.optimizer.impl
+        impl.zero_grad()
+        if self._fused_xent:
+            logits = self._forward_train(x)
+            loss, _ = self.loss.fused_logits_loss(logits, y)
+            pred = logits
+        else:
+            pred = self(x, training=True)
+            loss = self.loss(y, pred, sample_weight)
+        reg = self._regularization()
+        total = loss + reg if reg is not None else loss
+        total.backward()
+        if self._reducer is not None:
+            self._reducer.finish()
+        impl.step()
+        n = _length(x)
+        self._loss_tracker.update_state(loss.detach().float().reshape(1), sample_weight=[n])
+        with torch.no_grad():
+            for m in self.compiled_metrics:
+                m.update_state(y, pred.detach())
+        return loss
+
+    def _regularization(self):
+        regs = [m.regularization_loss() for m in self.modules() if hasattr(m, "regularization_loss")]
+        return sum(regs) if regs else None
+
+    def _input_dtype(self):
+        return global_policy().compute_dtype
+
+    def _logs(self, prefix="", reduce=True):
+        trackers = [self._loss_tracker] + list(self.compiled_metrics)
+        if reduce and self._strategy is not None and self._strategy.num_replicas_in_sync > 1:
+            state = torch.tensor([v for m in trackers for v in m.state()], dtype=torch.float64)
+            state = self._strategy.reduce(strat.ReduceOp.SUM, state)
+            for i, m in enumerate(trackers):
+                m.set_state(state[2 * i:2 * i + 2].tolist())
+        logs = {prefix + "loss": float(self._loss_tracker.result())}
+        for m in self.compiled_metrics:
+            logs[prefix + m.name] = float(m.result())
+        return logs
+
+    def _reset_metrics(self):
+        self._loss_tracker = metrics_mod.Mean(name="loss")
+        for m in self.compiled_metrics:
+            m.reset_state()
+
+    def _batches(self, x, y, batch_size, shuffle, epoch, seed=1234):
+        """Yield this replica's slice of every global batch."""
+        s = self._strategy
+        world, rank = s.num_replicas_in_sync, s.rank
+        if isinstance(x, Dataset):
+            ds = x.shard(world, rank) if world > 1 else x
+            for el in ds:
+                if isinstance(el, (tuple, list)) and len(el) >= 2:
+                    yield el[0], el[1]
+                else:
+                    yield el, None
+            return
+        n = _length(x)
+        bs = batch_size or 32
+        idx = np.random.default_rng(seed + epoch).permutation(n) if shuffle else np.arange(n)
+        per = -(-bs // world)
+        for start in range(0, n, bs):
+            gb = idx[start:start + bs]
+            mine = np.sort(gb[rank * per:(rank + 1) * per]) if world > 1 else gb
+            if len(mine) == 0:
+                continue
+            yield _slice(x, mine), (_slice(y, mine) if y is not None else None)
+
+    def fit(self, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callbacks=None, validation_split=0.0,
+            validation_data=None, shuffle=True, class_weight=None, sample_weight=None, initial_epoch=0,
+            steps_per_epoch=None, validation_steps=None, validation_batch_size=None, validation_freq=1, **kw):
+        if validation_split and not isinstance(x, Dataset):
+            n = _length(x)
+            cut = int(n * (1 - validation_split))
+            validation_data = (_slice(x, slice(cut, None)), _slice(y, slice(cut, None)))
+            x, y = _slice(x, slice(0, cut)), _slice(y, slice(0, cut))
+        sample = x if not isinstance(x, Dataset) else next(iter(x))[0]
+        s = self._setup(sample)
+        verbose = 1 if verbose == "auto" else verbose
+        history = cbks.History()
+        cb_list = list(callbacks or []) + ([cbks.ProgbarLogger()] if verbose else []) + [history]
+        steps = steps_per_epoch
+        if steps is None and not isinstance(x, Dataset):
+            steps = -(-_length(x) // (batch_size or 32))
+        callbacks_ = cbks.CallbackList(cb_list, model=self, params={"epochs": epochs, "steps": steps,
+                                                                        "verbose": verbose})
+        self.stop_training = False
+        self.train()
+        callbacks_.on_train_begin({})
+        persistent = None
+        if steps_per_epoch is not None:
+            persistent = iter(self._batches(x, y, batch_size, shuffle, 0))
+        from ..utils import faults
+
+        global_step = 0
+        for epoch in range(initial_epoch, epochs):
+            self._reset_metrics()
+            callbacks_.on_epoch_begin(epoch, {})
+            it = persistent if persistent is not None else self._batches(x, y, batch_size, shuffle, epoch)
+            step = 0
+            t0 = time.time()
+            while True:
+                if steps_per_epoch is not None and step >= steps_per_epoch:
+                    break
+                try:
+                    xb, yb = next(it)
+                except StopIteration:
+                    break
+                callbacks_.on_train_batch_begin(step, {})
+                faults.maybe_inject(global_step, rank=s.rank)
+                loss = self.train_step(xb, yb)
+                callbacks_.on_train_batch_end(step, {"loss": float(loss.detach())} if step % 50 == 0 else {})
+                step += 1
+                global_step += 1
+                if self.stop_training:
+                    break
+            logs = self._logs()
+            logs["epoch_time_s"] = time.time() - t0
+            if validation_data is not None and (epoch + 1) % validation_freq == 0:
+                vx, vy = (validation_data, None) if isinstance(validation_data, Dataset) else validation_data[:2]
+                vlogs = self.evaluate(vx, vy, batch_size=validation_batch_size or batch_size, verbose=0,
+                                      steps=validation_steps, return_dict=True, _internal=True)
+                logs.update({"val_" + k: v for k, v in vlogs.items()})
+                self.train()
+            callbacks_.on_epoch_end(epoch, logs)
+            if self.stop_training:
+                break
+        callbacks_.on_train_end({})
+        self.history = history
+        return history
+
+    def evaluate(self, x=None, y=None, batch_size=None, verbose="auto", sample_weight=None, steps=None,
+                 callbacks=None, return_dict=False, _internal=False, **kw):
+        sample = x if not isinstance(x, Dataset) else next(iter(x))[0]
+        if not _internal:
+            self._setup(sample)
+        dev = self._strategy.device
+        saved = (self._loss_tracker, [m.state() for m in self.compiled_metrics]) if hasattr(self, "_loss_tracker") \
+            else None
+        self._reset_metrics()
+        self.eval()
+        with torch.no_grad():
+            for i, (xb, yb) in enumerate(self._batches(x, y, batch_size, False, 0)):
+                if steps is not None and i >= steps:
+                    break
+                xt = _to_torch(xb, dev, self._input_dtype())
+                yt = _to_torch(yb, dev) if yb is not None else None
+                pred = self(xt, training=False)
+                if self.loss is not None and yt is not None:
+                    loss = self.loss(yt, pred)
+                    self._loss_tracker.update_state(loss.detach().float().reshape(1), sample_weight=[_length(xt)])
+                for m in self.compiled_metrics:
+                    m.update_state(yt, pred)
+        logs = self._logs()
+        if saved is not None and _internal:
+            self._loss_tracker = saved[0]
+            for m, st in zip(self.compiled_metrics, saved[1]):
+                m.set_state(st)
+        if return_dict:
+            return logs
+        vals = list(logs.values())
+        return vals[0] if len(vals) == 1 else vals
+
+    def predict(self, x, batch_size=None, verbose="auto", steps=None, callbacks=None, **kw):
+        s = strat.get_strategy()
+        sample = x if not isinstance(x, Dataset) else next(iter(x))[0]
+        if not any(True for _ in self.parameters()):
+            self._dry_build(sample)
+        dev = s.device
+        self.to(dev)
+        self.eval()
+        outs = []
+        bs = batch_size or 32
+        with torch.no_grad():
+            if isinstance(x, Dataset):
+                batches = (el[0] if isinstance(el, (tuple, list)) else el for el in x)
+            else:
+                n = _length(x)
+                batches = (_slice(x, slice(i, i + bs)) for i in range(0, n, bs))
+            for i, xb in enumerate(batches):
+                if steps is not None and i >= steps:
+                    break
+                outs.append(self(_to_torch(xb, dev, self._input_dtype()), training=False).float().cpu().numpy())
+        return np.concatenate(outs) if outs else np.zeros((0,))
+
+    def predict_on_batch(self, x):
+        return self.predict(x, batch_size=_length(x))
+
+    def train_on_batch(self, x, y):
+        self._setup(x)
+        self._reset_metrics()
+        self.train()
+        self.train_step(x, y)
+        return list(self._logs(reduce=False).values())
+
+    # --------------------------------------------------------------- weights I/O
+    def get_weights(self):
+        return [t.detach().float().cpu().numpy() for t in list(self.parameters()) + list(self.buffers())]
+
+    def set_weights(self, weights):
+        tensors = list(self.parameters()) + list(self.buffers())
+        with torch.no_grad():
+            for t, w in zip(tensors, weights):
+                t.copy_(torch.as_tensor(np.asarray(w)).to(t.dtype).reshape(t.shape))
+        self._sync_master()
+
+    def _sync_master(self):
+        impl = self.optimizer.impl if self.optimizer is not None else None
+        if impl is None:
+            return
+        with torch.no_grad():
+            for a in impl.arenas:
+                for sl in a.slots:
+                    a.master[sl.offset:sl.offset + sl.numel].copy_(sl.param.detach().reshape(-1).float())
+
+    def save_weights(self, filepath, overwrite=True, save_format=None):
+        d = os.path.dirname(os.path.abspath(filepath))
+        os.makedirs(d, exist_ok=True)
+        sd = {k: v.detach().cpu() for k, v in self.state_dict().items()}
+        torch.save(sd, filepath)
+
+    def load_weights(self, filepath, by_name=False, skip_mismatch=False):
+        sd = torch.load(filepath, map_location="cpu", weights_only=True)
+        self._load_state(sd)
+
+    def _load_state(self, sd):
+        own = self.state_dict()
+        if any(k not in own for k in sd) and any(True for _ in self.parameters()) is False:
+            raise ValueError("model must be built before loading weights")
+        if not own:
+            raise ValueError("model has no weights yet: build it (call it once or fit) before load_weights")
+        with torch.no_grad():
+            for k, v in sd.items():
+                if k in own:
+                    own[k].copy_(v.to(own[k].dtype))
+        self._sync_master()
+
+    def save(self, filepath, overwrite=True, include_optimizer=True, save_format=None):
+        from . import saving
+
+        saving.save_model(self, filepath, include_optimizer=include_optimizer)
+
+    # ---------------------------------------------------------------- summary
+    def count_params(self):
+        return int(sum(p.numel() for p in self.parameters()))
+
+    def summary(self, print_fn=print):
+        print_fn(f'Model: "{self.name}"')
+        print_fn("_" * 65)
+        print_fn(f"{'Layer (type)':<34}{'Param #':>12}")
+        print_fn("=" * 65)
+        for layer in self.layers:
+            print_fn(f"{layer.name + ' (' + type(layer).__name__ + ')':<34}{layer.count_params():>12,}")
+        print_fn("=" * 65)
+        tot = self.count_params()
+        tr = sum(p.numel() for p in self.parameters() if p.requires_grad)
+        print_fn(f"Total params: {tot:,}")
+        print_fn(f"Trainable params: {tr:,}")
+        print_fn(f"Non-trainable params: {tot - tr:,}")
+
+    def get_config(self):
+        if isinstance(self, Sequential):
+            return {"name": self.name, "layers": [{"class_name": type(layer).__name__,
+                                                   "config": layer.get_config()} for layer in self.layers]}
+        raise NotImplementedError("config serialisation is implemented for Sequential models")
+
+    def to_json(self):
+        return json.dumps({"class_name": type(self).__name__, "config": self.get_config(), "format": FORMAT})
+
+
+class Sequential(Model):
+    def __init__(self, layers=None, name=None, **kw):
+        super().__init__(name=name, **kw)
+        self._seq = torch.nn.ModuleList()
+        for layer in layers or []:
+            self.add(layer)
+
+    @property
+    def layers(self):
+        return list(self._seq)
+
+    def add(self, layer):
+        if isinstance(layer, KerasTensor):
+            return
+        self._seq.append(layer)
+        first = self._seq[0]
+        shape = getattr(first, "_input_shape_arg", None)
+        if shape is not None:
+            self._build_from_shape(shape)
+
+    def pop(self):
+        self._seq = torch.nn.ModuleList(list(self._seq)[:-1])
+
+    def _build_from_shape(self, shape):
+        x = torch.zeros((1,) + tuple(shape))
+        was = self.training
+        self.eval()
+        with torch.no_grad():
+            for layer in self._seq:
+                x = layer(x)
+        self.train(was)
+
+    def call(self, x, training=None):
+        for layer in self._seq:
+            x = layer(x, training=training)
+        return x
+
+    @classmethod
+    def from_config(cls, config):
+        from .layers import LAYERS
+
+        m = cls(name=config.get("name"))
+        for lc in config["layers"]:
+            m.add(LAYERS[lc["class_name"]].from_config(lc["config"]))
+        return m
+
+
+def clone_model(model):
+    import copy
+
+    return copy.deepcopy(model)
+
+
+def load_model(filepath, custom_objects=None, compile=True):
+    from . import saving
+
+    return saving.load_model(filepath, compile=compile)

@@ -1,0 +1,132 @@
+"""Keras optimizer front-ends (``tf.keras.optimizers``) bound lazily to a model.
+
+``compile(optimizer=Adam(1e-3))`` only records hyper-parameters; at the first
+``fit`` the model's parameters are moved into flat arenas and one of the
+fused HIP optimizers of :mod:`cloud_amd.optim` is created with
+``grad_scale = 1 / num_replicas`` (the data-parallel mean folded into the
+update kernel).  Learning-rate schedules are callables ``schedule(step)``.
+"""
+from __future__ import annotations
+
+from .. import optim as fused
+
+
+class schedules:  # namespace parity: tf.keras.optimizers.schedules
+    class LearningRateSchedule:
+        def __call__(self, step):  # pragma: no cover - abstract
+            raise NotImplementedError
+
+    class ExponentialDecay(LearningRateSchedule):
+        def __init__(self, initial_learning_rate, decay_steps, decay_rate, staircase=False):
+            self.lr0, self.steps, self.rate, self.staircase = initial_learning_rate, decay_steps, decay_rate, staircase
+
+        def __call__(self, step):
+            p = step / self.steps
+            if self.staircase:
+                p = int(p)
+            return self.lr0 * self.rate ** p
+
+    class PiecewiseConstantDecay(LearningRateSchedule):
+        def __init__(self, boundaries, values):
+            self.b, self.v = list(boundaries), list(values)
+
+        def __call__(self, step):
+            for b, v in zip(self.b, self.v):
+                if step <= b:
+                    return v
+            return self.v[-1]
+
+    class CosineDecay(LearningRateSchedule):
+        def __init__(self, initial_learning_rate, decay_steps, alpha=0.0, warmup_steps=0):
+            self.lr0, self.steps, self.alpha, self.warm = initial_learning_rate, decay_steps, alpha, warmup_steps
+
+        def __call__(self, step):
+            import math
+
+            if self.warm and step < self.warm:
+                return self.lr0 * (step + 1) / self.warm
+            t = min(step - self.warm, self.steps) / max(self.steps, 1)
+            return self.lr0 * ((1 - self.alpha) * 0.5 * (1 + math.cos(math.pi * t)) + self.alpha)
+
+
+class Optimizer:
+    fused_cls = None
+
+    def __init__(self, learning_rate=0.001, name=None, clipnorm=None, **kw):
+        self.learning_rate = learning_rate
+        self.clipnorm = clipnorm
+        self.kw = kw
+        self.name = name or type(self).__name__
+        self._impl = None
+
+    def bind(self, model, grad_scale=1.0):
+        self._impl = self.fused_cls(model, learning_rate=self.learning_rate, grad_scale=grad_scale,
+                                    clipnorm=self.clipnorm, **self.kw)
+        return self._impl
+
+    @property
+    def impl(self):
+        return self._impl
+
+    @property
+    def lr(self):
+        if self._impl is not None:
+            return self._impl.lr
+        lr = self.learning_rate
+        return lr(0) if callable(lr) else lr
+
+    @lr.setter
+    def lr(self, v):
+        self.learning_rate = v
+        if self._impl is not None:
+            self._impl.lr = v
+
+    @property
+    def iterations(self):
+        return self._impl.iterations if self._impl is not None else 0
+
+    def get_config(self):
+        lr = self.learning_rate
+        return {"name": self.name, "learning_rate": lr if not callable(lr) else None, **self.kw}
+
+
+class SGD(Optimizer):
+    fused_cls = fused.SGD
+
+    def __init__(self, learning_rate=0.01, momentum=0.0, nesterov=False, name=None, **kw):
+        super().__init__(learning_rate, name, momentum=momentum, nesterov=nesterov, **kw)
+
+
+class Adam(Optimizer):
+    fused_cls = fused.Adam
+
+    def __init__(self, learning_rate=0.001, beta_1=0.9, beta_2=0.999, epsilon=1e-7, amsgrad=False, name=None, **kw):
+        super().__init__(learning_rate, name, beta_1=beta_1, beta_2=beta_2, epsilon=epsilon, **kw)
+
+
+class AdamW(Optimizer):
+    fused_cls = fused.AdamW
+
+    def __init__(self, learning_rate=0.001, weight_decay=0.004, beta_1=0.9, beta_2=0.999, epsilon=1e-7, name=None,
+                 **kw):
+        super().__init__(learning_rate, name, weight_decay=weight_decay, beta_1=beta_1, beta_2=beta_2,
+                         epsilon=epsilon, **kw)
+
+
+class RMSprop(Optimizer):
+    fused_cls = fused.RMSprop
+
+    def __init__(self, learning_rate=0.001, rho=0.9, momentum=0.0, epsilon=1e-7, name=None, **kw):
+        super().__init__(learning_rate, name, rho=rho, momentum=momentum, epsilon=epsilon, **kw)
+
+
+_ALIASES = {"sgd": SGD, "adam": Adam, "adamw": AdamW, "rmsprop": RMSprop}
+
+
+def get(identifier):
+    if isinstance(identifier, Optimizer):
+        return identifier
+    try:
+        return _ALIASES[str(identifier).lower()]()
+    except KeyError as e:
+        raise ValueError(f"Unknown optimizer {identifier!r}") from e

@@ -1,0 +1,90 @@
+"""Multi-process data parallelism on CPU (gloo): the DP engine must make every
+rank's update equal the single-process large-batch update, and a Keras job
+launched through run() must stay replica-consistent."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from cloud_amd.optim import SGD
+    from cloud_amd.parallel.ddp import GradAllReducer
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+    if rank == 1:  # different init on purpose: broadcast must fix it
+        for p in model.parameters():
+            p.data.add_(1.0)
+    opt = SGD(model, learning_rate=0.1, momentum=0.9, grad_scale=1.0 / world)
+    red = GradAllReducer(opt.arenas, bucket_mb=0.0005)
+    assert len(red.buckets) > 1
+    red.broadcast_parameters()
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(8 * world, 16, generator=g)
+    Y = torch.randn(8 * world, 4, generator=g)
+    for _ in range(3):
+        opt.zero_grad()
+        xb, yb = X[rank * 8:(rank + 1) * 8], Y[rank * 8:(rank + 1) * 8]
+        loss = torch.nn.functional.mse_loss(model(xb), yb)
+        loss.backward()
+        red.finish()
+        opt.step()
+    torch.save({k: v.detach().clone() for k, v in model.state_dict().items()}, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_ddp_matches_single_process(tmp_path):
+    world = 2
+    port = 29000 + os.getpid() % 1000
+    mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
+    for k in r0:
+        torch.testing.assert_close(r0[k], r1[k])
+    # single-process reference on the full batch
+    sys.path.insert(0, ROOT)
+    from cloud_amd.optim import SGD
+
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+    opt = SGD(model, learning_rate=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(16, 16, generator=g)
+    Y = torch.randn(16, 4, generator=g)
+    for _ in range(3):
+        opt.zero_grad()
+        loss = 0.5 * (torch.nn.functional.mse_loss(model(X[:8]), Y[:8]) + torch.nn.functional.mse_loss(model(X[8:]), Y[8:]))
+        loss.backward()
+        opt.step()
+    for k, v in model.state_dict().items():
+        torch.testing.assert_close(r0[k], v, atol=1e-5, rtol=1e-5)
+
+
+def test_keras_job_via_run_two_workers(tmp_path):
+    env = dict(os.environ, CLOUD_AMD_EXAMPLE_CPU="1", CLOUD_AMD_NUM_GPUS="0", CLOUD_AMD_JOBS_DIR=str(tmp_path),
+               WORKERS="1", EPOCHS="2", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "mnist_mlp.py")], env=env,
+                       capture_output=True, text=True, timeout=600, cwd=os.path.join(ROOT, "examples"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Job submitted successfully." in r.stdout
+    res = [json.loads(ln[7:]) for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]
+    assert res and res[0]["replicas"] == 2 and res[0]["strategy"] == "MultiWorkerMirroredStrategy"
+    assert res[0]["loss"][-1] < res[0]["loss"][0] and res[0]["test_acc"] > 0.8
+    logs = os.listdir(os.path.join(tmp_path, os.listdir(tmp_path)[0], "logs"))
+    assert sorted(logs) == ["chief-0.log", "worker-0.log"]
+    other = [json.loads(ln[7:]) for ln in open(os.path.join(tmp_path, os.listdir(tmp_path)[0], "logs", "worker-0.log"))
+             if ln.startswith("RESULT ")]
+    assert abs(other[0]["weights_checksum"] - res[0]["weights_checksum"]) < 1e-6

@@ -1,0 +1,135 @@
+"""Keras-compatible API on CPU: the reference workloads' model/compile/fit/save
+patterns (README MLP, MNIST CNN, save_and_load.py, callbacks, functional API)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from cloud_amd import keras
+from cloud_amd.keras import layers
+from cloud_amd.parallel import strategy as S
+
+
+@pytest.fixture(autouse=True)
+def _one_device():
+    S.experimental_set_strategy(S.OneDeviceStrategy("/cpu:0"))
+    yield
+    S.experimental_set_strategy(None)
+
+
+def _mnist(n=2048):
+    (x, y), (xt, yt) = keras.datasets.mnist.load_data(n_train=n, n_test=512)
+    return (x.reshape(-1, 784).astype("float32") / 255, y), (xt.reshape(-1, 784).astype("float32") / 255, yt)
+
+
+def test_readme_mlp_fit_evaluate():
+    """README.md:71-81 MLP: Dense(512 relu) - Dropout(0.2) - Dense(10 softmax), SCCE, Adam."""
+    (x, y), (xt, yt) = _mnist()
+    model = keras.Sequential([layers.Dense(512, activation="relu", input_shape=(784,)), layers.Dropout(0.2),
+                              layers.Dense(10, activation="softmax")])
+    model.compile(loss="sparse_categorical_crossentropy", optimizer=keras.optimizers.Adam(1e-3),
+                  metrics=["accuracy"])
+    assert model.count_params() == 784 * 512 + 512 + 5130
+    h = model.fit(x, y, epochs=3, batch_size=128, verbose=0)
+    assert h.history["loss"][-1] < h.history["loss"][0]
+    loss, acc = model.evaluate(xt, yt, verbose=0)
+    assert acc > 0.8, acc
+    p = model.predict(xt[:10])
+    assert p.shape == (10, 10) and np.allclose(p.sum(-1), 1, atol=1e-4)
+
+
+def test_cnn_with_dataset_and_callbacks(tmp_path):
+    (x, y), _ = keras.datasets.mnist.load_data(n_train=512, n_test=64)
+    x = x[..., None].astype("float32") / 255
+    ds = keras.Dataset.from_tensor_slices((x, y.astype("int64"))).shuffle(512, seed=1).batch(64).prefetch(2)
+    model = keras.Sequential([
+        layers.Conv2D(32, 3, activation="relu", input_shape=(28, 28, 1)), layers.MaxPooling2D(),
+        layers.Flatten(), layers.Dense(64, activation="relu"), layers.Dense(10)])
+    model.compile(loss=keras.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer="adam",
+                  metrics=["accuracy"])
+    seen = []
+    sched = keras.callbacks.LearningRateScheduler(lambda e: 1e-3 if e < 1 else 5e-4)
+    ckpt = keras.callbacks.ModelCheckpoint(str(tmp_path / "ckpt_{epoch}.pt"), save_weights_only=True)
+    tb = keras.callbacks.TensorBoard(str(tmp_path / "tb"))
+    lam = keras.callbacks.LambdaCallback(on_epoch_end=lambda e, logs: seen.append(logs["loss"]))
+    h = model.fit(ds, epochs=2, callbacks=[sched, ckpt, tb, lam], verbose=0)
+    assert len(seen) == 2 and h.history["lr"] == [1e-3, 5e-4]
+    assert os.path.exists(tmp_path / "ckpt_2.pt")
+    rows = [json.loads(ln) for ln in open(tmp_path / "tb" / "train" / "scalars.jsonl")]
+    assert rows[-1]["epoch"] == 1 and "accuracy" in rows[-1]
+
+
+def test_early_stopping_and_validation():
+    (x, y), (xt, yt) = _mnist(1024)
+    model = keras.Sequential([layers.Dense(16, activation="relu", input_shape=(784,)), layers.Dense(10)])
+    model.compile(loss=keras.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer="sgd")
+    es = keras.callbacks.EarlyStopping(monitor="val_loss", patience=0, min_delta=10.0)
+    h = model.fit(x, y, epochs=5, validation_data=(xt, yt), callbacks=[es], verbose=0)
+    assert len(h.history["loss"]) == 2 and "val_loss" in h.history
+
+
+def test_save_and_load_roundtrip(tmp_path):
+    """save_and_load.py: weights/model saved, reloaded, evaluated and trained further."""
+    (x, y), (xt, yt) = _mnist(1024)
+    model = keras.Sequential([layers.Dense(64, activation="relu", input_shape=(784,)),
+                              layers.BatchNormalization(), layers.Dense(10, activation="softmax")])
+    model.compile(loss="sparse_categorical_crossentropy", optimizer="adam", metrics=["accuracy"])
+    model.fit(x, y, epochs=1, batch_size=64, verbose=0)
+    ref = model.evaluate(xt, yt, verbose=0)
+    model.save(str(tmp_path / "saved"))
+    m2 = keras.models.load_model(str(tmp_path / "saved"))
+    np.testing.assert_allclose(m2.evaluate(xt, yt, verbose=0), ref, rtol=1e-5, atol=1e-5)
+    m2.fit(x, y, epochs=1, batch_size=64, verbose=0)
+    model.save_weights(str(tmp_path / "w" / "cp.ckpt"))
+    m3 = keras.Sequential([layers.Dense(64, activation="relu", input_shape=(784,)),
+                           layers.BatchNormalization(), layers.Dense(10, activation="softmax")])
+    m3.load_weights(str(tmp_path / "w" / "cp.ckpt"))
+    m3.compile(loss="sparse_categorical_crossentropy", optimizer="adam", metrics=["accuracy"])
+    np.testing.assert_allclose(m3.evaluate(xt, yt, verbose=0), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_functional_api_and_summary(capsys):
+    inp = keras.Input(shape=(20,))
+    a = layers.Dense(8, activation="relu")(inp)
+    b = layers.Dense(8, activation="tanh")(inp)
+    out = layers.Dense(3)(layers.Concatenate()([a, b]))
+    model = keras.Model(inp, out)
+    assert out.shape == (None, 3)
+    model.compile(optimizer="rmsprop", loss="mse", metrics=["mae"])
+    x = np.random.randn(64, 20).astype("float32")
+    y = np.random.randn(64, 3).astype("float32")
+    h = model.fit(x, y, epochs=2, batch_size=16, verbose=0)
+    assert "mae" in h.history
+    model.summary()
+    assert "Total params" in capsys.readouterr().out
+
+
+def test_custom_training_loop_semantics():
+    """mnist_example_using_ctl.py: reduction NONE + compute_average_loss + strategy.reduce."""
+    loss_obj = keras.losses.SparseCategoricalCrossentropy(from_logits=True, reduction=keras.losses.Reduction.NONE)
+    logits = torch.randn(8, 10)
+    y = torch.randint(0, 10, (8,))
+    per = loss_obj(y, logits)
+    assert per.shape == (8,)
+    avg = keras.losses.compute_average_loss(per, global_batch_size=16)
+    torch.testing.assert_close(avg, per.sum() / 16)
+    s = S.get_strategy()
+    assert float(s.reduce(S.ReduceOp.SUM, torch.tensor(3.0))) == 3.0
+    acc = keras.metrics.SparseCategoricalAccuracy()
+    acc.update_state(y, torch.nn.functional.one_hot(y, 10).float())
+    assert acc.result() == 1.0
+
+
+def test_mixed_bfloat16_policy_cpu():
+    keras.mixed_precision.set_global_policy("mixed_bfloat16")
+    try:
+        model = keras.Sequential([layers.Dense(16, activation="relu", input_shape=(8,)), layers.Dense(2)])
+        assert model.layers[0].kernel.dtype == torch.bfloat16
+        model.compile(optimizer="sgd", loss="mse")
+        model.fit(np.random.randn(32, 8).astype("float32"), np.random.randn(32, 2).astype("float32"),
+                  epochs=1, verbose=0)
+        assert model.predict(np.zeros((2, 8), "float32")).dtype == np.float32
+    finally:
+        keras.mixed_precision.set_global_policy("float32")
