@@ -1,0 +1,44 @@
+"""HBM budgeting helpers (288 GB HBM3E per MI355X).
+
+Used by the trial scheduler to pack several small trials onto one GPU and by
+``describe()`` for job metadata.  Estimates are deliberately simple: bf16
+weights + fp32 master + optimizer moments + grads per parameter, plus an
+activation term measured from the first real step when available.
+"""
+from __future__ import annotations
+
+import os
+
+HBM_GB = float(os.environ.get("CLOUD_AMD_HBM_GB", 288))
+_last = {"params": 0}
+
+
+def param_bytes(n_params, optimizer="adam", compute_bytes=2):
+    state = {"sgd": 4, "adam": 8, "adamw": 8, "rmsprop": 8}.get(optimizer, 8)
+    return n_params * (compute_bytes + 4 + state + compute_bytes)
+
+
+def note_model(model):
+    try:
+        _last["params"] = sum(p.numel() for p in model.parameters())
+    except Exception:  # pragma: no cover
+        pass
+    return _last["params"]
+
+
+def trials_per_gpu(trial_gb, hbm_gb=None, reserve=0.1, cap=8):
+    hbm_gb = HBM_GB if hbm_gb is None else hbm_gb
+    if trial_gb <= 0:
+        return cap
+    return max(1, min(cap, int(hbm_gb * (1 - reserve) // trial_gb)))
+
+
+def peak_allocated_gb(device=None):
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            return torch.cuda.max_memory_allocated(device) / 2 ** 30
+    except Exception:  # pragma: no cover
+        pass
+    return 0.0

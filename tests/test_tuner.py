@@ -1,0 +1,256 @@
+"""Tuner: study_config converters (reference tuner/tests/unit/utils_test.py
+golden values), oracle lifecycle (tuner_test.py), local study service
+semantics (optimizer_client_test.py) and a real multi-process search."""
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+from cloud_amd.parallel import strategy as S
+from cloud_amd.tuner import CloudOracle, CloudTuner, HyperParameters, RandomSearch, GridSearch, Objective
+from cloud_amd.tuner import optimizer_client, utils
+from cloud_amd.tuner.scheduler import TrialScheduler
+from cloud_amd.tuner.study_service import StudyExists, StudyService, TooManyTrials
+from cloud_amd.tuner.trial import TrialStatus
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(autouse=True)
+def _cpu():
+    S.experimental_set_strategy(S.OneDeviceStrategy("/cpu:0"))
+    yield
+    S.experimental_set_strategy(None)
+
+
+def _cfg(params, metric="accuracy"):
+    return {"algorithm": "ALGORITHM_UNSPECIFIED", "metrics": [{"goal": "MAXIMIZE", "metric": metric}],
+            "parameters": params}
+
+
+def test_hps_to_study_config_golden():
+    hps = HyperParameters()
+    hps.Int("units", 32, 128, step=32)
+    assert utils._convert_hyperparams_to_optimizer_params(hps) == [
+        {"parameter": "units", "type": "DISCRETE", "discrete_value_spec": {"values": [32, 64, 96]}}]
+    hps = HyperParameters()
+    hps.Float("learning_rate", 1e-4, 1e-1, sampling="log")
+    assert utils._convert_hyperparams_to_optimizer_params(hps) == [
+        {"parameter": "learning_rate", "type": "DOUBLE", "double_value_spec": {"min_value": 1e-4, "max_value": 0.1},
+         "scale_type": "UNIT_LOG_SCALE"}]
+    hps = HyperParameters()
+    hps.Choice("model_type", ["LINEAR", "WIDE_AND_DEEP"])
+    hps.Boolean("has_beta")
+    hps.Fixed("beta", 1)
+    hps.Fixed("name", "x")
+    out = utils._convert_hyperparams_to_optimizer_params(hps)
+    assert out[0]["categorical_value_spec"] == {"values": ["LINEAR", "WIDE_AND_DEEP"]}
+    assert out[1]["categorical_value_spec"] == {"values": ["True", "False"]}
+    assert out[2] == {"parameter": "beta", "type": "DISCRETE", "discrete_value_spec": {"values": [1.0]}}
+    assert out[3]["categorical_value_spec"] == {"values": ["x"]}
+    hps = HyperParameters()
+    hps.Float("f", 0.0, 0.3, step=0.1)
+    assert np.allclose(utils._convert_hyperparams_to_optimizer_params(hps)[0]["discrete_value_spec"]["values"],
+                       [0.0, 0.1, 0.2])
+
+
+def test_study_config_to_hps_and_objective():
+    cfg = _cfg([{"parameter": "units", "type": "INTEGER", "integer_value_spec": {"min_value": 1, "max_value": 4}},
+                {"parameter": "lr", "type": "DOUBLE", "double_value_spec": {"min_value": 1e-4, "max_value": 0.1},
+                 "scale_type": "UNIT_LOG_SCALE"}])
+    hps = utils.convert_study_config_to_hps(cfg)
+    assert [type(h).__name__ for h in hps.space] == ["Int", "Float"] and hps.space[1].sampling == "log"
+    assert utils.convert_study_config_to_objective(cfg) == [Objective("accuracy", "max")]
+    with pytest.raises(ValueError, match="metrics"):
+        utils.convert_study_config_to_objective({"parameters": []})
+    with pytest.raises(ValueError, match="min_value"):
+        utils.convert_study_config_to_hps(_cfg([{"parameter": "x", "type": "DOUBLE",
+                                                 "double_value_spec": {"min_value": 1, "max_value": 2}}]))
+    assert utils.format_goal("max") == "MAXIMIZE" and utils.format_goal("MINIMIZE") == "min"
+    assert utils.format_objective("val_loss") == [Objective("val_loss", "min")]
+    t = {"name": "projects/p/locations/r/studies/s/trials/7", "parameters": [
+        {"parameter": "units", "intValue": "3"}, {"parameter": "lr", "floatValue": 0.01}]}
+    assert utils.get_trial_id(t) == "7"
+    assert utils.convert_optimizer_trial_to_hps(hps, t).values == {"units": 3, "lr": 0.01}
+
+
+def _hps():
+    hps = HyperParameters()
+    hps.Int("units", 8, 32, step=8)
+    hps.Choice("act", ["relu", "tanh"])
+    return hps
+
+
+def test_oracle_init_rules(tmp_path):
+    with pytest.raises(ValueError, match="either study_config"):
+        CloudOracle(objective="acc", hyperparameters=_hps(), study_config=_cfg([]), study_dir=str(tmp_path))
+    with pytest.raises(ValueError, match="must be set"):
+        CloudOracle(objective="acc", study_dir=str(tmp_path))
+    o = CloudOracle("proj", "reg", objective="acc", hyperparameters=_hps(), max_trials=3, study_id="abc",
+                    study_dir=str(tmp_path))
+    assert o.study_id == "CloudTuner_study_abc"
+    assert o.study_config["parameters"][0]["discrete_value_spec"]["values"] == [8, 16, 24]
+
+
+def test_oracle_lifecycle(tmp_path):
+    o = CloudOracle("proj", "reg", objective="acc", hyperparameters=_hps(), max_trials=3, study_id="life",
+                    study_dir=str(tmp_path))
+    t1 = o.create_trial("tuner0")
+    assert t1.status == TrialStatus.RUNNING and t1.trial_id == "1"
+    assert o.create_trial("tuner0").trial_id == "1"  # idempotent per client while ACTIVE
+    o.update_trial("1", {"acc": 0.5}, step=1)
+    o.end_trial("1")
+    assert o.trials["1"].score == 0.5
+    with pytest.raises(ValueError, match="not found"):
+        o.end_trial("1")
+    t2 = o.create_trial("tuner0")
+    with pytest.raises(ValueError, match="Unexpected status"):
+        o.end_trial(t2.trial_id, "RUNNING")
+    t2 = o.create_trial("tuner0")  # still ACTIVE in the study: same trial comes back
+    assert t2.trial_id == "2"
+    o.update_trial(t2.trial_id, {"acc": 0.9}, step=1)
+    o.end_trial(t2.trial_id, TrialStatus.COMPLETED)
+    t3 = o.create_trial("tuner1")
+    o.end_trial(t3.trial_id, TrialStatus.INVALID)
+    assert o.create_trial("tuner0").status == TrialStatus.STOPPED  # max_trials reached
+    best = o.get_best_trials(2)
+    assert [b.score for b in best] == [0.9, 0.5]
+
+
+def test_service_semantics(tmp_path):
+    svc = StudyService(str(tmp_path))
+    cfg = _cfg([{"parameter": "c", "type": "CATEGORICAL", "categorical_value_spec": {"values": ["a", "b"]}}])
+    cfg["algorithm"] = "GRID_SEARCH"
+    svc.create_study("projects/p/locations/r", "s1", cfg)
+    with pytest.raises(StudyExists):
+        svc.create_study("projects/p/locations/r", "s1", cfg)
+    c = optimizer_client.create_or_load_study("p", "r", "s1", cfg, root=str(tmp_path))  # 409 -> load
+    a = c.get_suggestions("t0")["trials"][0]
+    c.complete_trial(a["name"].split("/")[-1], False)
+    b = c.get_suggestions("t0")["trials"][0]
+    assert {a["parameters"][0]["stringValue"], b["parameters"][0]["stringValue"]} == {"a", "b"}
+    c.complete_trial("2", False)
+    assert c.get_suggestions("t0") == {}  # grid exhausted == HTTP 429
+    assert len(c.list_trials()) == 2 and c.list_studies()[0]["name"].endswith("/studies/s1")
+    c.delete_study()
+    with pytest.raises(ValueError, match="not found"):
+        c.delete_study()
+
+
+def test_service_concurrent_suggest_is_safe(tmp_path):
+    svc = StudyService(str(tmp_path))
+    cfg = _cfg([{"parameter": "x", "type": "DOUBLE", "double_value_spec": {"min_value": 0.0, "max_value": 1.0}}])
+    svc.create_study("projects/p/locations/r", "c", cfg)
+    got = []
+
+    def worker(i):
+        for _ in range(5):
+            r = svc.suggest("projects/p/locations/r/studies/c", f"t{i}")
+            tid = r["trials"][0]["name"]
+            svc.complete_trial(tid)
+            got.append(tid)
+
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    assert len(got) == 20 and len(set(got)) == 20
+
+
+def test_early_stopping_median_rule(tmp_path):
+    svc = StudyService(str(tmp_path))
+    cfg = _cfg([{"parameter": "x", "type": "DOUBLE", "double_value_spec": {"min_value": 0.0, "max_value": 1.0}}])
+    cfg["automatedStoppingConfig"] = {"decayCurveStoppingConfig": {"useElapsedTime": True}}
+    svc.create_study("projects/p/locations/r", "e", cfg)
+    name = "projects/p/locations/r/studies/e"
+    for i in range(3):
+        t = svc.suggest(name, "t")["trials"][0]["name"]
+        svc.add_measurement(t, {"stepCount": 1, "metrics": [{"metric": "accuracy", "value": 0.9}]})
+        svc.complete_trial(t)
+    t = svc.suggest(name, "t")["trials"][0]["name"]
+    svc.add_measurement(t, {"stepCount": 1, "metrics": [{"metric": "accuracy", "value": 0.1}]})
+    assert svc.check_early_stopping_state(t)["shouldStop"]
+
+
+def test_trial_cap_1000(tmp_path, monkeypatch):
+    from cloud_amd.tuner import study_service
+
+    monkeypatch.setattr(study_service, "MAX_TRIALS", 2)
+    svc = StudyService(str(tmp_path))
+    cfg = _cfg([{"parameter": "x", "type": "DOUBLE", "double_value_spec": {"min_value": 0.0, "max_value": 1.0}}])
+    svc.create_study("projects/p/locations/r", "cap", cfg)
+    name = "projects/p/locations/r/studies/cap"
+    for _ in range(2):
+        svc.complete_trial(svc.suggest(name, "t")["trials"][0]["name"])
+    with pytest.raises(TooManyTrials):
+        svc.suggest(name, "t")
+
+
+def _build(hp):
+    from cloud_amd import keras
+
+    m = keras.Sequential([keras.layers.Dense(hp.Int("units", 8, 32, step=8), activation=hp.Choice("act", ["relu",
+                                                                                                     "tanh"]),
+                                             input_shape=(20,)), keras.layers.Dense(2, activation="softmax")])
+    m.compile(optimizer="adam", loss="sparse_categorical_crossentropy", metrics=["acc"])
+    return m
+
+
+def test_cloud_tuner_search_and_summaries(tmp_path, capsys):
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=(256, 20)).astype("float32")
+    y = (x[:, 0] > 0).astype("int64")
+    tuner = CloudTuner(_build, project_id="p", region="r", objective="acc", hyperparameters=_hps(), max_trials=3,
+                       study_id="search", study_dir=str(tmp_path / "studies"), directory=str(tmp_path / "res"))
+    tuner.search_space_summary()
+    tuner.search(x, y, epochs=2, batch_size=32, validation_data=(x, y))
+    tuner.results_summary()
+    out = capsys.readouterr().out
+    import re
+
+    assert re.search(r"Search space summary(?=.*units \(Int\))(?=.*act \(Choice\))", out, re.DOTALL)
+    assert re.search(r"Results summary.*Trial .* summary.*Hyperparameters.*", out, re.DOTALL)
+    best = tuner.get_best_models(1)[0]
+    assert best.predict(x[:4]).shape == (4, 2)
+    assert len(tuner.get_best_hyperparameters(2)) == 2
+    assert os.path.exists(tmp_path / "res" / "untitled_project" / "trial_1" / "trial.json")
+
+
+def test_random_and_grid_search(tmp_path):
+    rng = np.random.default_rng(1)
+    x = rng.normal(size=(64, 20)).astype("float32")
+    y = (x[:, 0] > 0).astype("int64")
+    g = GridSearch(_build, objective="acc", max_trials=10, study_dir=str(tmp_path), directory=str(tmp_path / "g"))
+    g.search(x, y, epochs=1, batch_size=32)
+    trials = g.oracle.service.list_trials()
+    assert len(trials) == 6  # 3 units x 2 activations, then exhausted
+    r = RandomSearch(_build, objective="acc", max_trials=2, study_dir=str(tmp_path), directory=str(tmp_path / "r"))
+    r.search(x, y, epochs=1, batch_size=32)
+    assert len(r.oracle.service.list_trials()) == 2
+
+
+def test_failed_trial_is_infeasible(tmp_path, monkeypatch):
+    monkeypatch.setenv("CLOUD_AMD_FAULT", "0:0:raise")
+    rng = np.random.default_rng(2)
+    x = rng.normal(size=(64, 20)).astype("float32")
+    y = (x[:, 0] > 0).astype("int64")
+    tuner = CloudTuner(_build, objective="acc", hyperparameters=_hps(), max_trials=2, study_id="fail",
+                       study_dir=str(tmp_path), directory=str(tmp_path / "res"))
+    tuner.search(x, y, epochs=1, batch_size=32)
+    trials = tuner.oracle.service.list_trials()
+    assert all(t.get("trialInfeasible") for t in trials)
+
+
+def test_distributed_tuning_four_workers(tmp_path):
+    env = {"STUDY_ID": "dist", "STUDY_DIR": str(tmp_path), "PYTHONPATH": os.path.join(HERE, "data")}
+    import sys
+
+    sys.path.insert(0, os.path.join(HERE, "data"))
+    sched = TrialScheduler("tuner_worker:run", n_gpus=0, workers=4, env=env)
+    res = sched.run(timeout=600)
+    assert res["exit_codes"] == [0, 0, 0, 0]
+    with open(tmp_path / "CloudTuner_study_dist" / "study.json") as f:
+        trials = json.load(f)["trials"]
+    assert len(trials) == 6 and all(t["state"] == "COMPLETED" for t in trials)
+    assert len({t["clientId"] for t in trials}) >= 2
