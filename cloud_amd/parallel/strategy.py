@@ -250,7 +250,11 @@ def is_chief_task(tf_config=None):
     if not cfg:
         raise ValueError("TF_CONFIG is not set")
     task = cfg.get("task", {})
-    return task.get("type") == "chief" or task.get("index") == 0
+    if task.get("type") == "chief":
+        return True
+    # reference quirk (remote.py:151-154): index 0 counts as chief -- kept for
+    # worker-only clusters; with an explicit chief only the chief writes.
+    return task.get("index") == 0 and "chief" not in cfg.get("cluster", {})
 
 
 def experimental_set_strategy(strategy):
