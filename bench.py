@@ -110,6 +110,14 @@ def main():
     ips = global_batch * args.steps / elapsed
     first_lat = dist_env.all_reduce_max(first_step_latency, device)
     final_loss = float(loss.detach().float().item()) if loss is not None else float("nan")
+    try:
+        from cloud_amd import monitoring
+
+        monitoring.gauge(monitoring.THROUGHPUT, ips)
+        monitoring.gauge(monitoring.FIRST_STEP, first_lat)
+        monitoring.observe(monitoring.STEP_TIME, ms)
+    except Exception:
+        pass
     if rank == 0:
         out = {
             "metric": "images/sec ResNet-50 via run() at 1/2/4/8 MI355X; run()→first-step latency",

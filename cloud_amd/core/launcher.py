@@ -212,6 +212,12 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
         procs.append(p)
     job = Job(job_id, job_dir, procs, ranks, meta)
     job._write_meta()
+    try:
+        from .. import monitoring
+
+        monitoring.inc(monitoring.JOBS, 1, backend=meta["backend"], world=str(world))
+    except Exception:  # metrics are best-effort in the launcher
+        pass
     return job
 
 

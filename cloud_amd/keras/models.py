@@ -353,6 +353,10 @@ class Model(Layer):
                     break
             logs = self._logs()
             logs["epoch_time_s"] = time.time() - t0
+            from .. import monitoring
+
+            if step:
+                monitoring.observe(monitoring.STEP_TIME, 1000.0 * logs["epoch_time_s"] / step)
             if validation_data is not None and (epoch + 1) % validation_freq == 0:
                 vx, vy = (validation_data, None) if isinstance(validation_data, Dataset) else validation_data[:2]
                 vlogs = self.evaluate(vx, vy, batch_size=validation_batch_size or batch_size, verbose=0,
