@@ -12,6 +12,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from . import fused_block
 from .layers import BatchNormAct, Conv2d, GlobalAvgPool, Linear, MaxPool2d
 
 
@@ -28,6 +29,7 @@ class Bottleneck(nn.Module):
         self.conv3 = Conv2d(width, cout, 1, dtype=dtype, device=device)
         self.bn3 = BatchNormAct(cout, relu=True, zero_init=zero_init_residual, device=device)
         self.fused_stats = True
+        self.fused_block = True  # one autograd node per block when the params live in the grad arena
         self.downsample = None
         if stride != 1 or cin != cout:
             self.downsample = nn.ModuleDict({
@@ -36,6 +38,8 @@ class Bottleneck(nn.Module):
             })
 
     def forward(self, x):
+        if self.fused_block and fused_block.can_fuse(self, x):
+            return fused_block.bottleneck_forward(self, x)
         identity = x
         fs = self.fused_stats
         if self.downsample is not None:

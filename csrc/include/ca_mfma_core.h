@@ -65,6 +65,7 @@ struct CoreParams {
   // convolution geometry (NHWC input [Nb,H,W,Cin], output [Nb,OH,OW,Cout], weights [Cout][KH][KW][Cin])
   int Nb, H, W, Cin, OH, OW, Cout, KH, KW, sh, sw, ph, pw;
   FastDiv div_ow, div_oh, div_w, div_h, div_cin, div_cout, div_kw;
+  int cin_tile, cout_tile;  // Cin % BK == 0 / Cout % BK == 0: a K tile never straddles two taps
 };
 
 template <int R, bool KC>
@@ -109,49 +110,85 @@ __device__ __forceinline__ s8v zero8() { return s8v{0, 0, 0, 0, 0, 0, 0, 0}; }
 __device__ __forceinline__ s8v ld16(const bf16_t* p) { return *reinterpret_cast<const s8v*>(p); }
 
 // ---------------------------------------------------------------- loaders --
-// A loader fetches the chunk (row, col) of the tile whose corner is (r0, k0).
-// KC loaders: row = output-dim index offset, col = k offset.
-// NC loaders: row = k offset, col = output-dim offset.
+// A loader owns the CPT 16-B chunks a thread fetches per K tile.  Everything
+// that depends only on the chunk's output-dim coordinate (row pointers, pixel
+// decode) is computed ONCE in the constructor; load(i, k0) only adds the
+// k-dependent part -- keeps the address VALU work out of the MFMA loop.
+// KC loaders: chunk (row = output-dim offset, col = k offset).
+// NC loaders: chunk (row = k offset, col = output-dim offset).
 
 // Dense operand, K-contiguous: X[r][k] at p[r*ld + k].
-template <int R>
+template <int R, int CPT, int NT>
 struct DenseKC {
   static constexpr bool KC = true;
-  const bf16_t* p; long ld; int rlimit, K;
-  __device__ DenseKC(const CoreParams& P, bool isA) {
-    p = isA ? P.A : P.B; ld = isA ? P.lda : P.ldb; rlimit = isA ? P.M : P.N; K = P.K;
+  const bf16_t* rowp[CPT];
+  int col[CPT];
+  bool ok[CPT];
+  int K;
+  __device__ DenseKC(const CoreParams& P, bool isA, int r0, int tid) {
+    const bf16_t* p = isA ? P.A : P.B;
+    const long ld = isA ? P.lda : P.ldb;
+    const int rlimit = isA ? P.M : P.N;
+    K = P.K;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      int row, c;
+      chunk_coords<R, true>(tid + i * NT, row, c);
+      ok[i] = (r0 + row) < rlimit;
+      rowp[i] = p + (long)(ok[i] ? r0 + row : 0) * ld;
+      col[i] = c;
+    }
   }
-  __device__ __forceinline__ s8v load(int r0, int k0, int row, int col) const {
-    const int r = r0 + row, k = k0 + col;
-    return (r < rlimit && k < K) ? ld16(p + (long)r * ld + k) : zero8();
+  __device__ __forceinline__ s8v load(int i, int k0) const {
+    const int k = k0 + col[i];
+    return (ok[i] && k < K) ? ld16(rowp[i] + k) : zero8();
   }
 };
 
 // Dense operand, output-dim contiguous: X[r][k] at p[k*ld + r].
-template <int R>
+template <int R, int CPT, int NT>
 struct DenseNC {
   static constexpr bool KC = false;
-  const bf16_t* p; long ld; int rlimit, K;
-  __device__ DenseNC(const CoreParams& P, bool isA) {
-    p = isA ? P.A : P.B; ld = isA ? P.lda : P.ldb; rlimit = isA ? P.M : P.N; K = P.K;
+  const bf16_t* colp[CPT];
+  int row[CPT];
+  bool ok[CPT];
+  long ld;
+  int K;
+  __device__ DenseNC(const CoreParams& P, bool isA, int r0, int tid) {
+    const bf16_t* p = isA ? P.A : P.B;
+    ld = isA ? P.lda : P.ldb;
+    const int rlimit = isA ? P.M : P.N;
+    K = P.K;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      int r, c;
+      chunk_coords<R, false>(tid + i * NT, r, c);
+      ok[i] = (r0 + c) < rlimit;
+      colp[i] = p + (ok[i] ? r0 + c : 0);
+      row[i] = r;
+    }
   }
-  __device__ __forceinline__ s8v load(int r0, int k0, int row, int col) const {
-    const int k = k0 + row, r = r0 + col;
-    return (r < rlimit && k < K) ? ld16(p + (long)k * ld + r) : zero8();
+  __device__ __forceinline__ s8v load(int i, int k0) const {
+    const int k = k0 + row[i];
+    return (ok[i] && k < K) ? ld16(colp[i] + (long)k * ld) : zero8();
   }
 };
 
 // ------------------------------------------------------------------ core --
-template <int BM, int BN, int WM, int WN, class LA, class LB, int EPI>
+template <int BM, int BN, int WM, int WN, template <int, int, int> class LAT, template <int, int, int> class LBT,
+          int EPI, int NSTAGE = 2>
 __device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
   constexpr int NT = WM * WN * 64;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
-  using GA = TileGeom<BM, LA::KC>;
-  using GB = TileGeom<BN, LB::KC>;
+  constexpr bool A_KC = LAT<BM, 1, NT>::KC, B_KC = LBT<BN, 1, NT>::KC;
+  using GA = TileGeom<BM, A_KC>;
+  using GB = TileGeom<BN, B_KC>;
   constexpr int STAGE = GA::ELEMS + GB::ELEMS;
   constexpr int EPI_LD = BN + PAD;
-  constexpr int SMEM = (2 * STAGE > BM * EPI_LD ? 2 * STAGE : BM * EPI_LD);
+  constexpr int SMEM = (NSTAGE * STAGE > BM * EPI_LD ? NSTAGE * STAGE : BM * EPI_LD);
   constexpr int CPA = GA::CHUNKS / NT, CPB = GB::CHUNKS / NT;
+  using LA = LAT<BM, CPA, NT>;
+  using LB = LBT<BN, CPB, NT>;
   static_assert(GA::CHUNKS % NT == 0 && GB::CHUNKS % NT == 0, "tile chunks must divide threads");
   __shared__ __attribute__((aligned(16))) short smem[SMEM];
 
@@ -166,14 +203,14 @@ __device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
   if (kend > P.K) kend = P.K;
   const int nk = (kend - kbeg + BK - 1) / BK;
 
-  const LA la(P, true);
-  const LB lb(P, false);
+  const LA la(P, true, m0, tid);
+  const LB lb(P, false, n0, tid);
   s8v ra[CPA], rb[CPB];
   int arow[CPA], acol[CPA], brow[CPB], bcol[CPB];
 #pragma unroll
-  for (int i = 0; i < CPA; ++i) chunk_coords<BM, LA::KC>(tid + i * NT, arow[i], acol[i]);
+  for (int i = 0; i < CPA; ++i) chunk_coords<BM, A_KC>(tid + i * NT, arow[i], acol[i]);
 #pragma unroll
-  for (int i = 0; i < CPB; ++i) chunk_coords<BN, LB::KC>(tid + i * NT, brow[i], bcol[i]);
+  for (int i = 0; i < CPB; ++i) chunk_coords<BN, B_KC>(tid + i * NT, brow[i], bcol[i]);
 
   f4v acc[FM][FN];
 #pragma unroll
@@ -183,9 +220,9 @@ __device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
 
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < CPA; ++i) ra[i] = la.load(m0, k0, arow[i], acol[i]);
+    for (int i = 0; i < CPA; ++i) ra[i] = la.load(i, k0);
 #pragma unroll
-    for (int i = 0; i < CPB; ++i) rb[i] = lb.load(n0, k0, brow[i], bcol[i]);
+    for (int i = 0; i < CPB; ++i) rb[i] = lb.load(i, k0);
   };
   auto lstore = [&](short* base) {
 #pragma unroll
@@ -194,33 +231,46 @@ __device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
     for (int i = 0; i < CPB; ++i) *reinterpret_cast<s8v*>(base + GA::ELEMS + brow[i] * GB::LD + bcol[i]) = rb[i];
   };
 
-  if (nk > 0) {
-    gload(kbeg);
-    lstore(smem);
-  }
-  __syncthreads();
-  int cur = 0;
-  for (int t = 0; t < nk; ++t) {
-    const bool more = (t + 1) < nk;
-    if (more) gload(kbeg + (t + 1) * BK);
-    const short* As = smem + cur * STAGE;
+  auto compute = [&](const short* As) {
     const short* Bs = As + GA::ELEMS;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, LA::KC>(As, wm * (BM / WM) + i * 16, kk, lane);
+      for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, A_KC>(As, wm * (BM / WM) + i * 16, kk, lane);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, LB::KC>(Bs, wn * (BN / WN) + j * 16, kk, lane);
+      for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, B_KC>(Bs, wn * (BN / WN) + j * 16, kk, lane);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (more) lstore(smem + (cur ^ 1) * STAGE);
+  };
+  if constexpr (NSTAGE == 1) {
+    for (int t = 0; t < nk; ++t) {
+      gload(kbeg + t * BK);
+      if (t) __syncthreads();
+      lstore(smem);
+      __syncthreads();
+      compute(smem);
+    }
     __syncthreads();
-    cur ^= 1;
+  } else {
+    if (nk > 0) {
+      gload(kbeg);
+      lstore(smem);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int t = 0; t < nk; ++t) {
+      const bool more = (t + 1) < nk;
+      if (more) gload(kbeg + (t + 1) * BK);
+      compute(smem + cur * STAGE);
+      if (more) lstore(smem + (cur ^ 1) * STAGE);
+      __syncthreads();
+      cur ^= 1;
+    }
   }
 
   // C/D layout of mfma_f32_16x16x32: col = lane&15, row = (lane>>4)*4 + r

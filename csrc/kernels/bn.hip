@@ -259,14 +259,15 @@ __global__ void __launch_bounds__(BLK) bn_bwd_reduce_kernel(const bf16_t* __rest
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ ws, int nchunks, long M, int C,
                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ rstd, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta, float* __restrict__ coef) {
+                                       float* __restrict__ dbeta, float* __restrict__ coef, int accum) {
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
   double sd, sdx;
   wave_chunk_sum(ws, nchunks, (long)C, (long)nchunks * C, c, sd, sdx);
   if ((threadIdx.x & 63) != 0) return;
-  if (dgamma) dgamma[c] = (float)sdx;
-  if (dbeta) dbeta[c] = (float)sd;
+  // accum: parameter grads are summed into (flat arena slots), not overwritten
+  if (dgamma) dgamma[c] = (float)sdx + (accum ? dgamma[c] : 0.f);
+  if (dbeta) dbeta[c] = (float)sd + (accum ? dbeta[c] : 0.f);
   const double g = gamma ? gamma[c] : 1.0;
   const double rs = rstd[c], mu = mean[c];
   const double k1 = g * rs;
@@ -385,13 +386,15 @@ int ca_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, long M, int C,
               bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta,
               float* coef /* [3C] */, float* ws, int relu, hipStream_t s) {
   if (C % 8 != 0) return -1;
+  const int accum = (relu >> 1) & 1;  // flags: bit0 relu, bit1 accumulate dgamma/dbeta
+  relu &= 1;
   Tiling t = make_tiling(M, C);
   dim3 grid(t.ncol, t.nchunks);
   if (relu) bn_bwd_reduce_kernel<true><<<grid, BLK, 0, s>>>(dy, y, x, save_mean, save_rstd, M, C, ws);
   else bn_bwd_reduce_kernel<false><<<grid, BLK, 0, s>>>(dy, y, x, save_mean, save_rstd, M, C, ws);
   CA_LAUNCH_CHECK();
   bn_bwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(ws, t.nchunks, M, C, gamma, save_mean, save_rstd,
-                                                         dgamma, dbeta, coef);
+                                                         dgamma, dbeta, coef, accum);
   CA_LAUNCH_CHECK();
   if (relu && dres) bn_bwd_apply_kernel<true, true><<<grid, BLK, 0, s>>>(dy, y, x, coef, dx, dres, M, C);
   else if (relu) bn_bwd_apply_kernel<true, false><<<grid, BLK, 0, s>>>(dy, y, x, coef, dx, dres, M, C);

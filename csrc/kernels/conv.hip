@@ -27,41 +27,86 @@ __device__ __forceinline__ Pix decode(uint32_t m, const FastDiv& dw, const FastD
   return Pix{(int)n, (int)(t - n * dh.d), (int)x};
 }
 
+// (tap, channel) of reduction index k over `C` channels per tap.  When C is a
+// multiple of BK a K tile never straddles two taps, so the tap is uniform and
+// derived from the tile start only.
+__device__ __forceinline__ void tap_split(int k, int k0, int C, const FastDiv& dc, bool tile_in_tap, int& tap,
+                                          int& c) {
+  tap = (int)fdiv((uint32_t)(tile_in_tap ? k0 : k), dc);
+  c = k - tap * C;
+}
+
 // A of forward: rows = output pixels, k = (tap, ci).  KC.
-template <int R>
+template <int R, int CPT, int NT>
 struct ConvFwdA {
   static constexpr bool KC = true;
   const CoreParams& P;
-  __device__ ConvFwdA(const CoreParams& p, bool) : P(p) {}
-  __device__ __forceinline__ s8v load(int r0, int k0, int row, int col) const {
-    const int m = r0 + row, k = k0 + col;
-    if (m >= P.M || k >= P.K) return zero8();
-    const Pix o = decode((uint32_t)m, P.div_ow, P.div_oh);
-    const uint32_t tap = fdiv((uint32_t)k, P.div_cin);
-    const int ci = k - (int)tap * P.Cin;
-    const uint32_t kh = fdiv(tap, P.div_kw);
-    const int kw = (int)tap - (int)kh * P.KW;
-    const int ih = o.y * P.sh - P.ph + (int)kh, iw = o.x * P.sw - P.pw + kw;
+  const bf16_t* nbase[CPT];
+  int iy0[CPT], ix0[CPT], col[CPT];
+  __device__ ConvFwdA(const CoreParams& p, bool, int r0, int tid) : P(p) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      int row, c;
+      chunk_coords<R, true>(tid + i * NT, row, c);
+      const int m = r0 + row;
+      col[i] = c;
+      if (m < P.M) {
+        const Pix o = decode((uint32_t)m, P.div_ow, P.div_oh);
+        nbase[i] = P.A + (long)o.n * P.H * P.W * P.Cin;
+        iy0[i] = o.y * P.sh - P.ph;
+        ix0[i] = o.x * P.sw - P.pw;
+      } else {
+        nbase[i] = P.A;
+        iy0[i] = -(1 << 29);  // forces out-of-range
+        ix0[i] = 0;
+      }
+    }
+  }
+  __device__ __forceinline__ s8v load(int i, int k0) const {
+    const int k = k0 + col[i];
+    if (k >= P.K) return zero8();
+    int tap, ci;
+    tap_split(k, k0, P.Cin, P.div_cin, P.cin_tile, tap, ci);
+    const int kh = (int)fdiv((uint32_t)tap, P.div_kw), kw = tap - kh * P.KW;
+    const int ih = iy0[i] + kh, iw = ix0[i] + kw;
     if ((unsigned)ih >= (unsigned)P.H || (unsigned)iw >= (unsigned)P.W) return zero8();
-    return ld16(P.A + (((long)o.n * P.H + ih) * P.W + iw) * P.Cin + ci);
+    return ld16(nbase[i] + ((long)ih * P.W + iw) * P.Cin + ci);
   }
 };
 
 // A of dgrad: rows = input pixels, k = (tap, co) over dY.  KC.
-template <int R>
+template <int R, int CPT, int NT>
 struct ConvDgradA {
   static constexpr bool KC = true;
   const CoreParams& P;
-  __device__ ConvDgradA(const CoreParams& p, bool) : P(p) {}
-  __device__ __forceinline__ s8v load(int r0, int k0, int row, int col) const {
-    const int m = r0 + row, k = k0 + col;
-    if (m >= P.M || k >= P.K) return zero8();
-    const Pix i = decode((uint32_t)m, P.div_w, P.div_h);
-    const uint32_t tap = fdiv((uint32_t)k, P.div_cout);
-    const int co = k - (int)tap * P.Cout;
-    const uint32_t kh = fdiv(tap, P.div_kw);
-    const int kw = (int)tap - (int)kh * P.KW;
-    int oy = i.y + P.ph - (int)kh, ox = i.x + P.pw - kw;
+  const bf16_t* nbase[CPT];
+  int iy[CPT], ix[CPT], col[CPT];
+  __device__ ConvDgradA(const CoreParams& p, bool, int r0, int tid) : P(p) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      int row, c;
+      chunk_coords<R, true>(tid + i * NT, row, c);
+      const int m = r0 + row;
+      col[i] = c;
+      if (m < P.M) {
+        const Pix q = decode((uint32_t)m, P.div_w, P.div_h);
+        nbase[i] = P.A + (long)q.n * P.OH * P.OW * P.Cout;
+        iy[i] = q.y + P.ph;
+        ix[i] = q.x + P.pw;
+      } else {
+        nbase[i] = P.A;
+        iy[i] = -(1 << 29);
+        ix[i] = 0;
+      }
+    }
+  }
+  __device__ __forceinline__ s8v load(int i, int k0) const {
+    const int k = k0 + col[i];
+    if (k >= P.K) return zero8();
+    int tap, co;
+    tap_split(k, k0, P.Cout, P.div_cout, P.cout_tile, tap, co);
+    const int kh = (int)fdiv((uint32_t)tap, P.div_kw), kw = tap - kh * P.KW;
+    int oy = iy[i] - kh, ox = ix[i] - kw;
     if (oy < 0 || ox < 0) return zero8();
     if (P.sh > 1) {
       if (oy % P.sh) return zero8();
@@ -72,51 +117,75 @@ struct ConvDgradA {
       ox /= P.sw;
     }
     if (oy >= P.OH || ox >= P.OW) return zero8();
-    return ld16(P.A + (((long)i.n * P.OH + oy) * P.OW + ox) * P.Cout + co);
+    return ld16(nbase[i] + ((long)oy * P.OW + ox) * P.Cout + co);
   }
 };
 
 // B of dgrad: B[k=(tap,co)][ci] = W[co][tap][ci]  (ci contiguous -> NC).
-template <int R>
+template <int R, int CPT, int NT>
 struct ConvDgradB {
   static constexpr bool KC = false;
   const CoreParams& P;
-  __device__ ConvDgradB(const CoreParams& p, bool) : P(p) {}
-  __device__ __forceinline__ s8v load(int r0, int k0, int row, int col) const {
-    const int k = k0 + row, ci = r0 + col;
-    if (k >= P.K || ci >= P.N) return zero8();
-    const uint32_t tap = fdiv((uint32_t)k, P.div_cout);
-    const int co = k - (int)tap * P.Cout;
-    return ld16(P.B + ((long)co * (P.KH * P.KW) + tap) * P.Cin + ci);
+  int row[CPT], ci[CPT];
+  bool ok[CPT];
+  __device__ ConvDgradB(const CoreParams& p, bool, int r0, int tid) : P(p) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      int r, c;
+      chunk_coords<R, false>(tid + i * NT, r, c);
+      row[i] = r;
+      ci[i] = r0 + c;
+      ok[i] = ci[i] < P.N;
+    }
+  }
+  __device__ __forceinline__ s8v load(int i, int k0) const {
+    const int k = k0 + row[i];
+    if (!ok[i] || k >= P.K) return zero8();
+    int tap, co;
+    tap_split(k, k0, P.Cout, P.div_cout, P.cout_tile, tap, co);
+    return ld16(P.B + ((long)co * (P.KH * P.KW) + tap) * P.Cin + ci[i]);
   }
 };
 
 // B of wgrad: B[k=(n,oh,ow)][j=(tap,ci)] = X[n, oh*s-p+kh, ow*s-p+kw, ci]  (NC).
-template <int R>
+template <int R, int CPT, int NT>
 struct ConvWgradB {
   static constexpr bool KC = false;
   const CoreParams& P;
-  __device__ ConvWgradB(const CoreParams& p, bool) : P(p) {}
-  __device__ __forceinline__ s8v load(int r0, int k0, int row, int col) const {
-    const int k = k0 + row, j = r0 + col;
-    if (k >= P.K || j >= P.N) return zero8();
+  int row[CPT], kh[CPT], kw[CPT], ci[CPT];
+  bool ok[CPT];
+  __device__ ConvWgradB(const CoreParams& p, bool, int r0, int tid) : P(p) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      int r, c;
+      chunk_coords<R, false>(tid + i * NT, r, c);
+      row[i] = r;
+      const int j = r0 + c;
+      ok[i] = j < P.N;
+      int tap, cc;
+      tap_split(ok[i] ? j : 0, 0, P.Cin, P.div_cin, false, tap, cc);
+      const int h = (int)fdiv((uint32_t)tap, P.div_kw);
+      kh[i] = h;
+      kw[i] = tap - h * P.KW;
+      ci[i] = cc;
+    }
+  }
+  __device__ __forceinline__ s8v load(int i, int k0) const {
+    const int k = k0 + row[i];
+    if (!ok[i] || k >= P.K) return zero8();
     const Pix o = decode((uint32_t)k, P.div_ow, P.div_oh);
-    const uint32_t tap = fdiv((uint32_t)j, P.div_cin);
-    const int ci = j - (int)tap * P.Cin;
-    const uint32_t kh = fdiv(tap, P.div_kw);
-    const int kw = (int)tap - (int)kh * P.KW;
-    const int ih = o.y * P.sh - P.ph + (int)kh, iw = o.x * P.sw - P.pw + kw;
+    const int ih = o.y * P.sh - P.ph + kh[i], iw = o.x * P.sw - P.pw + kw[i];
     if ((unsigned)ih >= (unsigned)P.H || (unsigned)iw >= (unsigned)P.W) return zero8();
-    return ld16(P.B + (((long)o.n * P.H + ih) * P.W + iw) * P.Cin + ci);
+    return ld16(P.B + (((long)o.n * P.H + ih) * P.W + iw) * P.Cin + ci[i]);
   }
 };
 
-template <int BM, int BN, class LA, class LB, int EPI>
+template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
 __global__ void __launch_bounds__(256) conv_gemm_kernel(CoreParams P) {
-  mfma_gemm_body<BM, BN, 2, 2, LA, LB, EPI>(P);
+  mfma_gemm_body<BM, BN, 2, 2, LA, LB, EPI, 2>(P);
 }
 
-template <int BM, int BN, class LA, class LB, int EPI>
+template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
 int launch(const CoreParams& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   conv_gemm_kernel<BM, BN, LA, LB, EPI><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
@@ -133,6 +202,8 @@ CoreParams conv_params(int Nb, int H, int W, int Cin, int Cout, int KH, int KW, 
   p.div_ow = make_fastdiv(p.OW); p.div_oh = make_fastdiv(p.OH);
   p.div_w = make_fastdiv(W); p.div_h = make_fastdiv(H);
   p.div_cin = make_fastdiv(Cin); p.div_cout = make_fastdiv(Cout); p.div_kw = make_fastdiv(KW);
+  p.cin_tile = (Cin % BK == 0) ? 1 : 0;
+  p.cout_tile = (Cout % BK == 0) ? 1 : 0;
   return p;
 }
 
@@ -154,8 +225,8 @@ int ca_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   p.A = x; p.B = w; p.lda = Cin; p.ldb = (long)KH * KW * Cin; p.C = y; p.ldc = Cout;
   p.M = Nb * p.OH * p.OW; p.N = Cout; p.K = KH * KW * Cin; p.k_per_split = p.K;
   p.stats = stats;
-  if (Cout <= 64) return launch<128, 64, ConvFwdA<128>, DenseKC<64>, EPI_BF16>(p, 1, s);
-  return launch<128, 128, ConvFwdA<128>, DenseKC<128>, EPI_BF16>(p, 1, s);
+  if (Cout <= 64) return launch<128, 64, ConvFwdA, DenseKC, EPI_BF16>(p, 1, s);
+  return launch<128, 128, ConvFwdA, DenseKC, EPI_BF16>(p, 1, s);
 }
 
 // dx[Nb,H,W,Cin] = dgrad(dy[Nb,OH,OW,Cout], w) (+ beta * dx).
@@ -166,8 +237,8 @@ int ca_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb, int H, 
   p.A = dy; p.B = w; p.C = dx; p.ldc = Cin;
   p.M = Nb * H * W; p.N = Cin; p.K = KH * KW * Cout; p.k_per_split = p.K;
   p.beta = beta;
-  if (Cin <= 64) return launch<128, 64, ConvDgradA<128>, ConvDgradB<64>, EPI_BF16>(p, 1, s);
-  return launch<128, 128, ConvDgradA<128>, ConvDgradB<128>, EPI_BF16>(p, 1, s);
+  if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, EPI_BF16>(p, 1, s);
+  return launch<128, 128, ConvDgradA, ConvDgradB, EPI_BF16>(p, 1, s);
 }
 
 // dw[Cout, KH*KW*Cin] (+)= wgrad(dy, x) via split-K fp32 slabs in ws[splits][Cout][KH*KW*Cin].
@@ -183,8 +254,8 @@ int ca_conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, floa
   splits = (p.K + kps - 1) / kps;
   p.k_per_split = kps;
   p.C = ws; p.ldc = p.N; p.split_stride = (long)p.M * p.N;
-  int rc = (p.N <= 64) ? launch<128, 64, DenseNC<128>, ConvWgradB<64>, EPI_F32_PARTIAL>(p, splits, s)
-                       : launch<128, 128, DenseNC<128>, ConvWgradB<128>, EPI_F32_PARTIAL>(p, splits, s);
+  int rc = (p.N <= 64) ? launch<128, 64, DenseNC, ConvWgradB, EPI_F32_PARTIAL>(p, splits, s)
+                       : launch<128, 128, DenseNC, ConvWgradB, EPI_F32_PARTIAL>(p, splits, s);
   if (rc) return rc;
   return ca_splitk_reduce(ws, splits, (long)p.M * p.N, dw, dw_bf16, beta, s);
 }

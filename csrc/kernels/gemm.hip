@@ -13,9 +13,9 @@
 namespace {
 using namespace ca;
 
-template <int BM, int BN, class LA, class LB, int EPI>
+template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI, int NS>
 __global__ void __launch_bounds__(256) dense_gemm_kernel(CoreParams P) {
-  mfma_gemm_body<BM, BN, 2, 2, LA, LB, EPI>(P);
+  mfma_gemm_body<BM, BN, 2, 2, LA, LB, EPI, NS>(P);
 }
 
 template <bool OUT_BF16>
@@ -56,10 +56,14 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <int BM, int BN, class LA, class LB, int EPI>
+template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
 int launch(const CoreParams& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  dense_gemm_kernel<BM, BN, LA, LB, EPI><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
+  // a single K tile needs no double buffer: half the LDS -> twice the resident blocks
+  if (p.k_per_split <= BK)
+    dense_gemm_kernel<BM, BN, LA, LB, EPI, 1><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
+  else
+    dense_gemm_kernel<BM, BN, LA, LB, EPI, 2><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
   CA_LAUNCH_CHECK();
   return 0;
 }
@@ -69,14 +73,14 @@ int dispatch(int layout, const CoreParams& p, int splits, hipStream_t s) {
   const bool small_n = p.N <= 64;
   switch (layout) {
     case 0:
-      return small_n ? launch<128, 64, DenseKC<128>, DenseKC<64>, EPI>(p, splits, s)
-                     : launch<128, 128, DenseKC<128>, DenseKC<128>, EPI>(p, splits, s);
+      return small_n ? launch<128, 64, DenseKC, DenseKC, EPI>(p, splits, s)
+                     : launch<128, 128, DenseKC, DenseKC, EPI>(p, splits, s);
     case 1:
-      return small_n ? launch<128, 64, DenseKC<128>, DenseNC<64>, EPI>(p, splits, s)
-                     : launch<128, 128, DenseKC<128>, DenseNC<128>, EPI>(p, splits, s);
+      return small_n ? launch<128, 64, DenseKC, DenseNC, EPI>(p, splits, s)
+                     : launch<128, 128, DenseKC, DenseNC, EPI>(p, splits, s);
     case 2:
-      return small_n ? launch<128, 64, DenseNC<128>, DenseNC<64>, EPI>(p, splits, s)
-                     : launch<128, 128, DenseNC<128>, DenseNC<128>, EPI>(p, splits, s);
+      return small_n ? launch<128, 64, DenseNC, DenseNC, EPI>(p, splits, s)
+                     : launch<128, 128, DenseNC, DenseNC, EPI>(p, splits, s);
   }
   return -2;
 }
