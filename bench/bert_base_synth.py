@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""BASELINE.json config 5: BERT-base fine-tune on synthetic GLUE (sequence
+classification), data parallel, bf16 compute, fused AdamW.
+
+    python bench/bert_base_synth.py --steps 20 --warmup 5            # cloud_amd kernels
+    python bench/bert_base_synth.py --stock 1 --steps 20 --warmup 5  # HF transformers + torch AdamW, autocast bf16
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench/bert_base_synth.py --gpus 8
+
+Synthetic GLUE: random token ids (vocab 30522), segment ids (A|B split), a
+right-padded attention mask with per-example lengths in [S/2, S], 2 labels;
+random-init BERT-base weights.  Metric: sequences/s over all ranks (weak
+scaling, fixed per-GPU batch).  Same JSON contract as bench.py.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+T_START = time.time()
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--lr", type=float, default=2e-5)
+    ap.add_argument("--stock", type=int, default=0)
+    ap.add_argument("--layers", type=int, default=12)
+    return ap.parse_args()
+
+
+def synthetic_glue(B, S, device, seed):
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    ids = torch.randint(1000, 30522, (B, S), generator=g, device=device)
+    ids[:, 0] = 101  # [CLS]
+    lens = torch.randint(S // 2, S + 1, (B,), generator=g, device=device)
+    pos = torch.arange(S, device=device)[None]
+    am = (pos < lens[:, None]).long()
+    split = (lens // 2)[:, None]
+    tts = ((pos >= split) & (am == 1)).long()
+    ids = ids * am
+    labels = torch.randint(0, 2, (B,), generator=g, device=device)
+    return ids, tts, am, labels
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.nn.functional as F
+
+    from cloud_amd.utils import dist_env
+
+    rank, world, device = dist_env.init_distributed()
+    torch.manual_seed(1234)
+    B, S = args.batch, args.seq
+    ids, tts, am, labels = synthetic_glue(B, S, device, 1000 + rank)
+
+    if args.stock:
+        from transformers import BertConfig as HFConfig
+        from transformers import BertForSequenceClassification as HFBert
+
+        cfg = HFConfig(num_hidden_layers=args.layers, num_labels=2)
+        model = HFBert(cfg).to(device)
+        if world > 1:
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[device.index])
+        opt = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=0.01, fused=True)
+
+        def train_step():
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                logits = model(input_ids=ids, token_type_ids=tts, attention_mask=am).logits
+            loss = F.cross_entropy(logits.float(), labels)
+            loss.backward()
+            opt.step()
+            return loss
+        impl = "stock: transformers BertForSequenceClassification + torch.autocast(bf16) + AdamW(fused)"
+    else:
+        from cloud_amd.models.bert import BertConfig, BertForSequenceClassification
+        from cloud_amd.ops import softmax_cross_entropy
+        from cloud_amd.optim import AdamW
+        from cloud_amd.parallel.ddp import GradAllReducer
+
+        cfg = BertConfig.base(num_hidden_layers=args.layers, num_labels=2)
+        model = BertForSequenceClassification(cfg, device=device)
+        opt = AdamW(model, learning_rate=args.lr, weight_decay=0.01, grad_scale=1.0 / world)
+        reducer = GradAllReducer(opt.arenas)
+        reducer.broadcast_parameters()
+
+        def train_step():
+            opt.zero_grad()
+            logits = model(ids, tts, am)
+            loss, _ = softmax_cross_entropy(logits, labels, denom=B)
+            loss.backward()
+            reducer.finish()
+            opt.step()
+            return loss
+        impl = "cloud_amd: fused layer fwd/bwd, MFMA GEMM epilogues, fused attention/LN, AdamW arena"
+
+    loss = train_step()
+    torch.cuda.synchronize()
+    first = time.time() - T_START
+    for _ in range(max(args.warmup - 1, 0)):
+        loss = train_step()
+    dist_env.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = train_step()
+    torch.cuda.synchronize()
+    dist_env.barrier()
+    elapsed = dist_env.all_reduce_max(time.perf_counter() - t0, device)
+    sps = B * world * args.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": "sequences/sec BERT-base fine-tune synthetic GLUE (seq %d)" % S,
+            "value": round(sps, 2), "unit": "sequences/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic GLUE (random ids/segments/prefix masks/labels, random-init weights)",
+            "config": {"model": "bert-base" if args.layers == 12 else "bert-%dL" % args.layers,
+                       "global_batch": B * world, "seq_len": S, "per_gpu_batch": B, "parallelism": "dp%d" % world,
+                       "optimizer": "adamw"},
+            "impl": impl, "first_step_latency_s": round(first, 3),
+            "tokens_per_sec": round(sps * S, 1), "final_loss": round(float(loss.detach().float()), 4)}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -45,13 +45,20 @@ def run(remote_dir, distribution_strategy):
         log.info("Loading model from %s", os.path.join(remote_dir, "model"))
         model = keras.models.load_model(os.path.join(remote_dir, "model"))
         model.fit(**fit_kwargs)
+    # reference remote.py:130-145: the chief saves to output/, every other worker to a
+    # temporary dir it deletes again (per-worker writes, not the collective model.save)
+    from ...keras import saving
+
     if _is_current_worker_chief():
-        out = os.path.join(remote_dir, "output")
-        model.save(out)
+        saving._save_model(model, os.path.join(remote_dir, "output"))
     else:
         tmp = os.path.join(remote_dir, "output", "tmp", "workers_" + str(uuid.uuid4()))
-        model.save(tmp)
+        saving._save_model(model, tmp)
         _delete_dir(tmp)
+    import torch.distributed as dist
+
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.barrier()
     return model
 
 

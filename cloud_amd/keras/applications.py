@@ -48,8 +48,46 @@ class ResNet50(Model):
             raise ValueError("pretrained weights are not available offline; use weights=None")
         super().__init__(name=kw.pop("name", "resnet50"))
         self.body = _ResNetBody(include_top, classes, pooling)
+        self.include_top, self.pooling, self.classes = include_top, pooling, classes
+        if input_tensor is not None and input_shape is None:
+            input_shape = tuple(input_tensor.shape[1:])
         if input_shape is not None:
             self.body._maybe_build((None,) + tuple(input_shape))
+        self._sym_in = self._sym_out = None
+        if input_tensor is not None:  # functional use: base_model.output feeds further layers
+            self._sym_in = input_tensor
+            self._sym_out = self(input_tensor)
+
+    def compute_output_shape(self, input_shape):
+        _, h, w, _ = input_shape
+        if self.include_top:
+            return (None, self.classes)
+        if self.pooling in ("avg", "max"):
+            return (None, 2048)
+
+        def down(v):
+            if v is None:
+                return None
+            v = (v + 2 * 3 - 7) // 2 + 1       # stem 7x7/2
+            v = (v + 2 - 3) // 2 + 1           # maxpool 3x3/2
+            for _ in range(3):
+                v = (v + 2 - 3) // 2 + 1       # 3x3/2 in layers 2..4
+            return v
+        return (None, down(h), down(w), 2048)
 
     def call(self, x, training=None):
         return self.body(x, training=training)
+
+
+class resnet50:  # namespace parity: tf.keras.applications.resnet50
+    @staticmethod
+    def preprocess_input(x, data_format=None):
+        """Caffe-style: RGB -> BGR, minus the ImageNet channel means (0..255 inputs)."""
+        import numpy as np
+
+        mean = [103.939, 116.779, 123.68]
+        if isinstance(x, torch.Tensor):
+            x = x.float()[..., [2, 1, 0]]
+            return x - torch.tensor(mean, dtype=x.dtype, device=x.device)
+        x = np.asarray(x, dtype=np.float32)[..., ::-1]
+        return (x - np.asarray(mean, dtype=np.float32)).astype(np.float32)

@@ -174,13 +174,13 @@ class ModelCheckpoint(_Monitor):
                 return
             self.best = cur
         path = self.filepath.format(epoch=epoch + 1, **logs)
-        if _is_chief():
-            if self.save_weights_only:
-                self.model.save_weights(path)
-            else:
-                self.model.save(path)
-            if self.verbose:
-                print(f"\nEpoch {epoch + 1}: saving model to {path}")
+        # collective: every replica calls, the chief writes, all wait (saving.chief_only)
+        if self.save_weights_only:
+            self.model.save_weights(path)
+        else:
+            self.model.save(path)
+        if self.verbose and _is_chief():
+            print(f"\nEpoch {epoch + 1}: saving model to {path}")
 
 
 class TensorBoard(Callback):

@@ -182,7 +182,29 @@ class Layer(nn.Module):
     def call(self, inputs, training=None):  # pragma: no cover - abstract
         return inputs
 
+    def _eager_device(self):
+        for p in self.parameters():
+            return p.device
+        from ..parallel.strategy import get_strategy
+
+        return get_strategy().device or torch.device("cpu")
+
+    def _convert_inputs(self, inputs):
+        """numpy / python inputs -> tensors on the model's (or strategy's) device, floats as float32."""
+        def conv(a):
+            if isinstance(a, (np.ndarray, np.generic)):
+                t = torch.as_tensor(np.asarray(a))
+                if t.is_floating_point():
+                    t = t.float()
+                return t.to(self._eager_device())
+            return a
+
+        if isinstance(inputs, (list, tuple)):
+            return type(inputs)(conv(a) for a in inputs)
+        return conv(inputs)
+
     def __call__(self, inputs, *args, **kwargs):
+        inputs = self._convert_inputs(inputs)
         symbolic = isinstance(inputs, KerasTensor) or (
             isinstance(inputs, (list, tuple)) and inputs and all(isinstance(t, KerasTensor) for t in inputs))
         if symbolic:

@@ -15,7 +15,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from . import activations, initializers
-from .engine import InputLayer, Layer, global_policy  # noqa: F401
+from .engine import Input, InputLayer, Layer, global_policy  # noqa: F401
 
 
 def _pair(v):
@@ -401,6 +401,42 @@ class RandomZoom(_RandomAffine):
         return self._affine(x, theta)
 
 
+class _RandomResize(Layer):
+    """Keras RandomHeight / RandomWidth: one factor per batch, the output size changes."""
+
+    axis = 1
+
+    def __init__(self, factor, interpolation="bilinear", seed=None, **kw):
+        super().__init__(**kw)
+        self.factor = factor
+        self.interpolation = interpolation
+
+    def call(self, x, training=None):
+        if not training:
+            return x
+        lo, hi = (-self.factor, self.factor) if not isinstance(self.factor, (tuple, list)) else self.factor
+        f = 1.0 + float(torch.empty(()).uniform_(lo, hi))
+        size = [x.shape[1], x.shape[2]]
+        size[self.axis - 1] = max(1, int(round(size[self.axis - 1] * f)))
+        mode = "bilinear" if self.interpolation == "bilinear" else "nearest"
+        y = F.interpolate(x.permute(0, 3, 1, 2).float(), size=size, mode=mode,
+                          align_corners=False if mode == "bilinear" else None)
+        return y.permute(0, 2, 3, 1).to(x.dtype).contiguous()
+
+    def get_config(self):
+        c = super().get_config()
+        c["factor"] = self.factor
+        return c
+
+
+class RandomHeight(_RandomResize):
+    axis = 1
+
+
+class RandomWidth(_RandomResize):
+    axis = 2
+
+
 class RandomContrast(Layer):
     def __init__(self, factor, seed=None, **kw):
         super().__init__(**kw)
@@ -444,3 +480,15 @@ AvgPool2D = AveragePooling2D
 GlobalAvgPool2D = GlobalAveragePooling2D
 GlobalMaxPool2D = GlobalMaxPooling2D
 Convolution2D = Conv2D
+
+
+class experimental:  # namespace parity: tf.keras.layers.experimental.preprocessing (TF 2.3)
+    class preprocessing:
+        RandomFlip = RandomFlip
+        RandomRotation = RandomRotation
+        RandomTranslation = RandomTranslation
+        RandomZoom = RandomZoom
+        RandomContrast = RandomContrast
+        RandomHeight = RandomHeight
+        RandomWidth = RandomWidth
+        Rescaling = Rescaling

@@ -44,6 +44,8 @@ class Loss:
             self.name = name
 
     def __call__(self, y_true, y_pred, sample_weight=None):
+        if not isinstance(y_true, torch.Tensor):
+            y_true = torch.as_tensor(y_true).to(y_pred.device)
         per = self.per_example(y_true, y_pred)
         if sample_weight is not None:
             per = per * torch.as_tensor(sample_weight, device=per.device, dtype=per.dtype)

@@ -6,8 +6,31 @@ from __future__ import annotations
 import torch
 
 
+def _tensorize(args):
+    """numpy / python arguments -> tensors on the device of the tensor arguments."""
+    dev = next((a.device for a in args if isinstance(a, torch.Tensor)), None)
+    out = []
+    for a in args:
+        if a is not None and not isinstance(a, torch.Tensor):
+            a = torch.as_tensor(a)
+            if dev is not None:
+                a = a.to(dev)
+        out.append(a)
+    return out
+
+
 class Metric:
     name = "metric"
+
+    def __init_subclass__(cls, **kw):
+        super().__init_subclass__(**kw)
+        fn = cls.__dict__.get("update_state")
+        if fn is not None and not getattr(fn, "_tensorized", False):
+            def update_state(self, *args, sample_weight=None, _fn=fn):
+                return _fn(self, *_tensorize(args), sample_weight=sample_weight)
+
+            update_state._tensorized = True
+            cls.update_state = update_state
 
     def __init__(self, name=None, dtype=None):
         if name:

@@ -110,6 +110,32 @@ class Model(Layer):
         self.built = True
 
     @property
+    def inputs(self):
+        if getattr(self, "_sym_in", None) is not None:
+            return [self._sym_in]
+        return list(self._graph[0]) if self._graph is not None else None
+
+    @property
+    def outputs(self):
+        if getattr(self, "_sym_out", None) is not None:
+            return [self._sym_out]
+        return list(self._graph[1]) if self._graph is not None else None
+
+    @property
+    def input(self):
+        ins = self.inputs
+        if not ins:
+            raise AttributeError("model has no symbolic input (not built on Input tensors)")
+        return ins[0] if len(ins) == 1 else ins
+
+    @property
+    def output(self):
+        outs = self.outputs
+        if not outs:
+            raise AttributeError("model has no symbolic output (not built on Input tensors)")
+        return outs[0] if len(outs) == 1 else outs
+
+    @property
     def layers(self):
         if self._graph is not None:
             return list(self._layer_list)
@@ -455,10 +481,15 @@ class Model(Layer):
                     a.master[sl.offset:sl.offset + sl.numel].copy_(sl.param.detach().reshape(-1).float())
 
     def save_weights(self, filepath, overwrite=True, save_format=None):
-        d = os.path.dirname(os.path.abspath(filepath))
-        os.makedirs(d, exist_ok=True)
+        from .saving import chief_only
+
         sd = {k: v.detach().cpu() for k, v in self.state_dict().items()}
-        torch.save(sd, filepath)
+
+        def write():
+            os.makedirs(os.path.dirname(os.path.abspath(filepath)), exist_ok=True)
+            torch.save(sd, filepath)
+
+        chief_only(write)
 
     def load_weights(self, filepath, by_name=False, skip_mismatch=False):
         sd = torch.load(filepath, map_location="cpu", weights_only=True)

@@ -49,6 +49,13 @@ class schedules:  # namespace parity: tf.keras.optimizers.schedules
             return self.lr0 * ((1 - self.alpha) * 0.5 * (1 + math.cos(math.pi * t)) + self.alpha)
 
 
+class _Scalar(float):
+    """A float that also answers ``.numpy()`` (``model.optimizer.lr.numpy()`` in TF scripts)."""
+
+    def numpy(self):
+        return float(self)
+
+
 class Optimizer:
     fused_cls = None
 
@@ -68,12 +75,45 @@ class Optimizer:
     def impl(self):
         return self._impl
 
+    def apply_gradients(self, grads_and_vars):
+        """Custom-training-loop update (``optimizer.apply_gradients(zip(grads, vars))``).
+
+        On first use the variables move into flat arenas and the fused HIP
+        optimizer is created with ``grad_scale = 1``: as under TF's
+        MirroredStrategy, per-replica gradients are SUMMED across replicas (the
+        loss is already divided by the global batch via
+        ``compute_average_loss``).  Under a multi-replica strategy the arena is
+        all-reduced in buckets (RCCL / gloo) before the fused update.
+        """
+        pairs = [(g, v) for g, v in grads_and_vars]
+        if self._impl is None:
+            self._impl = self.fused_cls([v for _, v in pairs], learning_rate=self.learning_rate, grad_scale=1.0,
+                                        clipnorm=self.clipnorm, **self.kw)
+            self._reducer = None
+            from ..parallel.strategy import get_strategy
+
+            if get_strategy().num_replicas_in_sync > 1:
+                from ..parallel.ddp import GradAllReducer
+
+                self._reducer = GradAllReducer(self._impl.arenas, overlap=False)
+        impl = self._impl
+        impl.zero_grad()
+        for g, v in pairs:
+            if g is None:
+                continue
+            v.grad.copy_(g.detach().to(v.grad.dtype).reshape(v.grad.shape))
+        red = getattr(self, "_reducer", None)
+        if red is not None:
+            red.finish()
+        impl.step()
+        return impl.iterations
+
     @property
     def lr(self):
         if self._impl is not None:
-            return self._impl.lr
+            return _Scalar(self._impl.lr)
         lr = self.learning_rate
-        return lr(0) if callable(lr) else lr
+        return _Scalar(lr(0) if callable(lr) else lr)
 
     @lr.setter
     def lr(self, v):

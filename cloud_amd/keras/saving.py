@@ -22,7 +22,23 @@ import torch
 FORMAT = "cloud_amd.keras/1"
 
 
+def chief_only(write):
+    """Run ``write()`` on the chief (rank 0) only, then barrier so every replica can
+    read what was written (all replicas hold identical weights under DP)."""
+    import torch.distributed as dist
+
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    if not multi or dist.get_rank() == 0:
+        write()
+    if multi:
+        dist.barrier()
+
+
 def save_model(model, path, include_optimizer=True):
+    chief_only(lambda: _save_model(model, path, include_optimizer))
+
+
+def _save_model(model, path, include_optimizer=True):
     os.makedirs(path, exist_ok=True)
     meta = {"format": FORMAT, "class_name": type(model).__name__, "name": model.name}
     from .models import Sequential

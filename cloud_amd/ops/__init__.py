@@ -10,3 +10,4 @@ from .conv import conv2d_nhwc  # noqa: F401
 from .gemm import linear  # noqa: F401
 from .losses import softmax_cross_entropy  # noqa: F401
 from .pooling import global_avg_pool_nhwc, max_pool2d_nhwc  # noqa: F401
+from .dropout import dropout  # noqa: F401

@@ -130,3 +130,135 @@ def bn_bwd(dy, y, x, gamma, stats, relu, dgamma=None, dbeta=None, want_dres=Fals
                _ext.ptr(dres), _ext.ptr(dgamma), _ext.ptr(dbeta), coef.data_ptr(), ws.data_ptr(),
                int(relu) | (2 if accumulate else 0), _st(dev))
     return dx, dres
+
+
+# ------------------------------------------------------- dense / transformer
+ACT = {None: 0, "none": 0, "linear": 0, "gelu": 1, "relu": 2, "tanh": 3, "gelu_tanh": 4}
+
+
+def gemm(a, w, bias=None, act=None, preact=None, out=None, beta=0.0, layout=NT, dact_src=None, stats=None):
+    """Fused dense GEMM.  NT: out[M,N] = act(a[M,K] @ w[N,K]^T + bias); NN: a[M,K] @ w[K,N].
+    ``preact`` receives the pre-activation; ``dact_src`` switches to the backward
+    form out = (a @ w) * act'(dact_src).  Row strides of ``a`` are honoured."""
+    ext = _ext.load(required=True)
+    M, K = a.shape
+    N = w.shape[0] if layout == NT else w.shape[1]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    aux = preact if preact is not None else dact_src
+    ld_aux = aux.stride(0) if aux is not None else 0
+    ext.gemm_ex(layout, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0), M, N, K,
+                _ext.ptr(stats), float(beta), _ext.ptr(bias), ACT[act], _ext.ptr(preact), _ext.ptr(dact_src), ld_aux,
+                _st(a.device))
+    return out
+
+
+def wgrad_into(dy, x, out, beta=1.0):
+    """out[N_out, K_in] (+)= dy[M, N_out]^T @ x[M, K_in] (split-K over M), bf16 or fp32 out."""
+    ext = _ext.load(required=True)
+    M, n_out = dy.shape
+    k_in = x.shape[1]
+    # dense layers: K = tokens is moderate, so fewer/larger K slices (less slab traffic)
+    splits = ext.gemm_splitk_effective(M, wgrad_splits(n_out, k_in, M, target_blocks=512, min_k=1024))
+    ws = torch.empty(splits * n_out * k_in, dtype=torch.float32, device=dy.device)
+    ext.gemm_splitk(TN, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
+                    int(out.dtype == torch.bfloat16), float(beta), n_out, k_in, M, splits, ws.data_ptr(),
+                    _st(dy.device))
+    return out
+
+
+def colsum_into(x, out, accumulate=True):
+    """out[N] (+)= sum over rows of bf16 x[M, N] (bias gradient)."""
+    ext = _ext.load(required=True)
+    M, N = x.shape
+    ws = torch.empty(ext.colsum_workspace_floats(M, N), dtype=torch.float32, device=x.device)
+    ext.colsum(x.data_ptr(), M, N, x.stride(0), out.data_ptr(), int(accumulate), ws.data_ptr(), _st(x.device))
+    return out
+
+
+def ln_fwd(x, gamma, beta, eps, residual=None, p_in=0.0, seed_in=0, p_out=0.0, seed_out=0, keep_h=True):
+    """y = drop_out(LN(residual + drop_in(x))).  Returns (y, h, mean, rstd); h is the
+    pre-norm sum (None when it equals x: no residual, no input dropout, or keep_h=False)."""
+    ext = _ext.load(required=True)
+    C = x.shape[-1]
+    M = x.numel() // C
+    y = torch.empty_like(x)
+    need_h = keep_h and (residual is not None or p_in > 0)
+    h = torch.empty_like(x) if need_h else None
+    mean = torch.empty(M, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(M, dtype=torch.float32, device=x.device)
+    ext.ln_fwd(x.data_ptr(), _ext.ptr(residual), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), _ext.ptr(h),
+               mean.data_ptr(), rstd.data_ptr(), M, C, float(eps), float(p_in), int(seed_in), float(p_out),
+               int(seed_out), _st(x.device))
+    return y, h, mean, rstd
+
+
+def ln_bwd(dy, h, mean, rstd, gamma, dgamma=None, dbeta=None, p_in=0.0, seed_in=0, p_out=0.0, seed_out=0,
+           want_dx=False, accumulate=True):
+    """Returns (dh, dx): dh = grad wrt the pre-norm sum (also the residual grad); dx =
+    drop_in'(dh) when ``want_dx`` (else None)."""
+    ext = _ext.load(required=True)
+    C = dy.shape[-1]
+    M = dy.numel() // C
+    dh = torch.empty_like(dy)
+    dx = torch.empty_like(dy) if want_dx else None
+    ws = torch.empty(ext.ln_workspace_floats(M, C), dtype=torch.float32, device=dy.device)
+    ext.ln_bwd(dy.data_ptr(), h.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(), dh.data_ptr(),
+               _ext.ptr(dx), _ext.ptr(dgamma), _ext.ptr(dbeta), int(accumulate), ws.data_ptr(), M, C, float(p_in),
+               int(seed_in), float(p_out), int(seed_out), _st(dy.device))
+    return dh, dx
+
+
+def embed_sum(ids, tts, word, pos, type_, seq_len, pos_offset=0):
+    ext = _ext.load(required=True)
+    M = ids.numel()
+    C = word.shape[1]
+    h = torch.empty((M, C), dtype=torch.bfloat16, device=word.device)
+    ext.embed_sum(ids.data_ptr(), _ext.ptr(tts), word.data_ptr(), pos.data_ptr(), _ext.ptr(type_), h.data_ptr(), M,
+                  seq_len, C, pos_offset, _st(word.device))
+    return h
+
+
+def embed_bwd(dh, ids, tts, dword, dpos, dtype_, seq_len, n_types, pos_offset=0, pad_id=-1):
+    """Scatter-add (fp32 atomics) into dword, skipping ``pad_id`` rows; dpos/dtype_ reduced."""
+    ext = _ext.load(required=True)
+    M, C = dh.shape
+    ext.embed_bwd(dh.data_ptr(), ids.data_ptr(), _ext.ptr(tts), _ext.ptr(dword), _ext.ptr(dpos), _ext.ptr(dtype_), M,
+                  seq_len, C, n_types, pos_offset, int(pad_id), _st(dh.device))
+
+
+def attn_fwd(qkv, B, S, H, key_len=None, p_drop=0.0, seed=0, scale=None):
+    """qkv [B*S, 3*H*64] -> (ctx [B*S, H*64], lse [B, H, S])."""
+    ext = _ext.load(required=True)
+    C = H * 64
+    ctx = torch.empty((B * S, C), dtype=torch.bfloat16, device=qkv.device)
+    lse = torch.empty((B, H, S), dtype=torch.float32, device=qkv.device)
+    scale = 1.0 / 8.0 if scale is None else scale
+    ext.attn_fwd(qkv.data_ptr(), ctx.data_ptr(), lse.data_ptr(), _ext.ptr(key_len), B, S, H, float(scale),
+                 float(p_drop), int(seed), _st(qkv.device))
+    return ctx, lse
+
+
+def attn_bwd(qkv, ctx, dctx, lse, B, S, H, key_len=None, p_drop=0.0, seed=0, scale=None):
+    ext = _ext.load(required=True)
+    dqkv = torch.empty_like(qkv)
+    dvec = torch.empty_like(lse)
+    scale = 1.0 / 8.0 if scale is None else scale
+    ext.attn_bwd(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(), dvec.data_ptr(), dqkv.data_ptr(),
+                 _ext.ptr(key_len), B, S, H, float(scale), float(p_drop), int(seed), _st(qkv.device))
+    return dqkv
+
+
+def dropout(x, p, seed, out=None):
+    ext = _ext.load(required=True)
+    y = out if out is not None else torch.empty_like(x)
+    ext.dropout(x.data_ptr(), y.data_ptr(), x.numel(), float(p), int(seed), _st(x.device))
+    return y
+
+
+def dropout_mask(n, p, seed, base=0, device="cuda"):
+    """The keep-mask (uint8) the kernels use for elements base..base+n-1 (tests / references)."""
+    ext = _ext.load(required=True)
+    m = torch.empty(n, dtype=torch.uint8, device=device)
+    ext.dropout_mask(m.data_ptr(), n, base, float(p), int(seed), _st(m.device))
+    return m

@@ -43,6 +43,24 @@ int ca_splitk_reduce(const float*, int, long, void*, int, float, hipStream_t);
 int ca_gemm_splitk(int, const bf16_t*, long, const bf16_t*, long, void*, int, float, int, int, int, int, float*,
                    hipStream_t);
 int ca_gemm_splitk_effective(int, int);
+int ca_gemm_ex(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float*, float, const float*,
+               int, bf16_t*, const bf16_t*, long, hipStream_t);
+long ca_ln_workspace_floats(long, int);
+int ca_ln_fwd(const bf16_t*, const bf16_t*, const float*, const float*, bf16_t*, bf16_t*, float*, float*, long, int,
+              float, float, uint64_t, float, uint64_t, hipStream_t);
+int ca_ln_bwd(const bf16_t*, const bf16_t*, const float*, const float*, const float*, bf16_t*, bf16_t*, float*, float*,
+              int, float*, long, int, float, uint64_t, float, uint64_t, hipStream_t);
+long ca_colsum_workspace_floats(long, int);
+int ca_colsum(const bf16_t*, long, int, long, float*, int, float*, hipStream_t);
+int ca_embed_sum(const int32_t*, const int32_t*, const float*, const float*, const float*, bf16_t*, long, int, int, int,
+                 hipStream_t);
+int ca_embed_bwd(const bf16_t*, const int32_t*, const int32_t*, float*, float*, float*, long, int, int, int, int, int,
+                 hipStream_t);
+int ca_dropout(const bf16_t*, bf16_t*, long, float, uint64_t, hipStream_t);
+int ca_dropout_mask(uint8_t*, long, long, float, uint64_t, hipStream_t);
+int ca_attn_fwd(const bf16_t*, bf16_t*, float*, const int*, int, int, int, float, float, uint64_t, hipStream_t);
+int ca_attn_bwd(const bf16_t*, const bf16_t*, const bf16_t*, const float*, float*, bf16_t*, const int*, int, int, int,
+                float, float, uint64_t, hipStream_t);
 }
 
 #define P(T, x) reinterpret_cast<T>(static_cast<uintptr_t>(x))
@@ -154,5 +172,54 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_splitk_effective", [](int K, int splits) { return ca_gemm_splitk_effective(K, splits); });
   m.def("gap_bwd", [](u64 dy, int dybf, u64 dx, int N, int HW, int C, u64 s) {
     check(ca_gap_bwd(P(const void*, dy), dybf, P(bf16_t*, dx), N, HW, C, S(s)), "gap_bwd");
+  });
+  m.def("gemm_ex", [](int layout, u64 A, long lda, u64 B, long ldb, u64 C, long ldc, int M, int N, int K, u64 stats,
+                      float beta, u64 bias, int act, u64 preact, u64 dact_src, long ld_aux, u64 s) {
+    check(ca_gemm_ex(layout, P(const bf16_t*, A), lda, P(const bf16_t*, B), ldb, P(bf16_t*, C), ldc, M, N, K,
+                     P(float*, stats), beta, P(const float*, bias), act, P(bf16_t*, preact), P(const bf16_t*, dact_src),
+                     ld_aux, S(s)), "gemm_ex");
+  });
+  m.def("ln_workspace_floats", [](long M, int C) { return ca_ln_workspace_floats(M, C); });
+  m.def("ln_fwd", [](u64 x, u64 res, u64 g, u64 b, u64 y, u64 h, u64 mu, u64 rs, long M, int C, float eps, float p_in,
+                     u64 seed_in, float p_out, u64 seed_out, u64 s) {
+    check(ca_ln_fwd(P(const bf16_t*, x), P(const bf16_t*, res), P(const float*, g), P(const float*, b), P(bf16_t*, y),
+                    P(bf16_t*, h), P(float*, mu), P(float*, rs), M, C, eps, p_in, seed_in, p_out, seed_out, S(s)),
+          "ln_fwd");
+  });
+  m.def("ln_bwd", [](u64 dy, u64 h, u64 mu, u64 rs, u64 g, u64 dh, u64 dx, u64 dg, u64 db, int acc, u64 ws, long M,
+                     int C, float p_in, u64 seed_in, float p_out, u64 seed_out, u64 s) {
+    check(ca_ln_bwd(P(const bf16_t*, dy), P(const bf16_t*, h), P(const float*, mu), P(const float*, rs),
+                    P(const float*, g), P(bf16_t*, dh), P(bf16_t*, dx), P(float*, dg), P(float*, db), acc,
+                    P(float*, ws), M, C, p_in, seed_in, p_out, seed_out, S(s)), "ln_bwd");
+  });
+  m.def("colsum_workspace_floats", [](long M, int N) { return ca_colsum_workspace_floats(M, N); });
+  m.def("colsum", [](u64 x, long M, int N, long ld, u64 out, int acc, u64 ws, u64 s) {
+    check(ca_colsum(P(const bf16_t*, x), M, N, ld, P(float*, out), acc, P(float*, ws), S(s)), "colsum");
+  });
+  m.def("embed_sum", [](u64 ids, u64 tts, u64 word, u64 pos, u64 type, u64 h, long M, int S_, int C, int po, u64 s) {
+    check(ca_embed_sum(P(const int32_t*, ids), P(const int32_t*, tts), P(const float*, word), P(const float*, pos),
+                       P(const float*, type), P(bf16_t*, h), M, S_, C, po, S(s)), "embed_sum");
+  });
+  m.def("embed_bwd", [](u64 dh, u64 ids, u64 tts, u64 dw, u64 dp, u64 dt, long M, int S_, int C, int T, int po,
+                        int pad_id, u64 s) {
+    check(ca_embed_bwd(P(const bf16_t*, dh), P(const int32_t*, ids), P(const int32_t*, tts), P(float*, dw),
+                       P(float*, dp), P(float*, dt), M, S_, C, T, po, pad_id, S(s)), "embed_bwd");
+  });
+  m.def("dropout", [](u64 x, u64 y, long n, float p, u64 seed, u64 s) {
+    check(ca_dropout(P(const bf16_t*, x), P(bf16_t*, y), n, p, seed, S(s)), "dropout");
+  });
+  m.def("dropout_mask", [](u64 m_, long n, long base, float p, u64 seed, u64 s) {
+    check(ca_dropout_mask(P(uint8_t*, m_), n, base, p, seed, S(s)), "dropout_mask");
+  });
+  m.def("attn_fwd", [](u64 qkv, u64 ctx, u64 lse, u64 klen, int B, int S_, int H, float scale, float p, u64 seed,
+                       u64 s) {
+    check(ca_attn_fwd(P(const bf16_t*, qkv), P(bf16_t*, ctx), P(float*, lse), P(const int*, klen), B, S_, H, scale, p,
+                      seed, S(s)), "attn_fwd");
+  });
+  m.def("attn_bwd", [](u64 qkv, u64 out, u64 dout, u64 lse, u64 dvec, u64 dqkv, u64 klen, int B, int S_, int H,
+                       float scale, float p, u64 seed, u64 s) {
+    check(ca_attn_bwd(P(const bf16_t*, qkv), P(const bf16_t*, out), P(const bf16_t*, dout), P(const float*, lse),
+                      P(float*, dvec), P(bf16_t*, dqkv), P(const int*, klen), B, S_, H, scale, p, seed, S(s)),
+          "attn_bwd");
   });
 }

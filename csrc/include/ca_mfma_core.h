@@ -66,7 +66,48 @@ struct CoreParams {
   int Nb, H, W, Cin, OH, OW, Cout, KH, KW, sh, sw, ph, pw;
   FastDiv div_ow, div_oh, div_w, div_h, div_cin, div_cout, div_kw;
   int cin_tile, cout_tile;  // Cin % BK == 0 / Cout % BK == 0: a K tile never straddles two taps
+  // dense-layer epilogue (bf16 path): C = act(acc + bias) with the pre-activation
+  // optionally kept (preact), or, in the backward, C = acc * act'(dact_src).
+  const float* bias;      // [N] fp32 or null
+  int act;                // ACT_* below
+  bf16_t* preact;         // [M][ld_aux] or null
+  const bf16_t* dact_src; // [M][ld_aux] or null (backward: multiply by act'(src))
+  long ld_aux;
 };
+
+enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_GELU_TANH = 4 };
+
+__device__ __forceinline__ float act_fwd(int act, float x) {
+  switch (act) {
+    case ACT_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case ACT_RELU: return x > 0.f ? x : 0.f;
+    case ACT_TANH: return tanhf(x);
+    case ACT_GELU_TANH: {
+      const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+      return 0.5f * x * (1.f + tanhf(u));
+    }
+  }
+  return x;
+}
+
+// d act(x) / dx
+__device__ __forceinline__ float act_grad(int act, float x) {
+  switch (act) {
+    case ACT_GELU:
+      return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+    case ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    case ACT_TANH: {
+      const float t = tanhf(x);
+      return 1.f - t * t;
+    }
+    case ACT_GELU_TANH: {
+      const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+      const float t = tanhf(u);
+      return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.7978845608028654f * (1.f + 3.f * 0.044715f * x * x);
+    }
+  }
+  return 1.f;
+}
 
 template <int R, bool KC>
 struct TileGeom {
@@ -290,6 +331,17 @@ __device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
     return;
   } else {
     short* Cs = smem;
+    if (P.bias) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int gn = n0 + cbase + j * 16;
+        const float bv = gn < P.N ? P.bias[gn] : 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += bv;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -298,6 +350,7 @@ __device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
         for (int r = 0; r < 4; ++r)
           Cs[(rbase + i * 16 + r) * EPI_LD + cbase + j * 16] = (short)f2bf(acc[i][j][r]);
     __syncthreads();
+    const bool fx = P.act != ACT_NONE || P.dact_src != nullptr || P.preact != nullptr;
     bf16_t* Cg = reinterpret_cast<bf16_t*>(P.C);
     constexpr int CH = BM * BN / 8;
     for (int c = tid; c < CH; c += NT) {
@@ -306,13 +359,25 @@ __device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
       if (gm < P.M && gn < P.N) {
         s8v v = *reinterpret_cast<const s8v*>(Cs + row * EPI_LD + col);
         bf16_t* dst = Cg + (long)gm * P.ldc + gn;
+        if (fx) {
+          if (P.preact) *reinterpret_cast<s8v*>(P.preact + (long)gm * P.ld_aux + gn) = v;
+          if (P.dact_src) {
+            const s8v src = *reinterpret_cast<const s8v*>(P.dact_src + (long)gm * P.ld_aux + gn);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              v[j] = (short)f2bf(bf2f((bf16_t)v[j]) * act_grad(P.act, bf2f((bf16_t)src[j])));
+          } else if (P.act != ACT_NONE) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(act_fwd(P.act, bf2f((bf16_t)v[j])));
+          }
+        }
         if (P.beta != 0.f) {
           s8v o = *reinterpret_cast<const s8v*>(dst);
 #pragma unroll
           for (int j = 0; j < 8; ++j)
             v[j] = (short)f2bf(bf2f((bf16_t)v[j]) + P.beta * bf2f((bf16_t)o[j]));
-          if (P.stats) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
         }
+        if (P.stats && (fx || P.beta != 0.f)) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
         *reinterpret_cast<s8v*>(dst) = v;
       }
     }

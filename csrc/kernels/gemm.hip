@@ -119,6 +119,24 @@ int ca_gemm_bf16(int layout, const bf16_t* A, long lda, const bf16_t* B, long ld
   return dispatch<EPI_BF16>(layout, p, 1, s);
 }
 
+// Dense-layer GEMM with the fused epilogue: C = act(A*B + bias) (+ beta*C),
+// pre-activation kept in `preact` when given; backward form: C = (A*B) * act'(dact_src).
+int ca_gemm_ex(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N,
+               int K, float* stats, float beta, const float* bias, int act, bf16_t* preact, const bf16_t* dact_src,
+               long ld_aux, hipStream_t s) {
+  if (N % 8 != 0 || K % 8 != 0 || (layout == 2 && M % 8 != 0)) return -1;
+  if ((preact || dact_src) && ld_aux % 8 != 0) return -1;
+  CoreParams p = base_params(A, lda, B, ldb, C, ldc, M, N, K);
+  p.stats = stats;
+  p.beta = beta;
+  p.bias = bias;
+  p.act = act;
+  p.preact = preact;
+  p.dact_src = dact_src;
+  p.ld_aux = ld_aux;
+  return dispatch<EPI_BF16>(layout, p, 1, s);
+}
+
 int ca_gemm_splitk_effective(int K, int splits) {
   int kps = (K / splits + BK - 1) / BK * BK;
   if (kps < BK) kps = BK;

@@ -1,0 +1,462 @@
+// Row-wise kernels of the transformer path (K13 / K8 / K14 in SURVEY.md 2.7):
+//
+//  * LayerNorm forward with the residual add and BOTH dropouts fused:
+//        h = res + drop_in(x);   y = drop_out(LN(h) * gamma + beta)
+//    one wave per row (C <= 2048, 4 bf16 per lane per step), fp32 statistics;
+//  * LayerNorm backward: dh (= the residual-branch gradient) and, when the input
+//    was dropped, dx = drop_in'(dh), plus per-block dgamma/dbeta partials
+//    reduced deterministically and ACCUMULATED into the (arena) fp32 grads;
+//  * column sums of a bf16 matrix (bias gradients) into fp32, accumulated;
+//  * token + position + segment embedding gather/sum and its scatter-add
+//    backward (fp32 tables and grads, hardware fp32 atomics);
+//  * standalone dropout fwd/bwd and a mask materialiser for tests.
+// Dropout masks come from the stateless hash of ca_rng.h (never stored).
+#include "ca_common.h"
+#include "ca_rng.h"
+
+namespace {
+
+typedef unsigned short us4v __attribute__((ext_vector_type(4)));
+
+constexpr int LN_BLK = 256;  // 4 rows (waves) per block
+
+__device__ __forceinline__ void load4(const bf16_t* p, float* v) {
+  us4v u = *reinterpret_cast<const us4v*>(p);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = bf2f(u[j]);
+}
+__device__ __forceinline__ void store4(bf16_t* p, const float* v) {
+  us4v u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) u[j] = f2bf(v[j]);
+  *reinterpret_cast<us4v*>(p) = u;
+}
+
+template <int NV>
+__global__ void __launch_bounds__(LN_BLK) ln_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                        bf16_t* __restrict__ y, bf16_t* __restrict__ h_out,
+                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                        long M, int C, float eps, DropCfg din, DropCfg dout) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * (LN_BLK / 64) + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int C4 = C >> 2;
+  const long base = row * C;
+  float v[NV][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c4 = lane + 64 * i;
+    if (c4 < C4) {
+      load4(x + base + 4 * c4, v[i]);
+      if (din.on) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[i][j] *= drop_mul(din, base + 4 * c4 + j);
+      }
+      if (res) {
+        float r[4];
+        load4(res + base + 4 * c4, r);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[i][j] += r[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s += v[i][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[i][j] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    if (lane + 64 * i < C4) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[i][j] - mean;
+        q += d * d;
+      }
+    }
+  const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c4 = lane + 64 * i;
+    if (c4 >= C4) continue;
+    if (h_out) store4(h_out + base + 4 * c4, v[i]);
+    const f4 g = *reinterpret_cast<const f4*>(gamma + 4 * c4);
+    const f4 b = *reinterpret_cast<const f4*>(beta + 4 * c4);
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = (v[i][j] - mean) * rstd * g[j] + b[j];
+      if (dout.on) o[j] *= drop_mul(dout, base + 4 * c4 + j);
+    }
+    store4(y + base + 4 * c4, o);
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// grid-stride over rows; per-block [2][C] partials (dgamma, dbeta) in `part`.
+template <int NV>
+__global__ void __launch_bounds__(LN_BLK) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
+                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                        const float* __restrict__ gamma, bf16_t* __restrict__ dh,
+                                                        bf16_t* __restrict__ dx, float* __restrict__ part, long M,
+                                                        int C, DropCfg din, DropCfg dout) {
+  extern __shared__ float red[];  // [4 waves][2][C]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int C4 = C >> 2;
+  float ag[NV][4], ab[NV][4], g[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c4 = lane + 64 * i;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ag[i][j] = ab[i][j] = 0.f;
+      g[i][j] = c4 < C4 ? gamma[4 * c4 + j] : 0.f;
+    }
+  }
+  const float invC = 1.f / (float)C;
+  for (long row = (long)blockIdx.x * 4 + wave; row < M; row += (long)gridDim.x * 4) {
+    const long base = row * C;
+    const float mu = mean[row], rs = rstd[row];
+    float d[NV][4], xh[NV][4];
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < C4) {
+        load4(dy + base + 4 * c4, d[i]);
+        load4(h + base + 4 * c4, xh[i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (dout.on) d[i][j] *= drop_mul(dout, base + 4 * c4 + j);
+          xh[i][j] = (xh[i][j] - mu) * rs;
+          ag[i][j] += d[i][j] * xh[i][j];
+          ab[i][j] += d[i][j];
+          const float gd = g[i][j] * d[i][j];
+          sa += gd;
+          sb += gd * xh[i][j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[i][j] = xh[i][j] = 0.f;
+      }
+    }
+    const float a = wave_sum(sa) * invC, b = wave_sum(sb) * invC;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 >= C4) continue;
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] * d[i][j] - a - xh[i][j] * b);
+      store4(dh + base + 4 * c4, o);
+      if (dx) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] *= din.on ? drop_mul(din, base + 4 * c4 + j) : 1.f;
+        store4(dx + base + 4 * c4, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c4 = lane + 64 * i;
+    if (c4 < C4) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        red[(wave * 2 + 0) * C + 4 * c4 + j] = ag[i][j];
+        red[(wave * 2 + 1) * C + 4 * c4 + j] = ab[i][j];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * C; c += LN_BLK) {
+    const int k = c / C, col = c - k * C;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) t += red[(w * 2 + k) * C + col];
+    part[(long)blockIdx.x * 2 * C + c] = t;
+  }
+}
+
+// out[c] (+)= sum_p part[p*stride + c], for c < N; out2 (optional) gets columns N..2N-1.
+// Block = 16 columns x 16 part-lanes (enough waves in flight to hide the
+// partial-slab reads; deterministic fixed-order tree).
+__global__ void __launch_bounds__(256) col_finalize_kernel(const float* __restrict__ part, int nparts, long stride,
+                                                           int N, float* __restrict__ out, float* __restrict__ out2,
+                                                           int accumulate) {
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  const int total = out2 ? 2 * N : N;
+  float t = 0.f;
+  if (c < total) {
+#pragma unroll 4
+    for (int p = pl; p < nparts; p += 16) t += part[(long)p * stride + c];
+  }
+  red[pl][cl] = t;
+  __syncthreads();
+  if (pl != 0 || c >= total) return;
+  t = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t += red[k][cl];
+  float* dst = c < N ? out : out2;
+  if (!dst) return;
+  float* o = dst + (c < N ? c : c - N);
+  *o = accumulate ? *o + t : t;
+}
+
+// per-block column partial sums of bf16 X[M][N] (N % 8 == 0): block = 32 col-groups(8 cols) x 8 row lanes
+__global__ void __launch_bounds__(256) colsum_part_kernel(const bf16_t* __restrict__ x, long M, int N, long ld,
+                                                          float* __restrict__ part) {
+  __shared__ float red[8][256];
+  const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c0 = (blockIdx.x * 32 + cg) * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < N) {
+    for (long r = (long)blockIdx.y * 8 + rl; r < M; r += (long)gridDim.y * 8) {
+      us8 u = *reinterpret_cast<const us8*>(x + r * ld + c0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += bf2f(u[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][cg * 8 + j] = acc[j];
+  __syncthreads();
+  const int c = threadIdx.x;  // 256 columns of this block
+  const int gc = blockIdx.x * 256 + c;
+  if (gc < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][c];
+    part[(long)blockIdx.y * N + gc] = t;
+  }
+}
+
+// h[m] = word[id[m]] + pos[m % S] + type[tt[m]]   (fp32 tables, bf16 out), one wave per row.
+__global__ void __launch_bounds__(256) embed_sum_kernel(const int32_t* __restrict__ ids, const int32_t* __restrict__ tts,
+                                                        const float* __restrict__ word, const float* __restrict__ pos,
+                                                        const float* __restrict__ type, bf16_t* __restrict__ h,
+                                                        long M, int S, int C, int pos_offset) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* w = word + (long)ids[row] * C;
+  const float* p = pos + (long)(row % S + pos_offset) * C;
+  const float* t = type ? type + (long)(tts ? tts[row] : 0) * C : nullptr;
+  for (int c4 = lane; c4 < C / 4; c4 += 64) {
+    f4 a = *reinterpret_cast<const f4*>(w + 4 * c4) + *reinterpret_cast<const f4*>(p + 4 * c4);
+    if (t) a += *reinterpret_cast<const f4*>(t + 4 * c4);
+    float o[4] = {a[0], a[1], a[2], a[3]};
+    store4(h + row * C + 4 * c4, o);
+  }
+}
+
+// scatter-add backward of embed_sum.  Token rows: fp32 atomics, skipping the
+// padding id (its row gets no gradient, as nn.Embedding(padding_idx) / BERT);
+// the segment table (<= 2 rows in BERT) is pre-reduced per wave first.
+__global__ void __launch_bounds__(256) embed_bwd_kernel(const bf16_t* __restrict__ dh, const int32_t* __restrict__ ids,
+                                                        const int32_t* __restrict__ tts, float* __restrict__ dword,
+                                                        float* __restrict__ dtype, long M, int C, int T, int pad_id) {
+  const int lane = threadIdx.x & 63;
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long nw = (long)gridDim.x * 4;
+  for (int c4 = lane; c4 < C / 4; c4 += 64) {
+    float t0[4] = {0.f, 0.f, 0.f, 0.f}, t1[4] = {0.f, 0.f, 0.f, 0.f};
+    for (long row = wave; row < M; row += nw) {
+      float g[4];
+      load4(dh + row * C + 4 * c4, g);
+      const int id = ids[row];
+      const int tt = tts ? tts[row] : 0;
+      if (dword && id != pad_id) {
+        float* w = dword + (long)id * C + 4 * c4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) atomicAdd(w + j, g[j]);
+      }
+      if (dtype) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (T <= 2) {
+            if (tt == 0) t0[j] += g[j];
+            else t1[j] += g[j];
+          } else {
+            atomicAdd(dtype + (long)tt * C + 4 * c4 + j, g[j]);
+          }
+        }
+      }
+    }
+    if (dtype && T <= 2) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        atomicAdd(dtype + 4 * c4 + j, t0[j]);
+        if (T == 2) atomicAdd(dtype + C + 4 * c4 + j, t1[j]);
+      }
+    }
+  }
+}
+
+// dpos[s + off] += sum_b dh[b*S + s]  (deterministic, no atomics)
+__global__ void __launch_bounds__(256) embed_pos_bwd_kernel(const bf16_t* __restrict__ dh, float* __restrict__ dpos,
+                                                            long M, int S, int C, int pos_offset) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;  // over S * C/4
+  const int C4 = C / 4;
+  if (i >= (long)S * C4) return;
+  const int s = (int)(i / C4), c4 = (int)(i - (long)s * C4);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (long row = s; row < M; row += S) {
+    float g[4];
+    load4(dh + row * C + 4 * c4, g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] += g[j];
+  }
+  f4* o = reinterpret_cast<f4*>(dpos + (long)(s + pos_offset) * C + 4 * c4);
+  f4 v = *o;
+  v += f4{acc[0], acc[1], acc[2], acc[3]};
+  *o = v;
+}
+
+// y = drop(x) (bf16), 8 elements per thread, grid-stride; also used for the backward (same mask).
+__global__ void __launch_bounds__(256) dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, long n,
+                                                      DropCfg d) {
+  const long n8 = n / 8;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    us8 u = *reinterpret_cast<const us8*>(x + 8 * i);
+    us8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(u[j]) * drop_mul(d, 8 * i + j));
+    *reinterpret_cast<us8*>(y + 8 * i) = o;
+  }
+}
+
+__global__ void dropout_mask_kernel(uint8_t* __restrict__ m, long n, long base, DropCfg d) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    m[i] = drop_mul(d, base + i) != 0.f;
+}
+
+template <int NV>
+int ln_fwd_launch(const bf16_t* x, const bf16_t* res, const float* g, const float* b, bf16_t* y, bf16_t* h, float* mu,
+                  float* rs, long M, int C, float eps, DropCfg din, DropCfg dout, hipStream_t s) {
+  ln_fwd_kernel<NV><<<ca_cdiv(M, 4), LN_BLK, 0, s>>>(x, res, g, b, y, h, mu, rs, M, C, eps, din, dout);
+  return 0;
+}
+
+template <int NV>
+int ln_bwd_launch(const bf16_t* dy, const bf16_t* h, const float* mu, const float* rs, const float* g, bf16_t* dh,
+                  bf16_t* dx, float* part, int nblk, long M, int C, DropCfg din, DropCfg dout, hipStream_t s) {
+  ln_bwd_kernel<NV><<<nblk, LN_BLK, 8 * C * sizeof(float), s>>>(dy, h, mu, rs, g, dh, dx, part, M, C, din, dout);
+  return 0;
+}
+
+int ln_nblk(long M) {
+  long b = (M + 3) / 4;
+  return (int)(b < 512 ? b : 512);
+}
+
+}  // namespace
+
+extern "C" {
+
+long ca_ln_workspace_floats(long M, int C) { return (long)ln_nblk(M) * 2 * C; }
+
+// y = drop_out(LN(res + drop_in(x))); h_out (optional) keeps the pre-norm sum for the backward.
+int ca_ln_fwd(const bf16_t* x, const bf16_t* res, const float* gamma, const float* beta, bf16_t* y, bf16_t* h_out,
+              float* mean, float* rstd, long M, int C, float eps, float p_in, uint64_t seed_in, float p_out,
+              uint64_t seed_out, hipStream_t s) {
+  if (C % 4 != 0 || C > 2048) return -1;
+  const DropCfg din = make_drop(p_in, seed_in), dout = make_drop(p_out, seed_out);
+  const int nv = (C / 4 + 63) / 64;
+  int rc;
+  switch (nv) {
+    case 1: rc = ln_fwd_launch<1>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, s); break;
+    case 2: rc = ln_fwd_launch<2>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, s); break;
+    case 3: rc = ln_fwd_launch<3>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, s); break;
+    case 4: rc = ln_fwd_launch<4>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, s); break;
+    default: rc = ln_fwd_launch<8>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, s); break;
+  }
+  if (rc) return rc;
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+// dh = LN'(drop_out'(dy)); dx = drop_in'(dh) when dx != null; dgamma/dbeta (+)= column sums.
+int ca_ln_bwd(const bf16_t* dy, const bf16_t* h, const float* mean, const float* rstd, const float* gamma, bf16_t* dh,
+              bf16_t* dx, float* dgamma, float* dbeta, int accumulate, float* ws, long M, int C, float p_in,
+              uint64_t seed_in, float p_out, uint64_t seed_out, hipStream_t s) {
+  if (C % 4 != 0 || C > 2048) return -1;
+  const DropCfg din = make_drop(p_in, seed_in), dout = make_drop(p_out, seed_out);
+  const int nv = (C / 4 + 63) / 64;
+  const int nblk = ln_nblk(M);
+  switch (nv) {
+    case 1: ln_bwd_launch<1>(dy, h, mean, rstd, gamma, dh, dx, ws, nblk, M, C, din, dout, s); break;
+    case 2: ln_bwd_launch<2>(dy, h, mean, rstd, gamma, dh, dx, ws, nblk, M, C, din, dout, s); break;
+    case 3: ln_bwd_launch<3>(dy, h, mean, rstd, gamma, dh, dx, ws, nblk, M, C, din, dout, s); break;
+    case 4: ln_bwd_launch<4>(dy, h, mean, rstd, gamma, dh, dx, ws, nblk, M, C, din, dout, s); break;
+    default: ln_bwd_launch<8>(dy, h, mean, rstd, gamma, dh, dx, ws, nblk, M, C, din, dout, s); break;
+  }
+  CA_LAUNCH_CHECK();
+  if (dgamma || dbeta) {
+    col_finalize_kernel<<<ca_cdiv(2 * C, 16), 256, 0, s>>>(ws, nblk, 2L * C, C, dgamma, dbeta, accumulate);
+    CA_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+long ca_colsum_workspace_floats(long M, int N) { return 256L * N; }
+
+// out[n] (+)= sum_m x[m*ld + n]  (bias gradient), N % 8 == 0; ws >= 64*N floats.
+int ca_colsum(const bf16_t* x, long M, int N, long ld, float* out, int accumulate, float* ws, hipStream_t s) {
+  if (N % 8 != 0) return -1;
+  int ry = (int)((M + 63) / 64);
+  if (ry > 256) ry = 256;
+  if (ry < 1) ry = 1;
+  dim3 grid(ca_cdiv(N, 256), ry);
+  colsum_part_kernel<<<grid, 256, 0, s>>>(x, M, N, ld, ws);
+  CA_LAUNCH_CHECK();
+  col_finalize_kernel<<<ca_cdiv(N, 16), 256, 0, s>>>(ws, ry, N, N, out, nullptr, accumulate);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+int ca_embed_sum(const int32_t* ids, const int32_t* tts, const float* word, const float* pos, const float* type,
+                 bf16_t* h, long M, int S, int C, int pos_offset, hipStream_t s) {
+  if (C % 4 != 0) return -1;
+  embed_sum_kernel<<<ca_cdiv(M, 4), 256, 0, s>>>(ids, tts, word, pos, type, h, M, S, C, pos_offset);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+int ca_embed_bwd(const bf16_t* dh, const int32_t* ids, const int32_t* tts, float* dword, float* dpos, float* dtype,
+                 long M, int S, int C, int T, int pos_offset, int pad_id, hipStream_t s) {
+  if (C % 4 != 0) return -1;
+  if (dword || dtype) {
+    int grid = ca_cdiv(M, 4 * 16);  // each wave walks ~16 rows (segment pre-reduction)
+    if (grid < 1) grid = 1;
+    embed_bwd_kernel<<<grid, 256, 0, s>>>(dh, ids, tts, dword, dtype, M, C, T, pad_id);
+    CA_LAUNCH_CHECK();
+  }
+  if (dpos) {
+    embed_pos_bwd_kernel<<<ca_cdiv((long)S * (C / 4), 256), 256, 0, s>>>(dh, dpos, M, S, C, pos_offset);
+    CA_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+int ca_dropout(const bf16_t* x, bf16_t* y, long n, float p, uint64_t seed, hipStream_t s) {
+  if (n % 8 != 0) return -1;
+  dropout_kernel<<<ca_stream_grid(n / 8, 256), 256, 0, s>>>(x, y, n, make_drop(p, seed));
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+int ca_dropout_mask(uint8_t* m, long n, long base, float p, uint64_t seed, hipStream_t s) {
+  dropout_mask_kernel<<<ca_stream_grid(n, 256), 256, 0, s>>>(m, n, base, make_drop(p, seed));
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"
