@@ -4,7 +4,9 @@
 Metric (BASELINE.json): images/sec of ResNet-50 training at 1/2/4/8 MI355X,
 one process per GPU, data parallel over RCCL/xGMI, bf16 compute with fp32
 master weights, SGD(momentum 0.9) -- plus ``first_step_latency_s`` (process
-start -> end of first optimizer step).
+start -> end of first optimizer step) and, with ``--via-run 1``, the launch
+through ``cloud_amd.run()`` and ``run_to_first_step_s`` (run() call -> end of
+the first step on every rank, max over ranks).
 
     python bench.py --gpus 1 --steps 20 --warmup 10
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
@@ -40,11 +42,32 @@ def parse():
                     help="capture the training step in a HIP graph (1-GPU only unless forced)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--via-run", type=int, default=0,
+                    help="launch through cloud_amd.run() (stage -> spawn one rank per GPU) and report "
+                         "run()->first-step latency; the ranks' JSON line is streamed from rank 0's log")
     return ap.parse_args()
+
+
+def via_run(args):
+    """The BASELINE metric's 'via run()' form: this process only stages and launches
+    (it never touches the GPU); every rank re-runs this file with remote() True."""
+    import cloud_amd as tfc
+
+    argv = [a for a in sys.argv[1:]]
+    if "--via-run" in argv:
+        i = argv.index("--via-run")
+        del argv[i:i + 2]
+    cfg = tfc.COMMON_MACHINE_CONFIGS["MI355X_%dX" % args.gpus]
+    os.chdir(os.path.dirname(os.path.abspath(__file__)))
+    job = tfc.run(entry_point="bench.py", distribution_strategy=None, chief_config=cfg, worker_count=0,
+                  entry_point_args=argv, stream_logs=True, exit=False, wait=True)
+    sys.exit(job.returncode or 0)
 
 
 def main():
     args = parse()
+    if args.via_run and not (os.environ.get("CLOUD_AMD_RUNNING_REMOTELY") or os.environ.get("TORCHELASTIC_RUN_ID")):
+        return via_run(args)
     import torch
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -87,6 +110,8 @@ def main():
     loss = train_step()
     torch.cuda.synchronize()
     first_step_latency = time.time() - T_START
+    run_t0 = os.environ.get("CLOUD_AMD_RUN_T0")
+    run_to_first = (time.time() - float(run_t0)) if run_t0 else None
 
     use_graph = bool(args.graph) and (world == 1 or os.environ.get("CLOUD_AMD_GRAPH_FORCE") == "1")
     step_fn = train_step
@@ -109,6 +134,8 @@ def main():
     ms = elapsed / args.steps * 1000.0
     ips = global_batch * args.steps / elapsed
     first_lat = dist_env.all_reduce_max(first_step_latency, device)
+    if run_to_first is not None:
+        run_to_first = dist_env.all_reduce_max(run_to_first, device)
     final_loss = float(loss.detach().float().item()) if loss is not None else float("nan")
     try:
         from cloud_amd import monitoring
@@ -136,6 +163,8 @@ def main():
                        "image_size": S, "per_gpu_batch": B, "parallelism": f"dp{world}",
                        "optimizer": "sgd_momentum0.9_fused", "hip_graph": use_graph},
             "first_step_latency_s": round(first_lat, 3),
+            "run_to_first_step_s": round(run_to_first, 3) if run_to_first is not None else None,
+            "launched_via": "cloud_amd.run()" if run_t0 else "direct",
             "final_loss": round(final_loss, 4),
         }
         line = json.dumps(out)

@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""BASELINE.json config 4: CloudTuner HP search, 8 MNIST-CNN trials spread over
+the node's MI355X GPUs by the async trial scheduler (one tuner worker per GPU,
+all sharing one study through the local study service).
+
+    python bench/tuner_8trials.py                 # workers = visible GPUs (CPU workers if none)
+    python bench/tuner_8trials.py --workers 8
+
+Reports trials/hour and time-to-best (seconds from start until the trial that
+ends up best completed).  Synthetic MNIST (no network).  The CNN is the
+reference's ``mnist_example_using_fit.py`` model with tuned filters / dense
+width / learning rate.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def build_model(hp):
+    from cloud_amd import keras
+
+    model = keras.Sequential([
+        keras.layers.Conv2D(hp.Choice("filters", [16, 32, 64]), 3, activation="relu", input_shape=(28, 28, 1)),
+        keras.layers.MaxPooling2D(),
+        keras.layers.Flatten(),
+        keras.layers.Dense(hp.Int("units", 32, 128, step=32), activation="relu"),
+        keras.layers.Dense(10, activation="softmax"),
+    ])
+    model.compile(loss="sparse_categorical_crossentropy",
+                  optimizer=keras.optimizers.Adam(hp.Float("lr", 1e-4, 1e-2, sampling="log")),
+                  metrics=["accuracy"])
+    return model
+
+
+def worker(tuner_id, device):
+    """Scheduler target: one tuner process; trials come from the shared study."""
+    import numpy as np
+
+    from cloud_amd import keras
+    from cloud_amd.parallel import strategy as S
+    from cloud_amd.tuner import CloudTuner, HyperParameters
+
+    S.experimental_set_strategy(S.OneDeviceStrategy(device))
+    hps = HyperParameters()
+    hps.Choice("filters", [16, 32, 64])
+    hps.Int("units", 32, 128, step=32)
+    hps.Float("lr", 1e-4, 1e-2, sampling="log")
+    n = int(os.environ.get("BENCH_TRAIN", "8192"))
+    (x, y), (xt, yt) = keras.datasets.mnist.load_data(n_train=n, n_test=n // 8)
+    x = (x[..., None] / np.float32(255)).astype("float32")
+    xt = (xt[..., None] / np.float32(255)).astype("float32")
+    tuner = CloudTuner(build_model, project_id="local", region="node", objective="val_accuracy",
+                       hyperparameters=hps, max_trials=int(os.environ.get("BENCH_TRIALS", "8")),
+                       study_id=os.environ["STUDY_ID"], study_dir=os.environ["STUDY_DIR"],
+                       directory=os.path.join(os.environ["STUDY_DIR"], "results", tuner_id))
+    tuner.search(x, y, epochs=int(os.environ.get("BENCH_EPOCHS", "2")), batch_size=128, validation_data=(xt, yt),
+                 verbose=0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workers", type=int, default=None)
+    ap.add_argument("--trials", type=int, default=8)
+    ap.add_argument("--epochs", type=int, default=2)
+    ap.add_argument("--train", type=int, default=8192)
+    args = ap.parse_args()
+    from cloud_amd.core.topology import visible_gpu_count
+    from cloud_amd.tuner.scheduler import TrialScheduler, study_report
+
+    n_gpus = visible_gpu_count()
+    workers = args.workers or max(1, min(args.trials, n_gpus or 2))
+    study_dir = tempfile.mkdtemp(prefix="tuner_bench_")
+    env = {"STUDY_ID": "mnist_cnn_8", "STUDY_DIR": study_dir, "BENCH_TRIALS": str(args.trials),
+           "BENCH_EPOCHS": str(args.epochs), "BENCH_TRAIN": str(args.train), "PYTHONPATH": ROOT}
+    os.environ.update(env)
+    t0 = time.time()
+    sched = TrialScheduler("bench.tuner_8trials:worker", n_gpus=n_gpus, workers=workers, env=env)
+    res = sched.run(timeout=3000)
+    wall = time.time() - t0
+    sid = next(d for d in os.listdir(study_dir) if d.endswith("mnist_cnn_8"))  # CloudTuner prefixes the id
+    trials = study_report(study_dir, sid)
+    done = [t for t in trials if t["state"] == "COMPLETED" and t.get("finalMeasurement")]
+
+    def score(t):
+        for m in t["finalMeasurement"].get("metrics", []):
+            if m.get("metric") in ("val_accuracy", "val_acc"):
+                return float(m["value"])
+        return float("-inf")
+
+    best = max(done, key=score) if done else None
+    out = {
+        "metric": "trials/hour CloudTuner 8 MNIST-CNN trials (async trial scheduler)",
+        "value": round(len(done) / wall * 3600.0, 2), "unit": "trials/hour", "n_gpus": n_gpus,
+        "workers": workers, "trials_completed": len(done), "wall_s": round(wall, 2),
+        "time_to_best_s": round(best["endTs"] - t0, 2) if best and "endTs" in best else None,
+        "best_val_accuracy": round(score(best), 4) if best else None, "higher_is_better": True,
+        "exit_codes": res["exit_codes"], "data": "synthetic MNIST", "config": {"epochs": args.epochs,
+                                                                             "train_examples": args.train},
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -6,6 +6,9 @@ Two shared objects are produced next to this file:
   bindings (``csrc/bindings.cpp``).  Linked against ``libamdhip64.so.7``; at run
   time the SONAME resolves to the HIP runtime that ``import torch`` already
   mapped, so exactly one HIP runtime lives in the process.
+* ``_comm<EXT_SUFFIX>``     -- native RCCL communicator (``csrc/comm/rccl_comm.cpp``):
+  collectives on a side HIP stream for the bucketed DP engine.  Linked against
+  ``librccl.so.1``, which resolves to the RCCL ``import torch`` already mapped.
 * ``_monitoring<EXT_SUFFIX>`` -- the C++ metrics registry / periodic exporter
   (``csrc/monitoring/*.cpp``), host-only, no HIP dependency, so CPU boxes can use
   it (parity target: reference ``src/cpp/monitoring/*``).
@@ -108,6 +111,16 @@ def build_kernels(verbose=False, jobs=None) -> Path:
     return out
 
 
+def build_comm(verbose=False) -> Path:
+    hipcc = _hipcc()
+    src = CSRC / "comm" / "rccl_comm.cpp"
+    flags = ["-O2", "-fPIC", "-std=c++17", f"-I{ROCM / 'include'}", "-Wno-unused-command-line-argument"]
+    obj = _compile(hipcc, src, flags + _py_includes(), verbose)
+    out = PKG / f"_comm{EXT_SUFFIX}"
+    _link(hipcc, [obj], out, [f"-L{ROCM / 'lib'}", "-lrccl", "-lamdhip64"], verbose)
+    return out
+
+
 def build_monitoring(verbose=False) -> Path:
     cxx = shutil.which("g++") or "c++"
     inc = [f"-I{CSRC / 'include'}", f"-I{CSRC / 'monitoring'}"]
@@ -141,6 +154,8 @@ def build_monitoring_test(verbose=False) -> Path:
 
 def build_all(verbose=False):
     outs = [build_kernels(verbose)]
+    if (CSRC / "comm" / "rccl_comm.cpp").exists():
+        outs.append(build_comm(verbose))
     if (CSRC / "monitoring").exists() and any((CSRC / "monitoring").glob("*.cpp")):
         outs.append(build_monitoring(verbose))
     return outs

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import os
 import sys
+import time
 
 from . import launcher, machine_config, preprocess, stage, topology, validate
 
@@ -38,6 +39,7 @@ def run(entry_point=None, requirements_txt=None, distribution_strategy="auto", d
         **kwargs):
     if remote():
         return None
+    t_run = time.time()
     if kwargs:
         raise TypeError("Unknown keyword arguments: %s" % (kwargs.keys(),))
     job_labels = dict(job_labels or {})
@@ -71,8 +73,10 @@ def run(entry_point=None, requirements_txt=None, distribution_strategy="auto", d
         if wrapper is not None and os.path.exists(wrapper):
             os.remove(wrapper)
 
+    # ranks can report run() -> first-step latency against this clock (bench.py does)
     job = launcher.deploy_job(job_id, job_dir, target, chief_config, worker_count, worker_config,
-                              entry_point_args, stream_logs, job_labels=job_labels, wait=wait, profile=profile)
+                              entry_point_args, stream_logs, job_labels=job_labels, wait=wait, profile=profile,
+                              extra_env={"CLOUD_AMD_RUN_T0": repr(t_run)})
     do_exit = (not called_from_notebook) if exit is None else bool(exit)
     if do_exit:
         rc = job.wait() if (wait or stream_logs) else 0

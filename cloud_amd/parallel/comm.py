@@ -1,0 +1,93 @@
+"""Python face of the native RCCL communicator (``csrc/comm/rccl_comm.cpp``).
+
+``RcclComm`` bootstraps one ``ncclComm_t`` per process: rank 0 creates the
+128-byte unique id and publishes it through the rendezvous store of the default
+``torch.distributed`` process group (TCPStore at MASTER_ADDR:MASTER_PORT); all
+ranks then join with ``ncclCommInitRank``.  Collectives run on the
+communicator's own high-priority HIP stream, ordered after the compute stream
+by an event, so the DP engine (:mod:`cloud_amd.parallel.ddp`) can overlap
+bucket all-reduces with the rest of backward and ``join`` the compute stream
+only before the optimizer step.
+
+Selection: ``CLOUD_AMD_COMM=rccl`` (native communicator) or ``torch`` (default:
+``torch.distributed`` with the RCCL backend).  The native path is opt-in until
+it has been validated on a multi-GPU node; both run RCCL underneath.
+"""
+from __future__ import annotations
+
+import importlib
+import itertools
+import os
+
+import torch
+import torch.distributed as dist
+
+_DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3, torch.int64: 4, torch.uint8: 5}
+_OPS = {"sum": 0, "max": 1, "min": 2, "avg": 3}
+_ctr = itertools.count()
+
+
+def backend() -> str:
+    return os.environ.get("CLOUD_AMD_COMM", "torch").lower()
+
+
+def load():
+    return importlib.import_module("cloud_amd._comm")
+
+
+def _stream(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class RcclComm:
+    def __init__(self, rank=None, world=None, device=None, store=None, tag=None):
+        ext = load()
+        self.rank = dist.get_rank() if rank is None else rank
+        self.world = dist.get_world_size() if world is None else world
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        key = "cloud_amd/rccl_uid/%s" % (tag if tag is not None else next(_ctr))
+        if self.world > 1:
+            store = store or dist.distributed_c10d._get_default_store()
+            if self.rank == 0:
+                uid = ext.unique_id()
+                store.set(key, uid)
+            else:
+                uid = store.get(key)
+        else:
+            uid = ext.unique_id()
+        self.c = ext.Comm(self.world, self.rank, bytes(uid), self.device.index)
+
+    def _args(self, t):
+        assert t.is_cuda and t.is_contiguous(), "collectives need contiguous device tensors"
+        return t.data_ptr(), t.numel(), _DTYPES[t.dtype]
+
+    def all_reduce(self, t, op="sum"):
+        p, n, d = self._args(t)
+        self.c.all_reduce(p, n, d, _OPS[op], _stream(t.device))
+
+    def broadcast(self, t, root=0):
+        p, n, d = self._args(t)
+        self.c.broadcast(p, n, d, root, _stream(t.device))
+
+    def reduce_scatter(self, out, inp, op="sum"):
+        self.c.reduce_scatter(inp.data_ptr(), out.data_ptr(), out.numel(), _DTYPES[out.dtype], _OPS[op],
+                              _stream(out.device))
+
+    def all_gather(self, out, inp):
+        self.c.all_gather(inp.data_ptr(), out.data_ptr(), inp.numel(), _DTYPES[inp.dtype], _stream(inp.device))
+
+    def join(self, device=None):
+        """The current (compute) stream waits for every collective issued so far."""
+        self.c.join(_stream(device or self.device))
+
+    def synchronize(self):
+        self.c.synchronize()
+
+    def healthy(self) -> bool:
+        return self.c.async_error() == 0
+
+    def abort(self):
+        self.c.abort()
+
+    def close(self):
+        self.c.destroy()

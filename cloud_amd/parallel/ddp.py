@@ -18,6 +18,11 @@ Mechanics (one process per GPU, ``torch.distributed`` over RCCL/xGMI):
 * the 1/world mean is NOT a separate pass: it is folded into the optimizer
   kernel's ``grad_scale``.
 
+Transport: ``torch.distributed`` (RCCL backend) by default, or the native C++
+RCCL communicator (:mod:`cloud_amd.parallel.comm`, ``CLOUD_AMD_COMM=rccl``) whose
+collectives run on a dedicated high-priority stream joined once before the
+optimizer step.
+
 Bucket size: xGMI on MI355X is 7 point-to-point links per GPU; a ring
 all-reduce moves 2(N-1)/N of the bucket per link, so ~25-64 MB buckets keep
 RCCL's multi-channel rings busy while leaving enough buckets (>= 4-8 for
@@ -32,6 +37,8 @@ import weakref
 
 import torch
 import torch.distributed as dist
+
+from . import comm as _comm
 
 _ACTIVE = weakref.WeakSet()
 
@@ -65,6 +72,9 @@ class GradAllReducer:
         mb = float(bucket_mb if bucket_mb is not None else os.environ.get("CLOUD_AMD_BUCKET_MB", 16))
         self.bucket_bytes = int(mb * (1 << 20))
         self.overlap = overlap
+        self.comm = None
+        if self.world > 1 and _comm.backend() == "rccl" and self.arenas and self.arenas[0].grad.is_cuda:
+            self.comm = _comm.RcclComm()  # native communicator: side stream + events
         self.buckets = []
         self._param_bucket = {}
         self._next = 0
@@ -104,7 +114,10 @@ class GradAllReducer:
             self._launch_ready()
 
     def _launch(self, b):
-        b.work = dist.all_reduce(b.tensor, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        if self.comm is not None:
+            self.comm.all_reduce(b.tensor)
+        else:
+            b.work = dist.all_reduce(b.tensor, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         b.launched = True
 
     def _launch_ready(self):
@@ -119,6 +132,8 @@ class GradAllReducer:
         while self._next < len(self.buckets):
             self._launch(self.buckets[self._next])
             self._next += 1
+        if self.comm is not None:
+            self.comm.join()
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
@@ -136,9 +151,16 @@ class GradAllReducer:
         if self.world <= 1:
             return
         for a in self.arenas:
-            dist.broadcast(a.master, src, group=self.pg)
-            if a.model is not None:
-                dist.broadcast(a.model, src, group=self.pg)
+            if self.comm is not None:
+                self.comm.broadcast(a.master, src)
+                if a.model is not None:
+                    self.comm.broadcast(a.model, src)
+            else:
+                dist.broadcast(a.master, src, group=self.pg)
+                if a.model is not None:
+                    dist.broadcast(a.model, src, group=self.pg)
+        if self.comm is not None:
+            self.comm.join()
 
     def remove(self):
         for h in self._hooks:

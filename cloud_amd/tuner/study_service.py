@@ -198,6 +198,7 @@ class StudyService:
         def fn(t, _):
             t["state"] = "COMPLETED"
             t["endTime"] = _ts()
+            t["endTs"] = time.time()
             if trial_infeasible:
                 t["trialInfeasible"] = True
                 t["infeasibleReason"] = infeasible_reason

@@ -215,6 +215,115 @@ struct DenseNC {
   }
 };
 
+// Shared epilogue: fp32 split-K slab store, or bf16 through LDS with bias /
+// activation / pre-activation / act' / beta-accumulate / BN-statistics options.
+template <int BM, int BN, int WM, int WN, int EPI, int FM = BM / WM / 16, int FN = BN / WN / 16>
+__device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM][FN], short* smem, int m0, int n0,
+                                              int tm, int tid) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int EPI_LD = BN + PAD;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  // C/D layout of mfma_f32_16x16x32: col = lane&15, row = (lane>>4)*4 + r
+  const int rbase = wm * (BM / WM) + (lane >> 4) * 4;
+  const int cbase = wn * (BN / WN) + (lane & 15);
+  if constexpr (EPI == EPI_F32_PARTIAL) {
+    float* Cp = reinterpret_cast<float*>(P.C) + (long)blockIdx.z * P.split_stride;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gm = m0 + rbase + i * 16 + r, gn = n0 + cbase + j * 16;
+          if (gm < P.M && gn < P.N) Cp[(long)gm * P.ldc + gn] = acc[i][j][r];
+        }
+    return;
+  } else {
+    short* Cs = smem;
+    if (P.bias) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int gn = n0 + cbase + j * 16;
+        const float bv = gn < P.N ? P.bias[gn] : 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += bv;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(rbase + i * 16 + r) * EPI_LD + cbase + j * 16] = (short)f2bf(acc[i][j][r]);
+    __syncthreads();
+    const bool fx = P.act != ACT_NONE || P.dact_src != nullptr || P.preact != nullptr;
+    bf16_t* Cg = reinterpret_cast<bf16_t*>(P.C);
+    constexpr int CH = BM * BN / 8;
+    for (int c = tid; c < CH; c += NT) {
+      const int row = c / (BN / 8), col = (c % (BN / 8)) * 8;
+      const int gm = m0 + row, gn = n0 + col;
+      if (gm < P.M && gn < P.N) {
+        s8v v = *reinterpret_cast<const s8v*>(Cs + row * EPI_LD + col);
+        bf16_t* dst = Cg + (long)gm * P.ldc + gn;
+        if (fx) {
+          if (P.preact) *reinterpret_cast<s8v*>(P.preact + (long)gm * P.ld_aux + gn) = v;
+          if (P.dact_src) {
+            const s8v src = *reinterpret_cast<const s8v*>(P.dact_src + (long)gm * P.ld_aux + gn);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              v[j] = (short)f2bf(bf2f((bf16_t)v[j]) * act_grad(P.act, bf2f((bf16_t)src[j])));
+          } else if (P.act != ACT_NONE) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(act_fwd(P.act, bf2f((bf16_t)v[j])));
+          }
+        }
+        if (P.beta != 0.f) {
+          s8v o = *reinterpret_cast<const s8v*>(dst);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[j] = (short)f2bf(bf2f((bf16_t)v[j]) + P.beta * bf2f((bf16_t)o[j]));
+        }
+        if (P.stats && (fx || P.beta != 0.f)) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
+        *reinterpret_cast<s8v*>(dst) = v;
+      }
+    }
+    if (P.stats) {
+      // per-column sum / sum of squares of the stored bf16 values of this tile
+      constexpr int TPC = NT / BN;
+      const int col = tid % BN, part = tid / BN;
+      float s = 0.f, q = 0.f;
+      int rows = P.M - m0;
+      if (rows > BM) rows = BM;
+      __syncthreads();
+      for (int r = part; r < rows; r += TPC) {
+        const float v = bf2f((bf16_t)Cs[r * EPI_LD + col]);
+        s += v;
+        q += v * v;
+      }
+      __syncthreads();
+      float* sred = reinterpret_cast<float*>(smem);
+      sred[part * BN + col] = s;
+      sred[(TPC + part) * BN + col] = q;
+      __syncthreads();
+      if (part == 0 && n0 + col < P.N) {
+        float ts = 0.f, tq = 0.f;
+#pragma unroll
+        for (int pp = 0; pp < TPC; ++pp) {
+          ts += sred[pp * BN + col];
+          tq += sred[(TPC + pp) * BN + col];
+        }
+        float* st = P.stats + (long)tm * 2 * P.N;
+        st[n0 + col] = ts;
+        st[P.N + n0 + col] = tq;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ core --
 template <int BM, int BN, int WM, int WN, template <int, int, int> class LAT, template <int, int, int> class LBT,
           int EPI, int NSTAGE = 2>
@@ -314,104 +423,175 @@ __device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
     }
   }
 
-  // C/D layout of mfma_f32_16x16x32: col = lane&15, row = (lane>>4)*4 + r
-  const int rbase = wm * (BM / WM) + (lane >> 4) * 4;
-  const int cbase = wn * (BN / WN) + (lane & 15);
-  if constexpr (EPI == EPI_F32_PARTIAL) {
-    float* Cp = reinterpret_cast<float*>(P.C) + (long)blockIdx.z * P.split_stride;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int gm = m0 + rbase + i * 16 + r, gn = n0 + cbase + j * 16;
-          if (gm < P.M && gn < P.N) Cp[(long)gm * P.ldc + gn] = acc[i][j][r];
-        }
-    return;
+  gemm_epilogue<BM, BN, WM, WN, EPI>(P, acc, smem, m0, n0, tm, tid);
+}
+
+// ======================================================= LDS-DMA (glds) core --
+// Operand tiles are filled by global_load_lds_dwordx4 (16 B per lane straight
+// into LDS, no VGPR round trip, no ds_write pass).  The LDS image of a wave
+// instruction is lane-linear, so tiles are UNPADDED and bank conflicts are
+// removed by an XOR swizzle applied on the SOURCE side (each lane fetches the
+// logical chunk that belongs at its linear slot) and undone by the readers:
+//   K-contiguous tile [rows][64]  (8 x 16-B chunks per 128-B row):
+//       phys = logical ^ (row & 7)       -> ds_read_b128 fragment reads conflict-free
+//   N-contiguous tile [64 k][R]   (R/8 chunks per row), transposed reads:
+//       R = 128: phys = logical ^ 2*((k&3) | ((k>>3)&1)<<2)
+//       R =  64: phys = logical ^ 2*(((k>>1)&1) | ((k>>3)&1)<<1)
+//     -> the 8 k-rows one ds_read_b64_tr_b16 half-wave touches land in 8
+//        distinct 32-B bank slots.
+// Out-of-range K chunks read a 16-B zero page (rows/cols beyond M/N are clamped:
+// they only feed outputs that are never stored).  One LDS stage, two barriers
+// per K step; several blocks per CU hide the DMA latency.
+
+static __device__ __attribute__((aligned(16))) bf16_t ca_zero16[8];
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int R>
+__device__ __forceinline__ int nc_swz(int k) {
+  if constexpr (R >= 128) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
+  else return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+}
+
+template <int R, bool KC>
+__device__ __forceinline__ bf16x8 read_frag_sw(const short* lds, int r0, int k0, int lane) {
+  if constexpr (KC) {
+    const int row = r0 + (lane & 15);
+    const int pc = ((k0 >> 3) + (lane >> 4)) ^ (row & 7);
+    s8v v = *reinterpret_cast<const s8v*>(lds + row * BK + pc * 8);
+    return __builtin_bit_cast(bf16x8, v);
   } else {
-    short* Cs = smem;
-    if (P.bias) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int gn = n0 + cbase + j * 16;
-        const float bv = gn < P.N ? P.bias[gn] : 0.f;
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] += bv;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(rbase + i * 16 + r) * EPI_LD + cbase + j * 16] = (short)f2bf(acc[i][j][r]);
-    __syncthreads();
-    const bool fx = P.act != ACT_NONE || P.dact_src != nullptr || P.preact != nullptr;
-    bf16_t* Cg = reinterpret_cast<bf16_t*>(P.C);
-    constexpr int CH = BM * BN / 8;
-    for (int c = tid; c < CH; c += NT) {
-      const int row = c / (BN / 8), col = (c % (BN / 8)) * 8;
-      const int gm = m0 + row, gn = n0 + col;
-      if (gm < P.M && gn < P.N) {
-        s8v v = *reinterpret_cast<const s8v*>(Cs + row * EPI_LD + col);
-        bf16_t* dst = Cg + (long)gm * P.ldc + gn;
-        if (fx) {
-          if (P.preact) *reinterpret_cast<s8v*>(P.preact + (long)gm * P.ld_aux + gn) = v;
-          if (P.dact_src) {
-            const s8v src = *reinterpret_cast<const s8v*>(P.dact_src + (long)gm * P.ld_aux + gn);
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              v[j] = (short)f2bf(bf2f((bf16_t)v[j]) * act_grad(P.act, bf2f((bf16_t)src[j])));
-          } else if (P.act != ACT_NONE) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(act_fwd(P.act, bf2f((bf16_t)v[j])));
-          }
-        }
-        if (P.beta != 0.f) {
-          s8v o = *reinterpret_cast<const s8v*>(dst);
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            v[j] = (short)f2bf(bf2f((bf16_t)v[j]) + P.beta * bf2f((bf16_t)o[j]));
-        }
-        if (P.stats && (fx || P.beta != 0.f)) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
-        *reinterpret_cast<s8v*>(dst) = v;
-      }
-    }
-    if (P.stats) {
-      // per-column sum / sum of squares of the stored bf16 values of this tile
-      constexpr int TPC = NT / BN;
-      const int col = tid % BN, part = tid / BN;
-      float s = 0.f, q = 0.f;
-      int rows = P.M - m0;
-      if (rows > BM) rows = BM;
-      __syncthreads();
-      for (int r = part; r < rows; r += TPC) {
-        const float v = bf2f((bf16_t)Cs[r * EPI_LD + col]);
-        s += v;
-        q += v * v;
-      }
-      __syncthreads();
-      float* sred = reinterpret_cast<float*>(smem);
-      sred[part * BN + col] = s;
-      sred[(TPC + part) * BN + col] = q;
-      __syncthreads();
-      if (part == 0 && n0 + col < P.N) {
-        float ts = 0.f, tq = 0.f;
-#pragma unroll
-        for (int pp = 0; pp < TPC; ++pp) {
-          ts += sred[pp * BN + col];
-          tq += sred[(TPC + pp) * BN + col];
-        }
-        float* st = P.stats + (long)tm * 2 * P.N;
-        st[n0 + col] = ts;
-        st[P.N + n0 + col] = tq;
-      }
-    }
+    const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+    const int k = k0 + 8 * g + q;
+    const int lc = (r0 >> 3) + (p >> 1);
+    const int sub = 4 * (p & 1);
+    const short* b0 = lds + k * R + ((lc ^ nc_swz<R>(k)) << 3) + sub;
+    const short* b1 = lds + (k + 4) * R + ((lc ^ nc_swz<R>(k + 4)) << 3) + sub;
+    s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b0));
+    s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b1));
+    s8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
   }
+}
+
+// Dense K-contiguous operand for the glds core: X[r][k] at p[r*ld + k].
+// Chunk i of thread tid covers tile row (tid>>3) + i*(NT/8) and the swizzled
+// column slot (tid&7) ^ (row&7) -- the XOR term is the same for every i, so the
+// loader keeps one base row and one column (few VGPRs -> more blocks per CU).
+template <int R, int CPT, int NT>
+struct GDenseKC {
+  static constexpr bool KC = true;
+  const bf16_t* p;
+  long ld;
+  int row0, col, rlast, K;
+  __device__ GDenseKC(const CoreParams& P, bool isA, int r0, int tid) {
+    p = isA ? P.A : P.B;
+    ld = isA ? P.lda : P.ldb;
+    rlast = (isA ? P.M : P.N) - 1;
+    K = P.K;
+    const int row = tid >> 3;
+    row0 = r0 + row;
+    col = ((tid & 7) ^ (row & 7)) << 3;
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    int gr = row0 + i * (NT / 8);
+    gr = gr > rlast ? rlast : gr;
+    const int k = k0 + col;
+    return k < K ? p + (long)gr * ld + k : ca_zero16;
+  }
+};
+
+// Dense output-dim-contiguous operand for the glds core: X[r][k] at p[k*ld + r].
+// Chunk i covers k-row (tid / (R/8)) + i * (NT*8/R); its swizzle term is i-invariant.
+template <int R, int CPT, int NT>
+struct GDenseNC {
+  static constexpr bool KC = false;
+  const bf16_t* colp;
+  long ld;
+  int krow0, K;
+  __device__ GDenseNC(const CoreParams& P, bool isA, int r0, int tid) {
+    const bf16_t* p = isA ? P.A : P.B;
+    ld = isA ? P.lda : P.ldb;
+    const int rlimit = isA ? P.M : P.N;
+    K = P.K;
+    constexpr int CPR = R / 8;  // chunks per k-row
+    const int k = tid / CPR, pc = tid % CPR;
+    int n = r0 + ((pc ^ nc_swz<R>(k)) << 3);
+    if (n > rlimit - 8) n = rlimit - 8;
+    colp = p + n;
+    krow0 = k;
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const int k = k0 + krow0 + i * (NT * 8 / R);
+    return k < K ? colp + (long)k * ld : ca_zero16;
+  }
+};
+
+template <int BM, int BN, int WM, int WN, template <int, int, int> class LAT, template <int, int, int> class LBT,
+          int EPI>
+__device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;
+  constexpr int EPI_LD = BN + PAD;
+  constexpr int SMEM = (A_ELEMS + B_ELEMS > BM * EPI_LD ? A_ELEMS + B_ELEMS : BM * EPI_LD);
+  constexpr int CPA = A_ELEMS / 8 / NT, CPB = B_ELEMS / 8 / NT;
+  using LA = LAT<BM, CPA, NT>;
+  using LB = LBT<BN, CPB, NT>;
+  constexpr bool A_KC = LA::KC, B_KC = LB::KC;
+  static_assert(A_ELEMS % (8 * NT) == 0 && B_ELEMS % (8 * NT) == 0, "tile chunks must divide threads");
+  __shared__ __attribute__((aligned(16))) short smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_m = (P.M + BM - 1) / BM, tiles_n = (P.N + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.z * P.k_per_split;
+  int kend = kbeg + P.k_per_split;
+  if (kend > P.K) kend = P.K;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  const LA la(P, true, m0, tid);
+  const LB lb(P, false, n0, tid);
+  short* As = smem;
+  short* Bs = smem + A_ELEMS;
+
+  f4v acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  for (int t = 0; t < nk; ++t) {
+    const int k0 = kbeg + t * BK;
+#pragma unroll
+    for (int i = 0; i < CPA; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)la.src(i, k0), (lds_void*)(As + (i * NT + wave * 64) * 8), 16,
+                                       0, 0);
+#pragma unroll
+    for (int i = 0; i < CPB; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)lb.src(i, k0), (lds_void*)(Bs + (i * NT + wave * 64) * 8), 16,
+                                       0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = read_frag_sw<BM, A_KC>(As, wm * (BM / WM) + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = read_frag_sw<BN, B_KC>(Bs, wn * (BN / WN) + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  gemm_epilogue<BM, BN, WM, WN, EPI>(P, acc, smem, m0, n0, tm, tid);
 }
 
 }  // namespace ca

@@ -8,6 +8,8 @@
 // (csrc/include/ca_mfma_core.h) stages K-contiguous tiles for ds_read_b128
 // and M/N-contiguous tiles for the gfx950 transposed read ds_read_b64_tr_b16.
 // Split-K writes fp32 slabs reduced deterministically by splitk_reduce_kernel.
+#include <stdlib.h>
+
 #include "ca_mfma_core.h"
 
 namespace {
@@ -16,6 +18,21 @@ using namespace ca;
 template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI, int NS>
 __global__ void __launch_bounds__(256) dense_gemm_kernel(CoreParams P) {
   mfma_gemm_body<BM, BN, 2, 2, LA, LB, EPI, NS>(P);
+}
+
+template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) dense_gemm_glds_kernel(CoreParams P) {
+  mfma_gemm_glds<BM, BN, 2, 2, LA, LB, EPI>(P);
+}
+
+// CLOUD_AMD_GEMM_CORE=reg selects the register-staged core (A/B comparisons).
+bool use_glds() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_GEMM_CORE");
+    v = (e && e[0] == 'r') ? 0 : 1;
+  }
+  return v == 1;
 }
 
 template <bool OUT_BF16>
@@ -56,9 +73,15 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
-template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
+template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB,
+          template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
 int launch(const CoreParams& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  if (use_glds()) {
+    dense_gemm_glds_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
+    CA_LAUNCH_CHECK();
+    return 0;
+  }
   // a single K tile needs no double buffer: half the LDS -> twice the resident blocks
   if (p.k_per_split <= BK)
     dense_gemm_kernel<BM, BN, LA, LB, EPI, 1><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
@@ -73,14 +96,14 @@ int dispatch(int layout, const CoreParams& p, int splits, hipStream_t s) {
   const bool small_n = p.N <= 64;
   switch (layout) {
     case 0:
-      return small_n ? launch<128, 64, DenseKC, DenseKC, EPI>(p, splits, s)
-                     : launch<128, 128, DenseKC, DenseKC, EPI>(p, splits, s);
+      return small_n ? launch<128, 64, DenseKC, DenseKC, GDenseKC, GDenseKC, EPI>(p, splits, s)
+                     : launch<128, 128, DenseKC, DenseKC, GDenseKC, GDenseKC, EPI>(p, splits, s);
     case 1:
-      return small_n ? launch<128, 64, DenseKC, DenseNC, EPI>(p, splits, s)
-                     : launch<128, 128, DenseKC, DenseNC, EPI>(p, splits, s);
+      return small_n ? launch<128, 64, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI>(p, splits, s)
+                     : launch<128, 128, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI>(p, splits, s);
     case 2:
-      return small_n ? launch<128, 64, DenseNC, DenseNC, EPI>(p, splits, s)
-                     : launch<128, 128, DenseNC, DenseNC, EPI>(p, splits, s);
+      return small_n ? launch<128, 64, DenseNC, DenseNC, GDenseNC, GDenseNC, EPI>(p, splits, s)
+                     : launch<128, 128, DenseNC, DenseNC, GDenseNC, GDenseNC, EPI>(p, splits, s);
   }
   return -2;
 }

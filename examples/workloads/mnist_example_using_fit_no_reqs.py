@@ -2,6 +2,7 @@
 ``TFC/core/tests/testdata/mnist_example_using_fit_no_reqs.py``."""
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
@@ -18,5 +19,9 @@ model = tf.keras.Sequential([
     tf.keras.layers.Dense(10, activation="softmax"),
 ])
 model.compile(loss="sparse_categorical_crossentropy", optimizer=tf.keras.optimizers.Adam(), metrics=["accuracy"])
-hist = model.fit(x_train, y_train, epochs=n(10, 1), batch_size=128)
-print("RESULT mlp loss={:.4f}".format(hist.history["loss"][-1]))
+epochs = int(os.environ.get("MLP_EPOCHS", n(10, 1)))
+t0 = time.time()
+hist = model.fit(x_train, y_train, epochs=epochs, batch_size=128)
+fit_s = time.time() - t0
+print("RESULT mlp loss={:.4f} samples_per_s={:.1f} fit_s={:.3f}".format(hist.history["loss"][-1],
+                                                                       epochs * len(x_train) / fit_s, fit_s))

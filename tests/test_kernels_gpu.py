@@ -302,3 +302,25 @@ def test_fused_bottleneck_matches_fp32_and_unfused(cin, width, stride):
     for n, p in ref.named_parameters():
         assert rel(g_f[n], p.grad.float().reshape(g_f[n].shape)) < 1e-1, n
         close(g_f[n], g_u[n], 2e-2)
+
+
+def test_native_rccl_communicator_single_rank():
+    """The C++ RCCL communicator (world 1 on the one-GPU box): init via unique id,
+    side-stream collectives ordered after the compute stream, join before use."""
+    from cloud_amd.parallel.comm import RcclComm
+
+    c = RcclComm(rank=0, world=1, device=DEV)
+    x = torch.arange(1000, device=DEV, dtype=torch.float32)
+    y = x * 2  # produced on the compute stream right before the collective
+    c.all_reduce(y)
+    c.broadcast(y, root=0)
+    out = torch.empty(1000, device=DEV, dtype=torch.float32)
+    c.all_gather(out, y)
+    rs = torch.empty(1000, device=DEV, dtype=torch.float32)
+    c.reduce_scatter(rs, out)
+    b = torch.ones(64, device=DEV, dtype=torch.bfloat16)
+    c.all_reduce(b)
+    c.join()
+    assert torch.equal(rs, x * 2) and torch.equal(b, torch.ones_like(b))
+    assert c.healthy()
+    c.close()
