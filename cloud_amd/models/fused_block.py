@@ -65,9 +65,9 @@ def _conv_bn(conv, bn, x, residual=None):
     OW = raw.out_hw(W, conv.k, conv.stride, conv.padding)
     part = raw.stats_buffer(N * OH * OW, conv.cout, x.device)
     z = raw.conv_fwd(x, conv.weight, conv.stride, conv.padding, stats=part)
-    y, st = raw.bn_fwd(z, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, bn.momentum, bn.relu,
-                       residual=residual, partials=part)
-    return z, y, st
+    y, st, mask = raw.bn_fwd(z, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, bn.momentum,
+                             bn.relu, residual=residual, partials=part, keep_mask=True)
+    return z, y, (st, mask)
 
 
 class _BottleneckFn(torch.autograd.Function):
@@ -83,8 +83,9 @@ class _BottleneckFn(torch.autograd.Function):
         z3, out, s3 = _conv_bn(blk.conv3, blk.bn3, y2, residual=idn)
         del idn
         ctx.blk = blk
-        ctx.save_for_backward(x, z1, y1, z2, y2, z3, out, s1, s2, s3,
-                              *((zd, sd) if ds is not None else ()))
+        (s1, m1), (s2, m2), (s3, m3) = s1, s2, s3
+        ctx.save_for_backward(x, z1, y1, z2, y2, z3, s1, m1, s2, m2, s3, m3,
+                              *((zd, sd[0]) if ds is not None else ()))
         return out
 
     @staticmethod
@@ -94,12 +95,13 @@ class _BottleneckFn(torch.autograd.Function):
         blk = ctx.blk
         ds = blk.downsample
         saved = ctx.saved_tensors
-        x, z1, y1, z2, y2, z3, out, s1, s2, s3 = saved[:10]
+        x, z1, y1, z2, y2, z3, s1, m1, s2, m2, s3, m3 = saved[:12]
         dout = dout.contiguous()
 
-        def bn_back(bn, dy, y, z, st, want_dres=False):
-            r = raw.bn_bwd(dy, y, z, bn.weight, st, bn.relu, dgamma=bn.weight.grad, dbeta=bn.bias.grad,
-                           want_dres=want_dres, accumulate=1)
+        def bn_back(bn, dy, z, st, want_dres=False):
+            stats, mask = st
+            r = raw.bn_bwd(dy, None, z, bn.weight, stats, bn.relu, dgamma=bn.weight.grad, dbeta=bn.bias.grad,
+                           want_dres=want_dres, accumulate=1, mask=mask)
             ddp.notify_grad_ready(bn.weight)
             ddp.notify_grad_ready(bn.bias)
             return r
@@ -108,21 +110,21 @@ class _BottleneckFn(torch.autograd.Function):
             raw.conv_wgrad(dz, inp, conv.weight.shape, conv.stride, conv.padding, out=conv.weight.grad, beta=1.0)
             ddp.notify_grad_ready(conv.weight)
 
-        dz3, dres = bn_back(blk.bn3, dout, out, z3, s3, want_dres=True)
+        dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=True)
         del dout
         dy2 = raw.conv_dgrad(dz3, blk.conv3.weight, y2.shape, 1, 0)
         wgrad(blk.conv3, dz3, y2)
         del dz3
-        dz2, _ = bn_back(blk.bn2, dy2, y2, z2, s2)
+        dz2, _ = bn_back(blk.bn2, dy2, z2, (s2, m2))
         del dy2
         dy1 = raw.conv_dgrad(dz2, blk.conv2.weight, y1.shape, blk.conv2.stride, blk.conv2.padding)
         wgrad(blk.conv2, dz2, y1)
         del dz2
-        dz1, _ = bn_back(blk.bn1, dy1, y1, z1, s1)
+        dz1, _ = bn_back(blk.bn1, dy1, z1, (s1, m1))
         del dy1
         if ds is not None:
-            zd, sd = saved[10], saved[11]
-            dzd, _ = bn_back(ds["bn"], dres, zd, zd, sd)
+            zd, sd = saved[12], saved[13]
+            dzd, _ = bn_back(ds["bn"], dres, zd, (sd, None))
             del dres
             c = ds["conv"]
             dx = raw.conv_dgrad(dzd, c.weight, x.shape, c.stride, c.padding)

@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _ext
+from . import _ext, raw
 
 
 def _torch_bn_act(x, res, gamma, beta, running_mean, running_var, eps, momentum, relu, training):
@@ -44,32 +44,21 @@ def _torch_bn_act(x, res, gamma, beta, running_mean, running_var, eps, momentum,
 
 
 class _BNActFn(torch.autograd.Function):
+    """Autograd face of the HIP BN kernels (launchers in :mod:`.raw`); the ReLU gate of
+    the backward is the 1-bit-per-channel mask the forward apply wrote."""
+
     @staticmethod
     def forward(ctx, x, res, gamma, beta, running_mean, running_var, eps, momentum, relu, partials):
-        ext = _ext.load(required=True)
         assert x.dtype == torch.bfloat16 and x.is_contiguous(), "bn_act expects contiguous NHWC bf16"
         C = x.shape[-1]
-        M = x.numel() // C
-        dev = x.device
-        y = torch.empty_like(x)
-        stats = torch.empty(4 * C, dtype=torch.float32, device=dev)  # mean, rstd, scale, shift
         if res is not None:
             assert res.shape == x.shape and res.dtype == x.dtype
             res = res.contiguous()
         if partials is not None:
             assert partials.shape[1:] == (2, C), partials.shape
-            ext.bn_fwd_partials(x.data_ptr(), _ext.ptr(res), y.data_ptr(), M, C, partials.data_ptr(),
-                                partials.shape[0], _ext.ptr(gamma), _ext.ptr(beta), float(eps), float(momentum),
-                                _ext.ptr(running_mean), _ext.ptr(running_var), stats.data_ptr(),
-                                stats.data_ptr() + 4 * C, stats.data_ptr() + 8 * C, int(relu),
-                                _ext.stream_handle(dev))
-        else:
-            ws = torch.empty(ext.bn_workspace_floats(M, C), dtype=torch.float32, device=dev)
-            ext.bn_fwd(x.data_ptr(), _ext.ptr(res), y.data_ptr(), M, C, _ext.ptr(gamma), _ext.ptr(beta),
-                       float(eps), float(momentum), _ext.ptr(running_mean), _ext.ptr(running_var),
-                       stats.data_ptr(), stats.data_ptr() + 4 * C, stats.data_ptr() + 8 * C, ws.data_ptr(),
-                       int(relu), _ext.stream_handle(dev))
-        ctx.save_for_backward(x, y, gamma, stats)
+        y, stats, mask = raw.bn_fwd(x, gamma, beta, running_mean, running_var, eps, momentum, relu, residual=res,
+                                    partials=partials, keep_mask=True)
+        ctx.save_for_backward(x, mask, gamma, stats)
         ctx.relu = relu
         ctx.has_res = res is not None
         ctx.has_beta = beta is not None
@@ -77,23 +66,14 @@ class _BNActFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        ext = _ext.load(required=True)
-        x, y, gamma, stats = ctx.saved_tensors
-        dy = dy.contiguous()
+        x, mask, gamma, stats = ctx.saved_tensors
         C = x.shape[-1]
-        M = x.numel() // C
         dev = x.device
-        dx = torch.empty_like(x)
-        dres = torch.empty_like(x) if (ctx.has_res and ctx.needs_input_grad[1]) else None
+        want_dres = ctx.has_res and ctx.needs_input_grad[1]
         dgamma = torch.empty(C, dtype=torch.float32, device=dev) if gamma is not None else None
         dbeta = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_beta else None
-        coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
-        ws = torch.empty(ext.bn_workspace_floats(M, C), dtype=torch.float32, device=dev)
-        ext.bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), M, C, _ext.ptr(gamma), stats.data_ptr(),
-                   stats.data_ptr() + 4 * C, dx.data_ptr(), _ext.ptr(dres), _ext.ptr(dgamma), _ext.ptr(dbeta),
-                   coef.data_ptr(), ws.data_ptr(), int(ctx.relu), _ext.stream_handle(dev))
-        if dres is None and ctx.has_res and ctx.needs_input_grad[1]:
-            raise RuntimeError("residual grad requested but not produced")
+        dx, dres = raw.bn_bwd(dy.contiguous(), None, x, gamma, stats, ctx.relu, dgamma=dgamma, dbeta=dbeta,
+                              want_dres=want_dres, mask=mask)
         return dx, dres, dgamma, dbeta, None, None, None, None, None, None
 
 

@@ -92,31 +92,38 @@ def conv_wgrad(dy, x, w_shape, stride, padding, out, beta=1.0):
 
 
 # ------------------------------------------------------------------ batchnorm
-def bn_fwd(x, gamma, beta, running_mean, running_var, eps, momentum, relu, residual=None, partials=None):
-    """Training BN(+res)(+ReLU).  Returns (y, stats[4C] = mean, rstd, scale, shift)."""
+def bn_fwd(x, gamma, beta, running_mean, running_var, eps, momentum, relu, residual=None, partials=None,
+           keep_mask=False):
+    """Training BN(+res)(+ReLU).  Returns (y, stats[4C] = mean, rstd, scale, shift, mask) where
+    ``mask`` is the ReLU bitmask ([M, C/8] uint8, bit j = channel 8c+j active) when
+    ``keep_mask`` and ``relu`` (else None): the backward then reads it instead of y."""
     ext = _ext.load(required=True)
     C = x.shape[-1]
     M = x.numel() // C
     dev = x.device
     y = torch.empty_like(x)
     stats = torch.empty(4 * C, dtype=torch.float32, device=dev)
+    mask = torch.empty((M, C // 8), dtype=torch.uint8, device=dev) if (keep_mask and relu) else None
     sp = stats.data_ptr()
     if partials is not None:
+        gws = torch.empty(64 * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
         ext.bn_fwd_partials(x.data_ptr(), _ext.ptr(residual), y.data_ptr(), M, C, partials.data_ptr(),
                             partials.shape[0], _ext.ptr(gamma), _ext.ptr(beta), float(eps), float(momentum),
                             _ext.ptr(running_mean), _ext.ptr(running_var), sp, sp + 4 * C, sp + 8 * C, int(relu),
-                            _st(dev))
+                            _ext.ptr(mask), _ext.ptr(gws), _st(dev))
     else:
         ws = torch.empty(ext.bn_workspace_floats(M, C), dtype=torch.float32, device=dev)
         ext.bn_fwd(x.data_ptr(), _ext.ptr(residual), y.data_ptr(), M, C, _ext.ptr(gamma), _ext.ptr(beta),
                    float(eps), float(momentum), _ext.ptr(running_mean), _ext.ptr(running_var), sp, sp + 4 * C,
-                   sp + 8 * C, ws.data_ptr(), int(relu), _st(dev))
-    return y, stats
+                   sp + 8 * C, ws.data_ptr(), int(relu), _ext.ptr(mask), _st(dev))
+    return y, stats, mask
 
 
-def bn_bwd(dy, y, x, gamma, stats, relu, dgamma=None, dbeta=None, want_dres=False, dx_out=None, accumulate=0):
-    """BN(+res)(+ReLU) backward.  dgamma/dbeta (fp32 [C]) are written, or accumulated
-    into when ``accumulate`` is set.  Returns (dx, dres-or-None)."""
+def bn_bwd(dy, y, x, gamma, stats, relu, dgamma=None, dbeta=None, want_dres=False, dx_out=None, accumulate=0,
+           mask=None):
+    """BN(+res)(+ReLU) backward.  The ReLU gate comes from ``mask`` (forward bitmask) or
+    ``y``.  dgamma/dbeta (fp32 [C]) are written, or accumulated into when
+    ``accumulate`` is set.  Returns (dx, dres-or-None)."""
     ext = _ext.load(required=True)
     C = x.shape[-1]
     M = x.numel() // C
@@ -126,8 +133,8 @@ def bn_bwd(dy, y, x, gamma, stats, relu, dgamma=None, dbeta=None, want_dres=Fals
     coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
     ws = torch.empty(ext.bn_workspace_floats(M, C), dtype=torch.float32, device=dev)
     sp = stats.data_ptr()
-    ext.bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), M, C, _ext.ptr(gamma), sp, sp + 4 * C, dx.data_ptr(),
-               _ext.ptr(dres), _ext.ptr(dgamma), _ext.ptr(dbeta), coef.data_ptr(), ws.data_ptr(),
+    ext.bn_bwd(dy.data_ptr(), _ext.ptr(y), _ext.ptr(mask), x.data_ptr(), M, C, _ext.ptr(gamma), sp, sp + 4 * C,
+               dx.data_ptr(), _ext.ptr(dres), _ext.ptr(dgamma), _ext.ptr(dbeta), coef.data_ptr(), ws.data_ptr(),
                int(relu) | (2 if accumulate else 0), _st(dev))
     return dx, dres
 

@@ -44,7 +44,10 @@ class RcclComm:
         ext = load()
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if world is None else world
-        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        dev = torch.device("cuda") if device is None else torch.device(device)
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
         key = "cloud_amd/rccl_uid/%s" % (tag if tag is not None else next(_ctr))
         if self.world > 1:
             store = store or dist.distributed_c10d._get_default_store()

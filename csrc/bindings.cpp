@@ -20,12 +20,12 @@ int ca_sumsq(const void*, int, long, float*, hipStream_t);
 int ca_scale(void*, int, long, const float*, hipStream_t);
 long ca_bn_workspace_floats(long, int);
 int ca_bn_fwd(const bf16_t*, const bf16_t*, bf16_t*, long, int, const float*, const float*, float, float,
-              float*, float*, float*, float*, float*, float*, int, hipStream_t);
+              float*, float*, float*, float*, float*, float*, int, uint8_t*, hipStream_t);
 int ca_bn_apply(const bf16_t*, const bf16_t*, bf16_t*, long, int, const float*, int, hipStream_t);
 int ca_bn_fwd_partials(const bf16_t*, const bf16_t*, bf16_t*, long, int, const float*, int, const float*, const float*,
-                       float, float, float*, float*, float*, float*, float*, int, hipStream_t);
-int ca_bn_bwd(const bf16_t*, const bf16_t*, const bf16_t*, long, int, const float*, const float*, const float*,
-              bf16_t*, bf16_t*, float*, float*, float*, float*, int, hipStream_t);
+                       float, float, float*, float*, float*, float*, float*, int, uint8_t*, float*, hipStream_t);
+int ca_bn_bwd(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, long, int, const float*, const float*,
+              const float*, bf16_t*, bf16_t*, float*, float*, float*, float*, int, hipStream_t);
 int ca_softmax_xent(const void*, int, const int64_t*, int, int, float, float, float*, float*, void*, hipStream_t);
 int ca_maxpool_fwd(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ca_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -101,25 +101,28 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("bn_workspace_floats", [](long M, int C) { return ca_bn_workspace_floats(M, C); });
   m.def("bn_fwd", [](u64 x, u64 res, u64 y, long M, int C, u64 gamma, u64 beta, float eps, float momentum,
-                     u64 rm, u64 rv, u64 sm, u64 sr, u64 ss, u64 ws, int relu, u64 s) {
+                     u64 rm, u64 rv, u64 sm, u64 sr, u64 ss, u64 ws, int relu, u64 mask, u64 s) {
     check(ca_bn_fwd(P(const bf16_t*, x), P(const bf16_t*, res), P(bf16_t*, y), M, C, P(const float*, gamma),
                     P(const float*, beta), eps, momentum, P(float*, rm), P(float*, rv), P(float*, sm), P(float*, sr),
-                    P(float*, ss), P(float*, ws), relu, S(s)), "bn_fwd");
+                    P(float*, ss), P(float*, ws), relu, P(uint8_t*, mask), S(s)), "bn_fwd");
   });
   m.def("bn_fwd_partials", [](u64 x, u64 res, u64 y, long M, int C, u64 parts, int nparts, u64 gamma, u64 beta,
-                              float eps, float momentum, u64 rm, u64 rv, u64 sm, u64 sr, u64 ss, int relu, u64 s) {
+                              float eps, float momentum, u64 rm, u64 rv, u64 sm, u64 sr, u64 ss, int relu, u64 mask,
+                              u64 gws, u64 s) {
     check(ca_bn_fwd_partials(P(const bf16_t*, x), P(const bf16_t*, res), P(bf16_t*, y), M, C, P(const float*, parts),
                              nparts, P(const float*, gamma), P(const float*, beta), eps, momentum, P(float*, rm),
-                             P(float*, rv), P(float*, sm), P(float*, sr), P(float*, ss), relu, S(s)),
+                             P(float*, rv), P(float*, sm), P(float*, sr), P(float*, ss), relu, P(uint8_t*, mask),
+                             P(float*, gws), S(s)),
           "bn_fwd_partials");
   });
   m.def("bn_apply", [](u64 x, u64 res, u64 y, long M, int C, u64 ss, int relu, u64 s) {
     check(ca_bn_apply(P(const bf16_t*, x), P(const bf16_t*, res), P(bf16_t*, y), M, C, P(const float*, ss), relu,
                       S(s)), "bn_apply");
   });
-  m.def("bn_bwd", [](u64 dy, u64 y, u64 x, long M, int C, u64 gamma, u64 sm, u64 sr, u64 dx, u64 dres, u64 dg,
-                     u64 db, u64 coef, u64 ws, int relu, u64 s) {
-    check(ca_bn_bwd(P(const bf16_t*, dy), P(const bf16_t*, y), P(const bf16_t*, x), M, C, P(const float*, gamma),
+  m.def("bn_bwd", [](u64 dy, u64 y, u64 mask, u64 x, long M, int C, u64 gamma, u64 sm, u64 sr, u64 dx, u64 dres,
+                     u64 dg, u64 db, u64 coef, u64 ws, int relu, u64 s) {
+    check(ca_bn_bwd(P(const bf16_t*, dy), P(const bf16_t*, y), P(const uint8_t*, mask), P(const bf16_t*, x), M, C,
+                    P(const float*, gamma),
                     P(const float*, sm), P(const float*, sr), P(bf16_t*, dx), P(bf16_t*, dres), P(float*, dg),
                     P(float*, db), P(float*, coef), P(float*, ws), relu, S(s)), "bn_bwd");
   });

@@ -73,7 +73,22 @@ struct CoreParams {
   bf16_t* preact;         // [M][ld_aux] or null
   const bf16_t* dact_src; // [M][ld_aux] or null (backward: multiply by act'(src))
   long ld_aux;
+  // strided-conv dgrad by output-parity class (conv.hip): GEMM row m = (n, qy, qx) of
+  // the class is stored at input pixel (n, s*qy + py, s*qx + px); taps kh = kh0 + s*th.
+  int rowmap;
+  int dg_py, dg_px, dg_kh0, dg_kw0, dg_nh, dg_nw, dg_dy0, dg_dx0, Hq, Wq;
+  FastDiv div_wq, div_hq, div_nw;
 };
+
+// output row of GEMM row gm (identity unless the parity-class row map is on)
+__device__ __forceinline__ long out_row(const CoreParams& P, int gm) {
+  if (!P.rowmap) return gm;
+  const uint32_t t = fdiv((uint32_t)gm, P.div_wq);
+  const int qx = gm - (int)t * P.Wq;
+  const uint32_t n = fdiv(t, P.div_hq);
+  const int qy = (int)t - (int)n * P.Hq;
+  return ((long)n * P.H + P.sh * qy + P.dg_py) * P.W + P.sw * qx + P.dg_px;
+}
 
 enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_GELU_TANH = 4 };
 
@@ -268,7 +283,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
       const int gm = m0 + row, gn = n0 + col;
       if (gm < P.M && gn < P.N) {
         s8v v = *reinterpret_cast<const s8v*>(Cs + row * EPI_LD + col);
-        bf16_t* dst = Cg + (long)gm * P.ldc + gn;
+        bf16_t* dst = Cg + out_row(P, gm) * P.ldc + gn;
         if (fx) {
           if (P.preact) *reinterpret_cast<s8v*>(P.preact + (long)gm * P.ld_aux + gn) = v;
           if (P.dact_src) {
@@ -528,18 +543,28 @@ struct GDenseNC {
 };
 
 template <int BM, int BN, int WM, int WN, template <int, int, int> class LAT, template <int, int, int> class LBT,
-          int EPI>
+          int EPI, int NSTAGE = 1>
 __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
+  // Measured on MI355X (bench/conv_shapes.py, bench/gemm_core_ab.py): NSTAGE 1 at
+  // 4 blocks/CU beats NSTAGE 2 at 2 blocks/CU by 10-15% on every ResNet/BERT shape.
+  // NSTAGE 1: load -> wait -> barrier -> MFMA -> barrier; latency hidden by ~4
+  //           co-resident blocks (34 KB LDS each).
+  // NSTAGE 2: the DMA of K tile t+1 is in flight while tile t is multiplied; a
+  //           counted s_waitcnt vmcnt(loads per tile) retires exactly tile t and
+  //           RAW s_barriers (not __syncthreads, whose fence would drain the
+  //           in-flight DMA with vmcnt(0)) order the LDS image.
   constexpr int NT = WM * WN * 64;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
   constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;
+  constexpr int STAGE = A_ELEMS + B_ELEMS;
   constexpr int EPI_LD = BN + PAD;
-  constexpr int SMEM = (A_ELEMS + B_ELEMS > BM * EPI_LD ? A_ELEMS + B_ELEMS : BM * EPI_LD);
+  constexpr int SMEM = (NSTAGE * STAGE > BM * EPI_LD ? NSTAGE * STAGE : BM * EPI_LD);
   constexpr int CPA = A_ELEMS / 8 / NT, CPB = B_ELEMS / 8 / NT;
   using LA = LAT<BM, CPA, NT>;
   using LB = LBT<BN, CPB, NT>;
   constexpr bool A_KC = LA::KC, B_KC = LB::KC;
   static_assert(A_ELEMS % (8 * NT) == 0 && B_ELEMS % (8 * NT) == 0, "tile chunks must divide threads");
+  static_assert(CPA + CPB < 64, "vmcnt range");
   __shared__ __attribute__((aligned(16))) short smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -555,8 +580,6 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
 
   const LA la(P, true, m0, tid);
   const LB lb(P, false, n0, tid);
-  short* As = smem;
-  short* Bs = smem + A_ELEMS;
 
   f4v acc[FM][FN];
 #pragma unroll
@@ -564,18 +587,19 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  for (int t = 0; t < nk; ++t) {
+  auto issue = [&](int t, short* base) {
     const int k0 = kbeg + t * BK;
 #pragma unroll
     for (int i = 0; i < CPA; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)la.src(i, k0), (lds_void*)(As + (i * NT + wave * 64) * 8), 16,
+      __builtin_amdgcn_global_load_lds((const void*)la.src(i, k0), (lds_void*)(base + (i * NT + wave * 64) * 8), 16,
                                        0, 0);
 #pragma unroll
     for (int i = 0; i < CPB; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)lb.src(i, k0), (lds_void*)(Bs + (i * NT + wave * 64) * 8), 16,
-                                       0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+      __builtin_amdgcn_global_load_lds((const void*)lb.src(i, k0),
+                                       (lds_void*)(base + A_ELEMS + (i * NT + wave * 64) * 8), 16, 0, 0);
+  };
+  auto compute = [&](const short* As) {
+    const short* Bs = As + A_ELEMS;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 af[FM], bfr[FN];
@@ -589,7 +613,30 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
+  };
+
+  if constexpr (NSTAGE == 1) {
+    for (int t = 0; t < nk; ++t) {
+      issue(t, smem);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      compute(smem);
+      __syncthreads();
+    }
+  } else {
+    if (nk > 0) issue(0, smem);
+    for (int t = 0; t < nk; ++t) {
+      if (t + 1 < nk) {
+        issue(t + 1, smem + ((t + 1) & 1) * STAGE);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CPA + CPB) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      compute(smem + (t & 1) * STAGE);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
   }
   gemm_epilogue<BM, BN, WM, WN, EPI>(P, acc, smem, m0, n0, tm, tid);
 }

@@ -3,9 +3,10 @@
 //
 // Forward  : stats (1 read)  -> finalize (per-channel, tiny) -> apply (1 read + 1 write
 //            [+1 read residual]).
-// Backward : reduce (3 reads: dy, y, x) -> finalize -> apply (3 reads, 1-2 writes),
-//            ReLU mask recomputed from the saved output y, residual gradient emitted
-//            by the same pass.
+// Backward : reduce (dy, x + ReLU bitmask) -> finalize -> apply (same reads, 1-2
+//            writes); the ReLU mask is the 1-bit-per-channel map written by the
+//            forward apply (or recomputed from y when none was kept); the residual
+//            gradient is emitted by the same pass.
 //
 // Tiling: a block is 256 threads = TW column-vectors (8 channels, 16 B each) x RP
 // rows; each thread owns ONE column vector for the whole launch (so per-channel
@@ -86,6 +87,7 @@ __device__ __forceinline__ void wave_chunk_sum(const float* __restrict__ ws, int
                                                int c, double& a, double& b) {
   const int lane = threadIdx.x & 63;
   double sa = 0.0, sb = 0.0;
+#pragma unroll 8
   for (int k = lane; k < nchunks; k += 64) {
     sa += ws[(long)k * stride_k + c];
     sb += ws[(long)k * stride_k + off_q + c];
@@ -97,6 +99,40 @@ __device__ __forceinline__ void wave_chunk_sum(const float* __restrict__ ws, int
   }
   a = sa;
   b = sb;
+}
+
+// First level of the statistics reduction when there are many partial rows
+// (e.g. one per 128-row GEMM tile: 6272 for a 56x56x256 batch-256 layer):
+// block = 64 channels x 4 part-lanes, blockIdx.y = group g; out[g][0|1][C]
+// holds the group's sums of the two quantities (deterministic order).  The
+// finalize kernels then reduce only G rows -- enough blocks in flight instead
+// of one latency-bound wave per channel walking thousands of rows.
+__global__ void __launch_bounds__(256) chunk_group_reduce_kernel(const float* __restrict__ ws, int nchunks,
+                                                                 long stride_k, long off_q, int C,
+                                                                 float* __restrict__ out) {
+  __shared__ float ra[4][64], rb[4][64];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int G = gridDim.y, g = blockIdx.y;
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int k = g * 4 + pl; k < nchunks; k += G * 4) {
+      a += ws[(long)k * stride_k + c];
+      b += ws[(long)k * stride_k + off_q + c];
+    }
+  }
+  ra[pl][cl] = a;
+  rb[pl][cl] = b;
+  __syncthreads();
+  if (pl != 0 || c >= C) return;
+  out[(long)g * 2 * C + c] = (ra[0][cl] + ra[1][cl]) + (ra[2][cl] + ra[3][cl]);
+  out[(long)g * 2 * C + C + c] = (rb[0][cl] + rb[1][cl]) + (rb[2][cl] + rb[3][cl]);
+}
+
+int group_count(int nchunks) {
+  int g = (nchunks + 63) / 64;
+  return g < 1 ? 1 : (g > 64 ? 64 : g);
 }
 
 __global__ void __launch_bounds__(BLK) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
@@ -167,11 +203,14 @@ __global__ void bn_fwd_finalize_kernel(const float* __restrict__ ws, int nchunks
   }
 }
 
-// y = act(x*scale + shift [+ res])
+// y = act(x*scale + shift [+ res]); with a ReLU, optionally also the ReLU
+// bitmask (1 byte per 8 channels: bit j = y[c0+j] > 0) so the backward reads
+// 1/16 of the bytes of y for its mask.
 template <bool RELU, bool RES>
 __global__ void __launch_bounds__(BLK) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                       const float* __restrict__ scale, const float* __restrict__ shift,
-                                                      bf16_t* __restrict__ y, long M, int C) {
+                                                      bf16_t* __restrict__ y, uint8_t* __restrict__ mask, long M,
+                                                      int C) {
   const Tiling t = make_tiling(M, C);
   const int tx = threadIdx.x % t.TW, ty = threadIdx.x / t.TW;
   const int vc = blockIdx.x * t.TW + tx;
@@ -189,20 +228,41 @@ __global__ void __launch_bounds__(BLK) bn_apply_kernel(const bf16_t* __restrict_
     ld8bf(x + o, v);
     float rv[8];
     if (RES) ld8bf(res + o, rv);
+    uint32_t bits = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float z = v[j] * sc[j] + sh[j];
       if (RES) z += rv[j];
-      if (RELU) z = fmaxf(z, 0.f);
+      if (RELU) {
+        z = fmaxf(z, 0.f);
+        bits |= (z > 0.f ? 1u : 0u) << j;
+      }
       v[j] = z;
     }
     st8bf(y + o, v);
+    if (RELU && mask) mask[r * t.CT + vc] = (uint8_t)bits;
   }
 }
 
-// Backward reduce: dz = dy * (y > 0 if RELU); partial sums of dz and dz*xhat.
+__device__ __forceinline__ void relu_gate(float (&d)[8], const bf16_t* __restrict__ y, const uint8_t* __restrict__ mask,
+                                          long r, long o, int CT, int vc) {
+  if (mask) {
+    const uint32_t m = mask[r * CT + vc];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = ((m >> j) & 1u) ? d[j] : 0.f;
+  } else {
+    float yv[8];
+    ld8bf(y + o, yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = yv[j] > 0.f ? d[j] : 0.f;
+  }
+}
+
+// Backward reduce: dz = dy * relu'(y) (from the bitmask, or y when no mask);
+// partial sums of dz and dz*xhat.
 template <bool RELU>
 __global__ void __launch_bounds__(BLK) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                           const uint8_t* __restrict__ mask,
                                                            const bf16_t* __restrict__ x,
                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
                                                            long M, int C, float* __restrict__ ws) {
@@ -222,32 +282,31 @@ __global__ void __launch_bounds__(BLK) bn_bwd_reduce_kernel(const bf16_t* __rest
     long r = r0 + ty;
     for (; r + t.RP < r1; r += 2 * t.RP) {
       const long o0 = r * C + off0, o1 = (r + t.RP) * C + off0;
-      float d0[8], x0[8], d1[8], x1[8], y0[8], y1[8];
+      float d0[8], x0[8], d1[8], x1[8];
       ld8bf(dy + o0, d0);
       ld8bf(x + o0, x0);
       ld8bf(dy + o1, d1);
       ld8bf(x + o1, x1);
-      if (RELU) { ld8bf(y + o0, y0); ld8bf(y + o1, y1); }
+      if (RELU) {
+        relu_gate(d0, y, mask, r, o0, t.CT, vc);
+        relu_gate(d1, y, mask, r + t.RP, o1, t.CT, vc);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float a = d0[j], b = d1[j];
-        if (RELU) { a = y0[j] > 0.f ? a : 0.f; b = y1[j] > 0.f ? b : 0.f; }
-        sd[j] += a + b;
-        sdx[j] += a * (x0[j] - mu[j]) * rs[j] + b * (x1[j] - mu[j]) * rs[j];
+        sd[j] += d0[j] + d1[j];
+        sdx[j] += d0[j] * (x0[j] - mu[j]) * rs[j] + d1[j] * (x1[j] - mu[j]) * rs[j];
       }
     }
     for (; r < r1; r += t.RP) {
       const long o0 = r * C + off0;
-      float d0[8], x0[8], y0[8];
+      float d0[8], x0[8];
       ld8bf(dy + o0, d0);
       ld8bf(x + o0, x0);
-      if (RELU) ld8bf(y + o0, y0);
+      if (RELU) relu_gate(d0, y, mask, r, o0, t.CT, vc);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float a = d0[j];
-        if (RELU) a = y0[j] > 0.f ? a : 0.f;
-        sd[j] += a;
-        sdx[j] += a * (x0[j] - mu[j]) * rs[j];
+        sd[j] += d0[j];
+        sdx[j] += d0[j] * (x0[j] - mu[j]) * rs[j];
       }
     }
   }
@@ -256,14 +315,15 @@ __global__ void __launch_bounds__(BLK) bn_bwd_reduce_kernel(const bf16_t* __rest
 
 // dgamma = sum(dz*xhat), dbeta = sum(dz); coefficients so that
 // dx = A*dz + B*x + D.
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ ws, int nchunks, long M, int C,
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ ws, int nchunks, long stride_k, long off_q, long M,
+                                       int C,
                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ rstd, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta, float* __restrict__ coef, int accum) {
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
   double sd, sdx;
-  wave_chunk_sum(ws, nchunks, (long)C, (long)nchunks * C, c, sd, sdx);
+  wave_chunk_sum(ws, nchunks, stride_k, off_q, c, sd, sdx);
   if ((threadIdx.x & 63) != 0) return;
   // accum: parameter grads are summed into (flat arena slots), not overwritten
   if (dgamma) dgamma[c] = (float)sdx + (accum ? dgamma[c] : 0.f);
@@ -279,6 +339,7 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ ws, int nchunks
 
 template <bool RELU, bool DRES>
 __global__ void __launch_bounds__(BLK) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                          const uint8_t* __restrict__ mask,
                                                           const bf16_t* __restrict__ x, const float* __restrict__ coef,
                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
                                                           long M, int C) {
@@ -299,14 +360,10 @@ __global__ void __launch_bounds__(BLK) bn_bwd_apply_kernel(const bf16_t* __restr
   const long off0 = (long)vc * 8;
   for (long r = r0 + ty; r < r1; r += t.RP) {
     const long o = r * C + off0;
-    float d[8], xv[8], yv[8];
+    float d[8], xv[8];
     ld8bf(dy + o, d);
     ld8bf(x + o, xv);
-    if (RELU) ld8bf(y + o, yv);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (RELU) d[j] = yv[j] > 0.f ? d[j] : 0.f;
-    }
+    if (RELU) relu_gate(d, y, mask, r, o, t.CT, vc);
     if (DRES) st8bf(dres + o, d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = A[j] * d[j] + B[j] * xv[j] + D[j];
@@ -321,13 +378,13 @@ extern "C" {
 // Workspace floats needed by the stats / bwd-reduce kernels: 2 * nchunks * C.
 long ca_bn_workspace_floats(long M, int C) {
   Tiling t = make_tiling(M, C);
-  return 2L * t.nchunks * C;
+  return 2L * t.nchunks * C + 2L * 64 * C;
 }
 
 int ca_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
               const float* gamma, const float* beta, float eps, float momentum,
               float* run_mean, float* run_var, float* save_mean, float* save_rstd,
-              float* scale_shift /* [2C] */, float* ws, int relu, hipStream_t s) {
+              float* scale_shift /* [2C] */, float* ws, int relu, uint8_t* mask, hipStream_t s) {
   if (C % 8 != 0) return -1;
   Tiling t = make_tiling(M, C);
   dim3 grid(t.ncol, t.nchunks);
@@ -338,10 +395,10 @@ int ca_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
                                                          run_mean, run_var, save_mean, save_rstd,
                                                          scale_shift, scale_shift + C);
   CA_LAUNCH_CHECK();
-  if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
-  else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
-  else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
-  else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
   CA_LAUNCH_CHECK();
   return 0;
 }
@@ -351,18 +408,28 @@ int ca_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
 int ca_bn_fwd_partials(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, const float* partials,
                        int nparts, const float* gamma, const float* beta, float eps, float momentum,
                        float* run_mean, float* run_var, float* save_mean, float* save_rstd,
-                       float* scale_shift, int relu, hipStream_t s) {
+                       float* scale_shift, int relu, uint8_t* mask, float* gws /* [64][2][C] or null */,
+                       hipStream_t s) {
   if (C % 8 != 0) return -1;
   Tiling t = make_tiling(M, C);
   dim3 grid(t.ncol, t.nchunks);
-  bn_fwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(partials, nparts, 2L * C, (long)C, M, C, gamma, beta, eps,
+  const float* fin = partials;
+  int nfin = nparts;
+  if (nparts > 64 && gws) {
+    const int G = group_count(nparts);
+    chunk_group_reduce_kernel<<<dim3(ca_cdiv(C, 64), G), 256, 0, s>>>(partials, nparts, 2L * C, (long)C, C, gws);
+    CA_LAUNCH_CHECK();
+    fin = gws;
+    nfin = G;
+  }
+  bn_fwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(fin, nfin, 2L * C, (long)C, M, C, gamma, beta, eps,
                                                          momentum, run_mean, run_var, save_mean, save_rstd,
                                                          scale_shift, scale_shift + C);
   CA_LAUNCH_CHECK();
-  if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
-  else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
-  else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
-  else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
   CA_LAUNCH_CHECK();
   return 0;
 }
@@ -370,18 +437,20 @@ int ca_bn_fwd_partials(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, in
 // Inference / frozen-stat apply with precomputed scale/shift.
 int ca_bn_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
                 const float* scale_shift, int relu, hipStream_t s) {
+  uint8_t* mask = nullptr;
   if (C % 8 != 0) return -1;
   Tiling t = make_tiling(M, C);
   dim3 grid(t.ncol, t.nchunks);
-  if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
-  else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
-  else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
-  else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, M, C);
+  if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
   CA_LAUNCH_CHECK();
   return 0;
 }
 
-int ca_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, long M, int C,
+// y may be null when `mask` (the forward's ReLU bitmask) is given.
+int ca_bn_bwd(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16_t* x, long M, int C,
               const float* gamma, const float* save_mean, const float* save_rstd,
               bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta,
               float* coef /* [3C] */, float* ws, int relu, hipStream_t s) {
@@ -390,16 +459,22 @@ int ca_bn_bwd(const bf16_t* dy, const bf16_t* y, const bf16_t* x, long M, int C,
   relu &= 1;
   Tiling t = make_tiling(M, C);
   dim3 grid(t.ncol, t.nchunks);
-  if (relu) bn_bwd_reduce_kernel<true><<<grid, BLK, 0, s>>>(dy, y, x, save_mean, save_rstd, M, C, ws);
-  else bn_bwd_reduce_kernel<false><<<grid, BLK, 0, s>>>(dy, y, x, save_mean, save_rstd, M, C, ws);
+  if (relu) bn_bwd_reduce_kernel<true><<<grid, BLK, 0, s>>>(dy, y, mask, x, save_mean, save_rstd, M, C, ws);
+  else bn_bwd_reduce_kernel<false><<<grid, BLK, 0, s>>>(dy, y, mask, x, save_mean, save_rstd, M, C, ws);
   CA_LAUNCH_CHECK();
-  bn_bwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(ws, t.nchunks, M, C, gamma, save_mean, save_rstd,
+  // ws = [nchunks][C] (a) ++ [nchunks][C] (b); group-reduce into the tail of ws
+  float* gws = ws + 2L * t.nchunks * C;
+  const int G = group_count(t.nchunks);
+  chunk_group_reduce_kernel<<<dim3(ca_cdiv(C, 64), G), 256, 0, s>>>(ws, t.nchunks, (long)C, (long)t.nchunks * C, C,
+                                                                     gws);
+  CA_LAUNCH_CHECK();
+  bn_bwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(gws, G, 2L * C, (long)C, M, C, gamma, save_mean, save_rstd,
                                                          dgamma, dbeta, coef, accum);
   CA_LAUNCH_CHECK();
-  if (relu && dres) bn_bwd_apply_kernel<true, true><<<grid, BLK, 0, s>>>(dy, y, x, coef, dx, dres, M, C);
-  else if (relu) bn_bwd_apply_kernel<true, false><<<grid, BLK, 0, s>>>(dy, y, x, coef, dx, dres, M, C);
-  else if (dres) bn_bwd_apply_kernel<false, true><<<grid, BLK, 0, s>>>(dy, y, x, coef, dx, dres, M, C);
-  else bn_bwd_apply_kernel<false, false><<<grid, BLK, 0, s>>>(dy, y, x, coef, dx, dres, M, C);
+  if (relu && dres) bn_bwd_apply_kernel<true, true><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
+  else if (relu) bn_bwd_apply_kernel<true, false><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
+  else if (dres) bn_bwd_apply_kernel<false, true><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
+  else bn_bwd_apply_kernel<false, false><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
   CA_LAUNCH_CHECK();
   return 0;
 }

@@ -12,6 +12,8 @@
 // Every operand chunk is 8 consecutive channels of one pixel (16 B), gathered
 // per lane; the MFMA core (ca_mfma_core.h) does the rest.  wgrad is split-K
 // over the N*OH*OW reduction with fp32 slabs.
+#include <stdlib.h>
+
 #include "ca_mfma_core.h"
 
 namespace {
@@ -180,14 +182,245 @@ struct ConvWgradB {
   }
 };
 
+// ---------------------------------------------------------------------------
+// LDS-DMA (glds) versions of the gather loaders: they return the 16-B source
+// address of each chunk (the zero page for padding / out-of-range taps) and
+// follow the swizzled chunk order of mfma_gemm_glds (ca_mfma_core.h).  Row
+// (pixel) state that differs per chunk is precomputed; the swizzled column
+// slot is the same for every chunk of a thread.
+
+template <int R, int CPT, int NT>
+struct GConvFwdA {
+  static constexpr bool KC = true;
+  const CoreParams& P;
+  const bf16_t* nbase[CPT];
+  int iy0[CPT], ix0[CPT];
+  int col;
+  __device__ GConvFwdA(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    const int row_t = tid >> 3;
+    col = ((tid & 7) ^ (row_t & 7)) << 3;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int m = r0 + row_t + i * (NT / 8);
+      if (m < P.M) {
+        const Pix o = decode((uint32_t)m, P.div_ow, P.div_oh);
+        nbase[i] = P.A + (long)o.n * P.H * P.W * P.Cin;
+        iy0[i] = o.y * P.sh - P.ph;
+        ix0[i] = o.x * P.sw - P.pw;
+      } else {
+        nbase[i] = P.A;
+        iy0[i] = -(1 << 29);
+        ix0[i] = 0;
+      }
+    }
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const int k = k0 + col;
+    if (k >= P.K) return ca_zero16;
+    int tap, ci;
+    tap_split(k, k0, P.Cin, P.div_cin, P.cin_tile, tap, ci);
+    const int kh = (int)fdiv((uint32_t)tap, P.div_kw), kw = tap - kh * P.KW;
+    const int ih = iy0[i] + kh, iw = ix0[i] + kw;
+    if ((unsigned)ih >= (unsigned)P.H || (unsigned)iw >= (unsigned)P.W) return ca_zero16;
+    return nbase[i] + ((long)ih * P.W + iw) * P.Cin + ci;
+  }
+};
+
+template <int R, int CPT, int NT>
+struct GConvDgradA {
+  static constexpr bool KC = true;
+  const CoreParams& P;
+  const bf16_t* nbase[CPT];
+  int iy[CPT], ix[CPT];
+  int col;
+  __device__ GConvDgradA(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    const int row_t = tid >> 3;
+    col = ((tid & 7) ^ (row_t & 7)) << 3;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int m = r0 + row_t + i * (NT / 8);
+      if (m < P.M) {
+        const Pix q = decode((uint32_t)m, P.div_w, P.div_h);
+        nbase[i] = P.A + (long)q.n * P.OH * P.OW * P.Cout;
+        iy[i] = q.y + P.ph;
+        ix[i] = q.x + P.pw;
+      } else {
+        nbase[i] = P.A;
+        iy[i] = -(1 << 29);
+        ix[i] = 0;
+      }
+    }
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const int k = k0 + col;
+    if (k >= P.K) return ca_zero16;
+    int tap, co;
+    tap_split(k, k0, P.Cout, P.div_cout, P.cout_tile, tap, co);
+    const int kh = (int)fdiv((uint32_t)tap, P.div_kw), kw = tap - kh * P.KW;
+    int oy = iy[i] - kh, ox = ix[i] - kw;
+    if (oy < 0 || ox < 0) return ca_zero16;
+    if (P.sh > 1) {
+      if (oy % P.sh) return ca_zero16;
+      oy /= P.sh;
+    }
+    if (P.sw > 1) {
+      if (ox % P.sw) return ca_zero16;
+      ox /= P.sw;
+    }
+    if (oy >= P.OH || ox >= P.OW) return ca_zero16;
+    return nbase[i] + ((long)oy * P.OW + ox) * P.Cout + co;
+  }
+};
+
+// B of dgrad: B[k=(tap,co)][ci] = W[co][tap][ci] (NC).
+template <int R, int CPT, int NT>
+struct GConvDgradB {
+  static constexpr bool KC = false;
+  const CoreParams& P;
+  int krow0, ci;
+  __device__ GConvDgradB(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    constexpr int CPR = R / 8;
+    const int k = tid / CPR, pc = tid % CPR;
+    int n = r0 + ((pc ^ nc_swz<R>(k)) << 3);
+    if (n > P.N - 8) n = P.N - 8;
+    ci = n;
+    krow0 = k;
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const int k = k0 + krow0 + i * (NT * 8 / R);
+    if (k >= P.K) return ca_zero16;
+    int tap, co;
+    tap_split(k, k0, P.Cout, P.div_cout, P.cout_tile, tap, co);
+    return P.B + ((long)co * (P.KH * P.KW) + tap) * P.Cin + ci;
+  }
+};
+
+// B of wgrad: B[k=(n,oh,ow)][j=(tap,ci)] = X[n, oh*s-p+kh, ow*s-p+kw, ci] (NC).
+template <int R, int CPT, int NT>
+struct GConvWgradB {
+  static constexpr bool KC = false;
+  const CoreParams& P;
+  int krow0, kh, kw, ci;
+  __device__ GConvWgradB(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    constexpr int CPR = R / 8;
+    const int k = tid / CPR, pc = tid % CPR;
+    int j = r0 + ((pc ^ nc_swz<R>(k)) << 3);
+    if (j > P.N - 8) j = P.N - 8;
+    int tap, cc;
+    tap_split(j, 0, P.Cin, P.div_cin, false, tap, cc);
+    kh = (int)fdiv((uint32_t)tap, P.div_kw);
+    kw = tap - kh * P.KW;
+    ci = cc;
+    krow0 = k;
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const int k = k0 + krow0 + i * (NT * 8 / R);
+    if (k >= P.K) return ca_zero16;
+    const Pix o = decode((uint32_t)k, P.div_ow, P.div_oh);
+    const int ih = o.y * P.sh - P.ph + kh, iw = o.x * P.sw - P.pw + kw;
+    if ((unsigned)ih >= (unsigned)P.H || (unsigned)iw >= (unsigned)P.W) return ca_zero16;
+    return P.B + (((long)o.n * P.H + ih) * P.W + iw) * P.Cin + ci;
+  }
+};
+
+// ---- strided dgrad by output-parity class (sub-pixel decomposition) ----------
+// For stride s the input pixels with (iy % s, ix % s) = (py, px) only receive
+// taps kh = kh0 + s*th (kh0 = (py + ph) % s), kw likewise, from dY row
+// oy = qy + dy0 - th.  One GEMM per class: M = N*Hq*Wq, K = nh*nw*Cout -- no
+// MFMA work on the (s^2-1)/s^2 structurally-zero products.
+
+// A: rows = class pixels (n, qy, qx); k = (t = th*nw + tw, co) over dY.  KC.
+template <int R, int CPT, int NT>
+struct GConvDgradSA {
+  static constexpr bool KC = true;
+  const CoreParams& P;
+  const bf16_t* nbase[CPT];
+  int qy[CPT], qx[CPT];
+  int col;
+  __device__ GConvDgradSA(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    const int row_t = tid >> 3;
+    col = ((tid & 7) ^ (row_t & 7)) << 3;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int m = r0 + row_t + i * (NT / 8);
+      if (m < P.M) {
+        const Pix q = decode((uint32_t)m, P.div_wq, P.div_hq);
+        nbase[i] = P.A + (long)q.n * P.OH * P.OW * P.Cout;
+        qy[i] = q.y + P.dg_dy0;
+        qx[i] = q.x + P.dg_dx0;
+      } else {
+        nbase[i] = P.A;
+        qy[i] = -(1 << 29);
+        qx[i] = 0;
+      }
+    }
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const int k = k0 + col;
+    if (k >= P.K) return ca_zero16;
+    int t, co;
+    tap_split(k, k0, P.Cout, P.div_cout, P.cout_tile, t, co);
+    const int th = (int)fdiv((uint32_t)t, P.div_nw), tw = t - th * P.dg_nw;
+    const int oy = qy[i] - th, ox = qx[i] - tw;
+    if ((unsigned)oy >= (unsigned)P.OH || (unsigned)ox >= (unsigned)P.OW) return ca_zero16;
+    return nbase[i] + ((long)oy * P.OW + ox) * P.Cout + co;
+  }
+};
+
+// B: B[k=(t,co)][ci] = W[co][kh0 + s*th][kw0 + s*tw][ci]  (NC).
+template <int R, int CPT, int NT>
+struct GConvDgradSB {
+  static constexpr bool KC = false;
+  const CoreParams& P;
+  int krow0, ci;
+  __device__ GConvDgradSB(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    constexpr int CPR = R / 8;
+    const int k = tid / CPR, pc = tid % CPR;
+    int n = r0 + ((pc ^ nc_swz<R>(k)) << 3);
+    if (n > P.N - 8) n = P.N - 8;
+    ci = n;
+    krow0 = k;
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const int k = k0 + krow0 + i * (NT * 8 / R);
+    if (k >= P.K) return ca_zero16;
+    int t, co;
+    tap_split(k, k0, P.Cout, P.div_cout, P.cout_tile, t, co);
+    const int th = (int)fdiv((uint32_t)t, P.div_nw), tw = t - th * P.dg_nw;
+    const int kh = P.dg_kh0 + P.sh * th, kw = P.dg_kw0 + P.sw * tw;
+    return P.B + ((long)co * (P.KH * P.KW) + kh * P.KW + kw) * P.Cin + ci;
+  }
+};
+
+template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) conv_glds_kernel(CoreParams P) {
+  mfma_gemm_glds<BM, BN, 2, 2, LA, LB, EPI>(P);
+}
+
+// CLOUD_AMD_GEMM_CORE=reg selects the register-staged core (A/B comparisons).
+bool use_glds() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_GEMM_CORE");
+    v = (e && e[0] == 'r') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
 __global__ void __launch_bounds__(256) conv_gemm_kernel(CoreParams P) {
   mfma_gemm_body<BM, BN, 2, 2, LA, LB, EPI, 2>(P);
 }
 
-template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
+template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB,
+          template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
 int launch(const CoreParams& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  if (use_glds()) {
+    conv_glds_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
+    CA_LAUNCH_CHECK();
+    return 0;
+  }
   conv_gemm_kernel<BM, BN, LA, LB, EPI><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
   CA_LAUNCH_CHECK();
   return 0;
@@ -225,8 +458,8 @@ int ca_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   p.A = x; p.B = w; p.lda = Cin; p.ldb = (long)KH * KW * Cin; p.C = y; p.ldc = Cout;
   p.M = Nb * p.OH * p.OW; p.N = Cout; p.K = KH * KW * Cin; p.k_per_split = p.K;
   p.stats = stats;
-  if (Cout <= 64) return launch<128, 64, ConvFwdA, DenseKC, EPI_BF16>(p, 1, s);
-  return launch<128, 128, ConvFwdA, DenseKC, EPI_BF16>(p, 1, s);
+  if (Cout <= 64) return launch<128, 64, ConvFwdA, DenseKC, GConvFwdA, GDenseKC, EPI_BF16>(p, 1, s);
+  return launch<128, 128, ConvFwdA, DenseKC, GConvFwdA, GDenseKC, EPI_BF16>(p, 1, s);
 }
 
 // dx[Nb,H,W,Cin] = dgrad(dy[Nb,OH,OW,Cout], w) (+ beta * dx).
@@ -237,8 +470,38 @@ int ca_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb, int H, 
   p.A = dy; p.B = w; p.C = dx; p.ldc = Cin;
   p.M = Nb * H * W; p.N = Cin; p.K = KH * KW * Cout; p.k_per_split = p.K;
   p.beta = beta;
-  if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, EPI_BF16>(p, 1, s);
-  return launch<128, 128, ConvDgradA, ConvDgradB, EPI_BF16>(p, 1, s);
+  if ((sh > 1 || sw > 1) && use_glds()) {
+    // one GEMM per output-parity class; classes without taps get zeros (or beta*dx)
+    for (int py = 0; py < sh; ++py)
+      for (int px = 0; px < sw; ++px) {
+        CoreParams q = p;
+        q.rowmap = 1;
+        q.dg_py = py;
+        q.dg_px = px;
+        q.dg_kh0 = (py + ph) % sh;
+        q.dg_kw0 = (px + pw) % sw;
+        q.dg_nh = q.dg_kh0 < KH ? (KH - q.dg_kh0 + sh - 1) / sh : 0;
+        q.dg_nw = q.dg_kw0 < KW ? (KW - q.dg_kw0 + sw - 1) / sw : 0;
+        q.dg_dy0 = (py + ph - q.dg_kh0) / sh;
+        q.dg_dx0 = (px + pw - q.dg_kw0) / sw;
+        q.Hq = (H - py + sh - 1) / sh;
+        q.Wq = (W - px + sw - 1) / sw;
+        if (q.Hq <= 0 || q.Wq <= 0) continue;
+        q.div_hq = make_fastdiv(q.Hq);
+        q.div_wq = make_fastdiv(q.Wq);
+        q.div_nw = make_fastdiv(q.dg_nw > 0 ? q.dg_nw : 1);
+        q.M = Nb * q.Hq * q.Wq;
+        q.K = q.dg_nh * q.dg_nw * Cout;
+        q.k_per_split = q.K;
+        int rc = (Cin <= 64)
+                     ? launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradSA, GConvDgradSB, EPI_BF16>(q, 1, s)
+                     : launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradSA, GConvDgradSB, EPI_BF16>(q, 1, s);
+        if (rc) return rc;
+      }
+    return 0;
+  }
+  if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI_BF16>(p, 1, s);
+  return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI_BF16>(p, 1, s);
 }
 
 // dw[Cout, KH*KW*Cin] (+)= wgrad(dy, x) via split-K fp32 slabs in ws[splits][Cout][KH*KW*Cin].
@@ -254,8 +517,8 @@ int ca_conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, floa
   splits = (p.K + kps - 1) / kps;
   p.k_per_split = kps;
   p.C = ws; p.ldc = p.N; p.split_stride = (long)p.M * p.N;
-  int rc = (p.N <= 64) ? launch<128, 64, DenseNC, ConvWgradB, EPI_F32_PARTIAL>(p, splits, s)
-                       : launch<128, 128, DenseNC, ConvWgradB, EPI_F32_PARTIAL>(p, splits, s);
+  int rc = (p.N <= 64) ? launch<128, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s)
+                       : launch<128, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s);
   if (rc) return rc;
   return ca_splitk_reduce(ws, splits, (long)p.M * p.N, dw, dw_bf16, beta, s);
 }
