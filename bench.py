@@ -93,17 +93,23 @@ def main():
     y = torch.randint(0, args.classes, (B,), generator=gen, device=device)
     global_batch = B * world
 
+    from cloud_amd.utils import trace
+
     def fwd_bwd():
-        logits = model(x)
-        loss, _ = softmax_cross_entropy(logits, y, denom=B)
-        loss.backward()
+        with trace.range("forward"):
+            logits = model(x)
+            loss, _ = softmax_cross_entropy(logits, y, denom=B)
+        with trace.range("backward"):
+            loss.backward()
         return loss
 
     def train_step():
         opt.zero_grad()
         loss = fwd_bwd()
-        reducer.finish()
-        opt.step()
+        with trace.range("allreduce_join"):
+            reducer.finish()
+        with trace.range("optimizer"):
+            opt.step()
         return loss
 
     # first step = end-to-end "first-step latency" (process start -> step done)

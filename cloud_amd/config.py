@@ -1,0 +1,104 @@
+"""The ``CLOUD_AMD_*`` environment namespace in one place.
+
+Every switch the framework reads is declared here with its type, default and
+meaning; ``get(name)`` parses it.  ``python -m cloud_amd.config`` prints the
+table.  A test (``tests/test_config_env.py``) fails if code reads a
+``CLOUD_AMD_*`` variable that is not declared here.  The reference-compatible
+variables (``TF_CONFIG``, ``TF_KERAS_RUNNING_REMOTELY``) keep their names.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+
+@dataclass(frozen=True)
+class Var:
+    name: str
+    type: type
+    default: object
+    doc: str
+    area: str
+
+
+_VARS = [
+    # launcher / run()
+    Var("CLOUD_AMD_JOBS_DIR", str, "./jobs", "where run() stages job directories", "launcher"),
+    Var("CLOUD_AMD_NUM_GPUS", int, None, "override the visible-GPU count (0 = CPU node)", "launcher"),
+    Var("CLOUD_AMD_RUNNING_REMOTELY", str, "", "set by the launcher inside job ranks (remote() is True)", "launcher"),
+    Var("CLOUD_AMD_JOB_ID", str, "", "job id (set in every rank)", "launcher"),
+    Var("CLOUD_AMD_JOB_DIR", str, "", "job directory (set in every rank)", "launcher"),
+    Var("CLOUD_AMD_LAUNCH_TIME", float, None, "launcher spawn time, epoch seconds (set in every rank)", "launcher"),
+    Var("CLOUD_AMD_RUN_T0", float, None, "run() entry time, for run()->first-step latency (set in ranks)",
+        "launcher"),
+    Var("CLOUD_AMD_PIP_INSTALL", bool, False, "pip install --user the job's requirements (needs an index)",
+        "launcher"),
+    Var("CLOUD_AMD_REGION", str, "local", "region string reported by topology.get_region()", "launcher"),
+    Var("CLOUD_AMD_PROJECT", str, "local", "project name reported to the tuner / cloud_fit", "launcher"),
+    Var("CLOUD_AMD_DEVICE", str, None, "force the strategy device (e.g. 'cpu')", "launcher"),
+    Var("CLOUD_AMD_PG_TIMEOUT_S", float, 1800.0, "torch.distributed process-group timeout", "launcher"),
+    # kernels / ops
+    Var("CLOUD_AMD_OPS", str, "native", "'native' HIP kernels or 'torch' stock ops", "ops"),
+    Var("CLOUD_AMD_GEMM", str, "native", "dense GEMMs: 'native' or 'torch'", "ops"),
+    Var("CLOUD_AMD_CONV", str, "native", "convolutions: 'native' or 'torch'", "ops"),
+    Var("CLOUD_AMD_GEMM_CORE", str, "glds", "GEMM/conv staging core: 'glds' (LDS-DMA) or 'reg' (register)", "ops"),
+    Var("CLOUD_AMD_PRECISION", str, "bf16", "compute dtype of the Keras front end", "ops"),
+    Var("CLOUD_AMD_ARCH", str, "gfx950", "offload arch of the native build", "build"),
+    Var("CLOUD_AMD_SANITIZE", bool, False, "build the C++ test binary with ASan/UBSan", "build"),
+    # distributed
+    Var("CLOUD_AMD_COMM", str, "torch", "DP transport: 'torch' (torch.distributed/RCCL) or 'rccl' (native)",
+        "distributed"),
+    Var("CLOUD_AMD_BUCKET_MB", float, 16.0, "gradient bucket size (MB) of the DP engine", "distributed"),
+    Var("CLOUD_AMD_GRAD_CHECK_EVERY", int, 0, "cross-rank gradient fingerprint check every N steps (0 = off)",
+        "distributed"),
+    # observability
+    Var("CLOUD_AMD_TRACE", bool, False, "emit roctx ranges (forward/backward/allreduce/optimizer)", "observability"),
+    Var("CLOUD_AMD_MONITORING_EXPORTER_ENABLED", bool, False, "start the C++ metrics exporter", "observability"),
+    Var("CLOUD_AMD_MONITORING_PROJECT_ID", str, "", "project id stamped on exported series", "observability"),
+    Var("CLOUD_AMD_MONITORING_METRICS_WHITELIST", str, "", "comma-separated metric allow-list", "observability"),
+    Var("CLOUD_AMD_MONITORING_INTERVAL_S", float, 10.0, "export interval", "observability"),
+    Var("CLOUD_AMD_MONITORING_DIR", str, None, "exporter output directory (default: the job dir)", "observability"),
+    # fault injection / tuner / data
+    Var("CLOUD_AMD_FAULT", str, "", "fault injection 'rank:step:kind' (exit|raise|hang)", "testing"),
+    Var("CLOUD_AMD_FAULT_HANG_S", float, 3600.0, "how long an injected hang sleeps", "testing"),
+    Var("CLOUD_AMD_TUNER_ID", str, None, "tuner id of a scheduler worker", "tuner"),
+    Var("CLOUD_AMD_TUNER_DIR", str, None, "default KerasTuner results directory", "tuner"),
+    Var("CLOUD_AMD_STUDY_DIR", str, None, "local study-service directory", "tuner"),
+    Var("CLOUD_AMD_HBM_GB", float, 288.0, "HBM per GPU used for trial packing", "tuner"),
+    Var("CLOUD_AMD_DATA", str, None, "directory of real .npz datasets (else synthetic)", "data"),
+    # benchmarks / examples
+    Var("CLOUD_AMD_BENCH_BATCH", int, 256, "per-GPU batch of bench.py", "bench"),
+    Var("CLOUD_AMD_GRAPH", bool, False, "capture the bench step in a HIP graph", "bench"),
+    Var("CLOUD_AMD_GRAPH_FORCE", bool, False, "allow graph capture with world > 1", "bench"),
+    Var("CLOUD_AMD_EXAMPLE_CPU", bool, False, "examples: launch CPU ranks instead of GPUs", "examples"),
+    Var("CLOUD_AMD_EXAMPLE_SMALL", bool, False, "examples: tiny datasets (tests)", "examples"),
+    Var("CLOUD_AMD_EXAMPLE_OUT", str, None, "examples: output directory", "examples"),
+]
+
+VARS = {v.name: v for v in _VARS}
+
+
+def _parse(v: Var, raw: str):
+    if v.type is bool:
+        return raw.strip().lower() in ("1", "true", "yes", "on")
+    return v.type(raw)
+
+
+def get(name: str):
+    """Typed value of a declared variable (its default when unset)."""
+    v = VARS[name]
+    raw = os.environ.get(name)
+    if raw is None or raw == "":
+        return v.default
+    return _parse(v, raw)
+
+
+def describe() -> str:
+    rows = ["%-42s %-7s %-10s %s" % ("variable", "type", "default", "meaning")]
+    for v in _VARS:
+        rows.append("%-42s %-7s %-10s %s" % (v.name, v.type.__name__, v.default, v.doc))
+    return "\n".join(rows)
+
+
+if __name__ == "__main__":
+    print(describe())

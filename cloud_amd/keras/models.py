@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from ..parallel import strategy as strat
+from ..utils import trace
 from . import callbacks as cbks
 from . import losses as losses_mod
 from . import metrics as metrics_mod
@@ -262,19 +263,23 @@ class Model(Layer):
         y = _to_torch(yb, dev) if yb is not None else None
         impl = self.optimizer.impl
         impl.zero_grad()
-        if self._fused_xent:
-            logits = self._forward_train(x)
-            loss, _ = self.loss.fused_logits_loss(logits, y)
-            pred = logits
-        else:
-            pred = self(x, training=True)
-            loss = self.loss(y, pred, sample_weight)
-        reg = self._regularization()
-        total = loss + reg if reg is not None else loss
-        total.backward()
+        with trace.range("forward"):
+            if self._fused_xent:
+                logits = self._forward_train(x)
+                loss, _ = self.loss.fused_logits_loss(logits, y)
+                pred = logits
+            else:
+                pred = self(x, training=True)
+                loss = self.loss(y, pred, sample_weight)
+            reg = self._regularization()
+            total = loss + reg if reg is not None else loss
+        with trace.range("backward"):
+            total.backward()
         if self._reducer is not None:
-            self._reducer.finish()
-        impl.step()
+            with trace.range("allreduce_join"):
+                self._reducer.finish()
+        with trace.range("optimizer"):
+            impl.step()
         n = _length(x)
         self._loss_tracker.update_state(loss.detach().float().reshape(1), sample_weight=[n])
         with torch.no_grad():

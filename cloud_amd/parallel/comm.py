@@ -92,5 +92,40 @@ class RcclComm:
     def abort(self):
         self.c.abort()
 
+    def start_watchdog(self, interval_s=1.0, on_error=None):
+        """Background thread polling ncclCommGetAsyncError: on an
+        asynchronous RCCL failure the communicator is aborted (unblocking any rank stuck
+        in a collective) and ``on_error(code)`` runs (default: log + os._exit(75) so the
+        launcher's watchdog tears the job down)."""
+        import threading
+
+        def loop():
+            while not self._stop.wait(interval_s):
+                try:
+                    err = self.c.async_error()
+                except RuntimeError:
+                    return
+                if err not in (0, 7):  # 7 = ncclInProgress
+                    self.c.abort()
+                    if on_error is not None:
+                        on_error(err)
+                    else:
+                        import sys
+
+                        print("[cloud_amd] RCCL async error %d: communicator aborted" % err, file=sys.stderr,
+                              flush=True)
+                        os._exit(75)
+                    return
+
+        self._stop = threading.Event()
+        self._wd = threading.Thread(target=loop, name="rccl-watchdog", daemon=True)
+        self._wd.start()
+        return self._wd
+
+    def stop_watchdog(self):
+        if getattr(self, "_stop", None) is not None:
+            self._stop.set()
+
     def close(self):
+        self.stop_watchdog()
         self.c.destroy()

@@ -38,6 +38,7 @@ import weakref
 import torch
 import torch.distributed as dist
 
+from ..utils import trace
 from . import comm as _comm
 
 _ACTIVE = weakref.WeakSet()
@@ -72,9 +73,12 @@ class GradAllReducer:
         mb = float(bucket_mb if bucket_mb is not None else os.environ.get("CLOUD_AMD_BUCKET_MB", 16))
         self.bucket_bytes = int(mb * (1 << 20))
         self.overlap = overlap
+        self.check_every = int(os.environ.get("CLOUD_AMD_GRAD_CHECK_EVERY", "0"))
+        self._steps = 0
         self.comm = None
         if self.world > 1 and _comm.backend() == "rccl" and self.arenas and self.arenas[0].grad.is_cuda:
             self.comm = _comm.RcclComm()  # native communicator: side stream + events
+            self.comm.start_watchdog()
         self.buckets = []
         self._param_bucket = {}
         self._next = 0
@@ -114,6 +118,7 @@ class GradAllReducer:
             self._launch_ready()
 
     def _launch(self, b):
+        trace.mark("bucket%d" % b.index)
         if self.comm is not None:
             self.comm.all_reduce(b.tensor)
         else:
@@ -138,6 +143,31 @@ class GradAllReducer:
             if b.work is not None:
                 b.work.wait()
         self.reset()
+        self._steps += 1
+        if self.check_every and self._steps % self.check_every == 0:
+            self.check_consistency()
+
+    def check_consistency(self, rtol=0.0):
+        """Desync detector: after the all-reduce every replica must hold
+        the same gradients.  Compares an fp64 (sum, sum of squares, sum of |x|) fingerprint
+        of every arena across ranks; raises RuntimeError on mismatch.  Cheap -- meant to
+        run every N steps (``CLOUD_AMD_GRAD_CHECK_EVERY``)."""
+        if self.world <= 1:
+            return True
+        fp = []
+        for a in self.arenas:
+            g = a.grad.double()
+            fp += [g.sum(), (g * g).sum(), g.abs().sum()]
+        mine = torch.stack(fp)
+        allfp = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(allfp, mine, group=self.pg)
+        ref = allfp[0]
+        for r, other in enumerate(allfp[1:], 1):
+            tol = rtol * ref.abs() + 1e-12
+            if bool(((other - ref).abs() > tol).any()):
+                raise RuntimeError("gradient desync: rank %d fingerprint %s != rank 0 %s"
+                                   % (r, other.tolist(), ref.tolist()))
+        return True
 
     def reset(self):
         for b in self.buckets:

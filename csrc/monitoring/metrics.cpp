@@ -449,14 +449,18 @@ bool Exporter::PeriodicallyExportMetrics() {
   if (!config_.enabled) return false;
   if (started_) return true;
   started_ = true;
-  stop_ = false;
+  stop_.store(false);
+  // Sleep in <= 10 ms slices on an atomic flag (no condition variable: Stop()
+  // returns promptly and the thread is clean under ThreadSanitizer).
   thread_ = std::thread([this] {
-    std::unique_lock<std::mutex> lk(mu_);
-    while (!stop_) {
-      if (cv_.wait_for(lk, std::chrono::milliseconds(config_.interval_millis), [this] { return stop_; })) break;
-      lk.unlock();
+    const auto interval = std::chrono::milliseconds(config_.interval_millis);
+    while (!stop_.load(std::memory_order_acquire)) {
+      const auto deadline = std::chrono::steady_clock::now() + interval;
+      while (!stop_.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < deadline)
+        std::this_thread::sleep_for(std::min<std::chrono::steady_clock::duration>(
+            std::chrono::milliseconds(10), deadline - std::chrono::steady_clock::now()));
+      if (stop_.load(std::memory_order_acquire)) break;
       ExportMetrics();
-      lk.lock();
     }
   });
   return true;
@@ -496,18 +500,14 @@ void Exporter::ExportMetrics() {
   if (sink_->CreateTimeSeries(req) != Status::kOk) {
     std::fprintf(stderr, "[cloud_amd.monitoring] failed to export %zu time series\n", req.time_series.size());
   }
-  ++exports_;
+  exports_.fetch_add(1, std::memory_order_release);
 }
 
 void Exporter::Stop() {
-  {
-    std::lock_guard<std::mutex> l(mu_);
-    if (!started_) return;
-    stop_ = true;
-  }
-  cv_.notify_all();
-  if (thread_.joinable()) thread_.join();
   std::lock_guard<std::mutex> l(mu_);
+  if (!started_) return;
+  stop_.store(true, std::memory_order_release);
+  if (thread_.joinable()) thread_.join();
   started_ = false;
 }
 

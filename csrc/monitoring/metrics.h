@@ -16,6 +16,7 @@
 //                        filtering (stackdriver_exporter.cc:38-126).
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <map>
@@ -216,7 +217,7 @@ class Exporter {
   bool PeriodicallyExportMetrics();
   void ExportMetrics();
   void Stop();
-  int64_t exports() const { return exports_; }
+  int64_t exports() const { return exports_.load(std::memory_order_acquire); }
 
   static bool ShouldExport(const PointSet& ps, const ExporterConfig& cfg);
 
@@ -227,11 +228,11 @@ class Exporter {
   ExporterConfig config_;
   std::mutex mu_;
   std::mutex export_mu_;
-  std::condition_variable cv_;
-  bool started_ = false, stop_ = false;
+  bool started_ = false;
+  std::atomic<bool> stop_{false};
   std::thread thread_;
   std::set<std::string> exported_descriptors_;
-  int64_t exports_ = 0;
+  std::atomic<int64_t> exports_{0};  // read by other threads (found by the TSan CI variant)
 };
 
 }  // namespace monitoring

@@ -88,3 +88,51 @@ def test_keras_job_via_run_two_workers(tmp_path):
     other = [json.loads(ln[7:]) for ln in open(os.path.join(tmp_path, os.listdir(tmp_path)[0], "logs", "worker-0.log"))
              if ln.startswith("RESULT ")]
     assert abs(other[0]["weights_checksum"] - res[0]["weights_checksum"]) < 1e-6
+
+
+def _desync_worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), CLOUD_AMD_GRAD_CHECK_EVERY="1")
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from cloud_amd.optim import SGD
+    from cloud_amd.parallel.ddp import GradAllReducer
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    model = torch.nn.Linear(8, 4)
+    opt = SGD(model, learning_rate=0.1, grad_scale=1.0 / world)
+    red = GradAllReducer(opt.arenas)
+    red.broadcast_parameters()
+    opt.zero_grad()
+    model(torch.randn(4, 8)).sum().backward()
+    red.finish()  # check_every=1: the post-all-reduce fingerprints agree
+    ok = True
+    if rank == 1:
+        opt.arenas[0].grad[0] += 1.0  # simulate a desynchronised replica
+    try:
+        red.check_consistency()
+    except RuntimeError as e:
+        ok = "desync" in str(e)
+    else:
+        ok = False
+    with open(os.path.join(out_dir, f"desync{rank}"), "w") as f:
+        f.write("caught" if ok else "missed")
+    dist.destroy_process_group()
+
+
+def test_grad_desync_detector(tmp_path):
+    world = 2
+    port = 29500 + os.getpid() % 1000
+    mp.spawn(_desync_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    assert [open(tmp_path / f"desync{r}").read() for r in range(world)] == ["caught", "caught"]
+
+
+def test_trace_ranges_are_noops_when_disabled():
+    sys.path.insert(0, ROOT)
+    from cloud_amd.utils import trace
+
+    with trace.range("fwd"):
+        trace.mark("x")
+    assert trace.enabled() in (False, True)
