@@ -36,7 +36,7 @@ _VARS = [
     Var("CLOUD_AMD_REGION", str, "local", "region string reported by topology.get_region()", "launcher"),
     Var("CLOUD_AMD_PROJECT", str, "local", "project name reported to the tuner / cloud_fit", "launcher"),
     Var("CLOUD_AMD_DEVICE", str, None, "force the strategy device (e.g. 'cpu')", "launcher"),
-    Var("CLOUD_AMD_PG_TIMEOUT_S", float, 1800.0, "torch.distributed process-group timeout", "launcher"),
+    Var("CLOUD_AMD_PG_TIMEOUT_S", float, 600.0, "torch.distributed process-group timeout", "launcher"),
     # kernels / ops
     Var("CLOUD_AMD_OPS", str, "native", "'native' HIP kernels or 'torch' stock ops", "ops"),
     Var("CLOUD_AMD_GEMM", str, "native", "dense GEMMs: 'native' or 'torch'", "ops"),
