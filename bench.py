@@ -101,7 +101,7 @@ def main():
             loss, _ = softmax_cross_entropy(logits, y, denom=B)
         with trace.range("backward"):
             loss.backward()
-        return loss
+        return loss.detach()  # never keep the autograd graph alive across steps (graph capture)
 
     def train_step():
         opt.zero_grad()
@@ -122,6 +122,7 @@ def main():
     use_graph = bool(args.graph) and (world == 1 or os.environ.get("CLOUD_AMD_GRAPH_FORCE") == "1")
     step_fn = train_step
     if use_graph:
+        loss = None
         from cloud_amd.runtime.graph import capture_train_step
 
         step_fn = capture_train_step(fwd_bwd, opt, reducer, warmup=3)

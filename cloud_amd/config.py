@@ -49,6 +49,8 @@ _VARS = [
     Var("CLOUD_AMD_COMM", str, "torch", "DP transport: 'torch' (torch.distributed/RCCL) or 'rccl' (native)",
         "distributed"),
     Var("CLOUD_AMD_BUCKET_MB", float, 16.0, "gradient bucket size (MB) of the DP engine", "distributed"),
+    Var("CLOUD_AMD_DDP_ORDER", str, "event", "bucket ordering: 'event' (comm stream waits on a compute event), "
+        "'sync' (debug), 'backend'", "distributed"),
     Var("CLOUD_AMD_GRAD_CHECK_EVERY", int, 0, "cross-rank gradient fingerprint check every N steps (0 = off)",
         "distributed"),
     # observability

@@ -103,11 +103,13 @@ class Job:
 
     def _watchdog(self):
         failed_at = None
+        first_failure = None
         while True:
             codes = [p.poll() for p in self.procs]
             bad = [c for c in codes if c not in (None, 0)]
             if bad and failed_at is None:
                 failed_at = time.time()
+                first_failure = bad[0]  # the rank that failed, before the watchdog kills the rest
                 for p in self.procs:
                     if p.poll() is None:
                         try:
@@ -127,7 +129,7 @@ class Job:
         codes = [p.returncode for p in self.procs]
         self.meta["exit_codes"] = codes
         self.meta["end_time"] = time.time()
-        self.returncode = next((c for c in codes if c != 0), 0)
+        self.returncode = first_failure if first_failure is not None else next((c for c in codes if c != 0), 0)
         self.meta["state"] = "SUCCEEDED" if self.returncode == 0 else "FAILED"
         self._write_meta()
         self._done.set()

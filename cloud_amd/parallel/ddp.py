@@ -42,6 +42,9 @@ from ..utils import trace
 from . import comm as _comm
 
 _ACTIVE = weakref.WeakSet()
+# "event" (default): explicit compute->comm-stream event per bucket; "sync": also
+# host-synchronise (debug); "backend": leave ordering to the process-group backend.
+_DDP_ORDER = os.environ.get("CLOUD_AMD_DDP_ORDER", "event")
 
 
 def notify_grad_ready(param):
@@ -76,6 +79,10 @@ class GradAllReducer:
         self.check_every = int(os.environ.get("CLOUD_AMD_GRAD_CHECK_EVERY", "0"))
         self._steps = 0
         self.comm = None
+        self._side = None
+        on_gpu = bool(self.arenas) and self.arenas[0].grad.is_cuda
+        if self.world > 1 and on_gpu and _comm.backend() != "rccl" and _DDP_ORDER != "backend":
+            self._side = torch.cuda.Stream(self.arenas[0].grad.device, priority=-1)
         if self.world > 1 and _comm.backend() == "rccl" and self.arenas and self.arenas[0].grad.is_cuda:
             self.comm = _comm.RcclComm()  # native communicator: side stream + events
             self.comm.start_watchdog()
@@ -121,6 +128,19 @@ class GradAllReducer:
         trace.mark("bucket%d" % b.index)
         if self.comm is not None:
             self.comm.all_reduce(b.tensor)
+        elif self._side is not None:
+            # Explicit ordering: the collective is issued from a dedicated comm stream that
+            # first waits on an event recorded on the compute stream (where the kernels that
+            # wrote this bucket's gradients were queued).  Do not rely on the backend picking
+            # up the caller's stream: hooks and notify_grad_ready() run on autograd threads.
+            mode = _DDP_ORDER
+            if mode == "sync":
+                torch.cuda.current_stream(b.tensor.device).synchronize()
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(b.tensor.device))
+            self._side.wait_event(ev)
+            with torch.cuda.stream(self._side):
+                b.work = dist.all_reduce(b.tensor, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         else:
             b.work = dist.all_reduce(b.tensor, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         b.launched = True
@@ -139,9 +159,16 @@ class GradAllReducer:
             self._next += 1
         if self.comm is not None:
             self.comm.join()
-        for b in self.buckets:
-            if b.work is not None:
-                b.work.wait()
+        if self._side is not None:
+            with torch.cuda.stream(self._side):
+                for b in self.buckets:
+                    if b.work is not None:
+                        b.work.wait()
+            torch.cuda.current_stream(self._side.device).wait_stream(self._side)
+        else:
+            for b in self.buckets:
+                if b.work is not None:
+                    b.work.wait()
         self.reset()
         self._steps += 1
         if self.check_every and self._steps % self.check_every == 0:

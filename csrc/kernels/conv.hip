@@ -13,6 +13,7 @@
 // per lane; the MFMA core (ca_mfma_core.h) does the rest.  wgrad is split-K
 // over the N*OH*OW reduction with fp32 slabs.
 #include <stdlib.h>
+#include <string.h>
 
 #include "ca_mfma_core.h"
 
@@ -397,15 +398,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) c
   mfma_gemm_glds<BM, BN, 2, 2, LA, LB, EPI>(P);
 }
 
+// 8 waves (2 x 4, wave tile 64 x BN/4) with a double-buffered LDS-DMA pipeline:
+// same 16 waves/CU occupancy as the 4-wave single-stage kernel, but the next K
+// tile's DMA overlaps this tile's MFMAs (CLOUD_AMD_GEMM_CORE=glds8).
+template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) conv_glds8_kernel(CoreParams P) {
+  mfma_gemm_glds<BM, BN, 2, 4, LA, LB, EPI, 2>(P);
+}
+
 // CLOUD_AMD_GEMM_CORE=reg selects the register-staged core (A/B comparisons).
-bool use_glds() {
+// 0 = register-staged, 1 = glds single stage (4 waves), 2 = glds double-buffered (8 waves)
+int core_kind() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("CLOUD_AMD_GEMM_CORE");
-    v = (e && e[0] == 'r') ? 0 : 1;
+    v = !e ? 1 : (e[0] == 'r' ? 0 : (strcmp(e, "glds8") == 0 ? 2 : 1));
   }
-  return v == 1;
+  return v;
 }
+bool use_glds() { return core_kind() != 0; }
 
 template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
 __global__ void __launch_bounds__(256) conv_gemm_kernel(CoreParams P) {
@@ -416,6 +427,11 @@ template <int BM, int BN, template <int, int, int> class LA, template <int, int,
           template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
 int launch(const CoreParams& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  if (BN == 128 && core_kind() == 2) {
+    conv_glds8_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 512, 0, s>>>(p);
+    CA_LAUNCH_CHECK();
+    return 0;
+  }
   if (use_glds()) {
     conv_glds_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
     CA_LAUNCH_CHECK();

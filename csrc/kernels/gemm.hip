@@ -9,6 +9,7 @@
 // and M/N-contiguous tiles for the gfx950 transposed read ds_read_b64_tr_b16.
 // Split-K writes fp32 slabs reduced deterministically by splitk_reduce_kernel.
 #include <stdlib.h>
+#include <string.h>
 
 #include "ca_mfma_core.h"
 
@@ -25,15 +26,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) d
   mfma_gemm_glds<BM, BN, 2, 2, LA, LB, EPI>(P);
 }
 
+// 8 waves (2 x 4, wave tile 64 x BN/4) with a double-buffered LDS-DMA pipeline:
+// same 16 waves/CU occupancy as the 4-wave single-stage kernel, but the next K
+// tile's DMA overlaps this tile's MFMAs (CLOUD_AMD_GEMM_CORE=glds8).
+template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) dense_gemm_glds8_kernel(CoreParams P) {
+  mfma_gemm_glds<BM, BN, 2, 4, LA, LB, EPI, 2>(P);
+}
+
 // CLOUD_AMD_GEMM_CORE=reg selects the register-staged core (A/B comparisons).
-bool use_glds() {
+// 0 = register-staged, 1 = glds single stage (4 waves), 2 = glds double-buffered (8 waves)
+int core_kind() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("CLOUD_AMD_GEMM_CORE");
-    v = (e && e[0] == 'r') ? 0 : 1;
+    v = !e ? 1 : (e[0] == 'r' ? 0 : (strcmp(e, "glds8") == 0 ? 2 : 1));
   }
-  return v == 1;
+  return v;
 }
+bool use_glds() { return core_kind() != 0; }
 
 template <bool OUT_BF16>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int S, long MN,
@@ -77,6 +88,11 @@ template <int BM, int BN, template <int, int, int> class LA, template <int, int,
           template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
 int launch(const CoreParams& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  if (BN == 128 && core_kind() == 2) {
+    dense_gemm_glds8_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 512, 0, s>>>(p);
+    CA_LAUNCH_CHECK();
+    return 0;
+  }
   if (use_glds()) {
     dense_gemm_glds_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
     CA_LAUNCH_CHECK();
@@ -91,9 +107,22 @@ int launch(const CoreParams& p, int splits, hipStream_t s) {
   return 0;
 }
 
+// Fraction of CU-slots doing work when `tiles` equal blocks are spread over the
+// 256 CUs in rounds (wave quantisation).
+static double tile_balance(long tiles) {
+  const long cus = 256;
+  const long rounds = (tiles + cus - 1) / cus;
+  return (double)tiles / (double)(rounds * cus);
+}
+
 template <int EPI>
 int dispatch(int layout, const CoreParams& p, int splits, hipStream_t s) {
-  const bool small_n = p.N <= 64;
+  // 128-wide N tiles unless N is small, or the 128-wide grid would leave a badly
+  // filled last round (e.g. M=8192, N=768: 384 tiles -> 1.5 rounds) and halving
+  // the tile width balances it (768 tiles -> 3 full rounds).
+  const long tm = (p.M + 127) / 128;
+  const long t128 = tm * ((p.N + 127) / 128) * splits, t64 = tm * ((p.N + 63) / 64) * splits;
+  const bool small_n = p.N <= 64 || (tile_balance(t128) < 0.8 && tile_balance(t64) > tile_balance(t128) + 0.1);
   switch (layout) {
     case 0:
       return small_n ? launch<128, 64, DenseKC, DenseKC, GDenseKC, GDenseKC, EPI>(p, splits, s)

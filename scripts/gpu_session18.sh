@@ -1,0 +1,7 @@
+#!/usr/bin/env bash
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+S=scripts/gpu_step.sh
+$S 300 ddp_log.log python scripts/ddp_probe.py || exit 1
+echo SESSION_DONE
