@@ -89,6 +89,8 @@ class GradAllReducer:
         self.buckets = []
         self._param_bucket = {}
         self._next = 0
+        self._seen = set()
+        self._sync_enabled = True
         self._hooks = []
         self._build()
         if self.world > 1 and overlap:
@@ -117,6 +119,14 @@ class GradAllReducer:
                 self._hooks.append(s.param.register_post_accumulate_grad_hook(self._on_grad))
 
     def _on_grad(self, p):
+        # A parameter can be reported twice per step: explicitly by an op that wrote its
+        # arena gradient in place (notify_grad_ready), and again by autograd's
+        # post-accumulate hook (which fires for Function inputs even when the Function
+        # returned no gradient for them).  Count each parameter once per step, or a
+        # bucket would launch before all its gradients exist.
+        if not self._sync_enabled or id(p) in self._seen:
+            return
+        self._seen.add(id(p))
         b = self._param_bucket.get(id(p))
         if b is None or b.launched:
             return
@@ -174,6 +184,21 @@ class GradAllReducer:
         if self.check_every and self._steps % self.check_every == 0:
             self.check_consistency()
 
+    def no_sync(self):
+        """Gradient accumulation: backward passes inside this context only accumulate into
+        the arena; the all-reduce happens on the first backward after it (DDP.no_sync)."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def ctx():
+            prev, self._sync_enabled = self._sync_enabled, False
+            try:
+                yield
+            finally:
+                self._sync_enabled = prev
+
+        return ctx()
+
     def check_consistency(self, rtol=0.0):
         """Desync detector: after the all-reduce every replica must hold
         the same gradients.  Compares an fp64 (sum, sum of squares, sum of |x|) fingerprint
@@ -197,6 +222,7 @@ class GradAllReducer:
         return True
 
     def reset(self):
+        self._seen = set()
         for b in self.buckets:
             b.pending = len(b.slots)
             b.work = None

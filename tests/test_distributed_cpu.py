@@ -136,3 +136,27 @@ def test_trace_ranges_are_noops_when_disabled():
     with trace.range("fwd"):
         trace.mark("x")
     assert trace.enabled() in (False, True)
+
+
+def test_grad_ready_counts_each_param_once():
+    """A parameter reported both by notify_grad_ready (in-place arena write) and by
+    autograd's post-accumulate hook must only count once towards its bucket."""
+    sys.path.insert(0, ROOT)
+    from cloud_amd.optim import SGD
+    from cloud_amd.parallel.ddp import GradAllReducer
+
+    model = torch.nn.Sequential(torch.nn.Linear(8, 8), torch.nn.Linear(8, 8))
+    opt = SGD(model, learning_rate=0.1)
+    red = GradAllReducer(opt.arenas, bucket_mb=1000)  # one bucket per arena
+    launched = []
+    red._launch = lambda b: (launched.append(b.index), setattr(b, "launched", True))
+    params = list(model.parameters())
+    for p in params[:-1]:
+        red._on_grad(p)
+        red._on_grad(p)  # duplicate report
+    assert launched == []  # the last parameter has not been reported yet
+    red._on_grad(params[-1])
+    assert launched == [0]
+    with red.no_sync():
+        red._on_grad(params[0])
+    assert launched == [0]
