@@ -26,7 +26,21 @@ from __future__ import annotations
 
 import torch
 
+from .. import config
 from ..ops import _ext, raw
+
+_WGRAD_STREAMS = {}
+
+
+def _wgrad_stream(dev):
+    """The per-device side stream for weight gradients (None when disabled)."""
+    if not config.get("CLOUD_AMD_WGRAD_STREAM"):
+        return None
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _WGRAD_STREAMS.get(key)
+    if st is None:
+        st = _WGRAD_STREAMS[key] = torch.cuda.Stream(torch.device("cuda", key))
+    return st
 
 
 def _arena_grad(p, dtype):
@@ -106,9 +120,25 @@ class _BottleneckFn(torch.autograd.Function):
             ddp.notify_grad_ready(bn.bias)
             return r
 
+        main = torch.cuda.current_stream(x.device)
+        side = _wgrad_stream(x.device)
+        deferred = []
+
         def wgrad(conv, dz, inp):
-            raw.conv_wgrad(dz, inp, conv.weight.shape, conv.stride, conv.padding, out=conv.weight.grad, beta=1.0)
-            ddp.notify_grad_ready(conv.weight)
+            if side is None:
+                raw.conv_wgrad(dz, inp, conv.weight.shape, conv.stride, conv.padding, out=conv.weight.grad,
+                               beta=1.0)
+                ddp.notify_grad_ready(conv.weight)
+                return
+            # fork: the side stream sees everything queued so far on the main stream (dz, inp,
+            # the zeroed arena); the inputs must outlive the side-stream kernels that read them
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                raw.conv_wgrad(dz, inp, conv.weight.shape, conv.stride, conv.padding, out=conv.weight.grad,
+                               beta=1.0)
+            dz.record_stream(side)
+            inp.record_stream(side)
+            deferred.append(conv.weight)
 
         dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=True)
         del dout
@@ -134,6 +164,12 @@ class _BottleneckFn(torch.autograd.Function):
             dx = dres  # identity gradient; conv1's input gradient is summed into it below
         raw.conv_dgrad(dz1, blk.conv1.weight, x.shape, 1, 0, out=dx, beta=1.0)
         wgrad(blk.conv1, dz1, x)
+        if deferred:
+            # join: later kernels on the main stream (and DDP's bucket events recorded on it)
+            # are ordered after this block's weight gradients
+            main.wait_stream(side)
+            for w in deferred:
+                ddp.notify_grad_ready(w)
         return (dx, None) + (None,) * (len(ctx.needs_input_grad) - 2)
 
 
