@@ -12,7 +12,12 @@ the first step on every rank, max over ranks).
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 10
 
-Weak scaling: the per-GPU batch is fixed (``--batch``), global batch = batch x N.
+Weak scaling: the per-GPU batch is fixed (``--batch``, default 512), global batch =
+batch x N.  512 images per GPU is sized for 288 GB of HBM3E (``peak_mem_gb`` in the
+JSON line reports the step's peak) and halves the per-image share of the step's fixed
+costs (~570 kernel boundaries at ~1.8 us each, per-layer BN finalize kernels)
+relative to 256; the sweep 128..1024 and the stock comparator at 256 and 512
+are in BASELINE.md.
 Synthetic data: random NHWC bf16 images and random labels, generated once on
 the device (no input pipeline in the timed region, as in tf_cnn_benchmarks'
 synthetic mode).  Random-init weights.  Every timed step runs the full forward,
@@ -34,7 +39,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("CLOUD_AMD_BENCH_BATCH", 256)),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("CLOUD_AMD_BENCH_BATCH", 512)),
                     help="per-GPU batch")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--classes", type=int, default=1000)
@@ -173,6 +178,7 @@ def main():
             "run_to_first_step_s": round(run_to_first, 3) if run_to_first is not None else None,
             "launched_via": "cloud_amd.run()" if run_t0 else "direct",
             "final_loss": round(final_loss, 4),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2),
         }
         line = json.dumps(out)
         print(line, flush=True)
