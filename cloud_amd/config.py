@@ -44,6 +44,8 @@ _VARS = [
     Var("CLOUD_AMD_GEMM_CORE", str, "glds", "GEMM/conv staging core: 'glds' (LDS-DMA) or 'reg' (register)", "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block backward: weight-gradient GEMMs on a second HIP "
         "stream, overlapping the memory-bound BN/dgrad chain", "ops"),
+    Var("CLOUD_AMD_BN_BWD_EPILOGUE", bool, True, "ResNet block backward: BatchNorm-backward statistics from the "
+        "dgrad GEMM epilogues (skips the BN reduction pass)", "ops"),
     Var("CLOUD_AMD_PRECISION", str, "bf16", "compute dtype of the Keras front end", "ops"),
     Var("CLOUD_AMD_ARCH", str, "gfx950", "offload arch of the native build", "build"),
     Var("CLOUD_AMD_SANITIZE", bool, False, "build the C++ test binary with ASan/UBSan", "build"),

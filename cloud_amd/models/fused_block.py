@@ -17,7 +17,18 @@ This module runs the whole block as ONE autograd node:
   its slice of the flat gradient arena and the BN ``dgamma/dbeta`` are summed
   into their arena slots by the BN finalize kernel; the DDP engine is notified
   per parameter so bucketed all-reduces still overlap with the rest of the
-  backward.
+  backward;
+* the weight-gradient GEMMs (compute bound) run on a second HIP stream so they
+  overlap the memory-bound BN-backward / dgrad chain of the main stream; the
+  block joins that stream before reporting its conv weights to DDP
+  (``CLOUD_AMD_WGRAD_STREAM``);
+* the BN-backward statistics come from the dgrad GEMM epilogues: the GEMM that
+  produces a BN output's gradient also sums g = dy * relu' and g * z per column
+  and tile (``raw.conv_dgrad(..., bn=(z, mask))``), so the BN backward skips its
+  own read pass over dy and z.  Inside a block that covers bn2 (conv3's dgrad)
+  and bn1 (conv2's dgrad); across blocks, conv1's dgrad of block i+1 -- the
+  launch that completes the block-input gradient -- computes block i's bn3
+  statistics and parks them for block i's backward (``CLOUD_AMD_BN_BWD_EPILOGUE``).
 
 Parity: the block computes exactly what :class:`cloud_amd.models.resnet.Bottleneck`
 computes op by op (same kernels, same order) -- tests compare the two.
@@ -41,6 +52,26 @@ def _wgrad_stream(dev):
     if st is None:
         st = _WGRAD_STREAMS[key] = torch.cuda.Stream(torch.device("cuda", key))
     return st
+
+
+# Cross-block hand-off of bn3 statistics (one slot: blocks run backward one after
+# another).  The parked gradient is held so its memory cannot be reused by another
+# tensor while parked; the consumer checks identity (storage, shape, version).
+_HANDOFF = {"grad": None, "version": -1, "partials": None}
+
+
+def _park(grad, partials):
+    _HANDOFF.update(grad=grad, version=grad._version, partials=partials)
+
+
+def _take(dout):
+    g, ver, part = _HANDOFF["grad"], _HANDOFF["version"], _HANDOFF["partials"]
+    _HANDOFF.update(grad=None, version=-1, partials=None)
+    if g is None or part is None:
+        return None
+    if g.data_ptr() != dout.data_ptr() or g.shape != dout.shape or dout._version != ver:
+        return None
+    return part
 
 
 def _arena_grad(p, dtype):
@@ -86,7 +117,10 @@ def _conv_bn(conv, bn, x, residual=None):
 
 class _BottleneckFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, blk, *params):
+    def forward(ctx, x, blk, prev_src, *params):
+        # prev_src: (z, mask) of the BatchNorm+ReLU that produced x (the previous fused
+        # block's bn3), or None -- this block's backward computes its statistics
+        ctx.prev_src = prev_src
         ds = blk.downsample
         z1, y1, s1 = _conv_bn(blk.conv1, blk.bn1, x)
         z2, y2, s2 = _conv_bn(blk.conv2, blk.bn2, y1)
@@ -100,6 +134,7 @@ class _BottleneckFn(torch.autograd.Function):
         (s1, m1), (s2, m2), (s3, m3) = s1, s2, s3
         ctx.save_for_backward(x, z1, y1, z2, y2, z3, s1, m1, s2, m2, s3, m3,
                               *((zd, sd[0]) if ds is not None else ()))
+        blk._ca_out_src = (z3, m3)
         return out
 
     @staticmethod
@@ -112,13 +147,23 @@ class _BottleneckFn(torch.autograd.Function):
         x, z1, y1, z2, y2, z3, s1, m1, s2, m2, s3, m3 = saved[:12]
         dout = dout.contiguous()
 
-        def bn_back(bn, dy, z, st, want_dres=False):
+        epi = config.get("CLOUD_AMD_BN_BWD_EPILOGUE")
+
+        def bn_back(bn, dy, z, st, want_dres=False, partials=None):
             stats, mask = st
             r = raw.bn_bwd(dy, None, z, bn.weight, stats, bn.relu, dgamma=bn.weight.grad, dbeta=bn.bias.grad,
-                           want_dres=want_dres, accumulate=1, mask=mask)
+                           want_dres=want_dres, accumulate=1, mask=mask, partials=partials)
             ddp.notify_grad_ready(bn.weight)
             ddp.notify_grad_ready(bn.bias)
             return r
+
+        def dgrad(conv, dz, shape, bn_src, out=None, beta=0.0):
+            """Input gradient; with ``bn_src`` = (z, mask) of the BN that consumes it,
+            also that BN's backward statistics from the epilogue."""
+            if epi and bn_src is not None:
+                return raw.conv_dgrad(dz, conv.weight, shape, conv.stride, conv.padding, out=out, beta=beta,
+                                      bn=bn_src)
+            return raw.conv_dgrad(dz, conv.weight, shape, conv.stride, conv.padding, out=out, beta=beta), None
 
         main = torch.cuda.current_stream(x.device)
         side = _wgrad_stream(x.device)
@@ -140,18 +185,18 @@ class _BottleneckFn(torch.autograd.Function):
             inp.record_stream(side)
             deferred.append(conv.weight)
 
-        dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=True)
+        dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=True, partials=_take(dout) if epi else None)
         del dout
-        dy2 = raw.conv_dgrad(dz3, blk.conv3.weight, y2.shape, 1, 0)
+        dy2, p2 = dgrad(blk.conv3, dz3, y2.shape, (z2, m2))
         wgrad(blk.conv3, dz3, y2)
         del dz3
-        dz2, _ = bn_back(blk.bn2, dy2, z2, (s2, m2))
-        del dy2
-        dy1 = raw.conv_dgrad(dz2, blk.conv2.weight, y1.shape, blk.conv2.stride, blk.conv2.padding)
+        dz2, _ = bn_back(blk.bn2, dy2, z2, (s2, m2), partials=p2)
+        del dy2, p2
+        dy1, p1 = dgrad(blk.conv2, dz2, y1.shape, (z1, m1))
         wgrad(blk.conv2, dz2, y1)
         del dz2
-        dz1, _ = bn_back(blk.bn1, dy1, z1, (s1, m1))
-        del dy1
+        dz1, _ = bn_back(blk.bn1, dy1, z1, (s1, m1), partials=p1)
+        del dy1, p1
         if ds is not None:
             zd, sd = saved[12], saved[13]
             dzd, _ = bn_back(ds["bn"], dres, zd, (sd, None))
@@ -162,7 +207,11 @@ class _BottleneckFn(torch.autograd.Function):
             del dzd
         else:
             dx = dres  # identity gradient; conv1's input gradient is summed into it below
-        raw.conv_dgrad(dz1, blk.conv1.weight, x.shape, 1, 0, out=dx, beta=1.0)
+        # the last write of dx: its epilogue sees the complete block-input gradient
+        _, p_prev = dgrad(blk.conv1, dz1, x.shape, ctx.prev_src, out=dx, beta=1.0)
+        if p_prev is not None:
+            _park(dx, p_prev)
+        ctx.prev_src = None
         wgrad(blk.conv1, dz1, x)
         if deferred:
             # join: later kernels on the main stream (and DDP's bucket events recorded on it)
@@ -170,8 +219,13 @@ class _BottleneckFn(torch.autograd.Function):
             main.wait_stream(side)
             for w in deferred:
                 ddp.notify_grad_ready(w)
-        return (dx, None) + (None,) * (len(ctx.needs_input_grad) - 2)
+        return (dx, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
 
 def bottleneck_forward(blk, x):
-    return _BottleneckFn.apply(x, blk, *block_params(blk))
+    prev = getattr(x, "_ca_bn_src", None) if config.get("CLOUD_AMD_BN_BWD_EPILOGUE") else None
+    out = _BottleneckFn.apply(x, blk, prev, *block_params(blk))
+    src = blk.__dict__.pop("_ca_out_src", None)
+    if src is not None:
+        out._ca_bn_src = src  # (z3, mask3): the next fused block computes bn3's backward statistics
+    return out

@@ -56,12 +56,32 @@ def conv_fwd(x, w, stride, padding, stats=None):
     return y
 
 
-def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0):
-    """dx (+= beta * out) for y = conv(x, w)."""
+def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None):
+    """dx (+= beta * out) for y = conv(x, w).
+
+    ``bn=(z, mask)``: dx is the gradient of a BatchNorm(+ReLU) output whose input was
+    ``z`` (``mask``: its ReLU bitmask, or None).  The GEMM epilogue then also writes the
+    BN-backward statistics partials [tiles][2][Cin] = [sum g | sum g*z], g = dx * relu',
+    and ``(dx, partials)`` is returned: :func:`bn_bwd` takes them and skips its own
+    reduction pass over dx and z."""
     ext = _ext.load(required=True)
     N, H, W, Cin = x_shape
     Cout, KH, KW, _ = w.shape
     dx = out if out is not None else torch.empty(x_shape, dtype=torch.bfloat16, device=dy.device)
+    if bn is not None:
+        z, mask = bn
+        assert z.shape == dx.shape and z.is_contiguous() and (mask is None or mask.shape == (N * H * W, Cin // 8))
+        if is_gemm_conv(w, stride, padding):
+            part = torch.empty(((N * H * W + 127) // 128, 2, Cin), dtype=torch.float32, device=dy.device)
+            ext.gemm_bf16_bnstats(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin, Cout,
+                                  float(beta), z.data_ptr(), _ext.ptr(mask), part.data_ptr(), _st(dy.device))
+        else:
+            rows = ext.conv_dgrad_stat_tiles(N, H, W, stride, stride)
+            part = torch.empty((rows, 2, Cin), dtype=torch.float32, device=dy.device)
+            ext.conv_dgrad_bnstats(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, KH, KW, stride,
+                                   stride, padding, padding, float(beta), z.data_ptr(), _ext.ptr(mask),
+                                   part.data_ptr(), _st(dy.device))
+        return dx, part
     if is_gemm_conv(w, stride, padding):
         ext.gemm_bf16(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin, Cout, 0,
                       float(beta), _st(dy.device))
@@ -120,10 +140,12 @@ def bn_fwd(x, gamma, beta, running_mean, running_var, eps, momentum, relu, resid
 
 
 def bn_bwd(dy, y, x, gamma, stats, relu, dgamma=None, dbeta=None, want_dres=False, dx_out=None, accumulate=0,
-           mask=None):
+           mask=None, partials=None):
     """BN(+res)(+ReLU) backward.  The ReLU gate comes from ``mask`` (forward bitmask) or
     ``y``.  dgamma/dbeta (fp32 [C]) are written, or accumulated into when
-    ``accumulate`` is set.  Returns (dx, dres-or-None)."""
+    ``accumulate`` is set.  ``partials``: the [tiles][2][C] statistics written by the
+    epilogue of the dgrad that produced ``dy`` (:func:`conv_dgrad` ``bn=``) -- the
+    reduction pass is skipped.  Returns (dx, dres-or-None)."""
     ext = _ext.load(required=True)
     C = x.shape[-1]
     M = x.numel() // C
@@ -131,8 +153,16 @@ def bn_bwd(dy, y, x, gamma, stats, relu, dgamma=None, dbeta=None, want_dres=Fals
     dx = dx_out if dx_out is not None else torch.empty_like(x)
     dres = torch.empty_like(x) if want_dres else None
     coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
-    ws = torch.empty(ext.bn_workspace_floats(M, C), dtype=torch.float32, device=dev)
     sp = stats.data_ptr()
+    if partials is not None:
+        assert partials.shape[1:] == (2, C)
+        gws = torch.empty(64 * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
+        ext.bn_bwd_partials(dy.data_ptr(), _ext.ptr(y), _ext.ptr(mask), x.data_ptr(), M, C, partials.data_ptr(),
+                            partials.shape[0], _ext.ptr(gamma), sp, sp + 4 * C, dx.data_ptr(), _ext.ptr(dres),
+                            _ext.ptr(dgamma), _ext.ptr(dbeta), coef.data_ptr(), _ext.ptr(gws),
+                            int(relu) | (2 if accumulate else 0), _st(dev))
+        return dx, dres
+    ws = torch.empty(ext.bn_workspace_floats(M, C), dtype=torch.float32, device=dev)
     ext.bn_bwd(dy.data_ptr(), _ext.ptr(y), _ext.ptr(mask), x.data_ptr(), M, C, _ext.ptr(gamma), sp, sp + 4 * C,
                dx.data_ptr(), _ext.ptr(dres), _ext.ptr(dgamma), _ext.ptr(dbeta), coef.data_ptr(), ws.data_ptr(),
                int(relu) | (2 if accumulate else 0), _st(dev))

@@ -26,6 +26,14 @@ int ca_bn_fwd_partials(const bf16_t*, const bf16_t*, bf16_t*, long, int, const f
                        float, float, float*, float*, float*, float*, float*, int, uint8_t*, float*, hipStream_t);
 int ca_bn_bwd(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, long, int, const float*, const float*,
               const float*, bf16_t*, bf16_t*, float*, float*, float*, float*, int, hipStream_t);
+int ca_bn_bwd_partials(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, long, int, const float*, int,
+                       const float*, const float*, const float*, bf16_t*, bf16_t*, float*, float*, float*, float*, int,
+                       hipStream_t);
+int ca_gemm_bf16_bnstats(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float,
+                         const bf16_t*, const uint8_t*, float*, hipStream_t);
+long ca_conv_dgrad_stat_tiles(int, int, int, int, int);
+int ca_conv_dgrad_bnstats(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
+                          int, float, const bf16_t*, const uint8_t*, float*, hipStream_t);
 int ca_softmax_xent(const void*, int, const int64_t*, int, int, float, float, float*, float*, void*, hipStream_t);
 int ca_maxpool_fwd(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ca_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -125,6 +133,30 @@ PYBIND11_MODULE(_C, m) {
                     P(const float*, gamma),
                     P(const float*, sm), P(const float*, sr), P(bf16_t*, dx), P(bf16_t*, dres), P(float*, dg),
                     P(float*, db), P(float*, coef), P(float*, ws), relu, S(s)), "bn_bwd");
+  });
+  m.def("bn_bwd_partials", [](u64 dy, u64 y, u64 mask, u64 x, long M, int C, u64 parts, int nparts, u64 gamma,
+                              u64 sm, u64 sr, u64 dx, u64 dres, u64 dg, u64 db, u64 coef, u64 gws, int relu, u64 s) {
+    check(ca_bn_bwd_partials(P(const bf16_t*, dy), P(const bf16_t*, y), P(const uint8_t*, mask), P(const bf16_t*, x), M,
+                             C, P(const float*, parts), nparts, P(const float*, gamma), P(const float*, sm),
+                             P(const float*, sr), P(bf16_t*, dx), P(bf16_t*, dres), P(float*, dg), P(float*, db),
+                             P(float*, coef), P(float*, gws), relu, S(s)),
+          "bn_bwd_partials");
+  });
+  m.def("gemm_bf16_bnstats", [](int layout, u64 A, long lda, u64 B, long ldb, u64 C, long ldc, int M, int N, int K,
+                                float beta, u64 z, u64 mask, u64 stats, u64 s) {
+    check(ca_gemm_bf16_bnstats(layout, P(const bf16_t*, A), lda, P(const bf16_t*, B), ldb, P(bf16_t*, C), ldc, M, N, K,
+                               beta, P(const bf16_t*, z), P(const uint8_t*, mask), P(float*, stats), S(s)),
+          "gemm_bf16_bnstats");
+  });
+  m.def("conv_dgrad_stat_tiles", [](int Nb, int H, int W, int sh, int sw) {
+    return ca_conv_dgrad_stat_tiles(Nb, H, W, sh, sw);
+  });
+  m.def("conv_dgrad_bnstats", [](u64 dy, u64 w, u64 dx, int Nb, int H, int W, int Cin, int Cout, int KH, int KW,
+                                 int sh, int sw, int ph, int pw, float beta, u64 z, u64 mask, u64 stats, u64 s) {
+    check(ca_conv_dgrad_bnstats(P(const bf16_t*, dy), P(const bf16_t*, w), P(bf16_t*, dx), Nb, H, W, Cin, Cout, KH, KW,
+                                sh, sw, ph, pw, beta, P(const bf16_t*, z), P(const uint8_t*, mask), P(float*, stats),
+                                S(s)),
+          "conv_dgrad_bnstats");
   });
   m.def("softmax_xent", [](u64 z, int zbf, u64 labels, int B, int C, float gscale, float ls, u64 loss, u64 correct,
                            u64 dz, u64 s) {

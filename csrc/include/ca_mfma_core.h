@@ -58,6 +58,11 @@ struct CoreParams {
   const bf16_t* B; long ldb;
   void* C; long ldc;
   float* stats;          // optional: per-M-tile column [sum | sumsq] partials [tiles_m][2][N]
+  // BN-backward statistics epilogue (dgrad GEMMs whose output dy feeds a BatchNorm(+ReLU)
+  // backward): with bnz set, `stats` receives per-tile column [sum g | sum g*z] where
+  // g = dy * relu'(mask) and z is the BN input (same [rows][ldc] layout as C).
+  const bf16_t* bnz;
+  const uint8_t* bnmask;  // ReLU bitmask [rows][N/8] (bit j = channel 8c+j active) or null
   float beta;            // C = acc + beta * C_old (bf16 epilogue)
   int M, N, K;
   int k_per_split;
@@ -277,6 +282,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
     __syncthreads();
     const bool fx = P.act != ACT_NONE || P.dact_src != nullptr || P.preact != nullptr;
     bf16_t* Cg = reinterpret_cast<bf16_t*>(P.C);
+    float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, bzsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     constexpr int CH = BM * BN / 8;
     for (int c = tid; c < CH; c += NT) {
       const int row = c / (BN / 8), col = (c % (BN / 8)) * 8;
@@ -302,11 +308,46 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
           for (int j = 0; j < 8; ++j)
             v[j] = (short)f2bf(bf2f((bf16_t)v[j]) + P.beta * bf2f((bf16_t)o[j]));
         }
-        if (P.stats && (fx || P.beta != 0.f)) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
+        if (P.stats && !P.bnz && (fx || P.beta != 0.f)) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
         *reinterpret_cast<s8v*>(dst) = v;
+        if (P.bnz) {
+          // NT is a multiple of BN/8, so this thread always owns the same 8 columns
+          const long orow = out_row(P, gm);
+          const s8v zv = *reinterpret_cast<const s8v*>(P.bnz + orow * P.ldc + gn);
+          const uint32_t mb = P.bnmask ? (uint32_t)P.bnmask[orow * (P.N / 8) + (gn >> 3)] : 0xffu;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float g = ((mb >> j) & 1u) ? bf2f((bf16_t)v[j]) : 0.f;
+            bsum[j] += g;
+            bzsum[j] += g * bf2f((bf16_t)zv[j]);
+          }
+        }
       }
     }
-    if (P.stats) {
+    if (P.bnz) {
+      constexpr int CG = BN / 8, PARTS = NT / CG;
+      static_assert(NT % CG == 0, "column groups must divide the threads");
+      const int cg = tid % CG, part = tid / CG;
+      __syncthreads();  // Cs (aliases sred) fully consumed
+      float* sred = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sred[part * BN + cg * 8 + j] = bsum[j];
+        sred[(PARTS + part) * BN + cg * 8 + j] = bzsum[j];
+      }
+      __syncthreads();
+      for (int c = tid; c < BN; c += NT) {
+        if (n0 + c >= P.N) continue;
+        float ts = 0.f, tq = 0.f;
+        for (int pp = 0; pp < PARTS; ++pp) {
+          ts += sred[pp * BN + c];
+          tq += sred[(PARTS + pp) * BN + c];
+        }
+        float* st = P.stats + (long)tm * 2 * P.N;
+        st[n0 + c] = ts;
+        st[P.N + n0 + c] = tq;
+      }
+    } else if (P.stats) {
       // per-column sum / sum of squares of the stored bf16 values of this tile
       constexpr int TPC = NT / BN;
       const int col = tid % BN, part = tid / BN;

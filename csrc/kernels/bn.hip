@@ -319,12 +319,15 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ ws, int nchunks
                                        int C,
                                        const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ rstd, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta, float* __restrict__ coef, int accum) {
+                                       float* __restrict__ dbeta, float* __restrict__ coef, int accum,
+                                       int raw_moments) {
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
   double sd, sdx;
   wave_chunk_sum(ws, nchunks, stride_k, off_q, c, sd, sdx);
   if ((threadIdx.x & 63) != 0) return;
+  // partials from a GEMM epilogue hold sum(dz*x): sum(dz*xhat) = rstd*(sum(dz*x) - mean*sum(dz))
+  if (raw_moments) sdx = (double)rstd[c] * (sdx - (double)mean[c] * sd);
   // accum: parameter grads are summed into (flat arena slots), not overwritten
   if (dgamma) dgamma[c] = (float)sdx + (accum ? dgamma[c] : 0.f);
   if (dbeta) dbeta[c] = (float)sd + (accum ? dbeta[c] : 0.f);
@@ -469,7 +472,39 @@ int ca_bn_bwd(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16
                                                                      gws);
   CA_LAUNCH_CHECK();
   bn_bwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(gws, G, 2L * C, (long)C, M, C, gamma, save_mean, save_rstd,
-                                                         dgamma, dbeta, coef, accum);
+                                                         dgamma, dbeta, coef, accum, 0);
+  CA_LAUNCH_CHECK();
+  if (relu && dres) bn_bwd_apply_kernel<true, true><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
+  else if (relu) bn_bwd_apply_kernel<true, false><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
+  else if (dres) bn_bwd_apply_kernel<false, true><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
+  else bn_bwd_apply_kernel<false, false><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+// Backward from the [nparts][2][C] partials [sum dz | sum dz*x] written by a dgrad
+// GEMM's BN-statistics epilogue (ca_gemm_bf16_bnstats / ca_conv_dgrad_bnstats): no
+// reduction pass over dy and x; finalize (+group reduce) then the apply pass.
+int ca_bn_bwd_partials(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16_t* x, long M, int C,
+                       const float* partials, int nparts, const float* gamma, const float* save_mean,
+                       const float* save_rstd, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta,
+                       float* coef /* [3C] */, float* gws /* [64][2][C] */, int relu, hipStream_t s) {
+  if (C % 8 != 0 || (nparts > 64 && !gws)) return -1;
+  const int accum = (relu >> 1) & 1;
+  relu &= 1;
+  Tiling t = make_tiling(M, C);
+  dim3 grid(t.ncol, t.nchunks);
+  const float* fin = partials;
+  int nfin = nparts;
+  if (nparts > 64) {
+    const int G = group_count(nparts);
+    chunk_group_reduce_kernel<<<dim3(ca_cdiv(C, 64), G), 256, 0, s>>>(partials, nparts, 2L * C, (long)C, C, gws);
+    CA_LAUNCH_CHECK();
+    fin = gws;
+    nfin = G;
+  }
+  bn_bwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(fin, nfin, 2L * C, (long)C, M, C, gamma, save_mean, save_rstd,
+                                                         dgamma, dbeta, coef, accum, 1);
   CA_LAUNCH_CHECK();
   if (relu && dres) bn_bwd_apply_kernel<true, true><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
   else if (relu) bn_bwd_apply_kernel<true, false><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);

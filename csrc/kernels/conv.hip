@@ -478,15 +478,32 @@ int ca_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   return launch<128, 128, ConvFwdA, DenseKC, GConvFwdA, GDenseKC, EPI_BF16>(p, 1, s);
 }
 
-// dx[Nb,H,W,Cin] = dgrad(dy[Nb,OH,OW,Cout], w) (+ beta * dx).
-int ca_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb, int H, int W, int Cin, int Cout, int KH,
-                  int KW, int sh, int sw, int ph, int pw, float beta, hipStream_t s) {
+// Rows of the BN-backward statistics partials ca_conv_dgrad_bnstats writes: one per
+// 128-row GEMM tile, summed over the output-parity classes of a strided dgrad.
+long ca_conv_dgrad_stat_tiles(int Nb, int H, int W, int sh, int sw) {
+  if ((sh == 1 && sw == 1) || !use_glds()) return ((long)Nb * H * W + 127) / 128;
+  long t = 0;
+  for (int py = 0; py < sh; ++py)
+    for (int px = 0; px < sw; ++px) {
+      const long hq = (H - py + sh - 1) / sh, wq = (W - px + sw - 1) / sw;
+      if (hq > 0 && wq > 0) t += ((long)Nb * hq * wq + 127) / 128;
+    }
+  return t;
+}
+
+static int conv_dgrad_impl(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb, int H, int W, int Cin, int Cout,
+                           int KH, int KW, int sh, int sw, int ph, int pw, float beta, const bf16_t* bnz,
+                           const uint8_t* bnmask, float* stats, hipStream_t s) {
   CoreParams p = conv_params(Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw);
   if (!geom_ok(Cin, Cout, (long)Nb * H * W)) return -1;
   p.A = dy; p.B = w; p.C = dx; p.ldc = Cin;
   p.M = Nb * H * W; p.N = Cin; p.K = KH * KW * Cout; p.k_per_split = p.K;
   p.beta = beta;
+  p.bnz = bnz;
+  p.bnmask = bnmask;
+  p.stats = bnz ? stats : nullptr;
   if ((sh > 1 || sw > 1) && use_glds()) {
+    long stat_row = 0;
     // one GEMM per output-parity class; classes without taps get zeros (or beta*dx)
     for (int py = 0; py < sh; ++py)
       for (int px = 0; px < sw; ++px) {
@@ -509,6 +526,10 @@ int ca_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb, int H, 
         q.M = Nb * q.Hq * q.Wq;
         q.K = q.dg_nh * q.dg_nw * Cout;
         q.k_per_split = q.K;
+        if (bnz) {
+          q.stats = stats + stat_row * 2 * Cin;  // this class's tiles follow the previous classes'
+          stat_row += (q.M + 127) / 128;
+        }
         int rc = (Cin <= 64)
                      ? launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradSA, GConvDgradSB, EPI_BF16>(q, 1, s)
                      : launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradSA, GConvDgradSB, EPI_BF16>(q, 1, s);
@@ -518,6 +539,21 @@ int ca_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb, int H, 
   }
   if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI_BF16>(p, 1, s);
   return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI_BF16>(p, 1, s);
+}
+
+// dx[Nb,H,W,Cin] = dgrad(dy[Nb,OH,OW,Cout], w) (+ beta * dx).
+int ca_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb, int H, int W, int Cin, int Cout, int KH,
+                  int KW, int sh, int sw, int ph, int pw, float beta, hipStream_t s) {
+  return conv_dgrad_impl(dy, w, dx, Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw, beta, nullptr, nullptr, nullptr, s);
+}
+
+// Same, plus the BN-backward statistics epilogue (see ca_gemm_bf16_bnstats): `stats`
+// has ca_conv_dgrad_stat_tiles(...) rows of [2][Cin]; z / mask are indexed like dx.
+int ca_conv_dgrad_bnstats(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb, int H, int W, int Cin, int Cout,
+                          int KH, int KW, int sh, int sw, int ph, int pw, float beta, const bf16_t* bnz,
+                          const uint8_t* bnmask, float* stats, hipStream_t s) {
+  if (!bnz || !stats) return -1;
+  return conv_dgrad_impl(dy, w, dx, Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw, beta, bnz, bnmask, stats, s);
 }
 
 // dw[Cout, KH*KW*Cin] (+)= wgrad(dy, x) via split-K fp32 slabs in ws[splits][Cout][KH*KW*Cin].

@@ -171,6 +171,22 @@ int ca_gemm_bf16(int layout, const bf16_t* A, long lda, const bf16_t* B, long ld
   return dispatch<EPI_BF16>(layout, p, 1, s);
 }
 
+// Input-gradient GEMM (NN: dX = dY W) whose output feeds a BatchNorm(+ReLU) backward:
+// the epilogue also writes per-128-row-tile column partials [sum g | sum g*z] into
+// `stats` ([tiles_m][2][N]), g = C * relu'(mask), z = the BN input (ld = ldc) -- the
+// BN backward then skips its own reduction pass over dy and z.
+int ca_gemm_bf16_bnstats(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc,
+                         int M, int N, int K, float beta, const bf16_t* bnz, const uint8_t* bnmask, float* stats,
+                         hipStream_t s) {
+  if (N % 8 != 0 || K % 8 != 0 || layout == 2 || !bnz || !stats) return -1;
+  CoreParams p = base_params(A, lda, B, ldb, C, ldc, M, N, K);
+  p.stats = stats;
+  p.beta = beta;
+  p.bnz = bnz;
+  p.bnmask = bnmask;
+  return dispatch<EPI_BF16>(layout, p, 1, s);
+}
+
 // Dense-layer GEMM with the fused epilogue: C = act(A*B + bias) (+ beta*C),
 // pre-activation kept in `preact` when given; backward form: C = (A*B) * act'(dact_src).
 int ca_gemm_ex(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N,

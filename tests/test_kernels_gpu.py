@@ -324,3 +324,97 @@ def test_native_rccl_communicator_single_rank():
     assert torch.equal(rs, x * 2) and torch.equal(b, torch.ones_like(b))
     assert c.healthy()
     c.close()
+
+
+def _relu_bits(mask_bool):
+    """[M, C] bool -> the kernels' ReLU bitmask [M, C/8] uint8 (bit j = channel 8c+j)."""
+    M, C = mask_bool.shape
+    w = (1 << torch.arange(8, device=mask_bool.device)).to(torch.int32)
+    return (mask_bool.view(M, C // 8, 8).to(torch.int32) * w).sum(-1).to(torch.uint8)
+
+
+@pytest.mark.parametrize("k,s,p,beta", [(1, 1, 0, 0.0), (1, 1, 0, 1.0), (3, 1, 1, 0.0), (3, 2, 1, 0.0)])
+def test_dgrad_bn_backward_stats_epilogue(k, s, p, beta):
+    """dgrad GEMM epilogue statistics [sum g | sum g*z], g = dx * relu' (fp32 reference),
+    and the BN backward fed from them == the BN backward with its own reduction."""
+    from cloud_amd.ops import raw
+
+    torch.manual_seed(12)
+    N, H, Cin, Cout = 3, 15, 64, 128
+    OH = (H + 2 * p - k) // s + 1
+    dy = torch.randn(N, OH, OH, Cout, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(Cout, k, k, Cin, device=DEV) / (k * k * Cin) ** 0.5).to(torch.bfloat16)
+    z = (torch.randn(N, H, H, Cin, device=DEV) * 2 + 0.5).to(torch.bfloat16)
+    keep = torch.rand(N * H * H, Cin, device=DEV) > 0.4
+    bits = _relu_bits(keep)
+    base = torch.randn(N, H, H, Cin, device=DEV).to(torch.bfloat16)
+    ref = raw.conv_dgrad(dy, w, z.shape, s, p, out=base.clone() if beta else None, beta=beta)
+    dx, part = raw.conv_dgrad(dy, w, z.shape, s, p, out=base.clone() if beta else None, beta=beta, bn=(z, bits))
+    assert torch.equal(dx, ref)
+    g = dx.float().reshape(-1, Cin) * keep
+    zf = z.float().reshape(-1, Cin)
+    torch.testing.assert_close(part[:, 0].sum(0), g.sum(0), atol=2e-2 * N * H, rtol=1e-3)
+    torch.testing.assert_close(part[:, 1].sum(0), (g * zf).sum(0), atol=5e-2 * N * H, rtol=1e-3)
+
+    # BN(+ReLU) backward: partials path vs reduction path (same forward stats)
+    gamma, beta_ = torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV)
+    _, st, mask = raw.bn_fwd(z, gamma, beta_, None, None, 1e-5, 0.1, True, keep_mask=True)
+    dg_a, db_a = torch.zeros(Cin, device=DEV), torch.zeros(Cin, device=DEV)
+    dg_b, db_b = torch.zeros(Cin, device=DEV), torch.zeros(Cin, device=DEV)
+    dx2, part2 = raw.conv_dgrad(dy, w, z.shape, s, p, bn=(z, mask))
+    a, _ = raw.bn_bwd(dx2, None, z, gamma, st, True, dgamma=dg_a, dbeta=db_a, mask=mask, partials=part2)
+    b, _ = raw.bn_bwd(dx2, None, z, gamma, st, True, dgamma=dg_b, dbeta=db_b, mask=mask)
+    torch.testing.assert_close(dg_a, dg_b, atol=1e-2 * N * H, rtol=1e-3)
+    torch.testing.assert_close(db_a, db_b, atol=1e-2 * N * H, rtol=1e-3)
+    torch.testing.assert_close(a.float(), b.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_fused_bottleneck_chain_hands_off_bn_statistics(monkeypatch):
+    """Two consecutive fused blocks: block 2's conv1 dgrad computes block 1's bn3
+    backward statistics (cross-block hand-off); gradients match the op-by-op path."""
+    from cloud_amd.models import fused_block
+    from cloud_amd.models.resnet import Bottleneck
+    from cloud_amd.ops import raw
+    from cloud_amd.optim import SGD
+
+    torch.manual_seed(13)
+    net = torch.nn.Sequential(
+        Bottleneck(64, 16, 1, dtype=torch.bfloat16, device=DEV, zero_init_residual=False),
+        Bottleneck(64, 16, 1, dtype=torch.bfloat16, device=DEV, zero_init_residual=False),
+        Bottleneck(64, 32, 2, dtype=torch.bfloat16, device=DEV, zero_init_residual=False))
+    opt = SGD(net, learning_rate=0.0)
+    x = torch.randn(4, 16, 16, 64, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(4, 8, 8, 128, device=DEV).to(torch.bfloat16)
+    taken = []
+    orig_take = fused_block._take
+
+    def spy(dout):
+        r = orig_take(dout)
+        taken.append(r is not None)
+        return r
+
+    monkeypatch.setattr(fused_block, "_take", spy)
+
+    def run(fused, epi):
+        monkeypatch.setenv("CLOUD_AMD_BN_BWD_EPILOGUE", "1" if epi else "0")
+        for b in net:
+            b.fused_block = fused
+        opt.zero_grad()
+        xi = x.clone().requires_grad_()
+        out = net(xi)
+        out.backward(dy)
+        return xi.grad.float(), {n: p.grad.detach().float().clone() for n, p in net.named_parameters()}
+
+    dx_e, g_e = run(True, True)
+    assert taken == [False, True, True], taken  # last block has no producer; blocks 2 and 1 take
+    dx_n, g_n = run(True, False)
+    dx_u, g_u = run(False, False)
+
+    def close(a, b, tol=2e-2):
+        torch.testing.assert_close(a, b, atol=tol * (b.abs().max().item() + 1e-3), rtol=tol)
+
+    close(dx_e, dx_n)
+    close(dx_e, dx_u)
+    for n in g_e:
+        close(g_e[n], g_n[n])
+        close(g_e[n], g_u[n])
