@@ -32,7 +32,9 @@ typedef __attribute__((address_space(3))) s4v lds_s4v;
 constexpr int BK = 64;
 constexpr int PAD = 8;
 
-enum Epi { EPI_BF16 = 0, EPI_F32_PARTIAL = 1 };
+// EPI_BF16_BN: EPI_BF16 plus the BN-backward statistics (CoreParams::bnz); a separate
+// instantiation so the plain bf16 epilogue carries none of its registers.
+enum Epi { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_BF16_BN = 2 };
 
 // Fast unsigned division by a runtime constant (n < 2^31): q = (umulhi(n, m) + n) >> s.
 struct FastDiv {
@@ -283,13 +285,44 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
     const bool fx = P.act != ACT_NONE || P.dact_src != nullptr || P.preact != nullptr;
     bf16_t* Cg = reinterpret_cast<bf16_t*>(P.C);
     float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, bzsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    (void)bsum;
+    (void)bzsum;
+    // Each thread owns one 8-column group (NT is a multiple of BN/8) and walks IT rows.
+    // The global reads of the epilogue (old C for beta, BN input z and ReLU mask for
+    // the BN-backward statistics) are issued PF rows at a time before any is used, so
+    // a tile pays ceil(IT/PF) memory round trips instead of IT.
     constexpr int CH = BM * BN / 8;
-    for (int c = tid; c < CH; c += NT) {
-      const int row = c / (BN / 8), col = (c % (BN / 8)) * 8;
-      const int gm = m0 + row, gn = n0 + col;
-      if (gm < P.M && gn < P.N) {
+    static_assert(CH % NT == 0, "epilogue chunks must divide the threads");
+    constexpr int IT = CH / NT;
+    constexpr bool BNS = EPI == EPI_BF16_BN;
+    constexpr int PF = BNS ? (IT < 2 ? IT : 2) : 1;
+    const int col = (tid % (BN / 8)) * 8;
+    const int gn = n0 + col;
+    const bool has_beta = P.beta != 0.f;
+#pragma unroll 1
+    for (int it0 = 0; it0 < IT; it0 += PF) {
+      s8v opre[PF], zpre[BNS ? PF : 1];
+      uint32_t mpre[BNS ? PF : 1];
+      long orow[PF];
+      bool okr[PF];
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int gm = m0 + (tid + (it0 + u) * NT) / (BN / 8);
+        okr[u] = gm < P.M && gn < P.N;
+        orow[u] = okr[u] ? out_row(P, gm) : 0;
+        opre[u] = (has_beta && okr[u]) ? *reinterpret_cast<const s8v*>(Cg + orow[u] * P.ldc + gn) : zero8();
+        if constexpr (BNS) {
+          zpre[u] = okr[u] ? *reinterpret_cast<const s8v*>(P.bnz + orow[u] * P.ldc + gn) : zero8();
+          mpre[u] = (P.bnmask && okr[u]) ? (uint32_t)P.bnmask[orow[u] * (P.N / 8) + (gn >> 3)] : 0xffu;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        if (!okr[u]) continue;
+        const int row = (tid + (it0 + u) * NT) / (BN / 8);
+        const int gm = m0 + row;
         s8v v = *reinterpret_cast<const s8v*>(Cs + row * EPI_LD + col);
-        bf16_t* dst = Cg + out_row(P, gm) * P.ldc + gn;
+        bf16_t* dst = Cg + orow[u] * P.ldc + gn;
         if (fx) {
           if (P.preact) *reinterpret_cast<s8v*>(P.preact + (long)gm * P.ld_aux + gn) = v;
           if (P.dact_src) {
@@ -302,29 +335,24 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
             for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(act_fwd(P.act, bf2f((bf16_t)v[j])));
           }
         }
-        if (P.beta != 0.f) {
-          s8v o = *reinterpret_cast<const s8v*>(dst);
+        if (has_beta) {
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            v[j] = (short)f2bf(bf2f((bf16_t)v[j]) + P.beta * bf2f((bf16_t)o[j]));
+            v[j] = (short)f2bf(bf2f((bf16_t)v[j]) + P.beta * bf2f((bf16_t)opre[u][j]));
         }
-        if (P.stats && !P.bnz && (fx || P.beta != 0.f)) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
+        if (!BNS && P.stats && (fx || has_beta)) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
         *reinterpret_cast<s8v*>(dst) = v;
-        if (P.bnz) {
-          // NT is a multiple of BN/8, so this thread always owns the same 8 columns
-          const long orow = out_row(P, gm);
-          const s8v zv = *reinterpret_cast<const s8v*>(P.bnz + orow * P.ldc + gn);
-          const uint32_t mb = P.bnmask ? (uint32_t)P.bnmask[orow * (P.N / 8) + (gn >> 3)] : 0xffu;
+        if constexpr (BNS) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float g = ((mb >> j) & 1u) ? bf2f((bf16_t)v[j]) : 0.f;
+            const float g = ((mpre[u] >> j) & 1u) ? bf2f((bf16_t)v[j]) : 0.f;
             bsum[j] += g;
-            bzsum[j] += g * bf2f((bf16_t)zv[j]);
+            bzsum[j] += g * bf2f((bf16_t)zpre[u][j]);
           }
         }
       }
     }
-    if (P.bnz) {
+    if constexpr (BNS) {
       constexpr int CG = BN / 8, PARTS = NT / CG;
       static_assert(NT % CG == 0, "column groups must divide the threads");
       const int cg = tid % CG, part = tid / CG;

@@ -491,6 +491,21 @@ long ca_conv_dgrad_stat_tiles(int Nb, int H, int W, int sh, int sw) {
   return t;
 }
 
+}  // extern "C"
+
+template <int EPI>
+static int launch_dgrad(const CoreParams& p, int Cin, hipStream_t s) {
+  if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI>(p, 1, s);
+  return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI>(p, 1, s);
+}
+
+// one output-parity class of a strided dgrad (row map on)
+template <int EPI>
+static int launch_dgrad_s(const CoreParams& q, int Cin, hipStream_t s) {
+  if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradSA, GConvDgradSB, EPI>(q, 1, s);
+  return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradSA, GConvDgradSB, EPI>(q, 1, s);
+}
+
 static int conv_dgrad_impl(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb, int H, int W, int Cin, int Cout,
                            int KH, int KW, int sh, int sw, int ph, int pw, float beta, const bf16_t* bnz,
                            const uint8_t* bnmask, float* stats, hipStream_t s) {
@@ -530,16 +545,15 @@ static int conv_dgrad_impl(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb
           q.stats = stats + stat_row * 2 * Cin;  // this class's tiles follow the previous classes'
           stat_row += (q.M + 127) / 128;
         }
-        int rc = (Cin <= 64)
-                     ? launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradSA, GConvDgradSB, EPI_BF16>(q, 1, s)
-                     : launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradSA, GConvDgradSB, EPI_BF16>(q, 1, s);
+        int rc = bnz ? launch_dgrad_s<EPI_BF16_BN>(q, Cin, s) : launch_dgrad_s<EPI_BF16>(q, Cin, s);
         if (rc) return rc;
       }
     return 0;
   }
-  if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI_BF16>(p, 1, s);
-  return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI_BF16>(p, 1, s);
+  return bnz ? launch_dgrad<EPI_BF16_BN>(p, Cin, s) : launch_dgrad<EPI_BF16>(p, Cin, s);
 }
+
+extern "C" {
 
 // dx[Nb,H,W,Cin] = dgrad(dy[Nb,OH,OW,Cout], w) (+ beta * dx).
 int ca_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb, int H, int W, int Cin, int Cout, int KH,

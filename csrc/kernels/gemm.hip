@@ -115,14 +115,18 @@ static double tile_balance(long tiles) {
   return (double)tiles / (double)(rounds * cus);
 }
 
-template <int EPI>
-int dispatch(int layout, const CoreParams& p, int splits, hipStream_t s) {
-  // 128-wide N tiles unless N is small, or the 128-wide grid would leave a badly
-  // filled last round (e.g. M=8192, N=768: 384 tiles -> 1.5 rounds) and halving
-  // the tile width balances it (768 tiles -> 3 full rounds).
+// 128-wide N tiles unless N is small, or the 128-wide grid would leave a badly
+// filled last round (e.g. M=8192, N=768: 384 tiles -> 1.5 rounds) and halving
+// the tile width balances it (768 tiles -> 3 full rounds).
+static bool want_small_n(const CoreParams& p, int splits) {
   const long tm = (p.M + 127) / 128;
   const long t128 = tm * ((p.N + 127) / 128) * splits, t64 = tm * ((p.N + 63) / 64) * splits;
-  const bool small_n = p.N <= 64 || (tile_balance(t128) < 0.8 && tile_balance(t64) > tile_balance(t128) + 0.1);
+  return p.N <= 64 || (tile_balance(t128) < 0.8 && tile_balance(t64) > tile_balance(t128) + 0.1);
+}
+
+template <int EPI>
+int dispatch(int layout, const CoreParams& p, int splits, hipStream_t s) {
+  const bool small_n = want_small_n(p, splits);
   switch (layout) {
     case 0:
       return small_n ? launch<128, 64, DenseKC, DenseKC, GDenseKC, GDenseKC, EPI>(p, splits, s)
@@ -178,13 +182,14 @@ int ca_gemm_bf16(int layout, const bf16_t* A, long lda, const bf16_t* B, long ld
 int ca_gemm_bf16_bnstats(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc,
                          int M, int N, int K, float beta, const bf16_t* bnz, const uint8_t* bnmask, float* stats,
                          hipStream_t s) {
-  if (N % 8 != 0 || K % 8 != 0 || layout == 2 || !bnz || !stats) return -1;
+  if (N % 8 != 0 || K % 8 != 0 || layout != 1 || !bnz || !stats) return -1;
   CoreParams p = base_params(A, lda, B, ldb, C, ldc, M, N, K);
   p.stats = stats;
   p.beta = beta;
   p.bnz = bnz;
   p.bnmask = bnmask;
-  return dispatch<EPI_BF16>(layout, p, 1, s);
+  return want_small_n(p, 1) ? launch<128, 64, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI_BF16_BN>(p, 1, s)
+                            : launch<128, 128, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI_BF16_BN>(p, 1, s);
 }
 
 // Dense-layer GEMM with the fused epilogue: C = act(A*B + bias) (+ beta*C),
