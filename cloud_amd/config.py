@@ -42,8 +42,8 @@ _VARS = [
     Var("CLOUD_AMD_GEMM", str, "native", "dense GEMMs: 'native' or 'torch'", "ops"),
     Var("CLOUD_AMD_CONV", str, "native", "convolutions: 'native' or 'torch'", "ops"),
     Var("CLOUD_AMD_GEMM_CORE", str, "glds", "GEMM/conv staging core: 'glds' (LDS-DMA) or 'reg' (register)", "ops"),
-    Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block backward: weight-gradient GEMMs on a second HIP "
-        "stream, overlapping the memory-bound BN/dgrad chain", "ops"),
+    Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "
+        "second HIP stream, overlapping the memory-bound BN/LN/dgrad chain", "ops"),
     Var("CLOUD_AMD_BN_BWD_EPILOGUE", bool, True, "ResNet block backward: BatchNorm-backward statistics from the "
         "dgrad GEMM epilogues (skips the BN reduction pass)", "ops"),
     Var("CLOUD_AMD_PRECISION", str, "bf16", "compute dtype of the Keras front end", "ops"),

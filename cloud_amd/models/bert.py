@@ -38,6 +38,7 @@ import torch.nn.functional as F
 
 from ..ops import _ext, raw
 from ..ops.dropout import next_seed
+from ..runtime.side_stream import SideWork
 
 
 @dataclass
@@ -204,20 +205,29 @@ class _LayerFn(torch.autograd.Function):
             return sinks[id(p)]
 
         dy2 = dy2.contiguous()
+        # weight / bias gradients (compute-bound GEMMs + column sums) go to the side
+        # stream; the memory-bound LN / attention / dgrad chain stays on the main stream
+        side = SideWork(dy2.device)
+        deferred = []
+
+        def param_grads(dy, inp, w, b):
+            def fn():
+                raw.colsum_into(dy, G(b))
+                raw.wgrad_into(dy, inp, G(w))
+            side.run(fn, dy, inp)
+            if side.enabled:
+                deferred.extend((b, w))
+            else:
+                _notify(b), _notify(w)
+
         # LN2 (+ residual y1, + dropout on the FFN output)
         dh2, do = raw.ln_bwd(dy2, h2, m2, r2, layer.ln2_w, G(layer.ln2_w), G(layer.ln2_b), p_in=p_hidden, seed_in=s2,
                              want_dx=True)
         _notify(layer.ln2_b), _notify(layer.ln2_w)
-        raw.colsum_into(do, G(layer.b2))
-        _notify(layer.b2)
-        raw.wgrad_into(do, f, G(layer.w2))
-        _notify(layer.w2)
+        param_grads(do, f, layer.w2, layer.b2)
         dpre = raw.gemm(do, layer.w2, layout=raw.NN, act=cfg.hidden_act, dact_src=pre)
         del do, f
-        raw.colsum_into(dpre, G(layer.b1))
-        _notify(layer.b1)
-        raw.wgrad_into(dpre, y1, G(layer.w1))
-        _notify(layer.w1)
+        param_grads(dpre, y1, layer.w1, layer.b1)
         raw.gemm(dpre, layer.w1, layout=raw.NN, out=dh2, beta=1.0)  # dy1 = dh2 + dpre W1
         del dpre
         dy1 = dh2
@@ -226,20 +236,17 @@ class _LayerFn(torch.autograd.Function):
                              want_dx=True)
         _notify(layer.ln1_b), _notify(layer.ln1_w)
         del dy1
-        raw.colsum_into(da, G(layer.bo))
-        _notify(layer.bo)
-        raw.wgrad_into(da, ctx_, G(layer.wo))
-        _notify(layer.wo)
+        param_grads(da, ctx_, layer.wo, layer.bo)
         dctx = raw.gemm(da, layer.wo, layout=raw.NN)
         del da
         dqkv = raw.attn_bwd(qkv, ctx_, dctx, lse, B, S, H, key_len, p_attn, sa,
                             scale=1.0 / math.sqrt(cfg.hidden_size // H))
         del dctx
-        raw.colsum_into(dqkv, G(layer.bqkv))
-        _notify(layer.bqkv)
-        raw.wgrad_into(dqkv, x, G(layer.wqkv))
-        _notify(layer.wqkv)
+        param_grads(dqkv, x, layer.wqkv, layer.bqkv)
         raw.gemm(dqkv, layer.wqkv, layout=raw.NN, out=dh1, beta=1.0)  # dx = dh1 + dqkv Wqkv
+        side.join()
+        for p in deferred:
+            _notify(p)
         return (dh1, None, None, None, None, None, None) + tuple(owned)
 
 

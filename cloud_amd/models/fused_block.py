@@ -39,19 +39,7 @@ import torch
 
 from .. import config
 from ..ops import _ext, raw
-
-_WGRAD_STREAMS = {}
-
-
-def _wgrad_stream(dev):
-    """The per-device side stream for weight gradients (None when disabled)."""
-    if not config.get("CLOUD_AMD_WGRAD_STREAM"):
-        return None
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
-    st = _WGRAD_STREAMS.get(key)
-    if st is None:
-        st = _WGRAD_STREAMS[key] = torch.cuda.Stream(torch.device("cuda", key))
-    return st
+from ..runtime.side_stream import SideWork
 
 
 # Cross-block hand-off of bn3 statistics (one slot: blocks run backward one after
@@ -165,25 +153,16 @@ class _BottleneckFn(torch.autograd.Function):
                                       bn=bn_src)
             return raw.conv_dgrad(dz, conv.weight, shape, conv.stride, conv.padding, out=out, beta=beta), None
 
-        main = torch.cuda.current_stream(x.device)
-        side = _wgrad_stream(x.device)
+        side = SideWork(x.device)
         deferred = []
 
         def wgrad(conv, dz, inp):
-            if side is None:
-                raw.conv_wgrad(dz, inp, conv.weight.shape, conv.stride, conv.padding, out=conv.weight.grad,
-                               beta=1.0)
+            side.run(lambda: raw.conv_wgrad(dz, inp, conv.weight.shape, conv.stride, conv.padding,
+                                            out=conv.weight.grad, beta=1.0), dz, inp)
+            if side.enabled:
+                deferred.append(conv.weight)
+            else:
                 ddp.notify_grad_ready(conv.weight)
-                return
-            # fork: the side stream sees everything queued so far on the main stream (dz, inp,
-            # the zeroed arena); the inputs must outlive the side-stream kernels that read them
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                raw.conv_wgrad(dz, inp, conv.weight.shape, conv.stride, conv.padding, out=conv.weight.grad,
-                               beta=1.0)
-            dz.record_stream(side)
-            inp.record_stream(side)
-            deferred.append(conv.weight)
 
         dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=True, partials=_take(dout) if epi else None)
         del dout
@@ -213,12 +192,11 @@ class _BottleneckFn(torch.autograd.Function):
             _park(dx, p_prev)
         ctx.prev_src = None
         wgrad(blk.conv1, dz1, x)
-        if deferred:
-            # join: later kernels on the main stream (and DDP's bucket events recorded on it)
-            # are ordered after this block's weight gradients
-            main.wait_stream(side)
-            for w in deferred:
-                ddp.notify_grad_ready(w)
+        # join: later kernels on the main stream (and DDP's bucket events recorded on it)
+        # are ordered after this block's weight gradients
+        side.join()
+        for w in deferred:
+            ddp.notify_grad_ready(w)
         return (dx, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
 

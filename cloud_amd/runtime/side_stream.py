@@ -1,0 +1,64 @@
+"""Fork/join of independent backward work onto a second HIP stream.
+
+Weight-gradient GEMMs are compute bound, while the rest of a layer's backward
+(BatchNorm / LayerNorm backward, dgrad epilogues, attention backward) is mostly
+memory bound.  They are independent, so a layer's backward queues its weight
+gradients on a per-device side stream and the two streams share the CUs:
+
+    side = SideWork(device)
+    side.run(lambda: raw.wgrad_into(dy, x, w.grad), dy, x)   # fork
+    ...                                                       # main-stream work
+    side.join(); notify DDP for the deferred params           # join
+
+``run`` makes the side stream wait for everything queued so far on the main
+stream (the inputs and the zeroed gradient arena), launches ``fn`` under the
+side stream (its workspaces come from the side stream's allocator pool) and
+marks the input tensors as used by the side stream, so the caching allocator
+does not hand their memory to a main-stream tensor before the kernels that
+read them have run.  ``join`` orders all later main-stream work (including
+DDP's bucket events) after the side work.  Disabled (``CLOUD_AMD_WGRAD_STREAM=0``)
+or on CPU, ``run`` simply calls ``fn``.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import config
+
+_STREAMS = {}
+
+
+def side_stream(device):
+    """The per-device side stream (created once; normal priority)."""
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    st = _STREAMS.get(key)
+    if st is None:
+        st = _STREAMS[key] = torch.cuda.Stream(torch.device("cuda", key))
+    return st
+
+
+class SideWork:
+    def __init__(self, device, enabled=None):
+        if enabled is None:
+            enabled = config.get("CLOUD_AMD_WGRAD_STREAM")
+        self.enabled = bool(enabled) and device.type == "cuda"
+        self.main = torch.cuda.current_stream(device) if self.enabled else None
+        self.side = side_stream(device) if self.enabled else None
+        self.used = False
+
+    def run(self, fn, *tensors):
+        if not self.enabled:
+            return fn()
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            r = fn()
+        for t in tensors:
+            if t is not None:
+                t.record_stream(self.side)
+        self.used = True
+        return r
+
+    def join(self):
+        if self.used:
+            self.main.wait_stream(self.side)
+            self.used = False
