@@ -32,9 +32,11 @@ typedef __attribute__((address_space(3))) s4v lds_s4v;
 constexpr int BK = 64;
 constexpr int PAD = 8;
 
-// EPI_BF16_BN: EPI_BF16 plus the BN-backward statistics (CoreParams::bnz); a separate
-// instantiation so the plain bf16 epilogue carries none of its registers.
-enum Epi { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_BF16_BN = 2 };
+// EPI_BF16_BN: EPI_BF16 plus the BN-backward statistics (CoreParams::bnz);
+// EPI_BF16_ST: EPI_BF16 plus the BN-forward statistics [sum | sum of squares] of the
+// stored values, accumulated in registers by the storing thread.  Separate
+// instantiations, so the plain bf16 epilogue carries none of their registers.
+enum Epi { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_BF16_BN = 2, EPI_BF16_ST = 3 };
 
 // Fast unsigned division by a runtime constant (n < 2^31): q = (umulhi(n, m) + n) >> s.
 struct FastDiv {
@@ -294,7 +296,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
     constexpr int CH = BM * BN / 8;
     static_assert(CH % NT == 0, "epilogue chunks must divide the threads");
     constexpr int IT = CH / NT;
-    constexpr bool BNS = EPI == EPI_BF16_BN;
+    constexpr bool BNS = EPI == EPI_BF16_BN, STS = EPI == EPI_BF16_ST, RSTAT = BNS || STS;
     constexpr int PF = BNS ? (IT < 2 ? IT : 2) : 1;
     const int col = (tid % (BN / 8)) * 8;
     const int gn = n0 + col;
@@ -340,8 +342,16 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
           for (int j = 0; j < 8; ++j)
             v[j] = (short)f2bf(bf2f((bf16_t)v[j]) + P.beta * bf2f((bf16_t)opre[u][j]));
         }
-        if (!BNS && P.stats && (fx || has_beta)) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
+        if (!RSTAT && P.stats && (fx || has_beta)) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
         *reinterpret_cast<s8v*>(dst) = v;
+        if constexpr (STS) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float a = bf2f((bf16_t)v[j]);
+            bsum[j] += a;
+            bzsum[j] += a * a;
+          }
+        }
         if constexpr (BNS) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -352,7 +362,8 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
         }
       }
     }
-    if constexpr (BNS) {
+    if constexpr (RSTAT) {
+      // [sum | second moment] per column: registers -> LDS -> one thread per column
       constexpr int CG = BN / 8, PARTS = NT / CG;
       static_assert(NT % CG == 0, "column groups must divide the threads");
       const int cg = tid % CG, part = tid / CG;

@@ -474,6 +474,10 @@ int ca_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   p.A = x; p.B = w; p.lda = Cin; p.ldb = (long)KH * KW * Cin; p.C = y; p.ldc = Cout;
   p.M = Nb * p.OH * p.OW; p.N = Cout; p.K = KH * KW * Cin; p.k_per_split = p.K;
   p.stats = stats;
+  if (stats) {
+    if (Cout <= 64) return launch<128, 64, ConvFwdA, DenseKC, GConvFwdA, GDenseKC, EPI_BF16_ST>(p, 1, s);
+    return launch<128, 128, ConvFwdA, DenseKC, GConvFwdA, GDenseKC, EPI_BF16_ST>(p, 1, s);
+  }
   if (Cout <= 64) return launch<128, 64, ConvFwdA, DenseKC, GConvFwdA, GDenseKC, EPI_BF16>(p, 1, s);
   return launch<128, 128, ConvFwdA, DenseKC, GConvFwdA, GDenseKC, EPI_BF16>(p, 1, s);
 }

@@ -172,6 +172,9 @@ int ca_gemm_bf16(int layout, const bf16_t* A, long lda, const bf16_t* B, long ld
   CoreParams p = base_params(A, lda, B, ldb, C, ldc, M, N, K);
   p.stats = stats;
   p.beta = beta;
+  if (stats && layout == 0)  // forward 1x1 conv feeding a BatchNorm: register-accumulated statistics
+    return want_small_n(p, 1) ? launch<128, 64, DenseKC, DenseKC, GDenseKC, GDenseKC, EPI_BF16_ST>(p, 1, s)
+                              : launch<128, 128, DenseKC, DenseKC, GDenseKC, GDenseKC, EPI_BF16_ST>(p, 1, s);
   return dispatch<EPI_BF16>(layout, p, 1, s);
 }
 
