@@ -13,6 +13,7 @@ import torch
 import torch.nn as nn
 
 from . import fused_block
+from ..ops import conv as conv_ops
 from .layers import BatchNormAct, Conv2d, GlobalAvgPool, Linear, MaxPool2d
 
 
@@ -58,6 +59,7 @@ class ResNet(nn.Module):
         self.conv1 = Conv2d(self.stem_cin, 64, 7, stride=2, padding=3, dtype=dtype, device=device)
         self.bn1 = BatchNormAct(64, relu=True, device=device)
         self.maxpool = MaxPool2d(3, 2, 1)
+        self.stem_s2d = True  # space-to-depth stem on the native path (ops.conv.stem_conv_s2d)
         blocks = []
         cin = 64
         for i, (n, width) in enumerate(zip(layers, (64, 128, 256, 512))):
@@ -72,9 +74,15 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         """x: NHWC [N, H, W, in_channels] in the compute dtype -> logits [N, classes]."""
-        if self.stem_cin != self.in_channels:
-            x = torch.nn.functional.pad(x, (0, self.stem_cin - self.in_channels))
-        x = self.maxpool(self.bn1(self.conv1(x, stats=True)))
+        c1 = self.conv1
+        if self.stem_s2d and x.shape[-1] == self.in_channels and conv_ops.stem_s2d_ok(x, c1.weight, c1.stride,
+                                                                                         c1.padding):
+            # 7x7/2 stem as a 4x4/1 conv over the space-to-depth input (no channel pad pass)
+            x = self.maxpool(self.bn1(conv_ops.stem_conv_s2d(x, c1.weight, stats=True)))
+        else:
+            if self.stem_cin != self.in_channels:
+                x = torch.nn.functional.pad(x, (0, self.stem_cin - self.in_channels))
+            x = self.maxpool(self.bn1(self.conv1(x, stats=True)))
         x = self.layers(x)
         return self.fc(self.pool(x))
 

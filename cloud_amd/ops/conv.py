@@ -102,6 +102,88 @@ class _ConvFn(torch.autograd.Function):
         return dx, dw, dparam, None, None, None
 
 
+def _s2d_weight(w, cx):
+    """[Cout, 7, 7, Cin] -> [Cout, 4, 4, 16]: W'[o, ay, ax, (by, bx, c)] = W[o, 2ay+by, 2ax+bx, c] (zero
+    where 2a+b = 7 or c >= cx)."""
+    Cout = w.shape[0]
+    wp = F.pad(w[..., :cx], (0, 4 - cx, 0, 1, 0, 1))          # [Cout, 8, 8, 4]
+    return wp.view(Cout, 4, 2, 4, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(Cout, 4, 4, 16).contiguous()
+
+
+def _s2d_weight_grad(g, cx):
+    """Adjoint of :func:`_s2d_weight`: [Cout, 4, 4, 16] -> [Cout, 7, 7, cx]."""
+    Cout = g.shape[0]
+    return g.view(Cout, 4, 4, 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(Cout, 8, 8, 4)[:, :7, :7, :cx]
+
+
+class _StemS2DFn(torch.autograd.Function):
+    """7x7 / stride 2 / pad 3 stem convolution as a 4x4 / stride 1 convolution over the
+    space-to-depth input (K = 256 instead of 392 for the 8-channel padded input; the
+    input transform replaces the per-step channel pad).  Weight gradient only (the
+    network input needs none)."""
+
+    @staticmethod
+    def forward(ctx, x, w, param, stats):
+        ext = _ext.load(required=True)
+        N, H, W, cx = x.shape
+        Cout = w.shape[0]
+        OH, OW = _out(H, 7, 2, 3), _out(W, 7, 2, 3)
+        Hs, Ws = OH + 3, OW + 3
+        st = _ext.stream_handle(x.device)
+        xs = torch.empty((N, Hs, Ws, 16), dtype=torch.bfloat16, device=x.device)
+        ext.stem_s2d(x.data_ptr(), xs.data_ptr(), N, H, W, cx, Hs, Ws, 3, st)
+        ws = _s2d_weight(w, cx)
+        y = torch.empty((N, OH, OW, Cout), dtype=torch.bfloat16, device=x.device)
+        ext.conv_fwd(xs.data_ptr(), ws.data_ptr(), y.data_ptr(), N, Hs, Ws, 16, Cout, 4, 4, 1, 1, 0, 0,
+                     _ext.ptr(stats), st)
+        ctx.save_for_backward(xs)
+        ctx.param, ctx.cx, ctx.wshape = param, cx, w.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import raw
+
+        (xs,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        Cout = dy.shape[-1]
+        g = torch.zeros((Cout, 4, 4, 16), dtype=torch.float32, device=dy.device)
+        raw.conv_wgrad(dy, xs, g.shape, 1, 0, out=g, beta=0.0)
+        gw = _s2d_weight_grad(g, ctx.cx)
+        param = ctx.param
+        sink = gemm._grad_sink(param) if param is not None else None
+        if sink is not None:
+            sink[..., :ctx.cx] += gw.to(sink.dtype)
+            from ..parallel import ddp
+
+            ddp.notify_grad_ready(param)
+            return None, None, None, None
+        full = torch.zeros(ctx.wshape, dtype=torch.float32, device=dy.device)
+        full[..., :ctx.cx] = gw
+        if param is not None:
+            return None, None, full.to(param.dtype), None
+        return None, full.to(torch.bfloat16), None, None
+
+
+def stem_s2d_ok(x, w, stride, padding):
+    """The space-to-depth stem applies: native bf16, 7x7 / 2 / pad 3, <= 4 input channels."""
+    return (_conv_mode() == "native" and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and tuple(w.shape[1:3]) == (7, 7) and stride == 2 and padding == 3 and x.shape[-1] <= 4
+            and x.shape[-1] <= w.shape[-1] and x.is_contiguous() and not x.requires_grad and _ext.use_native(x, w))
+
+
+def stem_conv_s2d(x, w, stats=False):
+    """y = conv(x, w[..., :Cx], stride 2, pad 3) for the raw (unpadded) network input x
+    [N, H, W, Cx <= 4]; w: [Cout, 7, 7, Cin_w >= Cx].  ``stats`` as :func:`conv2d_nhwc`."""
+    N, H, W, _ = x.shape
+    Cout = w.shape[0]
+    OH, OW = _out(H, 7, 2, 3), _out(W, 7, 2, 3)
+    part = stats_buffer(N * OH * OW, Cout, x.device) if stats else None
+    param = w if (w.is_leaf and w.requires_grad) else None
+    y = _StemS2DFn.apply(x, w.detach() if param is not None else w, param, part)
+    return (y, part) if stats else y
+
+
 def stats_buffer(rows, channels, device):
     """Partials buffer for the fused BN-statistics epilogue: [ceil(rows/128)][2][C] fp32."""
     return torch.empty(((rows + 127) // 128, 2, channels), dtype=torch.float32, device=device)

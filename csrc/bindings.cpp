@@ -34,6 +34,7 @@ int ca_gemm_bf16_bnstats(int, const bf16_t*, long, const bf16_t*, long, bf16_t*,
 long ca_conv_dgrad_stat_tiles(int, int, int, int, int);
 int ca_conv_dgrad_bnstats(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
                           int, float, const bf16_t*, const uint8_t*, float*, hipStream_t);
+int ca_stem_s2d(const bf16_t*, bf16_t*, int, int, int, int, int, int, int, hipStream_t);
 int ca_softmax_xent(const void*, int, const int64_t*, int, int, float, float, float*, float*, void*, hipStream_t);
 int ca_maxpool_fwd(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ca_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -157,6 +158,9 @@ PYBIND11_MODULE(_C, m) {
                                 sh, sw, ph, pw, beta, P(const bf16_t*, z), P(const uint8_t*, mask), P(float*, stats),
                                 S(s)),
           "conv_dgrad_bnstats");
+  });
+  m.def("stem_s2d", [](u64 x, u64 y, int N, int H, int W, int C, int Hs, int Ws, int pad, u64 s) {
+    check(ca_stem_s2d(P(const bf16_t*, x), P(bf16_t*, y), N, H, W, C, Hs, Ws, pad, S(s)), "stem_s2d");
   });
   m.def("softmax_xent", [](u64 z, int zbf, u64 labels, int B, int C, float gscale, float ls, u64 loss, u64 correct,
                            u64 dz, u64 s) {

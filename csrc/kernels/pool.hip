@@ -136,7 +136,44 @@ __global__ void __launch_bounds__(256) gap_bwd_kernel(const TI* __restrict__ dy,
 
 }  // namespace
 
+// Space-to-depth of the network input for the 7x7/2 stem (pad 3):
+//   y[n, i, j, (by*2 + bx)*4 + c] = x[n, 2i + by - pad, 2j + bx - pad, c]   (c < C <= 4; else / outside: 0)
+// turns the stride-2 7x7 conv into a stride-1 4x4 conv over 16 channels (K = 256
+// instead of 7*7*8 = 392 with the 8-channel padded input).  One thread per output
+// pixel: 16 bf16 = two 16-B stores.
+__global__ void __launch_bounds__(256) stem_s2d_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N,
+                                                       int H, int W, int C, int Hs, int Ws, int pad) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)N * Hs * Ws;
+  if (idx >= total) return;
+  const int j = (int)(idx % Ws);
+  const long t = idx / Ws;
+  const int i = (int)(t % Hs);
+  const int n = (int)(t / Hs);
+  us8 out[2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int by = q >> 1, bx = q & 1;
+    const int u = 2 * i + by - pad, v = 2 * j + bx - pad;
+    const bool ok = (unsigned)u < (unsigned)H && (unsigned)v < (unsigned)W;
+    const bf16_t* src = x + (((long)n * H + (ok ? u : 0)) * W + (ok ? v : 0)) * C;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) out[q >> 1][(q & 1) * 4 + c] = (ok && c < C) ? src[c] : (bf16_t)0;
+  }
+  us8* dst = reinterpret_cast<us8*>(y + idx * 16);
+  dst[0] = out[0];
+  dst[1] = out[1];
+}
+
 extern "C" {
+
+int ca_stem_s2d(const bf16_t* x, bf16_t* y, int N, int H, int W, int C, int Hs, int Ws, int pad, hipStream_t st) {
+  if (C < 1 || C > 4) return -1;
+  const long total = (long)N * Hs * Ws;
+  stem_s2d_kernel<<<(unsigned)((total + 255) / 256), 256, 0, st>>>(x, y, N, H, W, C, Hs, Ws, pad);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
 
 int ca_maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH, int OW,
                    int k, int s, int p, hipStream_t st) {

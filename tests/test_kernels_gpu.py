@@ -418,3 +418,27 @@ def test_fused_bottleneck_chain_hands_off_bn_statistics(monkeypatch):
     for n in g_e:
         close(g_e[n], g_n[n])
         close(g_e[n], g_u[n])
+
+
+def test_stem_space_to_depth_matches_direct_conv():
+    """7x7/2/pad3 stem via space-to-depth (4x4/1 over 16 channels): output, BN statistics
+    partials and weight gradient equal the direct implicit-GEMM conv on the padded input."""
+    from cloud_amd.models.layers import Conv2d
+    from cloud_amd.ops import conv as conv_ops
+
+    torch.manual_seed(14)
+    conv = Conv2d(8, 64, 7, stride=2, padding=3, dtype=torch.bfloat16, device=DEV)
+    x = torch.randn(2, 30, 34, 3, device=DEV).to(torch.bfloat16)
+    assert conv_ops.stem_s2d_ok(x, conv.weight, 2, 3)
+    y1, p1 = conv_ops.stem_conv_s2d(x, conv.weight, stats=True)
+    dy = torch.randn_like(y1)
+    y1.backward(dy)
+    g1 = conv.weight.grad.detach().float().clone()
+    conv.weight.grad = None
+    y2, p2 = conv(torch.nn.functional.pad(x, (0, 5)), stats=True)
+    y2.backward(dy)
+    g2 = conv.weight.grad.detach().float()
+    torch.testing.assert_close(y1.float(), y2.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(p1.sum(0), p2.sum(0), atol=0.5, rtol=1e-2)
+    assert g1[..., 3:].abs().max().item() == 0.0
+    torch.testing.assert_close(g1[..., :3], g2[..., :3], atol=3e-2 * g2.abs().max().item(), rtol=3e-2)
