@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Memory-bound small-K GEMMs of ResNet-50 stage 1 at batch 512 (1x1 convs, NHWC):
+cloud_amd MFMA kernels vs hipBLASLt (torch.mm) vs a plain copy of the output size.
+Reports us and effective HBM TB/s (A read + C write [+ C read for beta]).  One JSON line per case."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench.gemm_shapes import timeit  # noqa: E402
+from cloud_amd.ops import _ext, raw  # noqa: E402
+
+
+def main():
+    ext = _ext.load(required=True)
+    dev = torch.device("cuda", 0)
+    st = _ext.stream_handle(dev)
+    for (M, K, N) in [(512 * 56 * 56, 64, 256), (512 * 56 * 56, 256, 64), (512 * 56 * 56, 64, 64),
+                      (512 * 28 * 28, 128, 512), (512 * 28 * 28, 512, 128)]:
+        a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        w = torch.randn(N, K, device=dev).to(torch.bfloat16)
+        c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        stats = torch.empty(((M + 127) // 128, 2, N), device=dev)
+        byts = (M * K + M * N) * 2
+
+        def ours():
+            ext.gemm_bf16(0, a.data_ptr(), K, w.data_ptr(), K, c.data_ptr(), N, M, N, K, 0, 0.0, st)
+
+        def ours_st():
+            ext.gemm_bf16(0, a.data_ptr(), K, w.data_ptr(), K, c.data_ptr(), N, M, N, K, stats.data_ptr(), 0.0, st)
+
+        def blas():
+            torch.mm(a, w.t(), out=c)
+
+        src = torch.empty_like(c)
+
+        def copy():
+            c.copy_(src)
+
+        def fill():
+            c.fill_(1.0)
+
+        def readsum():
+            torch.sum(src, dtype=torch.float32)
+
+        r = {"M": M, "K": K, "N": N}
+        for name, fn, b in [("ours", ours, byts), ("ours_stats", ours_st, byts), ("hipblaslt", blas, byts),
+                            ("copy_C", copy, 2 * M * N * 2),
+                            ("fill_C", fill, M * N * 2), ("read_C", readsum, M * N * 2)]:
+            us = timeit(fn, iters=20, warm=3)
+            r[name + "_us"] = round(us, 1)
+            r[name + "_TBs"] = round(b / us / 1e6, 2)
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -333,14 +333,15 @@ def _relu_bits(mask_bool):
     return (mask_bool.view(M, C // 8, 8).to(torch.int32) * w).sum(-1).to(torch.uint8)
 
 
-@pytest.mark.parametrize("k,s,p,beta", [(1, 1, 0, 0.0), (1, 1, 0, 1.0), (3, 1, 1, 0.0), (3, 2, 1, 0.0)])
-def test_dgrad_bn_backward_stats_epilogue(k, s, p, beta):
+@pytest.mark.parametrize("k,s,p,beta,Cin", [(1, 1, 0, 0.0, 64), (1, 1, 0, 1.0, 64), (3, 1, 1, 0.0, 64),
+                                            (3, 2, 1, 0.0, 64), (1, 1, 0, 1.0, 256)])
+def test_dgrad_bn_backward_stats_epilogue(k, s, p, beta, Cin):
     """dgrad GEMM epilogue statistics [sum g | sum g*z], g = dx * relu' (fp32 reference),
     and the BN backward fed from them == the BN backward with its own reduction."""
     from cloud_amd.ops import raw
 
     torch.manual_seed(12)
-    N, H, Cin, Cout = 3, 15, 64, 128
+    N, H, Cout = 3, 15, 128
     OH = (H + 2 * p - k) // s + 1
     dy = torch.randn(N, OH, OH, Cout, device=DEV).to(torch.bfloat16)
     w = (torch.randn(Cout, k, k, Cin, device=DEV) / (k * k * Cin) ** 0.5).to(torch.bfloat16)
