@@ -9,6 +9,9 @@ Two shared objects are produced next to this file:
 * ``_comm<EXT_SUFFIX>``     -- native RCCL communicator (``csrc/comm/rccl_comm.cpp``):
   collectives on a side HIP stream for the bucketed DP engine.  Linked against
   ``librccl.so.1``, which resolves to the RCCL ``import torch`` already mapped.
+* ``_data<EXT_SUFFIX>``     -- native input pipeline (``csrc/data/loader.cpp``): mmap'd
+  .npy arrays, shuffled / rank-sharded batches gathered by C++ worker threads into
+  pinned slot buffers; host-only.
 * ``_monitoring<EXT_SUFFIX>`` -- the C++ metrics registry / periodic exporter
   (``csrc/monitoring/*.cpp``), host-only, no HIP dependency, so CPU boxes can use
   it (parity target: reference ``src/cpp/monitoring/*``).
@@ -132,6 +135,15 @@ def build_monitoring(verbose=False) -> Path:
     return out
 
 
+def build_data(verbose=False) -> Path:
+    cxx = shutil.which("g++") or "c++"
+    src = CSRC / "data" / "loader.cpp"
+    obj = _compile(cxx, src, CXX_FLAGS + _py_includes(), verbose)
+    out = PKG / f"_data{EXT_SUFFIX}"
+    _link(cxx, [obj], out, ["-lpthread"], verbose)
+    return out
+
+
 def build_monitoring_test(verbose=False) -> Path:
     """Standalone C++ golden-test binary for the metrics library (no Python)."""
     cxx = shutil.which("g++") or "c++"
@@ -158,6 +170,8 @@ def build_all(verbose=False):
         outs.append(build_comm(verbose))
     if (CSRC / "monitoring").exists() and any((CSRC / "monitoring").glob("*.cpp")):
         outs.append(build_monitoring(verbose))
+    if (CSRC / "data" / "loader.cpp").exists():
+        outs.append(build_data(verbose))
     return outs
 
 

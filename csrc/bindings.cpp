@@ -4,10 +4,12 @@
 // the Python layer (cloud_amd/ops/*).  A non-zero HIP status raises.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 #include <stdint.h>
 
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace py = pybind11;
 typedef uint16_t bf16_t;
@@ -34,6 +36,7 @@ int ca_gemm_bf16_bnstats(int, const bf16_t*, long, const bf16_t*, long, bf16_t*,
 long ca_conv_dgrad_stat_tiles(int, int, int, int, int);
 int ca_conv_dgrad_bnstats(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
                           int, float, const bf16_t*, const uint8_t*, float*, hipStream_t);
+int ca_u8_normalize(const uint8_t*, bf16_t*, long, int, const float*, const float*, hipStream_t);
 int ca_stem_s2d(const bf16_t*, bf16_t*, int, int, int, int, int, int, int, hipStream_t);
 int ca_softmax_xent(const void*, int, const int64_t*, int, int, float, float, float*, float*, void*, hipStream_t);
 int ca_maxpool_fwd(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -158,6 +161,11 @@ PYBIND11_MODULE(_C, m) {
                                 sh, sw, ph, pw, beta, P(const bf16_t*, z), P(const uint8_t*, mask), P(float*, stats),
                                 S(s)),
           "conv_dgrad_bnstats");
+  });
+  m.def("u8_normalize", [](u64 x, u64 y, long n, std::vector<float> mean, std::vector<float> std_, u64 s) {
+    if (mean.size() != std_.size() || mean.empty()) throw std::invalid_argument("u8_normalize: mean/std size");
+    check(ca_u8_normalize(P(const uint8_t*, x), P(bf16_t*, y), n, (int)mean.size(), mean.data(), std_.data(), S(s)),
+          "u8_normalize");
   });
   m.def("stem_s2d", [](u64 x, u64 y, int N, int H, int W, int C, int Hs, int Ws, int pad, u64 s) {
     check(ca_stem_s2d(P(const bf16_t*, x), P(bf16_t*, y), N, H, W, C, Hs, Ws, pad, S(s)), "stem_s2d");

@@ -443,3 +443,43 @@ def test_stem_space_to_depth_matches_direct_conv():
     torch.testing.assert_close(p1.sum(0), p2.sum(0), atol=0.5, rtol=1e-2)
     assert g1[..., 3:].abs().max().item() == 0.0
     torch.testing.assert_close(g1[..., :3], g2[..., :3], atol=3e-2 * g2.abs().max().item(), rtol=3e-2)
+
+
+def test_device_loader_normalizes_on_copy_stream(tmp_path):
+    """cloud_amd.data.DeviceLoader: pinned slot -> GPU on a copy stream, uint8 -> bf16
+    normalisation kernel (csrc/kernels/input.hip) == (x - mean) / std in fp32."""
+    from cloud_amd.data import DeviceLoader, NpyBatchLoader, write_npy_dataset
+
+    xp, yp = write_npy_dataset(tmp_path / "ds", 40, image_shape=(6, 10, 3), classes=7, seed=2)
+    host = NpyBatchLoader([xp, yp], 8, seed=4, rank=0, world=1, slots=3)
+    mean, std = (123.7, 116.3, 103.5), (58.4, 57.1, 57.4)
+    dev = DeviceLoader(host, device=DEV, mean=mean, std=std)
+    ref_host = NpyBatchLoader([xp, yp], 8, seed=4, rank=0, world=1, slots=2)
+    refs = []
+    for slot, (xb, yb) in ref_host.epoch(0):
+        refs.append((xb.clone(), yb.clone()))
+        ref_host.release(slot)
+    got = list(dev.epoch(0))
+    torch.cuda.synchronize()
+    assert len(got) == len(refs) == 5
+    m = torch.tensor(mean, device=DEV)
+    s = torch.tensor(std, device=DEV)
+    for (x, y), (xr, yr) in zip(got, refs):
+        assert x.dtype == torch.bfloat16 and x.shape == xr.shape
+        torch.testing.assert_close(x.float(), (xr.to(DEV).float() - m) / s, atol=2e-2, rtol=1e-2)
+        assert torch.equal(y.cpu(), yr)
+
+
+def test_u8_normalize_odd_sizes():
+    from cloud_amd.ops import _ext
+
+    ext = _ext.load(required=True)
+    for n in (3, 48, 51, 4099 * 3):
+        x = torch.randint(0, 256, (n,), dtype=torch.uint8, device=DEV)
+        y = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        ext.u8_normalize(x.data_ptr(), y.data_ptr(), n, [10.0, 20.0, 30.0], [2.0, 4.0, 8.0],
+                         torch.cuda.current_stream().cuda_stream)
+        c = torch.arange(n, device=DEV) % 3
+        ref = (x.float() - torch.tensor([10.0, 20.0, 30.0], device=DEV)[c]) / torch.tensor([2.0, 4.0, 8.0],
+                                                                                            device=DEV)[c]
+        torch.testing.assert_close(y.float(), ref, atol=1e-2, rtol=1e-2)
