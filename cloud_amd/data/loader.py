@@ -31,9 +31,17 @@ _DTYPES = {"u1": torch.uint8, "i1": torch.int8, "i2": torch.int16, "i4": torch.i
 
 
 def _native():
-    from .. import _data  # noqa: WPS433  (built by cloud_amd._build)
+    """The C++ module; built in-tree on first use when missing (host-only, g++, seconds)."""
+    import importlib
 
-    return _data
+    try:
+        return importlib.import_module("cloud_amd._data")
+    except ImportError:
+        from .. import _build
+
+        _build.build_data()
+        importlib.invalidate_caches()
+        return importlib.import_module("cloud_amd._data")
 
 
 def _torch_dtype(descr):
