@@ -8,6 +8,7 @@ under the distribution strategies, ``optimizers`` (fused HIP kernels),
 save / load.  Layout is channels-last (NHWC).
 """
 from . import activations, applications, callbacks, datasets, initializers, layers, losses, metrics, optimizers  # noqa
+from . import regularizers  # noqa: F401
 from .data import AUTOTUNE, Dataset  # noqa: F401
 from .engine import Input, Layer, Policy, global_policy, set_global_policy  # noqa: F401
 from .models import Model, Sequential, clone_model, load_model  # noqa: F401

@@ -14,7 +14,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
-from . import activations, initializers
+from . import activations, initializers, regularizers
 from .engine import Input, InputLayer, Layer, global_policy  # noqa: F401
 
 
@@ -22,21 +22,44 @@ def _pair(v):
     return (v, v) if isinstance(v, int) else tuple(v)
 
 
-class Dense(Layer):
+class _Regularized:
+    """kernel/bias regularizers -> ``regularization_loss()`` (summed into the loss by Model)."""
+
+    def _set_regularizers(self, kernel_regularizer, bias_regularizer):
+        self.kernel_regularizer = regularizers.get(kernel_regularizer)
+        self.bias_regularizer = regularizers.get(bias_regularizer)
+
+    def regularization_loss(self):
+        out = None
+        for reg, w in ((self.kernel_regularizer, getattr(self, "kernel", None)),
+                       (self.bias_regularizer, getattr(self, "bias", None))):
+            if reg is not None and w is not None and self.trainable:
+                p = reg(w)
+                out = p if out is None else out + p
+        return out if out is not None else 0.0
+
+
+class Dense(_Regularized, Layer):
     def __init__(self, units, activation=None, use_bias=True, kernel_initializer="glorot_uniform",
-                 bias_initializer="zeros", **kw):
+                 bias_initializer="zeros", kernel_regularizer=None, bias_regularizer=None, **kw):
         super().__init__(**kw)
         self.units = int(units)
         self.activation = activations.get(activation)
         self.use_bias = use_bias
         self.kernel_initializer, self.bias_initializer = kernel_initializer, bias_initializer
+        self._set_regularizers(kernel_regularizer, bias_regularizer)
 
     def build(self, input_shape):
         fin = int(input_shape[-1])
         w = torch.empty(self.units, fin)
         initializers.get(self.kernel_initializer)(w)
         self.kernel = torch.nn.Parameter(w.to(self.compute_dtype))
-        self.bias = torch.nn.Parameter(torch.zeros(self.units, dtype=self.compute_dtype)) if self.use_bias else None
+        if self.use_bias:
+            b = torch.empty(self.units)
+            initializers.get(self.bias_initializer)(b)
+            self.bias = torch.nn.Parameter(b.to(self.compute_dtype))
+        else:
+            self.bias = None
 
     def call(self, x, training=None):
         x = x.to(self.kernel.dtype)
@@ -54,10 +77,12 @@ class Dense(Layer):
         return c
 
 
-class Conv2D(Layer):
+class Conv2D(_Regularized, Layer):
     def __init__(self, filters, kernel_size, strides=(1, 1), padding="valid", activation=None, use_bias=True,
-                 kernel_initializer="glorot_uniform", data_format=None, **kw):
+                 kernel_initializer="glorot_uniform", data_format=None, kernel_regularizer=None,
+                 bias_regularizer=None, **kw):
         super().__init__(**kw)
+        self._set_regularizers(kernel_regularizer, bias_regularizer)
         if data_format not in (None, "channels_last"):
             raise ValueError("cloud_amd layers are channels_last (NHWC) only")
         self.filters = int(filters)

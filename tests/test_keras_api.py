@@ -133,3 +133,29 @@ def test_mixed_bfloat16_policy_cpu():
         assert model.predict(np.zeros((2, 8), "float32")).dtype == np.float32
     finally:
         keras.mixed_precision.set_global_policy("float32")
+
+
+def test_regularizers_and_constant_initializer():
+    """kernel_regularizer adds its penalty to the training loss; Constant takes Keras-layout
+    values (the reference cloud_fit model: Dense(1, Constant([[0.5]]), l2(0.01)))."""
+    import numpy as np
+    import torch
+
+    from cloud_amd import tf
+
+    d = tf.keras.layers.Dense(2, kernel_initializer=tf.keras.initializers.Constant([[1.0, 2.0], [3.0, 4.0],
+                                                                                   [5.0, 6.0]]),
+                              bias_initializer=tf.keras.initializers.Constant(0.5),
+                              kernel_regularizer=tf.keras.regularizers.l2(0.1))
+    inp = tf.keras.layers.Input(shape=(3,))
+    m = tf.keras.Model(inp, d(inp))
+    k = d.kernel.detach().float()
+    assert torch.equal(k, torch.tensor([[1.0, 3.0, 5.0], [2.0, 4.0, 6.0]]))  # Keras [in, out] -> [out, in]
+    assert torch.equal(d.bias.detach().float(), torch.full((2,), 0.5))
+    assert abs(float(d.regularization_loss()) - 0.1 * float((k * k).sum())) < 1e-4
+    assert abs(float(m._regularization()) - 0.1 * float((k * k).sum())) < 1e-4
+    m.compile(loss="mse", optimizer=tf.keras.optimizers.SGD(0.01))
+    x = np.ones((4, 3), np.float32)
+    m.fit(x, np.zeros((4, 2), np.float32), epochs=1, verbose=0)
+    assert float((d.kernel.detach().float() ** 2).sum()) < float((k * k).sum())  # data + L2 both shrink it
+    assert isinstance(tf.keras.regularizers.get("l1_l2"), tf.keras.regularizers.L1L2)
