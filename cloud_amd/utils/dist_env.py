@@ -8,6 +8,7 @@ hostnames may not resolve).
 """
 from __future__ import annotations
 
+import atexit
 import datetime
 import os
 
@@ -49,7 +50,20 @@ def init_distributed(backend=None, timeout_s=None, device=None):
             dist.init_process_group(backend, rank=r, world_size=w, timeout=timeout, **kw)
         except TypeError:
             dist.init_process_group(backend, rank=r, world_size=w, timeout=timeout)
+        atexit.register(_shutdown)
     return r, w, device
+
+
+def _shutdown():
+    """Tear the default process group down before interpreter exit.  Left to the
+    destructors, the store / gloo background threads can outlive their owners and
+    the rank dies with ``terminate called without an active exception`` (SIGABRT)
+    after its work is done -- seen as rare non-zero exit codes of finished jobs."""
+    if dist.is_initialized():
+        try:
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001 - best effort at exit
+            pass
 
 
 def barrier():
