@@ -587,8 +587,13 @@ int ca_conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, floa
   splits = (p.K + kps - 1) / kps;
   p.k_per_split = kps;
   p.C = ws; p.ldc = p.N; p.split_stride = (long)p.M * p.N;
-  int rc = (p.N <= 64) ? launch<128, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s)
-                       : launch<128, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s);
+  int rc;
+  if (Cout <= 64)  // 64 output channels: 64-row tiles (no MFMA rows past Cout)
+    rc = (p.N <= 64) ? launch<64, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s)
+                     : launch<64, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s);
+  else
+    rc = (p.N <= 64) ? launch<128, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s)
+                     : launch<128, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s);
   if (rc) return rc;
   return ca_splitk_reduce(ws, splits, (long)p.M * p.N, dw, dw_bf16, beta, s);
 }

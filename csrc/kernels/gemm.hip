@@ -135,6 +135,11 @@ int dispatch(int layout, const CoreParams& p, int splits, hipStream_t s) {
       return small_n ? launch<128, 64, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI>(p, splits, s)
                      : launch<128, 128, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI>(p, splits, s);
     case 2:
+      // weight gradients with <= 64 output rows (64-channel layers): 64-row tiles, so
+      // half of every MFMA is not spent on rows beyond M
+      if (p.M <= 64)
+        return small_n ? launch<64, 64, DenseNC, DenseNC, GDenseNC, GDenseNC, EPI>(p, splits, s)
+                       : launch<64, 128, DenseNC, DenseNC, GDenseNC, GDenseNC, EPI>(p, splits, s);
       return small_n ? launch<128, 64, DenseNC, DenseNC, GDenseNC, GDenseNC, EPI>(p, splits, s)
                      : launch<128, 128, DenseNC, DenseNC, GDenseNC, GDenseNC, EPI>(p, splits, s);
   }
