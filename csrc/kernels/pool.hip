@@ -41,9 +41,11 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16_t* __restri
     for (int j = 0; j < 8; ++j) o[j] = f2bf(best[j]);
     const long oo = (((long)n * OH + oh) * OW + ow) * C + vc * 8;
     *reinterpret_cast<us8*>(y + oo) = o;
-    if (idx) {
+    if (idx) {  // the 8 argmax bytes as one 8-B store
+      uint64_t packed = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) idx[oo + j] = bi[j];
+      for (int j = 0; j < 8; ++j) packed |= (uint64_t)bi[j] << (8 * j);
+      *reinterpret_cast<uint64_t*>(idx + oo) = packed;
     }
   }
 }
@@ -165,6 +167,75 @@ __global__ void __launch_bounds__(256) stem_s2d_kernel(const bf16_t* __restrict_
   dst[1] = out[1];
 }
 
+// Backward of the 3x3 / stride 2 / pad 1 max-pool (the ResNet stem): one thread per
+// 2x2 block of input pixels (8 channels).  Input rows 2i, 2i+1 are covered only by
+// windows oh = i, i+1 (row 2i by oh = i alone), likewise for columns, so the thread
+// reads the <= 4 windows' gradients and argmax bytes once and writes 4 outputs --
+// the generic gather re-reads each window for every input pixel it covers.
+__global__ void __launch_bounds__(256) maxpool_bwd_s2k3_kernel(const bf16_t* __restrict__ dy,
+                                                              const uint8_t* __restrict__ idx, bf16_t* __restrict__ dx,
+                                                              int N, int H, int W, int C, int OH, int OW) {
+  const int CT = C / 8;
+  const int Hb = (H + 1) / 2, Wb = (W + 1) / 2;
+  const long total = (long)N * Hb * Wb * CT;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int vc = (int)(t % CT);
+    long r = t / CT;
+    const int bj = (int)(r % Wb); r /= Wb;
+    const int bi = (int)(r % Hb);
+    const int n = (int)(r / Hb);
+    float acc[2][2][8];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[a][b][j] = 0.f;
+#pragma unroll
+    for (int wy = 0; wy < 2; ++wy) {
+      const int oh = bi + wy;
+      if (oh >= OH) continue;
+#pragma unroll
+      for (int wx = 0; wx < 2; ++wx) {
+        const int ow = bj + wx;
+        if (ow >= OW) continue;
+        const long oo = (((long)n * OH + oh) * OW + ow) * C + vc * 8;
+        const us8 g = *reinterpret_cast<const us8*>(dy + oo);
+        const uint64_t id = *reinterpret_cast<const uint64_t*>(idx + oo);
+        // window origin (2oh-1, 2ow-1); input (2bi+a, 2bj+b) has tap (2bi+a-2oh+1)*3 + (2bj+b-2ow+1)
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const int kh = a + 1 - 2 * wy;  // 2bi+a - (2(bi+wy)-1)
+          if (kh < 0 || kh > 2) continue;
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int kw = b + 1 - 2 * wx;
+            if (kw < 0 || kw > 2) continue;
+            const uint32_t want = (uint32_t)(kh * 3 + kw);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (((id >> (8 * j)) & 0xff) == want) acc[a][b][j] += bf2f(g[j]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int h = 2 * bi + a;
+      if (h >= H) continue;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int w = 2 * bj + b;
+        if (w >= W) continue;
+        us8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[a][b][j]);
+        *reinterpret_cast<us8*>(dx + (((long)n * H + h) * W + w) * C + vc * 8) = o;
+      }
+    }
+  }
+}
+
 extern "C" {
 
 int ca_stem_s2d(const bf16_t* x, bf16_t* y, int N, int H, int W, int C, int Hs, int Ws, int pad, hipStream_t st) {
@@ -188,6 +259,12 @@ int ca_maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int 
                    int k, int s, int p, hipStream_t st) {
   if (C % 8) return -1;
   const long total = (long)N * H * W * (C / 8);
+  if (k == 3 && s == 2 && p == 1 && OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1) {
+    const long blocks = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+    maxpool_bwd_s2k3_kernel<<<ca_stream_grid(blocks, 256), 256, 0, st>>>(dy, idx, dx, N, H, W, C, OH, OW);
+    CA_LAUNCH_CHECK();
+    return 0;
+  }
   maxpool_bwd_kernel<<<ca_stream_grid(total, 256), 256, 0, st>>>(dy, idx, dx, N, H, W, C, OH, OW, k, s, p);
   CA_LAUNCH_CHECK();
   return 0;

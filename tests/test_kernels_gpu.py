@@ -94,6 +94,15 @@ def test_maxpool_and_gap():
     y.backward(dy)
     yr.backward(dy.float().permute(0, 3, 1, 2))
     torch.testing.assert_close(x.grad.float(), xr.grad.permute(0, 2, 3, 1), atol=2e-2, rtol=2e-2)
+    # generic gather path (not the 3x3/2/1 specialisation)
+    x3 = torch.randn(2, 9, 10, 16, device=DEV).to(torch.bfloat16).requires_grad_()
+    y3 = max_pool2d_nhwc(x3, 2, 2, 0)
+    x3r = x3.detach().float().permute(0, 3, 1, 2).requires_grad_()
+    y3r = F.max_pool2d(x3r, 2, 2, 0)
+    dy3 = torch.randn_like(y3)
+    y3.backward(dy3)
+    y3r.backward(dy3.float().permute(0, 3, 1, 2))
+    torch.testing.assert_close(x3.grad.float(), x3r.grad.permute(0, 2, 3, 1), atol=2e-2, rtol=2e-2)
 
     x2 = torch.randn(5, 7, 7, 256, device=DEV).to(torch.bfloat16).requires_grad_()
     g = global_avg_pool_nhwc(x2)
