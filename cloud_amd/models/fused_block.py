@@ -145,13 +145,13 @@ class _BottleneckFn(torch.autograd.Function):
             ddp.notify_grad_ready(bn.bias)
             return r
 
-        def dgrad(conv, dz, shape, bn_src, out=None, beta=0.0):
+        def dgrad(conv, dz, shape, bn_src, out=None, beta=0.0, res=None):
             """Input gradient; with ``bn_src`` = (z, mask) of the BN that consumes it,
             also that BN's backward statistics from the epilogue."""
-            if epi and bn_src is not None:
-                return raw.conv_dgrad(dz, conv.weight, shape, conv.stride, conv.padding, out=out, beta=beta,
-                                      bn=bn_src)
-            return raw.conv_dgrad(dz, conv.weight, shape, conv.stride, conv.padding, out=out, beta=beta), None
+            bn = bn_src if (epi and bn_src is not None) else None
+            r = raw.conv_dgrad(dz, conv.weight, shape, conv.stride, conv.padding, out=out, beta=beta, bn=bn,
+                               res=res)
+            return r if bn is not None else (r, None)
 
         side = SideWork(x.device)
         deferred = []
@@ -164,8 +164,11 @@ class _BottleneckFn(torch.autograd.Function):
             else:
                 ddp.notify_grad_ready(conv.weight)
 
-        dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=True, partials=_take(dout) if epi else None)
-        del dout
+        # identity blocks: the residual gradient dout * relu'(m3) is never materialised --
+        # conv1's dgrad epilogue gates it from dout on the fly (res=) at the end
+        gate_res = ds is None and m3 is not None
+        dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=not gate_res,
+                            partials=_take(dout) if epi else None)
         dy2, p2 = dgrad(blk.conv3, dz3, y2.shape, (z2, m2))
         wgrad(blk.conv3, dz3, y2)
         del dz3
@@ -184,10 +187,14 @@ class _BottleneckFn(torch.autograd.Function):
             dx = raw.conv_dgrad(dzd, c.weight, x.shape, c.stride, c.padding)
             wgrad(c, dzd, x)
             del dzd
+        elif gate_res:
+            dx = torch.empty_like(x)  # = conv1's input gradient + dout * relu'(m3), one epilogue
         else:
             dx = dres  # identity gradient; conv1's input gradient is summed into it below
         # the last write of dx: its epilogue sees the complete block-input gradient
-        _, p_prev = dgrad(blk.conv1, dz1, x.shape, ctx.prev_src, out=dx, beta=1.0)
+        _, p_prev = dgrad(blk.conv1, dz1, x.shape, ctx.prev_src, out=dx, beta=1.0,
+                          res=(dout, m3) if gate_res else None)
+        del dout
         if p_prev is not None:
             _park(dx, p_prev)
         ctx.prev_src = None

@@ -56,18 +56,35 @@ def conv_fwd(x, w, stride, padding, stats=None):
     return y
 
 
-def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None):
+def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res=None):
     """dx (+= beta * out) for y = conv(x, w).
 
     ``bn=(z, mask)``: dx is the gradient of a BatchNorm(+ReLU) output whose input was
     ``z`` (``mask``: its ReLU bitmask, or None).  The GEMM epilogue then also writes the
     BN-backward statistics partials [tiles][2][Cin] = [sum g | sum g*z], g = dx * relu',
     and ``(dx, partials)`` is returned: :func:`bn_bwd` takes them and skips its own
-    reduction pass over dx and z."""
+    reduction pass over dx and z.
+
+    ``res=(src, mask)`` (1x1 convolutions): dx = dgrad + beta * relu'(mask) * src -- a
+    residual-path gradient gated on the fly from the block's output gradient instead of
+    being materialised by the BN backward first."""
     ext = _ext.load(required=True)
     N, H, W, Cin = x_shape
     Cout, KH, KW, _ = w.shape
     dx = out if out is not None else torch.empty(x_shape, dtype=torch.bfloat16, device=dy.device)
+    if res is not None:
+        src, rmask = res
+        assert is_gemm_conv(w, stride, padding) and src.shape == dx.shape and src.is_contiguous()
+        assert rmask is None or rmask.shape == (N * H * W, Cin // 8)
+        part, zp, mp = None, 0, 0
+        if bn is not None:
+            z, mask = bn
+            assert z.shape == dx.shape and z.is_contiguous()
+            part = torch.empty(((N * H * W + 127) // 128, 2, Cin), dtype=torch.float32, device=dy.device)
+            zp, mp = z.data_ptr(), _ext.ptr(mask)
+        ext.dgrad_gemm(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin, Cout,
+                       float(beta), src.data_ptr(), _ext.ptr(rmask), zp, mp, _ext.ptr(part), _st(dy.device))
+        return (dx, part) if bn is not None else dx
     if bn is not None:
         z, mask = bn
         assert z.shape == dx.shape and z.is_contiguous() and (mask is None or mask.shape == (N * H * W, Cin // 8))

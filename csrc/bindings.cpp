@@ -34,6 +34,8 @@ int ca_bn_bwd_partials(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_
 int ca_gemm_bf16_bnstats(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float,
                          const bf16_t*, const uint8_t*, float*, hipStream_t);
 long ca_conv_dgrad_stat_tiles(int, int, int, int, int);
+int ca_dgrad_gemm(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float, const bf16_t*,
+                  const uint8_t*, const bf16_t*, const uint8_t*, float*, hipStream_t);
 int ca_conv_dgrad_bnstats(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
                           int, float, const bf16_t*, const uint8_t*, float*, hipStream_t);
 int ca_u8_normalize(const uint8_t*, bf16_t*, long, int, const float*, const float*, hipStream_t);
@@ -151,6 +153,13 @@ PYBIND11_MODULE(_C, m) {
     check(ca_gemm_bf16_bnstats(layout, P(const bf16_t*, A), lda, P(const bf16_t*, B), ldb, P(bf16_t*, C), ldc, M, N, K,
                                beta, P(const bf16_t*, z), P(const uint8_t*, mask), P(float*, stats), S(s)),
           "gemm_bf16_bnstats");
+  });
+  m.def("dgrad_gemm", [](int layout, u64 A, long lda, u64 B, long ldb, u64 C, long ldc, int M, int N, int K,
+                         float beta, u64 res, u64 res_mask, u64 z, u64 mask, u64 stats, u64 s) {
+    check(ca_dgrad_gemm(layout, P(const bf16_t*, A), lda, P(const bf16_t*, B), ldb, P(bf16_t*, C), ldc, M, N, K, beta,
+                        P(const bf16_t*, res), P(const uint8_t*, res_mask), P(const bf16_t*, z),
+                        P(const uint8_t*, mask), P(float*, stats), S(s)),
+          "dgrad_gemm");
   });
   m.def("conv_dgrad_stat_tiles", [](int Nb, int H, int W, int sh, int sw) {
     return ca_conv_dgrad_stat_tiles(Nb, H, W, sh, sw);

@@ -36,7 +36,9 @@ constexpr int PAD = 8;
 // EPI_BF16_ST: EPI_BF16 plus the BN-forward statistics [sum | sum of squares] of the
 // stored values, accumulated in registers by the storing thread.  Separate
 // instantiations, so the plain bf16 epilogue carries none of their registers.
-enum Epi { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_BF16_BN = 2, EPI_BF16_ST = 3 };
+// EPI_BF16_BNR: EPI_BF16_BN that also honours CoreParams::res_src / res_mask (the
+// plain bf16 epilogue always does; the BN-statistics one only in this instantiation).
+enum Epi { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_BF16_BN = 2, EPI_BF16_ST = 3, EPI_BF16_BNR = 4 };
 
 // Fast unsigned division by a runtime constant (n < 2^31): q = (umulhi(n, m) + n) >> s.
 struct FastDiv {
@@ -67,6 +69,10 @@ struct CoreParams {
   // g = dy * relu'(mask) and z is the BN input (same [rows][ldc] layout as C).
   const bf16_t* bnz;
   const uint8_t* bnmask;  // ReLU bitmask [rows][N/8] (bit j = channel 8c+j active) or null
+  // beta source other than C: C = acc + beta * relu'(res_mask) * res_src (same [rows][ldc]
+  // layout as C) -- a residual gradient gated on the fly instead of materialised first
+  const bf16_t* res_src;
+  const uint8_t* res_mask;
   float beta;            // C = acc + beta * C_old (bf16 epilogue)
   int M, N, K;
   int k_per_split;
@@ -296,7 +302,8 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
     constexpr int CH = BM * BN / 8;
     static_assert(CH % NT == 0, "epilogue chunks must divide the threads");
     constexpr int IT = CH / NT;
-    constexpr bool BNS = EPI == EPI_BF16_BN, STS = EPI == EPI_BF16_ST, RSTAT = BNS || STS;
+    constexpr bool BNS = EPI == EPI_BF16_BN || EPI == EPI_BF16_BNR, STS = EPI == EPI_BF16_ST, RSTAT = BNS || STS;
+    constexpr bool RES = EPI != EPI_BF16_BN;  // res_src / res_mask compiled in
     constexpr int PF = BNS ? (IT < 2 ? IT : 2) : 1;
     const int col = (tid % (BN / 8)) * 8;
     const int gn = n0 + col;
@@ -304,7 +311,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
 #pragma unroll 1
     for (int it0 = 0; it0 < IT; it0 += PF) {
       s8v opre[PF], zpre[BNS ? PF : 1];
-      uint32_t mpre[BNS ? PF : 1];
+      uint32_t mk[PF];  // bits 0-7: BN ReLU mask (BN-backward statistics), bits 8-15: res_mask
       long orow[PF];
       bool okr[PF];
 #pragma unroll
@@ -312,10 +319,15 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
         const int gm = m0 + (tid + (it0 + u) * NT) / (BN / 8);
         okr[u] = gm < P.M && gn < P.N;
         orow[u] = okr[u] ? out_row(P, gm) : 0;
-        opre[u] = (has_beta && okr[u]) ? *reinterpret_cast<const s8v*>(Cg + orow[u] * P.ldc + gn) : zero8();
+        const bf16_t* bsrc = (RES && P.res_src) ? P.res_src : Cg;
+        opre[u] = (has_beta && okr[u]) ? *reinterpret_cast<const s8v*>(bsrc + orow[u] * P.ldc + gn) : zero8();
+        mk[u] = 0xff00u;
+        if constexpr (RES) {
+          if (has_beta && P.res_mask && okr[u]) mk[u] = (uint32_t)P.res_mask[orow[u] * (P.N / 8) + (gn >> 3)] << 8;
+        }
         if constexpr (BNS) {
           zpre[u] = okr[u] ? *reinterpret_cast<const s8v*>(P.bnz + orow[u] * P.ldc + gn) : zero8();
-          mpre[u] = (P.bnmask && okr[u]) ? (uint32_t)P.bnmask[orow[u] * (P.N / 8) + (gn >> 3)] : 0xffu;
+          mk[u] |= (P.bnmask && okr[u]) ? (uint32_t)P.bnmask[orow[u] * (P.N / 8) + (gn >> 3)] : 0xffu;
         }
       }
 #pragma unroll
@@ -339,8 +351,10 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
         }
         if (has_beta) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            v[j] = (short)f2bf(bf2f((bf16_t)v[j]) + P.beta * bf2f((bf16_t)opre[u][j]));
+          for (int j = 0; j < 8; ++j) {
+            const float o = ((mk[u] >> (8 + j)) & 1u) ? bf2f((bf16_t)opre[u][j]) : 0.f;
+            v[j] = (short)f2bf(bf2f((bf16_t)v[j]) + P.beta * o);
+          }
         }
         if (!RSTAT && P.stats && (fx || has_beta)) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
         *reinterpret_cast<s8v*>(dst) = v;
@@ -355,7 +369,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
         if constexpr (BNS) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float g = ((mpre[u] >> j) & 1u) ? bf2f((bf16_t)v[j]) : 0.f;
+            const float g = ((mk[u] >> j) & 1u) ? bf2f((bf16_t)v[j]) : 0.f;
             bsum[j] += g;
             bzsum[j] += g * bf2f((bf16_t)zpre[u][j]);
           }

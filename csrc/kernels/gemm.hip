@@ -157,6 +157,10 @@ CoreParams base_params(const bf16_t* A, long lda, const bf16_t* B, long ldb, voi
 
 extern "C" {
 
+int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N,
+                  int K, float beta, const bf16_t* res_src, const uint8_t* res_mask, const bf16_t* bnz,
+                  const uint8_t* bnmask, float* stats, hipStream_t s);
+
 int ca_splitk_reduce(const float* ws, int splits, long MN, void* out, int out_bf16, float beta, hipStream_t s) {
   if (MN % 4) return -3;
   const long n4 = MN / 4;
@@ -190,12 +194,29 @@ int ca_gemm_bf16(int layout, const bf16_t* A, long lda, const bf16_t* B, long ld
 int ca_gemm_bf16_bnstats(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc,
                          int M, int N, int K, float beta, const bf16_t* bnz, const uint8_t* bnmask, float* stats,
                          hipStream_t s) {
-  if (N % 8 != 0 || K % 8 != 0 || layout != 1 || !bnz || !stats) return -1;
+  return ca_dgrad_gemm(layout, A, lda, B, ldb, C, ldc, M, N, K, beta, nullptr, nullptr, bnz, bnmask, stats, s);
+}
+
+// Input-gradient GEMM (NN) with the two backward epilogue options of a ResNet block:
+//   res_src [+ res_mask]: C = A*B + beta * relu'(res_mask) * res_src -- the block's
+//                         identity-path gradient gated from the output gradient on the
+//                         fly (never materialised);
+//   bnz / bnmask / stats: BN-backward statistics of C for the BN that consumes it.
+int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N,
+                  int K, float beta, const bf16_t* res_src, const uint8_t* res_mask, const bf16_t* bnz,
+                  const uint8_t* bnmask, float* stats, hipStream_t s) {
+  if (N % 8 != 0 || K % 8 != 0 || layout != 1 || (bnz && !stats)) return -1;
   CoreParams p = base_params(A, lda, B, ldb, C, ldc, M, N, K);
-  p.stats = stats;
   p.beta = beta;
+  p.res_src = res_src;
+  p.res_mask = res_mask;
+  if (!bnz) return dispatch<EPI_BF16>(layout, p, 1, s);
+  p.stats = stats;
   p.bnz = bnz;
   p.bnmask = bnmask;
+  if (res_src)
+    return want_small_n(p, 1) ? launch<128, 64, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI_BF16_BNR>(p, 1, s)
+                              : launch<128, 128, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI_BF16_BNR>(p, 1, s);
   return want_small_n(p, 1) ? launch<128, 64, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI_BF16_BN>(p, 1, s)
                             : launch<128, 128, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI_BF16_BN>(p, 1, s);
 }

@@ -492,3 +492,32 @@ def test_u8_normalize_odd_sizes():
         ref = (x.float() - torch.tensor([10.0, 20.0, 30.0], device=DEV)[c]) / torch.tensor([2.0, 4.0, 8.0],
                                                                                             device=DEV)[c]
         torch.testing.assert_close(y.float(), ref, atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("with_bn", [False, True])
+def test_dgrad_gated_residual_epilogue(with_bn):
+    """1x1 dgrad with res=(src, mask): dx = dgrad + relu'(mask) * src in one epilogue
+    (identity-block residual gradient never materialised), with and without the
+    BN-backward statistics of dx."""
+    from cloud_amd.ops import raw
+
+    torch.manual_seed(15)
+    N, H, Cin, Cout = 2, 14, 256, 64
+    dy = torch.randn(N, H, H, Cout, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(Cout, 1, 1, Cin, device=DEV) / 8).to(torch.bfloat16)
+    src = torch.randn(N, H, H, Cin, device=DEV).to(torch.bfloat16)
+    keep = torch.rand(N * H * H, Cin, device=DEV) > 0.5
+    bits = _relu_bits(keep)
+    base = raw.conv_dgrad(dy, w, src.shape, 1, 0)
+    ref = base.float() + (src.float().reshape(-1, Cin) * keep).reshape(src.shape)
+    if with_bn:
+        z = torch.randn(N, H, H, Cin, device=DEV).to(torch.bfloat16)
+        zkeep = torch.rand(N * H * H, Cin, device=DEV) > 0.3
+        dx, part = raw.conv_dgrad(dy, w, src.shape, 1, 0, beta=1.0, bn=(z, _relu_bits(zkeep)), res=(src, bits))
+        g = dx.float().reshape(-1, Cin) * zkeep
+        torch.testing.assert_close(part[:, 0].sum(0), g.sum(0), atol=5e-2 * N * H, rtol=1e-3)
+        torch.testing.assert_close(part[:, 1].sum(0), (g * z.float().reshape(-1, Cin)).sum(0), atol=1e-1 * N * H,
+                                   rtol=1e-3)
+    else:
+        dx = raw.conv_dgrad(dy, w, src.shape, 1, 0, beta=1.0, res=(src, bits))
+    torch.testing.assert_close(dx.float(), ref, atol=3e-2, rtol=2e-2)
