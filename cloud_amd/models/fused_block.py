@@ -137,9 +137,15 @@ class _BottleneckFn(torch.autograd.Function):
 
         epi = config.get("CLOUD_AMD_BN_BWD_EPILOGUE")
 
-        def bn_back(bn, dy, z, st, want_dres=False, partials=None):
+        def bn_back(bn, dy, z, st, want_dres=False, partials=None, gate=None):
+            """``gate``: a ReLU bitmask applied to dy on load (the shortcut BN of a projection
+            block gets dout gated by the block's output ReLU, never a materialised copy)."""
             stats, mask = st
-            r = raw.bn_bwd(dy, None, z, bn.weight, stats, bn.relu, dgamma=bn.weight.grad, dbeta=bn.bias.grad,
+            relu = bn.relu
+            if gate is not None:
+                assert not bn.relu
+                relu, mask = True, gate
+            r = raw.bn_bwd(dy, None, z, bn.weight, stats, relu, dgamma=bn.weight.grad, dbeta=bn.bias.grad,
                            want_dres=want_dres, accumulate=1, mask=mask, partials=partials)
             ddp.notify_grad_ready(bn.weight)
             ddp.notify_grad_ready(bn.bias)
@@ -164,9 +170,9 @@ class _BottleneckFn(torch.autograd.Function):
             else:
                 ddp.notify_grad_ready(conv.weight)
 
-        # identity blocks: the residual gradient dout * relu'(m3) is never materialised --
-        # conv1's dgrad epilogue gates it from dout on the fly (res=) at the end
-        gate_res = ds is None and m3 is not None
+        # the residual gradient dout * relu'(m3) is never materialised: identity blocks gate
+        # it in conv1's dgrad epilogue (res=), projection blocks in the shortcut BN backward
+        gate_res = m3 is not None
         dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=not gate_res,
                             partials=_take(dout) if epi else None)
         dy2, p2 = dgrad(blk.conv3, dz3, y2.shape, (z2, m2))
@@ -181,7 +187,10 @@ class _BottleneckFn(torch.autograd.Function):
         del dy1, p1
         if ds is not None:
             zd, sd = saved[12], saved[13]
-            dzd, _ = bn_back(ds["bn"], dres, zd, (sd, None))
+            if gate_res:
+                dzd, _ = bn_back(ds["bn"], dout, zd, (sd, None), gate=m3)
+            else:
+                dzd, _ = bn_back(ds["bn"], dres, zd, (sd, None))
             del dres
             c = ds["conv"]
             dx = raw.conv_dgrad(dzd, c.weight, x.shape, c.stride, c.padding)
@@ -193,7 +202,7 @@ class _BottleneckFn(torch.autograd.Function):
             dx = dres  # identity gradient; conv1's input gradient is summed into it below
         # the last write of dx: its epilogue sees the complete block-input gradient
         _, p_prev = dgrad(blk.conv1, dz1, x.shape, ctx.prev_src, out=dx, beta=1.0,
-                          res=(dout, m3) if gate_res else None)
+                          res=(dout, m3) if (gate_res and ds is None) else None)
         del dout
         if p_prev is not None:
             _park(dx, p_prev)
