@@ -113,11 +113,27 @@ class _BottleneckFn(torch.autograd.Function):
         z1, y1, s1 = _conv_bn(blk.conv1, blk.bn1, x)
         z2, y2, s2 = _conv_bn(blk.conv2, blk.bn2, y1)
         if ds is not None:
-            zd, idn, sd = _conv_bn(ds["conv"], ds["bn"], x)
+            # projection shortcut: its BN is folded into bn3's apply (statistics only here;
+            # the shortcut BN output is never written)
+            c, bnd = ds["conv"], ds["bn"]
+            N, H, W, _ = x.shape
+            OH, OW = raw.out_hw(H, c.k, c.stride, c.padding), raw.out_hw(W, c.k, c.stride, c.padding)
+            part_d = raw.stats_buffer(N * OH * OW, c.cout, x.device)
+            zd = raw.conv_fwd(x, c.weight, c.stride, c.padding, stats=part_d)
+            st_d = raw.bn_fwd_stats(zd, bnd.weight, bnd.bias, bnd.running_mean, bnd.running_var, bnd.eps,
+                                    bnd.momentum, part_d)
+            sd = (st_d, None)
+            c3, bn3 = blk.conv3, blk.bn3
+            part3 = raw.stats_buffer(y2.numel() // y2.shape[-1], c3.cout, x.device)
+            z3 = raw.conv_fwd(y2, c3.weight, c3.stride, c3.padding, stats=part3)
+            C3 = c3.cout
+            out, st3, mask3 = raw.bn_fwd(z3, bn3.weight, bn3.bias, bn3.running_mean, bn3.running_var, bn3.eps,
+                                         bn3.momentum, bn3.relu, residual=zd, partials=part3, keep_mask=True,
+                                         residual_ss=st_d[2 * C3:4 * C3])
+            s3 = (st3, mask3)
         else:
-            zd, idn, sd = None, x, None
-        z3, out, s3 = _conv_bn(blk.conv3, blk.bn3, y2, residual=idn)
-        del idn
+            zd, sd = None, None
+            z3, out, s3 = _conv_bn(blk.conv3, blk.bn3, y2, residual=x)
         ctx.blk = blk
         (s1, m1), (s2, m2), (s3, m3) = s1, s2, s3
         ctx.save_for_backward(x, z1, y1, z2, y2, z3, s1, m1, s2, m2, s3, m3,

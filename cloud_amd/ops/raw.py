@@ -129,8 +129,24 @@ def conv_wgrad(dy, x, w_shape, stride, padding, out, beta=1.0):
 
 
 # ------------------------------------------------------------------ batchnorm
+def bn_fwd_stats(x, gamma, beta, running_mean, running_var, eps, momentum, partials):
+    """Training BN statistics only (no apply pass): returns stats[4C] = mean, rstd, scale,
+    shift -- for a BN whose output is consumed on the fly (:func:`bn_fwd` ``residual_ss``)."""
+    ext = _ext.load(required=True)
+    C = x.shape[-1]
+    M = x.numel() // C
+    dev = x.device
+    stats = torch.empty(4 * C, dtype=torch.float32, device=dev)
+    gws = torch.empty(64 * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
+    sp = stats.data_ptr()
+    ext.bn_fwd_partials_ex(x.data_ptr(), 0, 0, 0, M, C, partials.data_ptr(), partials.shape[0], _ext.ptr(gamma),
+                           _ext.ptr(beta), float(eps), float(momentum), _ext.ptr(running_mean),
+                           _ext.ptr(running_var), sp, sp + 4 * C, sp + 8 * C, 0, 0, _ext.ptr(gws), _st(dev))
+    return stats
+
+
 def bn_fwd(x, gamma, beta, running_mean, running_var, eps, momentum, relu, residual=None, partials=None,
-           keep_mask=False):
+           keep_mask=False, residual_ss=None):
     """Training BN(+res)(+ReLU).  Returns (y, stats[4C] = mean, rstd, scale, shift, mask) where
     ``mask`` is the ReLU bitmask ([M, C/8] uint8, bit j = channel 8c+j active) when
     ``keep_mask`` and ``relu`` (else None): the backward then reads it instead of y."""
@@ -142,6 +158,14 @@ def bn_fwd(x, gamma, beta, running_mean, running_var, eps, momentum, relu, resid
     stats = torch.empty(4 * C, dtype=torch.float32, device=dev)
     mask = torch.empty((M, C // 8), dtype=torch.uint8, device=dev) if (keep_mask and relu) else None
     sp = stats.data_ptr()
+    if residual_ss is not None:  # residual = input of another BN with [scale | shift] = residual_ss
+        assert partials is not None and residual is not None and residual_ss.numel() == 2 * C
+        gws = torch.empty(64 * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
+        ext.bn_fwd_partials_ex(x.data_ptr(), residual.data_ptr(), residual_ss.data_ptr(), y.data_ptr(), M, C,
+                               partials.data_ptr(), partials.shape[0], _ext.ptr(gamma), _ext.ptr(beta), float(eps),
+                               float(momentum), _ext.ptr(running_mean), _ext.ptr(running_var), sp, sp + 4 * C,
+                               sp + 8 * C, int(relu), _ext.ptr(mask), _ext.ptr(gws), _st(dev))
+        return y, stats, mask
     if partials is not None:
         gws = torch.empty(64 * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
         ext.bn_fwd_partials(x.data_ptr(), _ext.ptr(residual), y.data_ptr(), M, C, partials.data_ptr(),

@@ -34,6 +34,9 @@ int ca_bn_bwd_partials(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_
 int ca_gemm_bf16_bnstats(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float,
                          const bf16_t*, const uint8_t*, float*, hipStream_t);
 long ca_conv_dgrad_stat_tiles(int, int, int, int, int);
+int ca_bn_fwd_partials_ex(const bf16_t*, const bf16_t*, const float*, bf16_t*, long, int, const float*, int,
+                          const float*, const float*, float, float, float*, float*, float*, float*, float*, int,
+                          uint8_t*, float*, hipStream_t);
 int ca_dgrad_gemm(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float, const bf16_t*,
                   const uint8_t*, const bf16_t*, const uint8_t*, float*, hipStream_t);
 int ca_conv_dgrad_bnstats(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
@@ -160,6 +163,15 @@ PYBIND11_MODULE(_C, m) {
                         P(const bf16_t*, res), P(const uint8_t*, res_mask), P(const bf16_t*, z),
                         P(const uint8_t*, mask), P(float*, stats), S(s)),
           "dgrad_gemm");
+  });
+  m.def("bn_fwd_partials_ex", [](u64 x, u64 res, u64 res_ss, u64 y, long M, int C, u64 parts, int nparts, u64 gamma,
+                                 u64 beta, float eps, float momentum, u64 rm, u64 rv, u64 sm, u64 sr, u64 ss, int relu,
+                                 u64 mask, u64 gws, u64 s) {
+    check(ca_bn_fwd_partials_ex(P(const bf16_t*, x), P(const bf16_t*, res), P(const float*, res_ss), P(bf16_t*, y), M,
+                                C, P(const float*, parts), nparts, P(const float*, gamma), P(const float*, beta), eps,
+                                momentum, P(float*, rm), P(float*, rv), P(float*, sm), P(float*, sr), P(float*, ss),
+                                relu, P(uint8_t*, mask), P(float*, gws), S(s)),
+          "bn_fwd_partials_ex");
   });
   m.def("conv_dgrad_stat_tiles", [](int Nb, int H, int W, int sh, int sw) {
     return ca_conv_dgrad_stat_tiles(Nb, H, W, sh, sw);

@@ -244,6 +244,56 @@ __global__ void __launch_bounds__(BLK) bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
+// y = act(x*scale + shift + (r*rscale + rshift)): the residual is the INPUT of another
+// BatchNorm (a projection shortcut) whose affine is applied on the fly, so that BN's own
+// output is never written or read back.
+template <bool RELU>
+__global__ void __launch_bounds__(BLK) bn_apply_resbn_kernel(const bf16_t* __restrict__ x,
+                                                            const bf16_t* __restrict__ r,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift,
+                                                            const float* __restrict__ rscale,
+                                                            const float* __restrict__ rshift, bf16_t* __restrict__ y,
+                                                            uint8_t* __restrict__ mask, long M, int C) {
+  const Tiling t = make_tiling(M, C);
+  const int tx = threadIdx.x % t.TW, ty = threadIdx.x / t.TW;
+  const int vc = blockIdx.x * t.TW + tx;
+  if (vc >= t.CT) return;
+  float sc[8], sh[8], rs[8], rh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = scale[vc * 8 + j];
+    sh[j] = shift[vc * 8 + j];
+    rs[j] = rscale[vc * 8 + j];
+    rh[j] = rshift[vc * 8 + j];
+  }
+  const long r0 = (long)blockIdx.y * t.rows_per_chunk;
+  long r1 = r0 + t.rows_per_chunk;
+  if (r1 > M) r1 = M;
+  const long off0 = (long)vc * 8;
+  for (long rr = r0 + ty; rr < r1; rr += t.RP) {
+    const long o = rr * C + off0;
+    float v[8], rv[8];
+    ld8bf(x + o, v);
+    ld8bf(r + o, rv);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      // the shortcut BN output rounded to bf16 exactly as if it had been stored, so the
+      // block stays bit-compatible with the op-by-op path
+      const float idn = bf2f(f2bf(rv[j] * rs[j] + rh[j]));
+      float z = v[j] * sc[j] + sh[j] + idn;
+      if (RELU) {
+        z = fmaxf(z, 0.f);
+        bits |= (z > 0.f ? 1u : 0u) << j;
+      }
+      v[j] = z;
+    }
+    st8bf(y + o, v);
+    if (RELU && mask) mask[rr * t.CT + vc] = (uint8_t)bits;
+  }
+}
+
 __device__ __forceinline__ void relu_gate(float (&d)[8], const bf16_t* __restrict__ y, const uint8_t* __restrict__ mask,
                                           long r, long o, int CT, int vc) {
   if (mask) {
@@ -433,6 +483,44 @@ int ca_bn_fwd_partials(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, in
   else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
   else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
   else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+// ca_bn_fwd_partials, extended: y == null -> statistics / finalize only (scale_shift,
+// save_*, running stats; no apply pass); res_ss != null -> the residual `res` is the input
+// of another BatchNorm with that [scale | shift] (y = act(BN(x) + BN'(res)), see
+// bn_apply_resbn_kernel).
+int ca_bn_fwd_partials_ex(const bf16_t* x, const bf16_t* res, const float* res_ss, bf16_t* y, long M, int C,
+                          const float* partials, int nparts, const float* gamma, const float* beta, float eps,
+                          float momentum, float* run_mean, float* run_var, float* save_mean, float* save_rstd,
+                          float* scale_shift, int relu, uint8_t* mask, float* gws, hipStream_t s) {
+  if (C % 8 != 0 || (res_ss && !res)) return -1;
+  if (y && !res_ss)
+    return ca_bn_fwd_partials(x, res, y, M, C, partials, nparts, gamma, beta, eps, momentum, run_mean, run_var,
+                              save_mean, save_rstd, scale_shift, relu, mask, gws, s);
+  Tiling t = make_tiling(M, C);
+  dim3 grid(t.ncol, t.nchunks);
+  const float* fin = partials;
+  int nfin = nparts;
+  if (nparts > 64 && gws) {
+    const int G = group_count(nparts);
+    chunk_group_reduce_kernel<<<dim3(ca_cdiv(C, 64), G), 256, 0, s>>>(partials, nparts, 2L * C, (long)C, C, gws);
+    CA_LAUNCH_CHECK();
+    fin = gws;
+    nfin = G;
+  }
+  bn_fwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(fin, nfin, 2L * C, (long)C, M, C, gamma, beta, eps,
+                                                         momentum, run_mean, run_var, save_mean, save_rstd,
+                                                         scale_shift, scale_shift + C);
+  CA_LAUNCH_CHECK();
+  if (!y) return 0;
+  if (relu)
+    bn_apply_resbn_kernel<true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, res_ss, res_ss + C, y,
+                                                     mask, M, C);
+  else
+    bn_apply_resbn_kernel<false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, res_ss, res_ss + C, y,
+                                                      mask, M, C);
   CA_LAUNCH_CHECK();
   return 0;
 }
