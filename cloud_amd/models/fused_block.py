@@ -28,7 +28,13 @@ This module runs the whole block as ONE autograd node:
   own read pass over dy and z.  Inside a block that covers bn2 (conv3's dgrad)
   and bn1 (conv2's dgrad); across blocks, conv1's dgrad of block i+1 -- the
   launch that completes the block-input gradient -- computes block i's bn3
-  statistics and parks them for block i's backward (``CLOUD_AMD_BN_BWD_EPILOGUE``).
+  statistics and parks them for block i's backward (``CLOUD_AMD_BN_BWD_EPILOGUE``);
+* no shortcut tensor is materialised in either direction: the projection
+  shortcut's BN is folded into bn3's apply (its statistics pass only; the affine
+  is applied to the shortcut conv output in registers, rounded to bf16 exactly as
+  a stored copy would be), and the residual gradient ``dout * relu'(mask3)`` is
+  gated on load -- by conv1's dgrad epilogue in identity blocks (``res=``), by the
+  shortcut BN backward in projection blocks.
 
 Parity: the block computes exactly what :class:`cloud_amd.models.resnet.Bottleneck`
 computes op by op (same kernels, same order) -- tests compare the two.
