@@ -47,6 +47,8 @@ _VARS = [
     Var("CLOUD_AMD_BN_BWD_EPILOGUE", bool, True, "ResNet block backward: BatchNorm-backward statistics from the "
         "dgrad GEMM epilogues (skips the BN reduction pass)", "ops"),
     Var("CLOUD_AMD_REPO", str, None, "example notebooks: repository root to put on sys.path", "examples"),
+    Var("CLOUD_AMD_DEBUG_SYNC", bool, False, "debug: synchronise after every native kernel launch so a fault is "
+        "reported by the op that caused it; run() also sets HIP_LAUNCH_BLOCKING/AMD_SERIALIZE_KERNEL", "ops"),
     Var("CLOUD_AMD_PRECISION", str, "bf16", "compute dtype of the Keras front end", "ops"),
     Var("CLOUD_AMD_ARCH", str, "gfx950", "offload arch of the native build", "build"),
     Var("CLOUD_AMD_SANITIZE", bool, False, "build the C++ test binary with ASan/UBSan", "build"),

@@ -202,6 +202,9 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if not any_gpu:
             env["CLOUD_AMD_DEVICE"] = "cpu"
+        if env.get("CLOUD_AMD_DEBUG_SYNC") == "1":  # kernel-fault localisation mode
+            env.setdefault("HIP_LAUNCH_BLOCKING", "1")
+            env.setdefault("AMD_SERIALIZE_KERNEL", "3")
         cmd = [python, target] + list(entry_point_args or [])
         if profile and info["rank"] == 0:
             prof_dir = os.path.join(job_dir, "profile")

@@ -5,10 +5,22 @@
 //   * vector memory access is 16 B per lane (8 x bf16 or 4 x fp32) -- Guideline 13.
 //   * wave = 64 lanes; block sizes are multiples of 64.
 //   * every launcher takes a hipStream_t and never allocates or synchronises,
-//     so it can be captured into a hipGraph.
+//     so it can be captured into a hipGraph -- except in the debug mode below.
+//   * CLOUD_AMD_DEBUG_SYNC=1: every launch is followed by hipDeviceSynchronize(), so a
+//     kernel fault is reported by the launcher (and the Python op) that caused it
+//     instead of by a later, unrelated call (not usable with graphs).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+inline bool ca_debug_sync() {
+  static const bool on = [] {
+    const char* e = getenv("CLOUD_AMD_DEBUG_SYNC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 
 #define CA_WAVE 64
 
@@ -18,7 +30,12 @@
     if (_e != hipSuccess) return (int)_e;                                      \
   } while (0)
 
-#define CA_LAUNCH_CHECK() CA_HIP_CHECK(hipGetLastError())
+#define CA_LAUNCH_CHECK()                                                      \
+  do {                                                                         \
+    hipError_t _le = hipGetLastError();                                        \
+    if (_le == hipSuccess && ca_debug_sync()) _le = hipDeviceSynchronize();    \
+    if (_le != hipSuccess) return (int)_le;                                    \
+  } while (0)
 
 typedef uint16_t bf16_t;
 typedef unsigned short us8 __attribute__((ext_vector_type(8)));

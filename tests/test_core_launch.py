@@ -144,3 +144,27 @@ def test_run_exits_when_called_from_script(tmp_path, monkeypatch):
     with pytest.raises(SystemExit) as e:
         run_mod.run(entry_point="train.py", chief_config=CPU, jobs_dir=str(tmp_path / "jobs"), stream_logs=True)
     assert e.value.code == 0
+
+
+def test_debug_sync_mode_serialises_rank_launches(tmp_path, monkeypatch):
+    """CLOUD_AMD_DEBUG_SYNC=1 reaches every rank with HIP's blocking-launch switches set
+    (fault localisation); the native launch check reads the same variable."""
+    app = tmp_path / "app"
+    app.mkdir()
+    (app / "probe.py").write_text(
+        "import json, os\n"
+        "keys = ['CLOUD_AMD_DEBUG_SYNC', 'HIP_LAUNCH_BLOCKING', 'AMD_SERIALIZE_KERNEL']\n"
+        "json.dump({k: os.environ.get(k) for k in keys},\n"
+        "          open(os.path.join(os.environ['CLOUD_AMD_JOB_DIR'], 'env.json'), 'w'))\n")
+    job_dir = tmp_path / "job"
+    (job_dir / "logs").mkdir(parents=True)
+    monkeypatch.setenv("CLOUD_AMD_NUM_GPUS", "0")
+    monkeypatch.setenv("CLOUD_AMD_DEBUG_SYNC", "1")
+    monkeypatch.delenv("HIP_LAUNCH_BLOCKING", raising=False)
+    monkeypatch.delenv("AMD_SERIALIZE_KERNEL", raising=False)
+    job = launcher.launch("dbg", str(job_dir), str(app / "probe.py"), CPU, 0, None)
+    assert job.wait(60) == 0
+    env = json.load(open(job_dir / "env.json"))
+    assert env == {"CLOUD_AMD_DEBUG_SYNC": "1", "HIP_LAUNCH_BLOCKING": "1", "AMD_SERIALIZE_KERNEL": "3"}
+    hdr = open(os.path.join(HERE, "..", "csrc", "include", "ca_common.h")).read()
+    assert 'getenv("CLOUD_AMD_DEBUG_SYNC")' in hdr and "hipDeviceSynchronize" in hdr
