@@ -55,6 +55,10 @@ _VARS = [
     # distributed
     Var("CLOUD_AMD_COMM", str, "torch", "DP transport: 'torch' (torch.distributed/RCCL) or 'rccl' (native)",
         "distributed"),
+    Var("CLOUD_AMD_DIST_BACKEND", str, None, "process-group backend override ('gloo' / 'nccl'); default nccl "
+        "(RCCL) on GPU, gloo on CPU", "distributed"),
+    Var("CLOUD_AMD_SHARED_GPU", bool, False, "rehearsal: every local rank uses cuda:0 (pair with "
+        "CLOUD_AMD_DIST_BACKEND=gloo on a one-GPU box)", "distributed"),
     Var("CLOUD_AMD_BUCKET_MB", float, 16.0, "gradient bucket size (MB) of the DP engine", "distributed"),
     Var("CLOUD_AMD_DDP_ORDER", str, "event", "bucket ordering: 'event' (comm stream waits on a compute event), "
         "'sync' (debug), 'backend'", "distributed"),

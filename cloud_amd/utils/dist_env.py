@@ -37,13 +37,18 @@ def init_distributed(backend=None, timeout_s=None, device=None):
     """Initialise the default process group if WORLD_SIZE > 1. Returns (rank, world, device)."""
     r, w, lr = rank(), world_size(), local_rank()
     if device is None:
-        device = torch.device("cuda", lr) if torch.cuda.is_available() else torch.device("cpu")
+        # CLOUD_AMD_SHARED_GPU=1 maps every local rank onto cuda:0: a rehearsal of the
+        # multi-rank path on a one-GPU box (with CLOUD_AMD_DIST_BACKEND=gloo; RCCL
+        # refuses two ranks on one device).
+        ordinal = 0 if os.environ.get("CLOUD_AMD_SHARED_GPU") == "1" else lr
+        device = torch.device("cuda", ordinal) if torch.cuda.is_available() else torch.device("cpu")
     if device.type == "cuda":
         torch.cuda.set_device(device)
     if w > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
-        backend = backend or ("nccl" if device.type == "cuda" else "gloo")
+        backend = backend or os.environ.get("CLOUD_AMD_DIST_BACKEND") or (
+            "nccl" if device.type == "cuda" else "gloo")
         timeout = datetime.timedelta(seconds=timeout_s or env_int("CLOUD_AMD_PG_TIMEOUT_S", 600))
         kw = {"device_id": device} if (backend == "nccl" and device.type == "cuda") else {}
         try:
