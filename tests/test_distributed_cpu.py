@@ -160,3 +160,35 @@ def test_grad_ready_counts_each_param_once():
     with red.no_sync():
         red._on_grad(params[0])
     assert launched == [0]
+
+
+def test_init_distributed_backend_and_shared_gpu_overrides(monkeypatch):
+    """CLOUD_AMD_DIST_BACKEND picks the process-group backend; CLOUD_AMD_SHARED_GPU maps
+    every local rank onto device 0 (the one-GPU rehearsal of the multi-rank bench)."""
+    import torch.distributed as dist
+
+    from cloud_amd.utils import dist_env
+
+    seen = {}
+
+    def fake_init(backend, rank, world_size, timeout, **kw):
+        seen.update(backend=backend, rank=rank, world=world_size)
+
+    monkeypatch.setattr(dist, "is_initialized", lambda: False)
+    monkeypatch.setattr(dist, "init_process_group", fake_init)
+    monkeypatch.setattr(dist_env.atexit, "register", lambda fn: None)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: seen.update(device=d))
+    monkeypatch.setenv("RANK", "1")
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    monkeypatch.setenv("CLOUD_AMD_DIST_BACKEND", "gloo")
+    monkeypatch.setenv("CLOUD_AMD_SHARED_GPU", "1")
+    r, w, dev = dist_env.init_distributed()
+    assert (r, w) == (1, 2)
+    assert dev == torch.device("cuda", 0) and seen["device"] == dev
+    assert seen["backend"] == "gloo" and seen["world"] == 2
+    monkeypatch.delenv("CLOUD_AMD_DIST_BACKEND")
+    monkeypatch.delenv("CLOUD_AMD_SHARED_GPU")
+    r, w, dev = dist_env.init_distributed()
+    assert dev == torch.device("cuda", 1) and seen["backend"] == "nccl"
