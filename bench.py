@@ -1,27 +1,37 @@
 #!/usr/bin/env python3
-"""Headline benchmark: ResNet-50 training throughput on synthetic ImageNet.
+"""Headline benchmark: ResNet-50 training throughput on synthetic ImageNet, launched
+through ``cloud_amd.run()``.
 
-Metric (BASELINE.json): images/sec of ResNet-50 training at 1/2/4/8 MI355X,
-one process per GPU, data parallel over RCCL/xGMI, bf16 compute with fp32
-master weights, SGD(momentum 0.9) -- plus ``first_step_latency_s`` (process
-start -> end of first optimizer step) and, with ``--via-run 1``, the launch
-through ``cloud_amd.run()`` and ``run_to_first_step_s`` (run() call -> end of
-the first step on every rank, max over ranks).
+Metric (BASELINE.json): images/sec of ResNet-50 training **via run()** at 1/2/4/8
+MI355X, one process per GPU, data parallel over RCCL/xGMI, bf16 compute with fp32
+master weights, SGD(momentum 0.9) -- plus ``run_to_first_step_s`` (``run()`` call ->
+end of the first optimizer step on every rank, max over ranks).
 
-    python bench.py --gpus 1 --steps 20 --warmup 10
+    python bench.py --gpus 8 --steps 20 --warmup 10          # stages + spawns 8 ranks via run()
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
-        --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 10
+        --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 10   # ranks started by torchrun
+
+Launch modes:
+
+* **not inside a launched job** (no ``WORLD_SIZE`` / ``CLOUD_AMD_RUNNING_REMOTELY`` /
+  ``TORCHELASTIC_RUN_ID``): this process only stages the job and spawns ``--gpus``
+  ranks through ``cloud_amd.run(chief_config=MI355X_<N>X)`` -- the reference's
+  ``run()`` -> strategy auto-selection -> multi-replica job path
+  (reference ``TFC/core/preprocess.py:137-146``, ``TFC/core/deploy.py:98-167``).  It
+  never touches the GPU: the launcher counts devices from KFD sysfs.  A node with
+  fewer GPUs than ``--gpus`` fails validation and exits non-zero.
+* **inside a rank** (spawned by run() or torchrun): trains; the world size actually
+  seen by torch.distributed MUST equal ``--gpus`` or the rank exits non-zero.
 
 Weak scaling: the per-GPU batch is fixed (``--batch``, default 512), global batch =
-batch x N.  512 images per GPU is sized for 288 GB of HBM3E (``peak_mem_gb`` in the
-JSON line reports the step's peak) and halves the per-image share of the step's fixed
-costs (~570 kernel boundaries at ~1.8 us each, per-layer BN finalize kernels)
-relative to 256; the sweep 128..1024 and the stock comparator at 256 and 512
-are in BASELINE.md.
-Synthetic data: random NHWC bf16 images and random labels, generated once on
-the device (no input pipeline in the timed region, as in tf_cnn_benchmarks'
-synthetic mode).  Random-init weights.  Every timed step runs the full forward,
-backward, gradient all-reduce and fused optimizer update.
+batch x N.  Synthetic data: random NHWC bf16 images and random labels generated once
+on the device; random-init weights.  Every timed step runs the full forward,
+backward, bucketed gradient all-reduce (overlapped with backward) and fused
+optimizer update.  The JSON line carries the communication breakdown of the timed
+steps: bucket count, all-reduce ms and exposed (not overlapped) communication ms.
+
+``--model tiny --device cpu`` runs the same code path on a small bottleneck ResNet on
+CPU ranks over gloo (CPU tests of the launch contract); its numbers are not a metric.
 """
 from __future__ import annotations
 
@@ -32,73 +42,86 @@ import sys
 import time
 
 T_START = time.time()
+METRIC = "images/sec ResNet-50 via run() at 1/2/4/8 MI355X; run()→first-step latency"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per MI355X)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("CLOUD_AMD_BENCH_BATCH", 512)),
                     help="per-GPU batch")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--classes", type=int, default=1000)
+    ap.add_argument("--model", choices=("resnet50", "tiny"), default="resnet50")
+    ap.add_argument("--device", choices=("auto", "cpu"), default="auto")
     ap.add_argument("--graph", type=int, default=int(os.environ.get("CLOUD_AMD_GRAPH", "0")),
-                    help="capture the training step in a HIP graph (1-GPU only unless forced)")
+                    help="capture the training step in a HIP graph (1 rank only)")
     ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="gradient all-reduce bucket size (default CLOUD_AMD_BUCKET_MB or 16)")
+    ap.add_argument("--grad-reduce-dtype", choices=("bf16", "fp32"), default=None,
+                    help="wire dtype of the gradient reduction of bf16 layers")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--via-run", type=int, default=0,
-                    help="launch through cloud_amd.run() (stage -> spawn one rank per GPU) and report "
-                         "run()->first-step latency; the ranks' JSON line is streamed from rank 0's log")
-    return ap.parse_args()
+    ap.add_argument("--via-run", type=int, default=int(os.environ.get("CLOUD_AMD_BENCH_VIA_RUN", "1")),
+                    help="1 (default): launch the ranks through cloud_amd.run(); 0: train in this process")
+    return ap.parse_args(argv)
 
 
 def via_run(args):
-    """The BASELINE metric's 'via run()' form: this process only stages and launches
-    (it never touches the GPU); every rank re-runs this file with remote() True."""
-    import cloud_amd as tfc
+    """Stage this script and launch ``--gpus`` ranks through ``cloud_amd.run()``.
+    This process never initialises HIP; rank 0's log (ending in the JSON line) is
+    streamed to stdout and the job's exit code becomes ours."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from cloud_amd.utils import benchlaunch
 
-    argv = [a for a in sys.argv[1:]]
-    if "--via-run" in argv:
-        i = argv.index("--via-run")
-        del argv[i:i + 2]
-    cfg = tfc.COMMON_MACHINE_CONFIGS["MI355X_%dX" % args.gpus]
-    os.chdir(os.path.dirname(os.path.abspath(__file__)))
-    job = tfc.run(entry_point="bench.py", distribution_strategy=None, chief_config=cfg, worker_count=0,
-                  entry_point_args=argv, stream_logs=True, exit=False, wait=True)
-    sys.exit(job.returncode or 0)
+    benchlaunch.launch_via_run(os.path.abspath(__file__), args.gpus, device=args.device)
 
 
 def main():
     args = parse()
-    if args.via_run and not (os.environ.get("CLOUD_AMD_RUNNING_REMOTELY") or os.environ.get("TORCHELASTIC_RUN_ID")):
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from cloud_amd.utils import benchlaunch
+
+    if args.via_run and not benchlaunch.inside_launched_rank():
         return via_run(args)
     import torch
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from cloud_amd.models import resnet50
+    from cloud_amd.models.resnet import resnet18_like_small
     from cloud_amd.ops import softmax_cross_entropy
     from cloud_amd.optim import SGD
     from cloud_amd.parallel.ddp import GradAllReducer
-    from cloud_amd.utils import dist_env
+    from cloud_amd.utils import dist_env, trace
 
-    rank, world, device = dist_env.init_distributed()
-    if world != args.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    dev_arg = torch.device("cpu") if args.device == "cpu" else None
+    rank, world, device = dist_env.init_distributed(device=dev_arg)
+    benchlaunch.check_world(args.gpus, world)
+    on_gpu = device.type == "cuda"
+    if not on_gpu and args.model == "resnet50" and os.environ.get("CLOUD_AMD_BENCH_ALLOW_CPU") != "1":
+        print("[bench] error: ResNet-50 bench needs a GPU (use --model tiny --device cpu for CPU runs)",
+              file=sys.stderr)
+        sys.exit(3)
+    dtype = torch.bfloat16 if on_gpu else torch.float32
     torch.manual_seed(1234)  # identical init on every rank (also broadcast below)
     B, S = args.batch, args.image_size
-    model = resnet50(num_classes=args.classes, dtype=torch.bfloat16, device=device)
+    build = resnet50 if args.model == "resnet50" else resnet18_like_small
+    model = build(num_classes=args.classes, dtype=dtype, device=device)
+    # mean over the GLOBAL batch: every rank holds B samples, so 1/world folds into the optimizer
     opt = SGD(model, learning_rate=args.lr, momentum=0.9, weight_decay=5e-5, grad_scale=1.0 / world)
-    reducer = GradAllReducer(opt.arenas)
+    reducer = GradAllReducer(opt.arenas, bucket_mb=args.bucket_mb, reduce_dtype=args.grad_reduce_dtype)
     reducer.broadcast_parameters()
 
     gen = torch.Generator(device=device)
     gen.manual_seed(1000 + rank)
-    x = torch.randn((B, S, S, 3), generator=gen, device=device, dtype=torch.float32).to(torch.bfloat16)
+    x = torch.randn((B, S, S, 3), generator=gen, device=device, dtype=torch.float32).to(dtype)
     y = torch.randint(0, args.classes, (B,), generator=gen, device=device)
     global_batch = B * world
 
-    from cloud_amd.utils import trace
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
 
     def fwd_bwd():
         with trace.range("forward"):
@@ -119,12 +142,12 @@ def main():
 
     # first step = end-to-end "first-step latency" (process start -> step done)
     loss = train_step()
-    torch.cuda.synchronize()
+    sync()
     first_step_latency = time.time() - T_START
     run_t0 = os.environ.get("CLOUD_AMD_RUN_T0")
     run_to_first = (time.time() - float(run_t0)) if run_t0 else None
 
-    use_graph = bool(args.graph) and (world == 1 or os.environ.get("CLOUD_AMD_GRAPH_FORCE") == "1")
+    use_graph = bool(args.graph) and on_gpu and (world == 1 or os.environ.get("CLOUD_AMD_GRAPH_FORCE") == "1")
     step_fn = train_step
     if use_graph:
         loss = None
@@ -135,19 +158,24 @@ def main():
     for _ in range(max(args.warmup - 1, 0)):
         loss = step_fn()
     dist_env.barrier()
-    torch.cuda.synchronize()
+    sync()
+    if not use_graph:
+        reducer.timing_start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step_fn()
-    torch.cuda.synchronize()
+    sync()
     dist_env.barrier()
     t1 = time.perf_counter()
+    comm = reducer.timing_summary()
     elapsed = dist_env.all_reduce_max(t1 - t0, device)
     ms = elapsed / args.steps * 1000.0
     ips = global_batch * args.steps / elapsed
     first_lat = dist_env.all_reduce_max(first_step_latency, device)
     if run_to_first is not None:
         run_to_first = dist_env.all_reduce_max(run_to_first, device)
+    comm["allreduce_ms"] = dist_env.all_reduce_max(comm["allreduce_ms"], device)
+    comm["exposed_comm_ms"] = dist_env.all_reduce_max(comm["exposed_comm_ms"], device)
     final_loss = float(loss.detach().float().item()) if loss is not None else float("nan")
     try:
         from cloud_amd import monitoring
@@ -158,8 +186,14 @@ def main():
     except Exception:
         pass
     if rank == 0:
+        launched = benchlaunch.launched_via()
+        backend = "none"
+        if world > 1:
+            import torch.distributed as dist
+
+            backend = dist.get_backend()
         out = {
-            "metric": "images/sec ResNet-50 via run() at 1/2/4/8 MI355X; run()→first-step latency",
+            "metric": METRIC,
             "value": round(ips, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -169,16 +203,22 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic (random NHWC bf16 images + random labels, random-init weights)",
-            "config": {"model": "resnet50", "global_batch": global_batch, "seq_len": None,
+            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "data": "synthetic (random NHWC images + random labels, random-init weights)",
+            "config": {"model": "resnet50" if args.model == "resnet50" else "tiny_bottleneck_resnet_cpu_test",
+                       "global_batch": global_batch, "seq_len": None,
                        "image_size": S, "per_gpu_batch": B, "parallelism": f"dp{world}",
                        "optimizer": "sgd_momentum0.9_fused", "hip_graph": use_graph},
+            "device": device.type,
+            "backend": backend if world > 1 else None,
+            "shared_gpu": os.environ.get("CLOUD_AMD_SHARED_GPU", "0") not in ("", "0", "false"),
+            "comm": dict(reducer.describe(), allreduce_ms=comm["allreduce_ms"],
+                         exposed_comm_ms=comm["exposed_comm_ms"]),
             "first_step_latency_s": round(first_lat, 3),
             "run_to_first_step_s": round(run_to_first, 3) if run_to_first is not None else None,
-            "launched_via": "cloud_amd.run()" if run_t0 else "direct",
+            "launched_via": launched,
             "final_loss": round(final_loss, 4),
-            "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2) if on_gpu else None,
         }
         line = json.dumps(out)
         print(line, flush=True)

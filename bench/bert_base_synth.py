@@ -2,9 +2,14 @@
 """BASELINE.json config 5: BERT-base fine-tune on synthetic GLUE (sequence
 classification), data parallel, bf16 compute, fused AdamW.
 
-    python bench/bert_base_synth.py --steps 20 --warmup 5            # cloud_amd kernels
+    python bench/bert_base_synth.py --steps 20 --warmup 5            # 1 rank via cloud_amd.run()
+    python bench/bert_base_synth.py --gpus 8                         # 8 ranks via cloud_amd.run()
     python bench/bert_base_synth.py --stock 1 --steps 20 --warmup 5  # HF transformers + torch AdamW, autocast bf16
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench/bert_base_synth.py --gpus 8
+
+Launch contract as bench.py (:mod:`cloud_amd.utils.benchlaunch`): outside a launched
+job the script stages itself and spawns ``--gpus`` ranks through ``cloud_amd.run()``
+(``--via-run 0`` trains in-process); inside a rank, WORLD_SIZE != --gpus is an error.
 
 Synthetic GLUE: random token ids (vocab 30522), segment ids (A|B split), a
 right-padded attention mask with per-example lengths in [S/2, S], 2 labels;
@@ -33,6 +38,9 @@ def parse():
     ap.add_argument("--lr", type=float, default=2e-5)
     ap.add_argument("--stock", type=int, default=0)
     ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--grad-reduce-dtype", choices=("bf16", "fp32"), default=None)
+    ap.add_argument("--via-run", type=int, default=int(os.environ.get("CLOUD_AMD_BENCH_VIA_RUN", "1")))
     return ap.parse_args()
 
 
@@ -55,12 +63,18 @@ def synthetic_glue(B, S, device, seed):
 
 def main():
     args = parse()
+    from cloud_amd.utils import benchlaunch
+
+    if args.via_run and not benchlaunch.inside_launched_rank():
+        return benchlaunch.launch_via_run(os.path.abspath(__file__), args.gpus, tag="bert")
     import torch
     import torch.nn.functional as F
 
     from cloud_amd.utils import dist_env
 
     rank, world, device = dist_env.init_distributed()
+    benchlaunch.check_world(args.gpus, world, tag="bert")
+    reducer = None
     torch.manual_seed(1234)
     B, S = args.batch, args.seq
     ids, tts, am, labels = synthetic_glue(B, S, device, 1000 + rank)
@@ -93,7 +107,7 @@ def main():
         cfg = BertConfig.base(num_hidden_layers=args.layers, num_labels=2)
         model = BertForSequenceClassification(cfg, device=device)
         opt = AdamW(model, learning_rate=args.lr, weight_decay=0.01, grad_scale=1.0 / world)
-        reducer = GradAllReducer(opt.arenas)
+        reducer = GradAllReducer(opt.arenas, bucket_mb=args.bucket_mb, reduce_dtype=args.grad_reduce_dtype)
         reducer.broadcast_parameters()
 
         def train_step():
@@ -109,10 +123,14 @@ def main():
     loss = train_step()
     torch.cuda.synchronize()
     first = time.time() - T_START
+    run_t0 = os.environ.get("CLOUD_AMD_RUN_T0")
+    run_to_first = (time.time() - float(run_t0)) if run_t0 else None
     for _ in range(max(args.warmup - 1, 0)):
         loss = train_step()
     dist_env.barrier()
     torch.cuda.synchronize()
+    if reducer is not None:
+        reducer.timing_start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = train_step()
@@ -120,6 +138,14 @@ def main():
     dist_env.barrier()
     elapsed = dist_env.all_reduce_max(time.perf_counter() - t0, device)
     sps = B * world * args.steps / elapsed
+    first = dist_env.all_reduce_max(first, device)
+    if run_to_first is not None:
+        run_to_first = dist_env.all_reduce_max(run_to_first, device)
+    comm = None
+    if reducer is not None:
+        t = reducer.timing_summary()
+        comm = dict(reducer.describe(), allreduce_ms=dist_env.all_reduce_max(t["allreduce_ms"], device),
+                    exposed_comm_ms=dist_env.all_reduce_max(t["exposed_comm_ms"], device))
     if rank == 0:
         print(json.dumps({
             "metric": "sequences/sec BERT-base fine-tune synthetic GLUE (seq %d)" % S,
@@ -131,6 +157,8 @@ def main():
                        "global_batch": B * world, "seq_len": S, "per_gpu_batch": B, "parallelism": "dp%d" % world,
                        "optimizer": "adamw"},
             "impl": impl, "first_step_latency_s": round(first, 3),
+            "run_to_first_step_s": round(run_to_first, 3) if run_to_first is not None else None,
+            "launched_via": benchlaunch.launched_via(), "comm": comm,
             "tokens_per_sec": round(sps * S, 1), "final_loss": round(float(loss.detach().float()), 4)}), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -16,8 +16,13 @@ but the "cluster" is the local node:
   exit codes go to ``job.json`` and the job is marked FAILED;
 * ``stream_logs=True`` tails the chief log (rank 0) to stdout until the job ends.
 
-The launcher process never initialises the GPU (it only counts devices), so
-spawning ranks is safe on the MI355X pool.
+The launcher process never initialises the GPU: it sizes the job from the KFD
+topology in sysfs (:mod:`cloud_amd.core.topology`) and never calls into HIP, so
+forking ranks is safe on the MI355X pool.
+
+Multi-GPU jobs also get RCCL transport defaults sized for the xGMI mesh
+(:func:`rccl_env`): every variable is ``setdefault`` -- a value the user exported
+wins -- and ``CLOUD_AMD_RCCL_ENV=0`` turns the whole set off.
 """
 from __future__ import annotations
 
@@ -78,6 +83,27 @@ def log_name(info):
     if info["gpu"] is not None and info["proc_in_machine"] > 0:
         name += "-gpu{}".format(info["proc_in_machine"])
     return name + ".log"
+
+
+def rccl_env(world, links):
+    """RCCL settings for a ``world``-rank job on one MI355X node with ``links``
+    point-to-point xGMI links per GPU (7 in the full 8-GPU mesh).
+
+    * ``NCCL_MIN_NCHANNELS`` = links: at least one ring/channel per xGMI link, so a
+      collective is never limited to a single ~153 GB/s link (one ring uses one link
+      per direction).  RCCL may pick more channels by itself; this is a floor.
+      ``CLOUD_AMD_RCCL_CHANNELS`` overrides the value.
+    * ``HSA_NO_SCRATCH_RECLAIM=1``: keeps the ROCr scratch pool of the RCCL kernels
+      resident instead of reclaiming it after every launch.
+    * ``NCCL_DEBUG=WARN`` surfaces transport problems in the rank logs.
+
+    Gradient buckets are sized separately (``CLOUD_AMD_BUCKET_MB``, bench
+    ``--bucket-mb``).  These values are a starting point that the driver's 8-GPU runs
+    measure (bench JSON ``comm``), not a tuned optimum."""
+    if world <= 1 or os.environ.get("CLOUD_AMD_RCCL_ENV", "1") == "0":
+        return {}
+    ch = os.environ.get("CLOUD_AMD_RCCL_CHANNELS") or str(max(links, 1))
+    return {"NCCL_MIN_NCHANNELS": ch, "HSA_NO_SCRATCH_RECLAIM": "1", "NCCL_DEBUG": "WARN"}
 
 
 def _print_logs_info(job_id, job_dir):
@@ -175,17 +201,22 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
     app_dir = os.path.dirname(target)
     python = python or sys.executable
     any_gpu = any(r["gpu"] is not None for r in ranks)
+    node = topology.describe_node()
+    n_gpu_ranks = sum(1 for r in ranks if r["gpu"] is not None)
+    comm_env = rccl_env(n_gpu_ranks, topology.xgmi_links_per_gpu(n_gpu_ranks)) if any_gpu else {}
     meta = {
         "job_id": job_id, "state": "RUNNING", "start_time": time.time(), "world_size": world,
         "chief_config": chief_config.to_dict(), "worker_count": worker_count,
         "worker_config": worker_config.to_dict() if worker_config is not None and worker_count > 0 else None,
         "labels": dict(job_labels or {}), "args": list(entry_point_args or []),
         "backend": "nccl(rccl)" if any_gpu else "gloo", "master_port": port,
-        "ranks": ranks, "node": {"gpus_visible": topology.visible_gpu_count()},
+        "ranks": ranks, "node": node, "comm_env": {k: os.environ.get(k, v) for k, v in comm_env.items()},
     }
     procs = []
     for info in ranks:
         env = dict(os.environ)
+        for k, v in comm_env.items():
+            env.setdefault(k, v)
         env.update(extra_env or {})
         env.update({
             "RANK": str(info["rank"]), "WORLD_SIZE": str(world),

@@ -33,6 +33,7 @@ keeps the first bucket ready early in backward; tune with
 from __future__ import annotations
 
 import os
+import time
 import weakref
 
 import torch
@@ -55,13 +56,15 @@ def notify_grad_ready(param):
 
 
 class Bucket:
-    __slots__ = ("arena", "lo", "hi", "slots", "pending", "work", "launched", "index")
+    __slots__ = ("arena", "lo", "hi", "slots", "pending", "work", "launched", "index", "wire", "ev")
 
     def __init__(self, arena, lo, hi, slots, index):
         self.arena, self.lo, self.hi, self.slots, self.index = arena, lo, hi, slots, index
         self.pending = len(slots)
         self.work = None
         self.launched = False
+        self.wire = None   # reduce-dtype copy on the wire (fp32 reduction of bf16 grads)
+        self.ev = None     # (start, end) timing events of this step's collective
 
     @property
     def tensor(self):
@@ -69,13 +72,24 @@ class Bucket:
 
 
 class GradAllReducer:
-    def __init__(self, arenas, process_group=None, bucket_mb=None, overlap=True):
+    def __init__(self, arenas, process_group=None, bucket_mb=None, overlap=True, reduce_dtype=None):
         self.arenas = arenas
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         mb = float(bucket_mb if bucket_mb is not None else os.environ.get("CLOUD_AMD_BUCKET_MB", 16))
+        self.bucket_mb = mb
         self.bucket_bytes = int(mb * (1 << 20))
         self.overlap = overlap
+        # Wire dtype of the reduction.  None = the gradient's own dtype (bf16 sums for bf16
+        # layers: half the bytes on xGMI); torch.float32 = reduce an fp32 copy (exact-er
+        # sums at 2x the bytes; the copy and the cast back run on the comm stream).
+        rd = reduce_dtype if reduce_dtype is not None else os.environ.get("CLOUD_AMD_GRAD_REDUCE_DTYPE")
+        if isinstance(rd, str):
+            rd = {"fp32": torch.float32, "float32": torch.float32, "bf16": None, "native": None}[rd]
+        self.reduce_dtype = rd
+        # Per-step communication timing (bench / monitoring): see timing_start/timing_summary.
+        self.timing = False
+        self._timing_log = []
         self.check_every = int(os.environ.get("CLOUD_AMD_GRAD_CHECK_EVERY", "0"))
         self._steps = 0
         self.comm = None
@@ -134,6 +148,12 @@ class GradAllReducer:
         if b.pending <= 0:
             self._launch_ready()
 
+    def _wire(self, b):
+        if self.reduce_dtype is None or self.reduce_dtype == b.tensor.dtype:
+            return b.tensor
+        b.wire = b.tensor.to(self.reduce_dtype)
+        return b.wire
+
     def _launch(self, b):
         trace.mark("bucket%d" % b.index)
         if self.comm is not None:
@@ -150,9 +170,14 @@ class GradAllReducer:
             ev.record(torch.cuda.current_stream(b.tensor.device))
             self._side.wait_event(ev)
             with torch.cuda.stream(self._side):
-                b.work = dist.all_reduce(b.tensor, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                if self.timing:
+                    b.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    b.ev[0].record(self._side)
+                b.work = dist.all_reduce(self._wire(b), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                if self.timing:
+                    b.ev[1].record(self._side)
         else:
-            b.work = dist.all_reduce(b.tensor, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            b.work = dist.all_reduce(self._wire(b), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         b.launched = True
 
     def _launch_ready(self):
@@ -164,6 +189,13 @@ class GradAllReducer:
         """Launch remaining buckets in order and join them onto the compute stream."""
         if self.world <= 1:
             return
+        on_gpu = self._side is not None or self.comm is not None
+        if self.timing:  # backward done (compute stream) -> comm joined = exposed communication
+            if on_gpu:
+                t_bwd = torch.cuda.Event(enable_timing=True)
+                t_bwd.record(torch.cuda.current_stream(self.arenas[0].grad.device))
+            else:
+                t_bwd = time.perf_counter()
         while self._next < len(self.buckets):
             self._launch(self.buckets[self._next])
             self._next += 1
@@ -174,11 +206,23 @@ class GradAllReducer:
                 for b in self.buckets:
                     if b.work is not None:
                         b.work.wait()
+                    if b.wire is not None:
+                        b.tensor.copy_(b.wire)
             torch.cuda.current_stream(self._side.device).wait_stream(self._side)
         else:
             for b in self.buckets:
                 if b.work is not None:
                     b.work.wait()
+                if b.wire is not None:
+                    b.tensor.copy_(b.wire)
+        if self.timing:
+            if on_gpu:
+                t_join = torch.cuda.Event(enable_timing=True)
+                t_join.record(torch.cuda.current_stream(self.arenas[0].grad.device))
+                self._timing_log.append((t_bwd, t_join, [b.ev for b in self.buckets if b.ev is not None]))
+            else:
+                dt = (time.perf_counter() - t_bwd) * 1e3
+                self._timing_log.append((dt, dt, []))
         self.reset()
         self._steps += 1
         if self.check_every and self._steps % self.check_every == 0:
@@ -227,7 +271,41 @@ class GradAllReducer:
             b.pending = len(b.slots)
             b.work = None
             b.launched = False
+            b.wire = None
+            b.ev = None
         self._next = 0
+
+    def timing_start(self):
+        """Record communication timing for every following step (events only; no sync)."""
+        self.timing = True
+        self._timing_log = []
+
+    def timing_summary(self):
+        """Mean per-step ``allreduce_ms`` (sum of bucket collective times on the comm
+        stream) and ``exposed_comm_ms`` (end of backward on the compute stream -> all
+        buckets joined).  Call after a device synchronize."""
+        self.timing = False
+        if self.world <= 1 or not self._timing_log:
+            return {"allreduce_ms": 0.0, "exposed_comm_ms": 0.0, "steps": len(self._timing_log)}
+        ar, ex = [], []
+        for t_bwd, t_join, evs in self._timing_log:
+            if isinstance(t_bwd, float):
+                ex.append(t_bwd)
+                ar.append(t_join)
+                continue
+            ex.append(t_bwd.elapsed_time(t_join))
+            ar.append(sum(s.elapsed_time(e) for s, e in evs) if evs else float("nan"))
+        n = len(ex)
+        return {"allreduce_ms": round(sum(ar) / n, 3), "exposed_comm_ms": round(sum(ex) / n, 3), "steps": n}
+
+    def describe(self):
+        """Bucket layout for reports: count, target size, wire dtype, transport."""
+        transport = ("native RcclComm" if self.comm is not None else
+                     "torch.distributed(%s)" % (dist.get_backend(self.pg) if dist.is_initialized() else "none"))
+        return {"buckets": len(self.buckets), "bucket_mb": self.bucket_mb,
+                "reduce_dtype": str(self.reduce_dtype or (self.arenas[0].grad.dtype if self.arenas else None)
+                                    ).replace("torch.", ""),
+                "transport": transport, "world": self.world}
 
     def broadcast_parameters(self, src=0):
         """C2: make every rank start from rank ``src``'s weights (one call per arena)."""

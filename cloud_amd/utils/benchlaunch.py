@@ -1,0 +1,71 @@
+"""Launch contract shared by the benchmarks (``bench.py``, ``bench/bert_base_synth.py``).
+
+* Outside a launched job, a bench stages itself and spawns ``--gpus`` ranks through
+  :func:`cloud_amd.run` (the reference's ``run()`` -> multi-replica job path,
+  ``TFC/core/deploy.py:98-167``); the launching process never initialises HIP.
+* Inside a rank, the world size seen by ``torch.distributed`` must equal ``--gpus``:
+  a mismatch is a hard error, never a silently relabelled number.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+
+def inside_launched_rank():
+    return bool(os.environ.get("CLOUD_AMD_RUNNING_REMOTELY") or os.environ.get("TORCHELASTIC_RUN_ID")
+                or os.environ.get("WORLD_SIZE"))
+
+
+def strip_flag(argv, flag):
+    out = list(argv)
+    for i, a in enumerate(out):
+        if a == flag:
+            return out[:i] + out[i + 2:]
+        if a.startswith(flag + "="):
+            return out[:i] + out[i + 1:]
+    return out
+
+
+def launch_via_run(script, gpus, device="auto", argv=None, tag="bench"):
+    """Stage ``script`` (its directory is the app) and run it on ``gpus`` ranks via
+    ``cloud_amd.run()``; stream rank 0's log; exit with the job's code."""
+    import cloud_amd as tfc
+    from cloud_amd.core.machine_config import AcceleratorType, MachineConfig
+
+    argv = strip_flag(sys.argv[1:] if argv is None else argv, "--via-run")
+    if device == "cpu":
+        cpu = tfc.COMMON_MACHINE_CONFIGS["CPU"]
+        chief, workers, wcfg = cpu, gpus - 1, cpu  # one process per CPU "machine", gloo
+    else:
+        chief = tfc.COMMON_MACHINE_CONFIGS.get("MI355X_%dX" % gpus) or MachineConfig(
+            cpu_cores=16 * gpus, memory=256 * gpus, accelerator_type=AcceleratorType.AMD_INSTINCT_MI355X,
+            accelerator_count=gpus)
+        workers, wcfg = 0, "auto"
+    script = os.path.abspath(script)
+    os.chdir(os.path.dirname(script))
+    try:
+        job = tfc.run(entry_point=os.path.basename(script), distribution_strategy=None, chief_config=chief,
+                      worker_config=wcfg, worker_count=workers, entry_point_args=argv, stream_logs=True,
+                      exit=False, wait=True)
+    except ValueError as e:
+        print("[%s] cannot launch %d rank(s) through cloud_amd.run(): %s" % (tag, gpus, e), file=sys.stderr)
+        sys.exit(2)
+    rc = job.returncode or 0
+    if rc:
+        print("[%s] job %s failed (exit codes %s); logs: %s" % (
+            tag, job.job_id, job.meta.get("exit_codes"), os.path.join(job.job_dir, "logs")), file=sys.stderr)
+    sys.exit(rc)
+
+
+def check_world(gpus, world, tag="bench"):
+    if world != gpus:
+        print("[%s] error: --gpus %d but the job has WORLD_SIZE=%d ranks; refusing to report a %d-rank "
+              "number as %d GPUs" % (tag, gpus, world, world, gpus), file=sys.stderr)
+        sys.exit(3)
+
+
+def launched_via():
+    if os.environ.get("CLOUD_AMD_RUN_T0"):
+        return "cloud_amd.run()"
+    return "torch.distributed.run" if os.environ.get("TORCHELASTIC_RUN_ID") else "direct"

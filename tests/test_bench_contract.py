@@ -1,0 +1,58 @@
+"""bench.py launch contract: by default the headline bench stages
+and spawns its ranks through cloud_amd.run(); the world size a rank sees must equal
+--gpus; a node with too few GPUs is a hard error."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TINY = ["--model", "tiny", "--device", "cpu", "--batch", "4", "--image-size", "32", "--classes", "10",
+        "--steps", "2", "--warmup", "1"]
+
+
+def _env(tmp_path, **kw):
+    env = dict(os.environ, CLOUD_AMD_JOBS_DIR=str(tmp_path / "jobs"), OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "CLOUD_AMD_RUNNING_REMOTELY", "TORCHELASTIC_RUN_ID",
+              "TF_KERAS_RUNNING_REMOTELY"):
+        env.pop(k, None)
+    env.update(kw)
+    return env
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def test_bench_two_ranks_via_run_cpu(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + TINY,
+                       env=_env(tmp_path), capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout[-3000:]
+    j = lines[0]
+    assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2"
+    assert j["launched_via"] == "cloud_amd.run()"
+    assert j["run_to_first_step_s"] is not None and j["run_to_first_step_s"] > 0
+    assert j["comm"]["buckets"] >= 1 and j["comm"]["allreduce_ms"] > 0
+    assert j["backend"] == "gloo" and j["config"]["global_batch"] == 8
+    job = os.listdir(tmp_path / "jobs")
+    assert len(job) == 1
+    meta = json.load(open(tmp_path / "jobs" / job[0] / "job.json"))
+    assert meta["world_size"] == 2 and meta["state"] == "SUCCEEDED"
+
+
+def test_bench_too_many_gpus_fails(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       env=_env(tmp_path, CLOUD_AMD_NUM_GPUS="1"), capture_output=True, text=True, timeout=300,
+                       cwd=str(tmp_path))
+    assert r.returncode != 0
+    assert "needs 2 GPUs" in r.stderr and not _json_lines(r.stdout)
+
+
+def test_bench_world_mismatch_is_an_error(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--via-run", "0"] + TINY,
+                       env=_env(tmp_path, WORLD_SIZE="1", RANK="0"), capture_output=True, text=True, timeout=300,
+                       cwd=str(tmp_path))
+    assert r.returncode == 3, r.stderr[-2000:]
+    assert "WORLD_SIZE=1" in r.stderr and not _json_lines(r.stdout)

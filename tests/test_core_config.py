@@ -125,3 +125,57 @@ def test_topology_counts(monkeypatch):
     assert topology.visible_gpu_count() == 2
     assert topology.xgmi_links_per_gpu(8) == 7
     assert topology.get_region() == os.environ.get("CLOUD_AMD_REGION", "local")
+
+
+def _fake_kfd(root, n_gpus=8, hbm=288 * 10**9, mesh=True):
+    """A KFD topology tree shaped like an 8x MI355X node: 2 CPU agents, then GPUs."""
+    def write(path, props):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            f.write("".join("%s %s\n" % kv for kv in props.items()))
+
+    for c in range(2):
+        write(os.path.join(root, str(c), "properties"), {"cpu_cores_count": 64, "simd_count": 0})
+    for g in range(n_gpus):
+        nid = 2 + g
+        base = os.path.join(root, str(nid))
+        write(os.path.join(base, "properties"), {"cpu_cores_count": 0, "simd_count": 1024, "simd_per_cu": 4,
+                                                 "gfx_target_version": 90500, "unique_id": 1000 + g})
+        write(os.path.join(base, "mem_banks", "0", "properties"), {"heap_type": 1, "size_in_bytes": hbm})
+        links = [(2, g // 4)]  # PCIe link to its CPU agent
+        if mesh:
+            links += [(11, 2 + o) for o in range(n_gpus) if o != g]
+        for i, (t, to) in enumerate(links):
+            write(os.path.join(base, "io_links", str(i), "properties"),
+                  {"type": t, "node_from": nid, "node_to": to, "weight": 15, "max_bandwidth": 153000})
+
+
+def test_topology_kfd_probe(tmp_path, monkeypatch):
+    for v in ("CLOUD_AMD_NUM_GPUS", "CLOUD_AMD_HBM_GB", "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+              "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    root = str(tmp_path / "nodes")
+    _fake_kfd(root)
+    gpus = topology.kfd_gpu_nodes(root)
+    assert [g["node"] for g in gpus] == list(range(2, 10))
+    assert gpus[0]["cu_count"] == 256 and gpus[0]["gfx_target_version"] == 90500
+    assert topology.visible_gpu_count(root) == 8
+    assert abs(topology.hbm_gb_per_gpu(root) - 288.0) < 1e-6
+    assert topology.xgmi_links_per_gpu(8, root) == 7
+    assert topology.xgmi_links_per_gpu(4, root) == 3
+    info = topology.describe_node(root)
+    assert info["source"] == "kfd" and info["arch"] == "gfx950" and len(info["xgmi_matrix"]) == 8
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1,5,6")
+    assert topology.visible_gpu_count(root) == 3
+    assert [g["node"] for g in topology.visible_gpus(root)] == [3, 7, 8]
+    assert topology.xgmi_links_per_gpu(3, root) == 2
+
+
+def test_topology_kfd_no_mesh_falls_back(tmp_path, monkeypatch):
+    for v in ("CLOUD_AMD_NUM_GPUS", "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    root = str(tmp_path / "nodes")
+    _fake_kfd(root, n_gpus=1, mesh=False)
+    assert topology.visible_gpu_count(root) == 1
+    assert topology.xgmi_links_per_gpu(1, root) == 0
+    assert topology.visible_gpu_count(str(tmp_path / "missing")) == 0

@@ -8,7 +8,7 @@ import sys
 
 import pytest
 
-from cloud_amd.core import launcher, machine_config as mc, preprocess, run as run_mod, stage
+from cloud_amd.core import launcher, machine_config as mc, preprocess, run as run_mod, stage, validate
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CPU = mc.COMMON_MACHINE_CONFIGS["CPU"]
@@ -168,3 +168,45 @@ def test_debug_sync_mode_serialises_rank_launches(tmp_path, monkeypatch):
     assert env == {"CLOUD_AMD_DEBUG_SYNC": "1", "HIP_LAUNCH_BLOCKING": "1", "AMD_SERIALIZE_KERNEL": "3"}
     hdr = open(os.path.join(HERE, "..", "csrc", "include", "ca_common.h")).read()
     assert 'getenv("CLOUD_AMD_DEBUG_SYNC")' in hdr and "hipDeviceSynchronize" in hdr
+
+
+def test_launcher_never_touches_hip_and_sets_rccl_env(tmp_path, monkeypatch):
+    """A 2-GPU job is sized from KFD sysfs (a fake tree here) with every torch.cuda entry
+    point booby-trapped in the launcher process; both ranks get the xGMI RCCL defaults."""
+    import torch
+
+    from test_core_config import _fake_kfd
+
+    def boom(*a, **k):
+        raise AssertionError("launcher initialised HIP")
+
+    for name in ("device_count", "is_available", "init", "_lazy_init", "current_device", "set_device"):
+        monkeypatch.setattr(torch.cuda, name, boom)
+    kfd = tmp_path / "kfd"
+    _fake_kfd(str(kfd), n_gpus=2)
+    for v in ("CLOUD_AMD_NUM_GPUS", "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+              "NCCL_MIN_NCHANNELS", "HSA_NO_SCRATCH_RECLAIM", "CLOUD_AMD_RCCL_CHANNELS", "CLOUD_AMD_RCCL_ENV"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("CLOUD_AMD_KFD_ROOT", str(kfd))
+    app = tmp_path / "app"
+    app.mkdir()
+    (app / "probe.py").write_text(
+        "import json, os\n"
+        "keys = ['RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'NCCL_MIN_NCHANNELS', 'HSA_NO_SCRATCH_RECLAIM']\n"
+        "json.dump({k: os.environ.get(k) for k in keys},\n"
+        "          open(os.path.join(os.environ['CLOUD_AMD_JOB_DIR'], 'env%s.json' % os.environ['RANK']), 'w'))\n")
+    job_dir = tmp_path / "job"
+    (job_dir / "logs").mkdir(parents=True)
+    validate.validate_node_capacity(mc.COMMON_MACHINE_CONFIGS["MI355X_2X"], None, 0)
+    with pytest.raises(ValueError, match="needs 4 GPUs"):
+        validate.validate_node_capacity(mc.COMMON_MACHINE_CONFIGS["MI355X_4X"], None, 0)
+    job = launcher.launch("kfd", str(job_dir), str(app / "probe.py"),
+                          mc.COMMON_MACHINE_CONFIGS["MI355X_2X"], 0, None)
+    assert job.wait(60) == 0
+    for r in range(2):
+        env = json.load(open(job_dir / ("env%d.json" % r)))
+        assert env == {"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": "2", "NCCL_MIN_NCHANNELS": "1",
+                       "HSA_NO_SCRATCH_RECLAIM": "1"}
+    meta = json.load(open(job_dir / "job.json"))
+    assert meta["node"]["source"] == "kfd" and meta["node"]["gpus"] == 2
+    assert meta["comm_env"]["NCCL_MIN_NCHANNELS"] == "1"
