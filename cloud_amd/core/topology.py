@@ -135,14 +135,15 @@ def visible_gpu_count(root=None) -> int:
 
 
 def hbm_gb_per_gpu(root=None) -> float:
-    """HBM per GPU in GB: measured from KFD when present, else the MI355X constant."""
+    """HBM per GPU in GiB (the "288 GB" of the MI355X datasheet is 288 GiB): measured
+    from the KFD memory banks when present, else the MI355X constant."""
     env = os.environ.get("CLOUD_AMD_HBM_GB")
     if env is not None:
         return float(env)
     gpus = visible_gpus(root)
     sizes = [g["hbm_bytes"] for g in gpus if g["hbm_bytes"] > 0]
     if sizes:
-        return min(sizes) / 1e9
+        return min(sizes) / 2**30
     return float(HBM_GB_PER_GPU)
 
 

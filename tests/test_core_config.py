@@ -127,7 +127,7 @@ def test_topology_counts(monkeypatch):
     assert topology.get_region() == os.environ.get("CLOUD_AMD_REGION", "local")
 
 
-def _fake_kfd(root, n_gpus=8, hbm=288 * 10**9, mesh=True):
+def _fake_kfd(root, n_gpus=8, hbm=288 * 2**30, mesh=True):
     """A KFD topology tree shaped like an 8x MI355X node: 2 CPU agents, then GPUs."""
     def write(path, props):
         os.makedirs(os.path.dirname(path), exist_ok=True)
@@ -179,3 +179,17 @@ def test_topology_kfd_no_mesh_falls_back(tmp_path, monkeypatch):
     assert topology.visible_gpu_count(root) == 1
     assert topology.xgmi_links_per_gpu(1, root) == 0
     assert topology.visible_gpu_count(str(tmp_path / "missing")) == 0
+
+
+def test_topology_real_mi355x_box_dump(monkeypatch):
+    """KFD tree dumped on a gpurun box (an 8x MI355X node of which one GPU is exposed to
+    the job: the other GPU nodes' properties are unreadable). Links of type 11 = xGMI."""
+    for v in ("CLOUD_AMD_NUM_GPUS", "CLOUD_AMD_HBM_GB", "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+              "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    root = os.path.join(os.path.dirname(__file__), "data", "kfd_mi355x_1of8")
+    gpus = topology.kfd_gpu_nodes(root)
+    assert len(gpus) == 1 and gpus[0]["gfx_target_version"] == 90500 and gpus[0]["cu_count"] == 256
+    assert abs(topology.hbm_gb_per_gpu(root) - 288.0) < 0.5
+    assert sum(1 for l in gpus[0]["links"] if l["type"] == topology.IOLINK_XGMI) == 7
+    assert topology.xgmi_links_per_gpu(1, root) == 0
