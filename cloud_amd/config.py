@@ -60,6 +60,17 @@ _VARS = [
     Var("CLOUD_AMD_SHARED_GPU", bool, False, "rehearsal: every local rank uses cuda:0 (pair with "
         "CLOUD_AMD_DIST_BACKEND=gloo on a one-GPU box)", "distributed"),
     Var("CLOUD_AMD_BUCKET_MB", float, 16.0, "gradient bucket size (MB) of the DP engine", "distributed"),
+    Var("CLOUD_AMD_GRAD_REDUCE_DTYPE", str, "bf16", "wire dtype of the gradient all-reduce of bf16 layers: "
+        "'bf16' (native, half the bytes) or 'fp32' (reduce an fp32 copy)", "distributed"),
+    Var("CLOUD_AMD_RCCL_ENV", bool, True, "launcher sets the xGMI RCCL defaults (NCCL_MIN_NCHANNELS, "
+        "HSA_NO_SCRATCH_RECLAIM, NCCL_DEBUG) for multi-GPU jobs", "distributed"),
+    Var("CLOUD_AMD_RCCL_CHANNELS", int, 0, "NCCL_MIN_NCHANNELS the launcher sets (0 = one per xGMI link)",
+        "distributed"),
+    Var("CLOUD_AMD_KFD_ROOT", str, "/sys/class/kfd/kfd/topology/nodes", "KFD topology root read by the "
+        "node probe (tests point it at a fake tree)", "launcher"),
+    Var("CLOUD_AMD_BENCH_VIA_RUN", bool, True, "bench scripts launch their ranks through cloud_amd.run()",
+        "bench"),
+    Var("CLOUD_AMD_BENCH_ALLOW_CPU", bool, False, "let bench.py run ResNet-50 on CPU (debug only)", "bench"),
     Var("CLOUD_AMD_DDP_ORDER", str, "event", "bucket ordering: 'event' (comm stream waits on a compute event), "
         "'sync' (debug), 'backend'", "distributed"),
     Var("CLOUD_AMD_GRAD_CHECK_EVERY", int, 0, "cross-rank gradient fingerprint check every N steps (0 = off)",

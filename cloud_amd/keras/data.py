@@ -9,6 +9,7 @@ pytrees; batching stacks them.  A background thread implements ``prefetch``.
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
 
@@ -133,8 +134,14 @@ class Dataset:
         return Dataset(gen, None)
 
     def shuffle(self, buffer_size, seed=None, reshuffle_each_iteration=True):
+        """Buffered shuffle.  An unseeded shuffle inside a launched job draws its seed
+        from the job id, so every replica sees the same global order (the replicas of
+        a data-parallel job each iterate the pipeline and cut their slice of every
+        global batch: they must agree on what the global batches are)."""
         src = self
         state = {"epoch": 0}
+        if seed is None:
+            seed = _job_seed()
 
         def gen():
             rng = np.random.default_rng(None if seed is None else seed + (state["epoch"] if reshuffle_each_iteration
@@ -263,6 +270,16 @@ class Dataset:
 
     def as_numpy_iterator(self):
         return iter(self)
+
+
+def _job_seed():
+    """A seed shared by all ranks of a launched job (None outside one)."""
+    job = os.environ.get("CLOUD_AMD_JOB_ID") or os.environ.get("TORCHELASTIC_RUN_ID")
+    if not job:
+        return None
+    import zlib
+
+    return zlib.crc32(job.encode()) & 0x7FFFFFFF
 
 
 class Options:

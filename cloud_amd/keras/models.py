@@ -65,6 +65,14 @@ def _slice(x, idx):
     return x[idx]
 
 
+def _replica_range(n, world, rank):
+    """[lo, hi) of replica ``rank``'s slice of an ``n``-row global batch: contiguous
+    ceil(n/world) chunks (the last replicas may get fewer rows, or none)."""
+    per = -(-n // world)
+    lo = min(rank * per, n)
+    return lo, min(lo + per, n)
+
+
 def _length(x):
     return len(_first(x))
 
@@ -257,7 +265,13 @@ class Model(Layer):
             if sm is not None:
                 sm._emit_logits = False
 
-    def train_step(self, xb, yb, sample_weight=None):
+    def train_step(self, xb, yb, sample_weight=None, loss_weight=1.0, n_real=None):
+        """One replica step.  ``loss_weight`` rescales this replica's mean loss so that the
+        cross-replica gradient SUM (times the optimizer's 1/world) is the gradient of the
+        mean over the GLOBAL batch, whatever the per-replica slice sizes were;
+        ``n_real=0`` marks a stand-in batch of a replica whose slice of the global batch
+        was empty: it still runs forward/backward (zero-weighted) so every replica
+        issues the same collectives, but it does not count in the metrics."""
         dev = self._strategy.device
         x = _to_torch(xb, dev, self._input_dtype())
         y = _to_torch(yb, dev) if yb is not None else None
@@ -272,7 +286,8 @@ class Model(Layer):
                 pred = self(x, training=True)
                 loss = self.loss(y, pred, sample_weight)
             reg = self._regularization()
-            total = loss + reg if reg is not None else loss
+            scaled = loss * loss_weight if loss_weight != 1.0 else loss
+            total = scaled + reg if reg is not None else scaled
         with trace.range("backward"):
             total.backward()
         if self._reducer is not None:
@@ -280,11 +295,12 @@ class Model(Layer):
                 self._reducer.finish()
         with trace.range("optimizer"):
             impl.step()
-        n = _length(x)
-        self._loss_tracker.update_state(loss.detach().float().reshape(1), sample_weight=[n])
-        with torch.no_grad():
-            for m in self.compiled_metrics:
-                m.update_state(y, pred.detach())
+        n = _length(x) if n_real is None else n_real
+        if n:
+            self._loss_tracker.update_state(loss.detach().float().reshape(1), sample_weight=[n])
+            with torch.no_grad():
+                for m in self.compiled_metrics:
+                    m.update_state(y, pred.detach())
         return loss
 
     def _regularization(self):
@@ -312,27 +328,44 @@ class Model(Layer):
             m.reset_state()
 
     def _batches(self, x, y, batch_size, shuffle, epoch, seed=1234):
-        """Yield this replica's slice of every global batch."""
+        """Yield ``(x, y, n_local, n_global)``: this replica's slice of every global batch.
+
+        Every replica walks the SAME sequence of global batches (arrays: one shared
+        permutation; datasets: every replica iterates the dataset, whose unseeded
+        shuffles are job-seeded, and cuts its slice) and yields once per global batch,
+        so all replicas run the same number of steps and issue the same collectives
+        -- the lock-step that TF's MirroredStrategy/MWMS input pipelines guarantee.
+        A replica whose slice is empty (global batch smaller than the replica count)
+        gets ``n_local == 0`` and a one-row stand-in it trains on with zero weight."""
         s = self._strategy
         world, rank = s.num_replicas_in_sync, s.rank
         if isinstance(x, Dataset):
-            ds = x.shard(world, rank) if world > 1 else x
-            for el in ds:
+            for el in x:
                 if isinstance(el, (tuple, list)) and len(el) >= 2:
-                    yield el[0], el[1]
+                    ex, ey = el[0], el[1]
                 else:
-                    yield el, None
+                    ex, ey = el, None
+                n = _length(ex)
+                if world == 1:
+                    yield ex, ey, n, n
+                    continue
+                lo, hi = _replica_range(n, world, rank)
+                if hi > lo:
+                    yield _slice(ex, slice(lo, hi)), _slice(ey, slice(lo, hi)), hi - lo, n
+                else:
+                    yield _slice(ex, slice(0, 1)), _slice(ey, slice(0, 1)), 0, n
             return
         n = _length(x)
         bs = batch_size or 32
         idx = np.random.default_rng(seed + epoch).permutation(n) if shuffle else np.arange(n)
-        per = -(-bs // world)
         for start in range(0, n, bs):
             gb = idx[start:start + bs]
-            mine = np.sort(gb[rank * per:(rank + 1) * per]) if world > 1 else gb
-            if len(mine) == 0:
+            if world == 1:
+                yield _slice(x, gb), (_slice(y, gb) if y is not None else None), len(gb), len(gb)
                 continue
-            yield _slice(x, mine), (_slice(y, mine) if y is not None else None)
+            lo, hi = _replica_range(len(gb), world, rank)
+            mine, real = (np.sort(gb[lo:hi]), hi - lo) if hi > lo else (gb[:1], 0)
+            yield _slice(x, mine), (_slice(y, mine) if y is not None else None), real, len(gb)
 
     def fit(self, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callbacks=None, validation_split=0.0,
             validation_data=None, shuffle=True, class_weight=None, sample_weight=None, initial_epoch=0,
@@ -371,12 +404,14 @@ class Model(Layer):
                 if steps_per_epoch is not None and step >= steps_per_epoch:
                     break
                 try:
-                    xb, yb = next(it)
+                    xb, yb, n_local, n_global = next(it)
                 except StopIteration:
                     break
                 callbacks_.on_train_batch_begin(step, {})
                 faults.maybe_inject(global_step, rank=s.rank)
-                loss = self.train_step(xb, yb)
+                world = s.num_replicas_in_sync
+                w = (n_local * world / n_global) if world > 1 else 1.0
+                loss = self.train_step(xb, yb, loss_weight=w, n_real=n_local)
                 callbacks_.on_train_batch_end(step, {"loss": float(loss.detach())} if step % 50 == 0 else {})
                 step += 1
                 global_step += 1
@@ -412,9 +447,11 @@ class Model(Layer):
         self._reset_metrics()
         self.eval()
         with torch.no_grad():
-            for i, (xb, yb) in enumerate(self._batches(x, y, batch_size, False, 0)):
+            for i, (xb, yb, n_local, _) in enumerate(self._batches(x, y, batch_size, False, 0)):
                 if steps is not None and i >= steps:
                     break
+                if n_local == 0:
+                    continue  # stand-in row of an empty replica slice: nothing to score
                 xt = _to_torch(xb, dev, self._input_dtype())
                 yt = _to_torch(yb, dev) if yb is not None else None
                 pred = self(xt, training=False)
