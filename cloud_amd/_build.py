@@ -63,7 +63,7 @@ def _hipcc():
 def _digest(src: Path, flags) -> str:
     h = hashlib.sha1()
     h.update(src.read_bytes())
-    for inc in sorted((CSRC / "include").glob("*.h")):
+    for inc in sorted((CSRC / "include").glob("*.h")) + sorted(src.parent.glob("*.h")):
         h.update(inc.read_bytes())
     h.update(" ".join(flags).encode())
     return h.hexdigest()[:16]
@@ -141,6 +141,28 @@ def build_data(verbose=False) -> Path:
     obj = _compile(cxx, src, CXX_FLAGS + _py_includes(), verbose)
     out = PKG / f"_data{EXT_SUFFIX}"
     _link(cxx, [obj], out, ["-lpthread"], verbose)
+    return out
+
+
+def build_loader_test(sanitize=None, verbose=False) -> Path:
+    """Standalone multi-threaded test of the input-pipeline core (csrc/data/loader_core.h,
+    no Python).  ``sanitize``: None, "address" (ASan+UBSan) or "thread" (TSan)."""
+    cxx = shutil.which("g++") or "c++"
+    src = CSRC / "data" / "loader_test.cpp"
+    tag = {None: "", "address": "_asan", "thread": "_tsan"}[sanitize]
+    out = BUILD / f"loader_test{tag}"
+    BUILD.mkdir(parents=True, exist_ok=True)
+    flags = ["-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", f"-I{CSRC / 'data'}"]
+    if sanitize == "address":
+        flags += ["-fsanitize=address,undefined"]
+    elif sanitize == "thread":
+        flags += ["-fsanitize=thread"]
+    cmd = [cxx, *flags, str(src), "-o", str(out), "-lpthread"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {src}\n{r.stdout}\n{r.stderr}")
     return out
 
 

@@ -224,7 +224,13 @@ def test_linear_autograd_writes_arena_grad():
     ref_dw = dy.float().reshape(-1, 128).t() @ x.detach().float().reshape(-1, 64)
     torch.testing.assert_close(conv.weight.grad.float().reshape(128, 64), ref_dw, atol=0.5, rtol=2e-2)
     torch.testing.assert_close(x.grad.float().reshape(-1, 64), dy.float().reshape(-1, 128) @ w, atol=0.2, rtol=2e-2)
-    assert conv.weight.grad.data_ptr() == opt.arenas[0].grad.data_ptr() + 0 or True
+    # the weight gradient lives inside the optimizer's flat arena, at the slot it was given
+    arena = next(a for a in opt.arenas if any(s.param is conv.weight for s in a.slots))
+    slot = next(s for s in arena.slots if s.param is conv.weight)
+    g = conv.weight.grad
+    assert g.untyped_storage().data_ptr() == arena.grad.untyped_storage().data_ptr()
+    assert g.data_ptr() == arena.grad.data_ptr() + slot.offset * arena.grad.element_size()
+    assert slot.offset + g.numel() <= arena.n
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout,k,s,p", [
