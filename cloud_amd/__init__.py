@@ -32,3 +32,27 @@ def __getattr__(name):
 
 
 __all__ = ["__version__", *_LAZY]
+
+
+def _autostart_monitoring():
+    """The analogue of the reference's ``REGISTER_TF_METRICS_EXPORTER``
+    (``src/cpp/monitoring/stackdriver_exporter.cc:128``): in a launched rank with
+    ``CLOUD_AMD_MONITORING_EXPORTER_ENABLED`` set, importing the package starts the
+    native periodic exporter -- no user code needed."""
+    import os
+
+    if os.environ.get("CLOUD_AMD_MONITORING_EXPORTER_ENABLED", "").lower() not in ("1", "true", "yes", "on"):
+        return
+    if not (os.environ.get("CLOUD_AMD_RUNNING_REMOTELY") or os.environ.get("TORCHELASTIC_RUN_ID")):
+        return  # only ranks export; the launching process does not
+    try:
+        from . import monitoring
+
+        monitoring.autostart()
+    except Exception as e:  # noqa: BLE001 - metrics must never break a job
+        import sys
+
+        print("[cloud_amd] monitoring exporter not started: %s" % e, file=sys.stderr)
+
+
+_autostart_monitoring()

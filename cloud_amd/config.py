@@ -81,6 +81,8 @@ _VARS = [
     Var("CLOUD_AMD_MONITORING_PROJECT_ID", str, "", "project id stamped on exported series", "observability"),
     Var("CLOUD_AMD_MONITORING_METRICS_WHITELIST", str, "", "comma-separated metric allow-list", "observability"),
     Var("CLOUD_AMD_MONITORING_INTERVAL_S", float, 10.0, "export interval", "observability"),
+    Var("CLOUD_AMD_MONITORING_SINK", str, "jsonl", "auto-started exporter sink: jsonl | prometheus",
+        "observability"),
     Var("CLOUD_AMD_MONITORING_DIR", str, None, "exporter output directory (default: the job dir)", "observability"),
     # fault injection / tuner / data
     Var("CLOUD_AMD_FAULT", str, "", "fault injection 'rank:step:kind' (exit|raise|hang)", "testing"),

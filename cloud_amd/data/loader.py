@@ -22,9 +22,12 @@ The loader does not decode images: datasets are stored as decoded uint8 arrays
 from __future__ import annotations
 
 import os
+import time
 
 import numpy as np
 import torch
+
+from .. import monitoring
 
 _DTYPES = {"u1": torch.uint8, "i1": torch.int8, "i2": torch.int16, "i4": torch.int32, "i8": torch.int64,
            "f2": torch.float16, "f4": torch.float32, "f8": torch.float64, "b1": torch.bool}
@@ -93,8 +96,12 @@ class NpyBatchLoader:
         for s in list(self._held):  # a new epoch recycles every slot
             self.release(s)
         n = self._L.start_epoch(int(epoch))
+        mon = monitoring.enabled()
         for _ in range(n):
+            t0 = time.perf_counter()
             slot, count = self._L.next()
+            if mon:
+                monitoring.observe(monitoring.GETNEXT, (time.perf_counter() - t0) * 1e6, source="native_loader")
             if slot < 0:
                 return
             self._held.add(slot)

@@ -26,6 +26,7 @@ import time
 import numpy as np
 import torch
 
+from .. import monitoring
 from ..parallel import strategy as strat
 from ..utils import trace
 from . import callbacks as cbks
@@ -400,18 +401,27 @@ class Model(Layer):
             it = persistent if persistent is not None else self._batches(x, y, batch_size, shuffle, epoch)
             step = 0
             t0 = time.time()
+            mon = monitoring.enabled()
+            t_prev = time.perf_counter()
             while True:
                 if steps_per_epoch is not None and step >= steps_per_epoch:
                     break
+                t_get = time.perf_counter()
                 try:
                     xb, yb, n_local, n_global = next(it)
                 except StopIteration:
                     break
+                if mon:
+                    monitoring.observe(monitoring.GETNEXT, (time.perf_counter() - t_get) * 1e6)
                 callbacks_.on_train_batch_begin(step, {})
                 faults.maybe_inject(global_step, rank=s.rank)
                 world = s.num_replicas_in_sync
                 w = (n_local * world / n_global) if world > 1 else 1.0
                 loss = self.train_step(xb, yb, loss_weight=w, n_real=n_local)
+                if mon:  # host-side step period (the device queue evens it out over steps)
+                    now = time.perf_counter()
+                    monitoring.observe(monitoring.STEP_TIME, (now - t_prev) * 1e3)
+                    t_prev = now
                 callbacks_.on_train_batch_end(step, {"loss": float(loss.detach())} if step % 50 == 0 else {})
                 step += 1
                 global_step += 1
@@ -419,10 +429,6 @@ class Model(Layer):
                     break
             logs = self._logs()
             logs["epoch_time_s"] = time.time() - t0
-            from .. import monitoring
-
-            if step:
-                monitoring.observe(monitoring.STEP_TIME, 1000.0 * logs["epoch_time_s"] / step)
             if validation_data is not None and (epoch + 1) % validation_freq == 0:
                 vx, vy = (validation_data, None) if isinstance(validation_data, Dataset) else validation_data[:2]
                 vlogs = self.evaluate(vx, vy, batch_size=validation_batch_size or batch_size, verbose=0,

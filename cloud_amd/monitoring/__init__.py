@@ -18,6 +18,7 @@ STEP_TIME = "/cloud_amd/train/step_time_ms"
 THROUGHPUT = "/cloud_amd/train/images_per_sec"
 FIRST_STEP = "/cloud_amd/train/first_step_latency_s"
 ALLREDUCE = "/cloud_amd/comm/allreduce_ms"
+EXPOSED_COMM = "/cloud_amd/comm/exposed_ms"
 GETNEXT = "/cloud_amd/data/getnext_duration_us"
 TRIALS = "/cloud_amd/tuner/trials"
 JOBS = "/cloud_amd/launcher/jobs"
@@ -42,7 +43,12 @@ def available():
 
 
 def _labels(labels):
-    return {str(k): str(v) for k, v in (labels or {}).items()}
+    """Caller labels plus this process's ``rank`` in a multi-rank job (every rank
+    exports into the same job directory)."""
+    out = {str(k): str(v) for k, v in (labels or {}).items()}
+    if "rank" not in out and os.environ.get("WORLD_SIZE", "1") not in ("", "1") and os.environ.get("RANK"):
+        out["rank"] = os.environ["RANK"]
+    return out
 
 
 def inc(name, delta=1, **labels):
@@ -70,6 +76,29 @@ def start_exporter(directory=None, sink="jsonl", interval_s=0.0, force=False):
         return False
     directory = directory or os.environ.get("CLOUD_AMD_MONITORING_DIR") or os.environ.get("CLOUD_AMD_JOB_DIR") or "."
     return native().start_exporter(os.path.abspath(directory), sink, float(interval_s), bool(force))
+
+
+_AUTO = {"started": False}
+
+
+def enabled():
+    return os.environ.get("CLOUD_AMD_MONITORING_EXPORTER_ENABLED", "").lower() in ("1", "true", "yes", "on")
+
+
+def autostart():
+    """Start the exporter once per process if the env switch is on (called from the
+    package import); a final export runs at interpreter exit so short jobs and the
+    last interval are not lost."""
+    if _AUTO["started"] or not enabled() or not available():
+        return False
+    sink = os.environ.get("CLOUD_AMD_MONITORING_SINK", "jsonl")
+    ok = start_exporter(sink=sink)
+    if ok:
+        import atexit
+
+        _AUTO["started"] = True
+        atexit.register(stop_exporter)
+    return ok
 
 
 def export_now():

@@ -88,7 +88,12 @@ class GradAllReducer:
             rd = {"fp32": torch.float32, "float32": torch.float32, "bf16": None, "native": None}[rd]
         self.reduce_dtype = rd
         # Per-step communication timing (bench / monitoring): see timing_start/timing_summary.
-        self.timing = False
+        # With the metrics exporter on, every step is timed and completed steps are drained
+        # into the ALLREDUCE / EXPOSED_COMM histograms by event query (never a host sync).
+        from .. import monitoring as _mon
+
+        self._mon = _mon if (_mon.enabled() and self.world > 1) else None
+        self.timing = self._mon is not None
         self._timing_log = []
         self.check_every = int(os.environ.get("CLOUD_AMD_GRAD_CHECK_EVERY", "0"))
         self._steps = 0
@@ -223,6 +228,8 @@ class GradAllReducer:
             else:
                 dt = (time.perf_counter() - t_bwd) * 1e3
                 self._timing_log.append((dt, dt, []))
+            if self._mon is not None:
+                self._drain_to_monitoring()
         self.reset()
         self._steps += 1
         if self.check_every and self._steps % self.check_every == 0:
@@ -275,6 +282,23 @@ class GradAllReducer:
             b.ev = None
         self._next = 0
 
+    def _drain_to_monitoring(self):
+        """Observe the per-step comm times of every finished step (event.query(): no sync)."""
+        keep = []
+        for entry in self._timing_log:
+            t_bwd, t_join, evs = entry
+            if isinstance(t_bwd, float):
+                self._mon.observe(self._mon.ALLREDUCE, t_join)
+                self._mon.observe(self._mon.EXPOSED_COMM, t_bwd)
+                continue
+            if not t_join.query():
+                keep.append(entry)
+                continue
+            self._mon.observe(self._mon.EXPOSED_COMM, t_bwd.elapsed_time(t_join))
+            if evs:
+                self._mon.observe(self._mon.ALLREDUCE, sum(a.elapsed_time(b) for a, b in evs))
+        self._timing_log = keep[-64:]
+
     def timing_start(self):
         """Record communication timing for every following step (events only; no sync)."""
         self.timing = True
@@ -284,7 +308,7 @@ class GradAllReducer:
         """Mean per-step ``allreduce_ms`` (sum of bucket collective times on the comm
         stream) and ``exposed_comm_ms`` (end of backward on the compute stream -> all
         buckets joined).  Call after a device synchronize."""
-        self.timing = False
+        self.timing = self._mon is not None
         if self.world <= 1 or not self._timing_log:
             return {"allreduce_ms": 0.0, "exposed_comm_ms": 0.0, "steps": len(self._timing_log)}
         ar, ex = [], []

@@ -25,6 +25,7 @@ import os
 import time
 import traceback
 
+from .. import monitoring
 from . import hyperparameters as hp_module
 from . import optimizer_client, utils
 from .trial import Objective, Trial, TrialStatus
@@ -119,6 +120,7 @@ class CloudOracle(Oracle):
                       trial_id=trial_id, status=TrialStatus.RUNNING)
         log.info("Hyperparameters requested by tuner (%s): %s ", tuner_id, trial.hyperparameters.values)
         self._start_time = time.time()
+        monitoring.inc(monitoring.TRIALS, 1, event="created", tuner=str(tuner_id))
         self.trials[trial_id] = trial
         self.ongoing_trials[tuner_id] = trial
         self._save_trial(trial)
@@ -145,6 +147,7 @@ class CloudOracle(Oracle):
         log.info("UpdateTrial: polls the stop decision.")
         if self.service.should_trial_stop(trial_id):
             trial.status = TrialStatus.STOPPED
+            monitoring.inc(monitoring.TRIALS, 1, event="early_stopped")
         return trial.status
 
     def end_trial(self, trial_id, status="COMPLETED"):
@@ -164,6 +167,7 @@ class CloudOracle(Oracle):
         else:
             raise ValueError('Unexpected status passed. Expected "COMPLETED" or "INVALID", found {}'.format(status))
         opt_trial = self.service.complete_trial(trial_id, infeasible, reason)
+        monitoring.inc(monitoring.TRIALS, 1, event=str(status).lower())
         if status == TrialStatus.COMPLETED and opt_trial.get("finalMeasurement"):
             fm = opt_trial["finalMeasurement"]
             trial.best_step = fm.get("stepCount", 1)

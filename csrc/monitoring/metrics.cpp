@@ -2,6 +2,9 @@
 // See metrics.h for the mapping onto reference src/cpp/monitoring/*.
 #include "metrics.h"
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -156,6 +159,7 @@ const std::vector<std::string>& ExporterConfig::DefaultWhitelist() {
   static const std::vector<std::string> kList = {
       "/cloud_amd/train/step_time_ms",       "/cloud_amd/train/images_per_sec",
       "/cloud_amd/train/first_step_latency_s", "/cloud_amd/comm/allreduce_ms",
+      "/cloud_amd/comm/exposed_ms",
       "/cloud_amd/data/getnext_duration_us", "/cloud_amd/data/getnext_period_us",
       "/cloud_amd/data/bytes_fetched",       "/cloud_amd/kernel/time_us",
       "/cloud_amd/tuner/trials",             "/cloud_amd/launcher/jobs",
@@ -340,25 +344,41 @@ static void MakeDirs(const std::string& dir) {
 
 JsonlFileSink::JsonlFileSink(std::string dir) : dir_(std::move(dir)) { MakeDirs(dir_); }
 
+// Every rank of a job appends to the same file: one export is formatted into one
+// buffer and written with a single write(2) on an O_APPEND descriptor, so lines of
+// different processes never interleave.
+static Status AppendAll(const std::string& path, const std::string& text) {
+  const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_APPEND, 0644);
+  if (fd < 0) return Status::kError;
+  size_t off = 0;
+  while (off < text.size()) {
+    const ssize_t w = ::write(fd, text.data() + off, text.size() - off);
+    if (w <= 0) {
+      ::close(fd);
+      return Status::kError;
+    }
+    off += (size_t)w;
+  }
+  ::close(fd);
+  return Status::kOk;
+}
+
 Status JsonlFileSink::CreateTimeSeries(const CreateTimeSeriesRequest& req) {
   if (req.time_series.empty()) return Status::kCancelled;
   std::lock_guard<std::mutex> l(mu_);
-  std::ofstream f(dir_ + "/metrics.jsonl", std::ios::app);
-  if (!f) return Status::kError;
   const int64_t now = NowMillis();
+  std::ostringstream os;
   for (const auto& ts : req.time_series)
-    f << "{\"name\":\"" << req.name << "\",\"exportTimeMillis\":" << now << ",\"timeSeries\":" << TimeSeriesToJson(ts)
-      << "}\n";
-  return Status::kOk;
+    os << "{\"name\":\"" << req.name << "\",\"exportTimeMillis\":" << now << ",\"timeSeries\":" << TimeSeriesToJson(ts)
+       << "}\n";
+  return AppendAll(dir_ + "/metrics.jsonl", os.str());
 }
 
 Status JsonlFileSink::CreateMetricDescriptor(const std::string& project_name, const MetricDescriptor& d,
                                              const std::string& metric_type) {
   std::lock_guard<std::mutex> l(mu_);
-  std::ofstream f(dir_ + "/descriptors.jsonl", std::ios::app);
-  if (!f) return Status::kError;
-  f << "{\"name\":\"" << project_name << "\",\"metricDescriptor\":" << DescriptorToJson(d, metric_type) << "}\n";
-  return Status::kOk;
+  return AppendAll(dir_ + "/descriptors.jsonl",
+                   "{\"name\":\"" + project_name + "\",\"metricDescriptor\":" + DescriptorToJson(d, metric_type) + "}\n");
 }
 
 PrometheusTextSink::PrometheusTextSink(std::string path) : path_(std::move(path)) {}

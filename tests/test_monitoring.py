@@ -60,3 +60,52 @@ def test_prometheus_sink(tmp_path):
 def test_exporter_disabled_by_default(tmp_path, monkeypatch):
     monkeypatch.delenv("CLOUD_AMD_MONITORING_EXPORTER_ENABLED", raising=False)
     assert monitoring.start_exporter(str(tmp_path)) is False
+
+
+def test_exporter_autostarts_in_a_two_rank_run_job(tmp_path):
+    """CLOUD_AMD_MONITORING_EXPORTER_ENABLED=1 on a run() job: every rank starts the
+    native exporter by importing the package (the REGISTER_TF_METRICS_EXPORTER analogue)
+    and the job dir's metrics.jsonl gets step-time, all-reduce and tuner-trial series."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    app = tmp_path / "app"
+    app.mkdir()
+    (app / "train.py").write_text(
+        "import os, sys\n"
+        "import numpy as np\n"
+        "import cloud_amd as tfc\n"
+        "from cloud_amd import keras\n"
+        "cpu = tfc.COMMON_MACHINE_CONFIGS['CPU']\n"
+        "tfc.run(chief_config=cpu, worker_config=cpu, worker_count=1, stream_logs=True)\n"
+        "x = np.random.default_rng(0).standard_normal((256, 8)).astype('float32')\n"
+        "y = (x[:, 0] > 0).astype('int64')\n"
+        "m = keras.Sequential([keras.layers.Dense(16, activation='relu'), keras.layers.Dense(2, activation='softmax')])\n"
+        "m.compile(optimizer='sgd', loss='sparse_categorical_crossentropy')\n"
+        "m.fit(x, y, batch_size=32, epochs=2, verbose=0)\n"
+        "from cloud_amd.tuner.tuner import CloudOracle\n"
+        "from cloud_amd.tuner import hyperparameters as hp\n"
+        "hps = hp.HyperParameters(); hps.Choice('units', [8, 16])\n"
+        "o = CloudOracle('p', 'r', objective='acc', hyperparameters=hps, max_trials=2,\n"
+        "                study_id='mon%s' % os.environ['RANK'], study_dir=os.path.join(os.environ['CLOUD_AMD_JOB_DIR'], 'st'))\n"
+        "t = o.create_trial('t0'); o.update_trial(t.trial_id, {'acc': 0.5}, step=1); o.end_trial(t.trial_id)\n"
+        "print('DONE', os.environ['RANK'], flush=True)\n")
+    env = dict(os.environ, CLOUD_AMD_NUM_GPUS="0", CLOUD_AMD_JOBS_DIR=str(tmp_path / "jobs"), PYTHONPATH=root,
+               CLOUD_AMD_MONITORING_EXPORTER_ENABLED="1", CLOUD_AMD_MONITORING_INTERVAL_S="0.5",
+               OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "CLOUD_AMD_RUNNING_REMOTELY", "TORCHELASTIC_RUN_ID", "CLOUD_AMD_MONITORING_DIR"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "train.py"], cwd=str(app), env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    job_dir = tmp_path / "jobs" / os.listdir(tmp_path / "jobs")[0]
+    lines = [json.loads(l) for l in open(job_dir / "metrics.jsonl")]  # every line is whole JSON
+    assert lines
+    text = open(job_dir / "metrics.jsonl").read()
+    for name in ("train/step_time_ms", "comm/allreduce_ms", "comm/exposed_ms", "tuner/trials",
+                 "data/getnext_duration_us"):
+        assert name in text, name
+    # both ranks exported, told apart by the rank label
+    assert '"rank":"0"' in text.replace(" ", "") and '"rank":"1"' in text.replace(" ", "")
