@@ -4,7 +4,8 @@ Replaces the Vizier-side parallelism of the reference (N processes with the
 same ``study_id`` and distinct ``tuner_id``, ``tuner_integration_test.py:82-116``)
 with an on-node scheduler: one worker per MI355X -- or several per GPU when
 the trials are small, packed by an HBM estimate into 288 GB (``trial_gb``) --
-each running ``tuner.search`` against the shared local study.  Workers are
+each running ``tuner.search`` against the shared local study; by default the
+per-GPU packing comes from the measured HBM footprint of the first trial.  Workers are
 independent processes (a crashed trial is INVALID, a crashed worker does not
 stop the others), results are read back from the study.
 
@@ -41,30 +42,104 @@ def _worker(target, tuner_id, device, env):
 
 
 class TrialScheduler:
-    def __init__(self, target, n_gpus=None, trial_gb=4.0, workers=None, max_workers=16, env=None):
+    """Run tuner workers on the node's GPUs.
+
+    Packing (how many workers share one GPU's 288 GB):
+
+    * ``workers=N``: exactly N workers, round-robin over the GPUs;
+    * ``trial_gb=G``: ``hbm.trials_per_gpu(G)`` workers per GPU;
+    * neither (default): **measured** -- a probe wave of one worker per GPU runs; the
+      first worker to finish a trial reports the allocator's peak reserved HBM
+      (``hbm.report_footprint``), and the scheduler then adds workers until each GPU
+      holds ``trials_per_gpu(peak * headroom)`` of them.
+
+    ``max_workers`` bounds the total (default: the CPUs this process may use, since
+    every worker also needs a core for its input pipeline and launches)."""
+
+    def __init__(self, target, n_gpus=None, trial_gb=None, workers=None, max_workers=None, env=None,
+                 hbm_gb=None, headroom=1.25, state_dir=None, probe_timeout_s=None):
         self.target = target
         if n_gpus is None:
-            from ..core.topology import visible_gpu_count
+            from ..core.topology import hbm_gb_per_gpu, visible_gpu_count
 
             n_gpus = visible_gpu_count()
+            hbm_gb = hbm_gb if hbm_gb is not None else (hbm_gb_per_gpu() if n_gpus else None)
         self.n_gpus = n_gpus
-        per = hbm.trials_per_gpu(trial_gb) if n_gpus else 1
-        self.workers = workers or max(1, min(max_workers, (n_gpus or 1) * per))
+        self.hbm_gb = hbm_gb
+        self.trial_gb = trial_gb
+        self.headroom = headroom
+        self.fixed_workers = workers
+        try:
+            cpus = len(os.sched_getaffinity(0))
+        except AttributeError:  # pragma: no cover
+            cpus = os.cpu_count() or 1
+        self.max_workers = max_workers or max(1, cpus)
         self.env = dict(env or {})
+        self.state_dir = state_dir
+        self.probe_timeout_s = probe_timeout_s
+        self.footprint_gb = None
+        self.per_gpu = None
+        if workers:
+            self.workers = workers
+        elif trial_gb:
+            self.per_gpu = hbm.trials_per_gpu(trial_gb, self.hbm_gb) if n_gpus else 1
+            self.workers = max(1, min(self.max_workers, (n_gpus or 1) * self.per_gpu))
+        else:
+            self.workers = None  # decided after the probe wave
+
+    def _slots(self):
+        return max(self.n_gpus, 1)
+
+    def _device(self, i):
+        return f"cuda:{i % self.n_gpus}" if self.n_gpus else "cpu"
 
     def devices(self):
-        if not self.n_gpus:
-            return ["cpu"] * self.workers
-        return [f"cuda:{i % self.n_gpus}" for i in range(self.workers)]
+        n = self.workers or self._slots()
+        return [self._device(i) for i in range(n)]
+
+    def _spawn(self, ctx, i, footprint_file=None):
+        env = dict(self.env)
+        if footprint_file:
+            env["CLOUD_AMD_FOOTPRINT_FILE"] = footprint_file
+        p = ctx.Process(target=_worker, args=(self.target, f"tuner{i}", self._device(i), env), daemon=False)
+        p.start()
+        return p
+
+    def packing_from_footprint(self, peak_gb):
+        """Workers per GPU for a measured per-trial peak (GiB)."""
+        hbm_gb = self.hbm_gb if self.hbm_gb is not None else hbm.HBM_GB
+        return hbm.trials_per_gpu(peak_gb * self.headroom, hbm_gb)
 
     def run(self, timeout=None):
+        import tempfile
+
         ctx = mp.get_context("spawn")
-        procs = []
         t0 = time.time()
-        for i, dev in enumerate(self.devices()):
-            p = ctx.Process(target=_worker, args=(self.target, f"tuner{i}", dev, self.env), daemon=False)
-            p.start()
-            procs.append(p)
+        procs = []
+        if self.workers is not None:
+            procs = [self._spawn(ctx, i) for i in range(self.workers)]
+        else:
+            state = self.state_dir or tempfile.mkdtemp(prefix="cloud_amd_sched_")
+            os.makedirs(state, exist_ok=True)
+            files = [os.path.join(state, f"footprint_tuner{i}.json") for i in range(self._slots())]
+            procs = [self._spawn(ctx, i, files[i]) for i in range(self._slots())]
+            limit = self.probe_timeout_s if self.probe_timeout_s is not None else timeout
+            while self.footprint_gb is None:
+                for f in files:
+                    if os.path.exists(f):
+                        with open(f) as fh:
+                            self.footprint_gb = float(json.load(fh)["peak_gb"])
+                        break
+                if self.footprint_gb is not None or all(not p.is_alive() for p in procs):
+                    break
+                if limit is not None and time.time() - t0 > limit:
+                    break
+                time.sleep(0.05)
+            self.per_gpu = self.packing_from_footprint(self.footprint_gb) if self.footprint_gb else 1
+            want = min(self.max_workers, self._slots() * self.per_gpu)
+            if any(p.is_alive() for p in procs):  # nothing left to pack into if the probe wave is done
+                procs += [self._spawn(ctx, i) for i in range(len(procs), want)]
+            self.workers = len(procs)
         for p in procs:
             p.join(None if timeout is None else max(0.0, timeout - (time.time() - t0)))
         codes = []
@@ -73,7 +148,8 @@ class TrialScheduler:
                 p.terminate()
                 p.join(5)
             codes.append(p.exitcode)
-        return {"workers": len(procs), "exit_codes": codes, "wall_s": time.time() - t0}
+        return {"workers": len(procs), "exit_codes": codes, "wall_s": time.time() - t0,
+                "trials_per_gpu": self.per_gpu, "footprint_gb": self.footprint_gb}
 
 
 def study_report(study_dir, study_id):

@@ -40,6 +40,85 @@ import numpy as np
 MAX_TRIALS = 1000
 
 
+def _curve(t, metric, use_elapsed):
+    """(x, y) points of a trial's measurements: x = stepCount or elapsed seconds."""
+    pts = []
+    for m in t.get("measurements", []):
+        vals = [m2["value"] for m2 in m.get("metrics", []) if m2.get("metric") == metric]
+        if not vals:
+            continue
+        x = float((m.get("elapsedTime") or {}).get("seconds", 0)) if use_elapsed else float(m.get("stepCount", 0))
+        pts.append((x, float(vals[0])))
+    return pts
+
+
+def _final_value(t, metric):
+    fm = t.get("finalMeasurement") or {}
+    vals = [m["value"] for m in fm.get("metrics", []) if m.get("metric") == metric]
+    return float(vals[0]) if vals else None
+
+
+def fit_decay_curve(xs, ys):
+    """Least-squares fit of a saturating learning curve ``y = a + b * x**(-c)``
+    (power-law decay toward an asymptote ``a``) over a small grid of exponents ``c``
+    (linear in a, b for fixed c).  Returns (predict(x), residual std)."""
+    x = np.maximum(np.asarray(xs, dtype=np.float64), 1e-9)
+    y = np.asarray(ys, dtype=np.float64)
+    best = None
+    for c in (0.25, 0.5, 0.75, 1.0, 1.5, 2.0):
+        A = np.stack([np.ones_like(x), x ** (-c)], 1)
+        coef, *_ = np.linalg.lstsq(A, y, rcond=None)
+        sse = float(((A @ coef - y) ** 2).sum())
+        if best is None or sse < best[0]:
+            best = (sse, c, coef)
+    sse, c, (a, b) = best
+    sigma = math.sqrt(sse / max(len(x) - 2, 1))
+    return (lambda q: float(a + b * max(float(q), 1e-9) ** (-c))), sigma
+
+
+def decay_curve_should_stop(trial, done, metric, maximize, use_elapsed=False, min_points=3, z=1.0):
+    """Stop if the trial's extrapolated final objective, moved ``z`` residual standard
+    deviations in the favourable direction, is still worse than the best completed
+    trial.  Needs ``min_points`` measurements at distinct x and >= 1 completed trial;
+    the horizon is the median final x of the completed trials (never below the
+    trial's own last x)."""
+    pts = _curve(trial, metric, use_elapsed)
+    finals = [(t, _final_value(t, metric)) for t in done]
+    finals = [(t, v) for t, v in finals if v is not None]
+    if len({x for x, _ in pts}) < min_points or not finals:
+        return False
+    horizons = [max((x for x, _ in _curve(t, metric, use_elapsed)), default=0.0) for t, _ in finals]
+    horizon = max(float(np.median(horizons)), max(x for x, _ in pts))
+    predict, sigma = fit_decay_curve([x for x, _ in pts], [y for _, y in pts])
+    pred = predict(horizon)
+    best = max(v for _, v in finals) if maximize else min(v for _, v in finals)
+    optimistic = pred + z * sigma if maximize else pred - z * sigma
+    return bool(optimistic < best if maximize else optimistic > best)
+
+
+def median_should_stop(trial, done, metric, maximize, use_elapsed=False, min_completed=3):
+    """Median rule: best value so far worse than the median of the completed trials'
+    best values up to the same x."""
+    mine_pts = _curve(trial, metric, use_elapsed)
+    if not mine_pts:
+        return False
+    upto = mine_pts[-1][0]
+
+    def best_upto(pts):
+        vals = [y for x, y in pts if x <= upto]
+        if not vals:
+            return None
+        return max(vals) if maximize else min(vals)
+
+    others = [best_upto(_curve(t, metric, use_elapsed)) for t in done]
+    others = [v for v in others if v is not None]
+    mine = best_upto(mine_pts)
+    if len(others) < min_completed or mine is None:
+        return False
+    med = float(np.median(others))
+    return bool(mine < med if maximize else mine > med)
+
+
 class StudyExists(Exception):
     pass
 
@@ -217,36 +296,35 @@ class StudyService:
 
     # -- early stopping ---------------------------------------------------------------
     def check_early_stopping_state(self, trial_name):
-        """Median rule: stop when the trial's best objective so far is worse than the
-        median of the completed trials' best objective up to the same step."""
+        """Automated early stopping (``checkEarlyStoppingState``) by the study's
+        ``automatedStoppingConfig``:
+
+        * ``decayCurveStoppingConfig`` (what reference ``tuner/utils.py:66-68`` emits):
+          extrapolate this trial's learning curve to the completed trials' typical
+          final step (or elapsed time with ``useElapsedTime``) and stop when even an
+          optimistic prediction is worse than the best completed trial;
+        * ``medianAutomatedStoppingConfig``: stop when the trial's best value so far is
+          worse than the median of the completed trials' best values up to the same
+          step (``useElapsedTime`` likewise switches the axis)."""
         sid = self.study_id_of(trial_name)
         data = self._read(sid)
         cfg = data["study"]["studyConfig"]
-        if not cfg.get("automatedStoppingConfig"):
+        asc = cfg.get("automatedStoppingConfig") or {}
+        if not asc:
             return {"shouldStop": False}
         metric = cfg["metrics"][0]["metric"]
         maximize = cfg["metrics"][0].get("goal") == "MAXIMIZE"
         trial = next((t for t in data["trials"] if t["name"] == trial_name), None)
         if trial is None or not trial.get("measurements"):
             return {"shouldStop": False}
-        step = trial["measurements"][-1].get("stepCount", 0)
-
-        def best_upto(t, s):
-            vals = [m2["value"] for m in t.get("measurements", []) if m.get("stepCount", 0) <= s
-                    for m2 in m.get("metrics", []) if m2.get("metric") == metric]
-            if not vals:
-                return None
-            return max(vals) if maximize else min(vals)
-
-        others = [best_upto(t, step) for t in data["trials"]
-                  if t["state"] == "COMPLETED" and not t.get("trialInfeasible") and t["name"] != trial_name]
-        others = [v for v in others if v is not None]
-        mine = best_upto(trial, step)
-        if len(others) < 3 or mine is None:
-            return {"shouldStop": False}
-        med = float(np.median(others))
-        worse = mine < med if maximize else mine > med
-        return {"shouldStop": bool(worse)}
+        done = [t for t in data["trials"]
+                if t["state"] == "COMPLETED" and not t.get("trialInfeasible") and t["name"] != trial_name]
+        if "decayCurveStoppingConfig" in asc:
+            rule = asc["decayCurveStoppingConfig"] or {}
+            return {"shouldStop": decay_curve_should_stop(trial, done, metric, maximize,
+                                                          bool(rule.get("useElapsedTime")))}
+        rule = asc.get("medianAutomatedStoppingConfig") or {}
+        return {"shouldStop": median_should_stop(trial, done, metric, maximize, bool(rule.get("useElapsedTime")))}
 
     # -- suggestion algorithms -------------------------------------------------------
     def _next_params(self, cfg, trials):

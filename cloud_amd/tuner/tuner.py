@@ -287,7 +287,9 @@ class Tuner:
 
     def search(self, *fit_args, **fit_kwargs):
         from ..utils import faults  # noqa: F401  (fault injection reaches trials through fit)
+        from ..utils import hbm
 
+        reported = False
         while True:
             trial = self.oracle.create_trial(self.tuner_id)
             if trial.status == TrialStatus.STOPPED:
@@ -300,6 +302,9 @@ class Tuner:
                 self.oracle.end_trial(trial.trial_id, TrialStatus.INVALID)
                 continue
             self.oracle.end_trial(trial.trial_id, TrialStatus.COMPLETED)
+            if not reported:  # the scheduler packs more workers per GPU from this measurement
+                hbm.report_footprint()
+                reported = True
 
     def get_best_hyperparameters(self, num_trials=1):
         return [t.hyperparameters for t in self.oracle.get_best_trials(num_trials)]

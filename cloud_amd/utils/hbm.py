@@ -26,11 +26,42 @@ def note_model(model):
     return _last["params"]
 
 
-def trials_per_gpu(trial_gb, hbm_gb=None, reserve=0.1, cap=8):
+def trials_per_gpu(trial_gb, hbm_gb=None, reserve=0.1, cap=64):
+    """How many trials of ``trial_gb`` fit in one GPU's HBM, keeping ``reserve`` of it
+    free.  ``cap`` is a sanity bound on processes per GPU, not a packing policy."""
     hbm_gb = HBM_GB if hbm_gb is None else hbm_gb
     if trial_gb <= 0:
         return cap
     return max(1, min(cap, int(hbm_gb * (1 - reserve) // trial_gb)))
+
+
+def trial_footprint_gb(device=None):
+    """Device memory a finished trial needed: the caching allocator's peak RESERVED
+    bytes (what another process on the same GPU cannot use), in GiB; None on CPU."""
+    try:
+        import torch
+
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            return torch.cuda.max_memory_reserved(device) / 2 ** 30
+    except Exception:  # pragma: no cover
+        pass
+    return None
+
+
+def report_footprint(gb=None, path=None):
+    """Write this worker's measured trial footprint for the scheduler
+    (``CLOUD_AMD_FOOTPRINT_FILE``); returns the value written (None: nothing to report)."""
+    path = path or os.environ.get("CLOUD_AMD_FOOTPRINT_FILE")
+    gb = trial_footprint_gb() if gb is None else gb
+    if not path or gb is None:
+        return None
+    import json
+
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump({"peak_gb": float(gb), "params": _last["params"]}, f)
+    os.replace(tmp, path)
+    return gb
 
 
 def peak_allocated_gb(device=None):

@@ -28,4 +28,8 @@ def run(tuner_id, device):
     tuner = CloudTuner(build_model, project_id="p", region="r", objective="acc", hyperparameters=hps,
                        max_trials=6, study_id=os.environ["STUDY_ID"], study_dir=os.environ["STUDY_DIR"],
                        directory=os.path.join(os.environ["STUDY_DIR"], "results", tuner_id))
+    if os.environ.get("FAKE_FOOTPRINT_GB"):  # CPU stand-in for the measured HBM peak of a GPU trial
+        from cloud_amd.utils import hbm
+
+        hbm.report_footprint(float(os.environ["FAKE_FOOTPRINT_GB"]))
     tuner.search(x, y, epochs=2, batch_size=32)

@@ -158,19 +158,56 @@ def test_service_concurrent_suggest_is_safe(tmp_path):
     assert len(got) == 20 and len(set(got)) == 20
 
 
-def test_early_stopping_median_rule(tmp_path):
+def _stop_study(tmp_path, rule):
     svc = StudyService(str(tmp_path))
     cfg = _cfg([{"parameter": "x", "type": "DOUBLE", "double_value_spec": {"min_value": 0.0, "max_value": 1.0}}])
-    cfg["automatedStoppingConfig"] = {"decayCurveStoppingConfig": {"useElapsedTime": True}}
+    cfg["automatedStoppingConfig"] = rule
     svc.create_study("projects/p/locations/r", "e", cfg)
-    name = "projects/p/locations/r/studies/e"
-    for i in range(3):
-        t = svc.suggest(name, "t")["trials"][0]["name"]
-        svc.add_measurement(t, {"stepCount": 1, "metrics": [{"metric": "accuracy", "value": 0.9}]})
+    return svc, "projects/p/locations/r/studies/e"
+
+
+def _trial_with_curve(svc, name, curve, complete):
+    # a fresh client per trial: suggest() hands a client its still-ACTIVE trial back
+    t = svc.suggest(name, "client%d" % len(svc.list_trials(name)))["trials"][0]["name"]
+    for step, acc in curve:
+        svc.add_measurement(t, {"stepCount": step, "elapsedTime": {"seconds": 10 * step},
+                                "metrics": [{"metric": "accuracy", "value": acc}]})
+    if complete:
         svc.complete_trial(t)
-    t = svc.suggest(name, "t")["trials"][0]["name"]
-    svc.add_measurement(t, {"stepCount": 1, "metrics": [{"metric": "accuracy", "value": 0.1}]})
+    return t
+
+
+def test_early_stopping_median_rule(tmp_path):
+    svc, name = _stop_study(tmp_path, {"medianAutomatedStoppingConfig": {"useElapsedTime": False}})
+    for _ in range(3):
+        _trial_with_curve(svc, name, [(1, 0.9)], True)
+    t = _trial_with_curve(svc, name, [(1, 0.1)], False)
     assert svc.check_early_stopping_state(t)["shouldStop"]
+    t2 = _trial_with_curve(svc, name, [(1, 0.95)], False)
+    assert not svc.check_early_stopping_state(t2)["shouldStop"]
+
+
+def test_decay_curve_rule_extrapolates_the_learning_curve(tmp_path):
+    """The oracle's default config (decayCurveStoppingConfig): a curve that is still
+    low but rising fast toward a good asymptote keeps running; one that has flattened
+    below the best completed trial stops -- even though at the last measured step both
+    are below every completed trial (where a median rule would stop both)."""
+    from cloud_amd.tuner.study_service import fit_decay_curve
+
+    pred, sigma = fit_decay_curve([1, 2, 4, 8], [0.9 - 0.8 / x ** 0.5 for x in (1, 2, 4, 8)])
+    assert abs(pred(100) - (0.9 - 0.08)) < 1e-6 and sigma < 1e-9
+    for use_elapsed in (False, True):
+        svc, name = _stop_study(tmp_path / str(use_elapsed), {"decayCurveStoppingConfig":
+                                                                  {"useElapsedTime": use_elapsed}})
+        steps = (1, 2, 3, 4, 6, 8, 12, 16, 24, 32)
+        _trial_with_curve(svc, name, [(s, 0.85 - 0.5 / s) for s in steps], True)   # best final ~0.83
+        _trial_with_curve(svc, name, [(s, 0.80 - 0.5 / s) for s in steps], True)
+        rising = _trial_with_curve(svc, name, [(s, 1.0 - 0.8 / s ** 0.5) for s in (1, 2, 3, 4)], False)
+        flat = _trial_with_curve(svc, name, [(s, 0.52 - 0.02 / s) for s in (1, 2, 3, 4)], False)
+        assert not svc.check_early_stopping_state(rising)["shouldStop"]   # -> ~0.86 at step 32
+        assert svc.check_early_stopping_state(flat)["shouldStop"]
+        few = _trial_with_curve(svc, name, [(1, 0.1), (2, 0.11)], False)  # too few points to judge
+        assert not svc.check_early_stopping_state(few)["shouldStop"]
 
 
 def test_trial_cap_1000(tmp_path, monkeypatch):
@@ -254,3 +291,38 @@ def test_distributed_tuning_four_workers(tmp_path):
         trials = json.load(f)["trials"]
     assert len(trials) == 6 and all(t["state"] == "COMPLETED" for t in trials)
     assert len({t["clientId"] for t in trials}) >= 2
+
+
+def test_scheduler_packs_from_measured_footprint(tmp_path):
+    """Default (measured) packing: a probe worker reports its trial's peak HBM and the
+    scheduler adds workers until the GPU holds trials_per_gpu(peak * headroom)."""
+    import sys
+
+    sys.path.insert(0, os.path.join(HERE, "data"))
+    env = {"STUDY_ID": "packed", "STUDY_DIR": str(tmp_path), "PYTHONPATH": os.path.join(HERE, "data"),
+           "FAKE_FOOTPRINT_GB": "1.0"}
+    sched = TrialScheduler("tuner_worker:run", n_gpus=0, env=env, hbm_gb=4.0, max_workers=8,
+                           state_dir=str(tmp_path / "sched"))
+    assert sched.packing_from_footprint(1.0) == 2          # 4 GB * 0.9 // (1.0 * 1.25)
+    assert sched.packing_from_footprint(0.05) == 57
+    res = sched.run(timeout=600)
+    assert res["footprint_gb"] == 1.0 and res["trials_per_gpu"] == 2 and res["workers"] == 2
+    assert res["exit_codes"] == [0, 0]
+    with open(tmp_path / "CloudTuner_study_packed" / "study.json") as f:
+        trials = json.load(f)["trials"]
+    assert len(trials) == 6 and all(t["state"] == "COMPLETED" for t in trials)
+
+
+def test_tuner_reports_footprint_after_first_trial(tmp_path, monkeypatch):
+    from cloud_amd.utils import hbm
+
+    out = tmp_path / "fp.json"
+    monkeypatch.setenv("CLOUD_AMD_FOOTPRINT_FILE", str(out))
+    monkeypatch.setattr(hbm, "trial_footprint_gb", lambda device=None: 3.5)
+    rng = np.random.default_rng(2)
+    x = rng.normal(size=(64, 20)).astype("float32")
+    y = (x[:, 0] > 0).astype("int64")
+    tuner = CloudTuner(_build, objective="acc", hyperparameters=_hps(), max_trials=2, study_id="fp",
+                       study_dir=str(tmp_path), directory=str(tmp_path / "res"))
+    tuner.search(x, y, epochs=1, batch_size=32)
+    assert json.load(open(out))["peak_gb"] == 3.5
