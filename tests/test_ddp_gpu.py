@@ -14,7 +14,10 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _worker(rank, world, port, out_dir, use_fused=True):
+def _worker(rank, world, port, out_dir, use_fused=True, emulate=1):
+    """``emulate`` > 1 (with world 1): one process runs every replica's half-batch
+    through forward/backward into the same arena (gradient accumulation) -- the
+    single-process large-batch update the DP run must reproduce."""
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     sys.path.insert(0, ROOT)
@@ -27,7 +30,8 @@ def _worker(rank, world, port, out_dir, use_fused=True):
     from cloud_amd.parallel.ddp import GradAllReducer
 
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.manual_seed(0)
     m = ResNet((1, 1, 1, 1), num_classes=10, stem_channels_pad=5, device="cuda")
     for b in m.layers:
@@ -36,28 +40,37 @@ def _worker(rank, world, port, out_dir, use_fused=True):
         with torch.no_grad():
             for p in m.parameters():
                 p.add_(0.01)  # broadcast must undo this
-    opt = SGD(m, learning_rate=0.05, momentum=0.9, grad_scale=1.0 / world)
+    reps = world * emulate
+    opt = SGD(m, learning_rate=0.05, momentum=0.9, grad_scale=1.0 / reps)
     red = GradAllReducer(opt.arenas, bucket_mb=0.05)
     red.broadcast_parameters()
     g = torch.Generator(device="cuda").manual_seed(1)
-    X = torch.randn(8 * world, 32, 32, 3, device="cuda", generator=g).to(torch.bfloat16)
-    Y = torch.randint(0, 10, (8 * world,), device="cuda", generator=g)
+    X = torch.randn(8 * reps, 32, 32, 3, device="cuda", generator=g).to(torch.bfloat16)
+    Y = torch.randint(0, 10, (8 * reps,), device="cuda", generator=g)
     xb, yb = X[rank * 8:(rank + 1) * 8].contiguous(), Y[rank * 8:(rank + 1) * 8].contiguous()
     fused = all(fused_block.can_fuse(b, torch.empty(1, 8, 8, b.conv1.cin, device="cuda", dtype=torch.bfloat16))
                 for b in m.layers) and use_fused
     launched_in_backward, losses = [], []
     for _ in range(4):
         opt.zero_grad()
-        loss, _ = softmax_cross_entropy(m(xb), yb, denom=8)
-        loss.backward()
-        launched_in_backward.append(red._next == len(red.buckets))
+        if emulate > 1:
+            for k in range(emulate):
+                xk, yk = X[k * 8:(k + 1) * 8].contiguous(), Y[k * 8:(k + 1) * 8].contiguous()
+                loss, _ = softmax_cross_entropy(m(xk), yk, denom=8)
+                loss.backward()
+            launched_in_backward.append(True)
+        else:
+            loss, _ = softmax_cross_entropy(m(xb), yb, denom=8)
+            loss.backward()
+            launched_in_backward.append(red._next == len(red.buckets))
         red.finish()
         opt.step()
         losses.append(float(loss))
     torch.save({"master": [a.master.detach().cpu() for a in opt.arenas], "fused": fused,
                 "launched": launched_in_backward, "buckets": len(red.buckets), "losses": losses},
                os.path.join(out_dir, f"r{rank}.pt"))
-    dist.destroy_process_group()
+    if world > 1:
+        dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("use_fused", [True, False])
@@ -77,3 +90,11 @@ def test_ddp_two_ranks_through_fused_blocks(tmp_path, use_fused):
                                  % (ai, idx.numel(), a.numel(), d.max().item(), idx[:8].tolist(),
                                     r[0]["losses"], r[1]["losses"]))
     assert all(torch.isfinite(torch.tensor(x["losses"])).all() for x in r)
+    # ... and equal the single-process update over the full (2 x 8) batch, up to the
+    # bf16 rounding of the gradient sums (accumulated in-arena vs summed on the wire)
+    single = tmp_path / "single"
+    single.mkdir()
+    mp.spawn(_worker, args=(1, port + 3, str(single), use_fused, world), nprocs=1, join=True)
+    ref = torch.load(single / "r0.pt", weights_only=True)
+    for a, b in zip(r[0]["master"], ref["master"]):
+        torch.testing.assert_close(a, b, atol=2e-3, rtol=2e-2)
