@@ -3,8 +3,8 @@
 the node's MI355X GPUs by the async trial scheduler (one tuner worker per GPU,
 all sharing one study through the local study service).
 
-    python bench/tuner_8trials.py                 # workers = visible GPUs (CPU workers if none)
-    python bench/tuner_8trials.py --workers 8
+    python bench/tuner_8trials.py                 # workers packed per GPU from the measured trial HBM
+    python bench/tuner_8trials.py --workers 8     # fixed worker count
 
 Reports trials/hour and time-to-best (seconds from start until the trial that
 ends up best completed).  Synthetic MNIST (no network).  The CNN is the
@@ -76,13 +76,16 @@ def main():
     from cloud_amd.tuner.scheduler import TrialScheduler, study_report
 
     n_gpus = visible_gpu_count()
-    workers = args.workers or max(1, min(args.trials, n_gpus or 2))
+    workers = args.workers if args.workers else (None if n_gpus else 2)
     study_dir = tempfile.mkdtemp(prefix="tuner_bench_")
     env = {"STUDY_ID": "mnist_cnn_8", "STUDY_DIR": study_dir, "BENCH_TRIALS": str(args.trials),
            "BENCH_EPOCHS": str(args.epochs), "BENCH_TRAIN": str(args.train), "PYTHONPATH": ROOT}
     os.environ.update(env)
     t0 = time.time()
-    sched = TrialScheduler("bench.tuner_8trials:worker", n_gpus=n_gpus, workers=workers, env=env)
+    # workers=None: probe one worker per GPU, then pack more per GPU from the first trial's
+    # measured peak HBM (no more workers than trials)
+    sched = TrialScheduler("bench.tuner_8trials:worker", n_gpus=n_gpus, workers=workers, env=env,
+                           max_workers=args.trials)
     res = sched.run(timeout=3000)
     wall = time.time() - t0
     sid = next(d for d in os.listdir(study_dir) if d.endswith("mnist_cnn_8"))  # CloudTuner prefixes the id
@@ -99,7 +102,9 @@ def main():
     out = {
         "metric": "trials/hour CloudTuner 8 MNIST-CNN trials (async trial scheduler)",
         "value": round(len(done) / wall * 3600.0, 2), "unit": "trials/hour", "n_gpus": n_gpus,
-        "workers": workers, "trials_completed": len(done), "wall_s": round(wall, 2),
+        "workers": res["workers"], "trials_per_gpu": res.get("trials_per_gpu"),
+        "trial_footprint_gb": round(res["footprint_gb"], 3) if res.get("footprint_gb") else None,
+        "trials_completed": len(done), "wall_s": round(wall, 2),
         "time_to_best_s": round(best["endTs"] - t0, 2) if best and "endTs" in best else None,
         "best_val_accuracy": round(score(best), 4) if best else None, "higher_is_better": True,
         "exit_codes": res["exit_codes"], "data": "synthetic MNIST", "config": {"epochs": args.epochs,

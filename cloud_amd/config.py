@@ -49,7 +49,8 @@ _VARS = [
     Var("CLOUD_AMD_REPO", str, None, "example notebooks: repository root to put on sys.path", "examples"),
     Var("CLOUD_AMD_DEBUG_SYNC", bool, False, "debug: synchronise after every native kernel launch so a fault is "
         "reported by the op that caused it; run() also sets HIP_LAUNCH_BLOCKING/AMD_SERIALIZE_KERNEL", "ops"),
-    Var("CLOUD_AMD_PRECISION", str, "bf16", "compute dtype of the Keras front end", "ops"),
+    Var("CLOUD_AMD_PRECISION", str, "auto", "Keras dtype policy: auto (mixed_bfloat16 on an MI355X, float32 on "
+        "CPU) | float32 | mixed_bfloat16 | bfloat16", "ops"),
     Var("CLOUD_AMD_ARCH", str, "gfx950", "offload arch of the native build", "build"),
     Var("CLOUD_AMD_SANITIZE", bool, False, "build the C++ test binary with ASan/UBSan", "build"),
     # distributed
@@ -68,6 +69,8 @@ _VARS = [
         "distributed"),
     Var("CLOUD_AMD_KFD_ROOT", str, "/sys/class/kfd/kfd/topology/nodes", "KFD topology root read by the "
         "node probe (tests point it at a fake tree)", "launcher"),
+    Var("CLOUD_AMD_FOOTPRINT_FILE", str, None, "where a tuner worker reports its first trial's peak HBM "
+        "(set by TrialScheduler for the probe wave)", "tuner"),
     Var("CLOUD_AMD_BENCH_VIA_RUN", bool, True, "bench scripts launch their ranks through cloud_amd.run()",
         "bench"),
     Var("CLOUD_AMD_BENCH_ALLOW_CPU", bool, False, "let bench.py run ResNet-50 on CPU (debug only)", "bench"),

@@ -38,8 +38,27 @@ def _snake(name):
     return "".join(out)
 
 
+def _auto_policy_name():
+    """``CLOUD_AMD_PRECISION=auto`` (default): ``mixed_bfloat16`` when this process
+    trains on an MI355X, else ``float32``.  Decided from the KFD device count and the
+    launcher's device pin -- never by initialising HIP.  This is the MI355X analogue
+    of TF's default on current GPUs, where "float32" Dense/Conv2D math already runs
+    at reduced (TF32) precision on the matrix units: here the matrix work is bf16 on
+    MFMA with fp32 master weights, fp32 losses and fp32 model outputs."""
+    if os.environ.get("CLOUD_AMD_DEVICE") == "cpu":
+        return "float32"
+    try:
+        from ..core.topology import visible_gpu_count
+
+        return "mixed_bfloat16" if visible_gpu_count() > 0 else "float32"
+    except Exception:  # pragma: no cover
+        return "float32"
+
+
 class Policy:
     def __init__(self, name="float32"):
+        if name == "auto":
+            name = _auto_policy_name()
         if name not in ("float32", "mixed_bfloat16", "bfloat16"):
             raise ValueError(f"Unsupported dtype policy {name!r}")
         self.name = name
@@ -56,10 +75,13 @@ class Policy:
         return f"<Policy {self.name}>"
 
 
-_POLICY = Policy(os.environ.get("CLOUD_AMD_PRECISION", "float32"))
+_POLICY = None
 
 
 def global_policy():
+    global _POLICY
+    if _POLICY is None:  # resolved on first use (after the launcher has pinned the device)
+        _POLICY = Policy(os.environ.get("CLOUD_AMD_PRECISION", "auto"))
     return _POLICY
 
 

@@ -14,12 +14,30 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops.dense import conv2d as conv_act_op
+from ..ops.dense import dense as dense_op
 from . import activations, initializers, regularizers
 from .engine import Input, InputLayer, Layer, global_policy  # noqa: F401
 
 
 def _pair(v):
     return (v, v) if isinstance(v, int) else tuple(v)
+
+
+_ACT_NAMES = {activations.linear: None, activations.relu: "relu", activations.elu: "elu",
+              activations.tanh: "tanh", activations.gelu: "gelu"}
+
+
+def _fused_act(fn):
+    """(epilogue activation name, remaining activation fn) for a Keras activation."""
+    if fn in _ACT_NAMES:
+        return _ACT_NAMES[fn], None
+    return None, fn
+
+
+def _bias_dtype(layer):
+    """Biases are variables: fp32 under the mixed policy (the epilogue adds them in fp32)."""
+    return layer._dtype_policy.variable_dtype if layer.compute_dtype == torch.bfloat16 else layer.compute_dtype
 
 
 class _Regularized:
@@ -57,17 +75,17 @@ class Dense(_Regularized, Layer):
         if self.use_bias:
             b = torch.empty(self.units)
             initializers.get(self.bias_initializer)(b)
-            self.bias = torch.nn.Parameter(b.to(self.compute_dtype))
+            self.bias = torch.nn.Parameter(b.to(_bias_dtype(self)))
         else:
             self.bias = None
 
     def call(self, x, training=None):
         x = x.to(self.kernel.dtype)
-        lead = x.shape[:-1]
-        y = ops.linear(x.reshape(-1, x.shape[-1]), self.kernel, self.bias).reshape(*lead, self.units)
         if getattr(self, "_emit_logits", False):  # fused softmax-xent training path (Model.fit)
-            return y
-        return self.activation(y)
+            return dense_op(x, self.kernel, self.bias, None)
+        act, rest = _fused_act(self.activation)
+        y = dense_op(x, self.kernel, self.bias, act)
+        return rest(y) if rest is not None else y
 
     def get_config(self):
         c = super().get_config()
@@ -99,7 +117,7 @@ class Conv2D(_Regularized, Layer):
         w = torch.empty(self.filters, kh, kw, cin)
         initializers.get(self.kernel_initializer)(w)
         self.kernel = torch.nn.Parameter(w.to(self.compute_dtype))
-        self.bias = torch.nn.Parameter(torch.zeros(self.filters, dtype=self.compute_dtype)) if self.use_bias else None
+        self.bias = torch.nn.Parameter(torch.zeros(self.filters, dtype=_bias_dtype(self))) if self.use_bias else None
 
     def _same_pads(self, H, W):
         out = []
@@ -120,8 +138,9 @@ class Conv2D(_Regularized, Layer):
                 pad = pt
             else:
                 x = F.pad(x, (0, 0, pl, pr, pt, pb))
-        y = ops.conv2d_nhwc(x.contiguous(), self.kernel, self.bias, self.strides[0], pad)
-        return self.activation(y)
+        act, rest = _fused_act(self.activation)
+        y = conv_act_op(x.contiguous(), self.kernel, self.bias, self.strides[0], pad, act)
+        return rest(y) if rest is not None else y
 
     def get_config(self):
         c = super().get_config()

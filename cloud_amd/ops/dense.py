@@ -1,0 +1,278 @@
+"""Keras ``Dense`` / ``Conv2D`` with bias and activation fused into the MFMA epilogue
+(K1 / K2 of SURVEY.md, the layers of the reference workloads:
+``mnist_example_using_fit.py:54-68``, ``keras_tuner_cifar_example.py:32-63``, README MLP).
+
+* forward: ``y = act(x W^T + b)`` -- one GEMM / implicit-GEMM launch whose bf16
+  epilogue adds the fp32 bias and applies the activation (``ca_gemm_ex`` /
+  ``ca_conv_fwd_ex``); no separate bias-add or activation pass;
+* backward: ``g = dy * act'(y)`` (one elementwise pass, from the saved output --
+  or the saved pre-activation for GELU), then the native dgrad / split-K wgrad
+  GEMMs and the native column-sum kernel for the bias gradient.  Gradients of
+  parameters that live in an optimizer arena are written there in place and the
+  data-parallel engine is notified (bucket launch during backward);
+* shapes the MFMA tiles do not take directly are padded, not sent to a library:
+  out-features / in-features to a multiple of 8 (the 10-way softmax heads, odd
+  input widths), conv input channels to a multiple of 8 (the Cin = 1 MNIST and
+  Cin = 3 CIFAR first layers).  Padding costs one small copy of the operand that
+  needs it; the batch dimension is never padded (row tails are masked in-kernel).
+
+CPU tensors (tests, CPU jobs) take the PyTorch reference path with the same math.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext, conv as _conv, gemm as _gemm
+
+# activation codes of the GEMM epilogue (csrc/include/ca_mfma_core.h, enum Act)
+ACT = {None: 0, "linear": 0, "gelu": 1, "relu": 2, "tanh": 3, "elu": 5}
+
+
+def _rup8(n):
+    return (n + 7) // 8 * 8
+
+
+def _arena_grad(p):
+    """The in-arena gradient view of parameter ``p`` (written in place), or None."""
+    if p is None:
+        return None
+    g = getattr(p, "grad", None)
+    if g is not None and getattr(p, "_ca_arena", False) and g.is_contiguous():
+        return g
+    return None
+
+
+def _act_grad(g, y, pre, act):
+    """dy * act'(.) in fp32, returned bf16 contiguous."""
+    if act in (None, "linear"):
+        return g.contiguous()
+    gf, yf = g.float(), y.float()
+    if act == "relu":
+        out = torch.where(yf > 0, gf, torch.zeros_like(gf))
+    elif act == "elu":
+        out = torch.where(yf > 0, gf, gf * (yf + 1.0))
+    elif act == "tanh":
+        out = gf * (1.0 - yf * yf)
+    elif act == "gelu":
+        pf = pre.float()
+        out = gf * (0.5 * (1.0 + torch.erf(pf * 0.7071067811865476)) + pf * 0.3989422804014327 * torch.exp(-0.5 * pf * pf))
+    else:  # pragma: no cover - guarded by fusable()
+        raise ValueError(act)
+    return out.to(torch.bfloat16).contiguous()
+
+
+def fusable(act):
+    return act in ACT
+
+
+def _deliver(param, full_grad, sliced):
+    """Add ``sliced`` (the parameter-shaped gradient) into the arena slot of ``param``
+    and notify the DP engine; returns the autograd gradient when there is no arena."""
+    sink = _arena_grad(param)
+    if sink is not None:
+        sink.view_as(sliced).add_(sliced.to(sink.dtype))
+        from ..parallel import ddp
+
+        ddp.notify_grad_ready(param)
+        return None
+    return sliced.to(param.dtype).view_as(param)
+
+
+class _DenseFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, act, wparam, bparam):
+        ext = _ext.load(required=True)
+        M, K = x.shape
+        N = w.shape[0]
+        Kp, Np = _rup8(K), _rup8(N)
+        xp = x if Kp == K else F.pad(x, (0, Kp - K))
+        wp = w if (Kp == K and Np == N) else F.pad(w, (0, Kp - K, 0, Np - N))
+        bp = None
+        if b is not None:
+            bp = b.float()
+            if Np != N:
+                bp = F.pad(bp, (0, Np - N))
+            bp = bp.contiguous()
+        xp, wp = xp.contiguous(), wp.contiguous()
+        st = _ext.stream_handle(x.device)
+        tiles = -(-M // 128) * -(-Np // 128)
+        if tiles < 32 and Kp >= 1024:
+            # skinny output, long reduction (a small batch through a wide Flatten->Dense):
+            # one tile would walk all of K alone -- split K over blocks into fp32 slabs,
+            # reduce, then bias + activation in one elementwise pass
+            splits = ext.gemm_splitk_effective(Kp, max(1, min(Kp // 512, 256 // tiles)))
+            y32 = torch.empty((M, Np), dtype=torch.float32, device=x.device)
+            ws = torch.empty(splits * M * Np, dtype=torch.float32, device=x.device)
+            ext.gemm_splitk(_gemm.NT, xp.data_ptr(), Kp, wp.data_ptr(), Kp, y32.data_ptr(), 0, 0.0, M, Np, Kp,
+                            splits, ws.data_ptr(), st)
+            if bp is not None:
+                y32 += bp
+            pre = y32.to(torch.bfloat16) if act == "gelu" else None
+            y = _torch_act(y32, act).to(torch.bfloat16)
+        else:
+            y = torch.empty((M, Np), dtype=torch.bfloat16, device=x.device)
+            pre = torch.empty((M, Np), dtype=torch.bfloat16, device=x.device) if act == "gelu" else None
+            ext.gemm_ex(_gemm.NT, xp.data_ptr(), Kp, wp.data_ptr(), Kp, y.data_ptr(), Np, M, Np, Kp, 0, 0.0,
+                        _ext.ptr(bp), ACT[act], _ext.ptr(pre), 0, Np if pre is not None else 0, st)
+        ctx.save_for_backward(xp, wp, y, pre)
+        ctx.act, ctx.dims = act, (M, K, N, Kp, Np)
+        ctx.wparam, ctx.bparam, ctx.has_b = wparam, bparam, b is not None
+        out = y if Np == N else y[:, :N]
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        ext = _ext.load(required=True)
+        xp, wp, y, pre = ctx.saved_tensors
+        M, K, N, Kp, Np = ctx.dims
+        dyp = dy if Np == N else F.pad(dy, (0, Np - N))
+        g = _act_grad(dyp, y, pre, ctx.act)
+        dx = dw = db = dwp = dbp = None
+        if ctx.needs_input_grad[0]:
+            dxp = _gemm.mm_nn(g, wp)
+            dx = dxp if Kp == K else dxp[:, :K]
+        if ctx.needs_input_grad[1] or ctx.wparam is not None:
+            sink = _arena_grad(ctx.wparam)
+            if sink is not None and sink.dtype == torch.bfloat16 and Np == N and Kp == K:
+                _gemm.mm_tn_into(g, xp, sink.view(N, K), beta=1.0)
+                from ..parallel import ddp
+
+                ddp.notify_grad_ready(ctx.wparam)
+            else:
+                full = torch.empty((Np, Kp), dtype=torch.float32, device=g.device)
+                _gemm.mm_tn_into(g, xp, full, beta=0.0)
+                sl = full[:N, :K]
+                if ctx.wparam is not None:
+                    dwp = _deliver(ctx.wparam, full, sl)
+                else:
+                    dw = sl.to(wp.dtype)
+        if ctx.has_b and (ctx.needs_input_grad[2] or ctx.bparam is not None):
+            acc = torch.zeros(Np, dtype=torch.float32, device=g.device)
+            ws = torch.empty(ext.colsum_workspace_floats(M, Np), dtype=torch.float32, device=g.device)
+            ext.colsum(g.data_ptr(), M, Np, Np, acc.data_ptr(), 0, ws.data_ptr(), _ext.stream_handle(g.device))
+            sl = acc[:N]
+            if ctx.bparam is not None:
+                dbp = _deliver(ctx.bparam, acc, sl)
+            else:
+                db = sl
+        return dx, dw, db, None, dwp, dbp
+
+
+def dense(x, w, b=None, act=None):
+    """``act(x @ w.T + b)`` for x [..., K], w [N, K] (bf16), b [N] (fp32 or bf16).
+
+    The native fused path runs for bf16 CUDA operands and a fusable activation; the
+    returned tensor is bf16.  Otherwise PyTorch computes the same expression."""
+    lead, K = x.shape[:-1], x.shape[-1]
+    x2 = x.reshape(-1, K)
+    if (x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and fusable(act)
+            and _gemm._gemm_mode() == "native" and x2.shape[0] > 0 and _ext.use_native(x2, w)):
+        wparam = w if (w.is_leaf and w.requires_grad) else None
+        bparam = b if (b is not None and b.is_leaf and b.requires_grad) else None
+        y = _DenseFn.apply(x2.contiguous(), w.detach() if wparam is not None else w,
+                           None if b is None else (b.detach() if bparam is not None else b), act, wparam, bparam)
+        return y.reshape(*lead, w.shape[0])
+    y = F.linear(x2, w.to(x2.dtype), None if b is None else b.to(x2.dtype))
+    y = _torch_act(y, act)
+    return y.reshape(*lead, w.shape[0])
+
+
+def _torch_act(y, act):
+    if act in (None, "linear"):
+        return y
+    if act == "relu":
+        return torch.relu(y)
+    if act == "elu":
+        return F.elu(y)
+    if act == "tanh":
+        return torch.tanh(y)
+    if act == "gelu":
+        return F.gelu(y)
+    raise ValueError(act)
+
+
+class _ConvActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, padding, act, wparam, bparam):
+        ext = _ext.load(required=True)
+        N, H, W, Cin = x.shape
+        Cout, KH, KW, _ = w.shape
+        Cp = _rup8(Cin)
+        xp = x if Cp == Cin else F.pad(x, (0, Cp - Cin))
+        wp = w if Cp == Cin else F.pad(w, (0, Cp - Cin))
+        xp, wp = xp.contiguous(), wp.contiguous()
+        OH, OW = _conv._out(H, KH, stride, padding), _conv._out(W, KW, stride, padding)
+        y = torch.empty((N, OH, OW, Cout), dtype=torch.bfloat16, device=x.device)
+        bp = b.float().contiguous() if b is not None else None
+        st = _ext.stream_handle(x.device)
+        ext.conv_fwd_ex(xp.data_ptr(), wp.data_ptr(), y.data_ptr(), N, H, W, Cp, Cout, KH, KW, stride, stride,
+                        padding, padding, _ext.ptr(bp), ACT[act], st)
+        ctx.save_for_backward(xp, wp, y)
+        ctx.cfg = (stride, padding, act, Cin, Cp)
+        ctx.wparam, ctx.bparam, ctx.has_b = wparam, bparam, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ext = _ext.load(required=True)
+        xp, wp, y = ctx.saved_tensors
+        stride, padding, act, Cin, Cp = ctx.cfg
+        N, H, W, _ = xp.shape
+        Cout, KH, KW, _ = wp.shape
+        OH, OW = y.shape[1], y.shape[2]
+        st = _ext.stream_handle(dy.device)
+        g = _act_grad(dy, y, None, act)
+        dx = dw = db = dwp = dbp = None
+        if ctx.needs_input_grad[0]:
+            dxp = torch.empty_like(xp)
+            ext.conv_dgrad(g.data_ptr(), wp.data_ptr(), dxp.data_ptr(), N, H, W, Cp, Cout, KH, KW, stride, stride,
+                           padding, padding, 0.0, st)
+            dx = dxp if Cp == Cin else dxp[..., :Cin]
+        if ctx.needs_input_grad[1] or ctx.wparam is not None:
+            ncols, kred = KH * KW * Cp, N * OH * OW
+            splits = ext.gemm_splitk_effective(kred, _conv.choose_wgrad_splits(Cout, ncols, kred))
+            ws = torch.empty(splits * Cout * ncols, dtype=torch.float32, device=dy.device)
+            sink = _arena_grad(ctx.wparam)
+            if sink is not None and sink.dtype == torch.bfloat16 and Cp == Cin:
+                ext.conv_wgrad(g.data_ptr(), xp.data_ptr(), sink.data_ptr(), 1, 1.0, N, H, W, Cp, Cout, KH, KW,
+                               stride, stride, padding, padding, splits, ws.data_ptr(), st)
+                from ..parallel import ddp
+
+                ddp.notify_grad_ready(ctx.wparam)
+            else:
+                full = torch.empty((Cout, KH, KW, Cp), dtype=torch.float32, device=dy.device)
+                ext.conv_wgrad(g.data_ptr(), xp.data_ptr(), full.data_ptr(), 0, 0.0, N, H, W, Cp, Cout, KH, KW,
+                               stride, stride, padding, padding, splits, ws.data_ptr(), st)
+                sl = full[..., :Cin]
+                if ctx.wparam is not None:
+                    dwp = _deliver(ctx.wparam, full, sl)
+                else:
+                    dw = sl.to(wp.dtype)
+        if ctx.has_b and (ctx.needs_input_grad[2] or ctx.bparam is not None):
+            acc = torch.zeros(Cout, dtype=torch.float32, device=dy.device)
+            M = N * OH * OW
+            wsb = torch.empty(ext.colsum_workspace_floats(M, Cout), dtype=torch.float32, device=dy.device)
+            ext.colsum(g.data_ptr(), M, Cout, Cout, acc.data_ptr(), 0, wsb.data_ptr(), st)
+            if ctx.bparam is not None:
+                dbp = _deliver(ctx.bparam, acc, acc)
+            else:
+                db = acc
+        return dx, dw, db, None, None, None, dwp, dbp
+
+
+def conv2d(x, w, b=None, stride=1, padding=0, act=None):
+    """``act(conv2d_nhwc(x, w) + b)``, NHWC x [N,H,W,Cin], w [Cout,KH,KW,Cin]."""
+    Cout = w.shape[0]
+    if (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and fusable(act) and Cout % 8 == 0
+            and _conv._conv_mode() == "native" and x.shape[0] > 0 and x.numel() < 2 ** 31
+            and _ext.use_native(x, w)):
+        wparam = w if (w.is_leaf and w.requires_grad) else None
+        bparam = b if (b is not None and b.is_leaf and b.requires_grad) else None
+        return _ConvActFn.apply(x.contiguous(), w.detach() if wparam is not None else w,
+                                None if b is None else (b.detach() if bparam is not None else b), stride, padding,
+                                act, wparam, bparam)
+    y = _conv.conv2d_nhwc(x.contiguous(), w.to(x.dtype), None, stride, padding)
+    if b is not None:
+        y = y + b.to(y.dtype)
+    return _torch_act(y, act)

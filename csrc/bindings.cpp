@@ -50,6 +50,8 @@ int ca_gap_fwd(const bf16_t*, void*, int, int, int, int, hipStream_t);
 int ca_gap_bwd(const void*, int, bf16_t*, int, int, int, hipStream_t);
 int ca_gemm_bf16(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float*, float,
                  hipStream_t);
+int ca_conv_fwd_ex(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int,
+                   const float*, int, hipStream_t);
 int ca_conv_fwd(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int, float*,
                 hipStream_t);
 int ca_conv_dgrad(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int, float,
@@ -218,6 +220,11 @@ PYBIND11_MODULE(_C, m) {
                        int ph, int pw, u64 stats, u64 s) {
     check(ca_conv_fwd(P(const bf16_t*, x), P(const bf16_t*, w), P(bf16_t*, y), Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph,
                       pw, P(float*, stats), S(s)), "conv_fwd");
+  });
+  m.def("conv_fwd_ex", [](u64 x, u64 w, u64 y, int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh,
+                          int sw, int ph, int pw, u64 bias, int act, u64 s) {
+    check(ca_conv_fwd_ex(P(const bf16_t*, x), P(const bf16_t*, w), P(bf16_t*, y), Nb, H, W, Cin, Cout, KH, KW, sh, sw,
+                         ph, pw, P(const float*, bias), act, S(s)), "conv_fwd_ex");
   });
   m.def("conv_dgrad", [](u64 dy, u64 w, u64 dx, int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh,
                          int sw, int ph, int pw, float beta, u64 s) {

@@ -105,7 +105,7 @@ __device__ __forceinline__ long out_row(const CoreParams& P, int gm) {
   return ((long)n * P.H + P.sh * qy + P.dg_py) * P.W + P.sw * qx + P.dg_px;
 }
 
-enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_GELU_TANH = 4 };
+enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_GELU_TANH = 4, ACT_ELU = 5 };
 
 __device__ __forceinline__ float act_fwd(int act, float x) {
   switch (act) {
@@ -116,6 +116,7 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
       const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
       return 0.5f * x * (1.f + tanhf(u));
     }
+    case ACT_ELU: return x > 0.f ? x : expm1f(x);
   }
   return x;
 }
@@ -135,6 +136,7 @@ __device__ __forceinline__ float act_grad(int act, float x) {
       const float t = tanhf(u);
       return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * 0.7978845608028654f * (1.f + 3.f * 0.044715f * x * x);
     }
+    case ACT_ELU: return x > 0.f ? 1.f : __expf(x);
   }
   return 1.f;
 }

@@ -482,6 +482,20 @@ int ca_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   return launch<128, 128, ConvFwdA, DenseKC, GConvFwdA, GDenseKC, EPI_BF16>(p, 1, s);
 }
 
+// Keras Conv2D forward: y = act(conv(x, w) + bias) with bias [Cout] fp32 (or null) and
+// act one of the core's ACT_* codes, applied in the bf16 epilogue (no separate passes).
+int ca_conv_fwd_ex(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int W, int Cin, int Cout, int KH,
+                   int KW, int sh, int sw, int ph, int pw, const float* bias, int act, hipStream_t s) {
+  CoreParams p = conv_params(Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw);
+  if (!geom_ok(Cin, Cout, (long)Nb * H * W)) return -1;
+  p.A = x; p.B = w; p.lda = Cin; p.ldb = (long)KH * KW * Cin; p.C = y; p.ldc = Cout;
+  p.M = Nb * p.OH * p.OW; p.N = Cout; p.K = KH * KW * Cin; p.k_per_split = p.K;
+  p.bias = bias;
+  p.act = act;
+  if (Cout <= 64) return launch<128, 64, ConvFwdA, DenseKC, GConvFwdA, GDenseKC, EPI_BF16>(p, 1, s);
+  return launch<128, 128, ConvFwdA, DenseKC, GConvFwdA, GDenseKC, EPI_BF16>(p, 1, s);
+}
+
 // Rows of the BN-backward statistics partials ca_conv_dgrad_bnstats writes: one per
 // 128-row GEMM tile, summed over the output-parity classes of a strided dgrad.
 long ca_conv_dgrad_stat_tiles(int Nb, int H, int W, int sh, int sw) {

@@ -1,0 +1,106 @@
+"""The reference workloads' Dense / Conv2D layers on the hand-written kernels (VERDICT r1
+item 3): fused bias + activation epilogues, skinny / odd widths (N in {2, 10, 64},
+K = 20), first-layer convolutions with Cin in {1, 3} -- forward, input gradient,
+weight and bias gradients against a plain PyTorch fp32 reference of the same op on
+the same bf16-rounded operands; and a Keras MNIST CNN whose training step runs with
+the PyTorch library GEMM / convolution entry points disabled."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ref_act(y, act):
+    return {None: lambda t: t, "relu": torch.relu, "elu": F.elu, "tanh": torch.tanh, "gelu": F.gelu}[act](y)
+
+
+@pytest.mark.parametrize("act", [None, "relu", "elu", "tanh", "gelu"])
+@pytest.mark.parametrize("M,K,N", [(64, 784, 512), (64, 512, 10), (37, 1600, 64), (32, 20, 2), (130, 64, 10),
+                                   (64, 5408, 64), (200, 4096, 10)])
+def test_dense_fused_vs_fp32(M, K, N, act):
+    from cloud_amd.ops import _ext
+    from cloud_amd.ops.dense import dense
+
+    _ext.load(required=True)
+    torch.manual_seed(M + K + N)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(torch.bfloat16).requires_grad_()
+    b = torch.randn(N, device=DEV).requires_grad_()
+    y = dense(x, w, b, act)
+    assert y.dtype == torch.bfloat16 and y.shape == (M, N)
+    dy = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = _ref_act(xr @ wr.t() + br, act)
+    yr.backward(dy.float())
+    tol = dict(atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=3e-2 * N ** 0.5, rtol=3e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=3e-2 * M ** 0.5, rtol=3e-2)
+    torch.testing.assert_close(b.grad, br.grad, atol=3e-2 * M ** 0.5, rtol=3e-2)
+
+
+@pytest.mark.parametrize("act", [None, "relu", "elu"])
+@pytest.mark.parametrize("N,H,Cin,Cout,k,p", [(8, 28, 1, 32, 3, 0), (4, 32, 3, 32, 3, 1), (4, 13, 32, 64, 3, 0),
+                                               (2, 16, 3, 16, 3, 1)])
+def test_conv_fused_vs_fp32(N, H, Cin, Cout, k, p, act):
+    from cloud_amd.ops import _ext
+    from cloud_amd.ops.dense import conv2d
+
+    _ext.load(required=True)
+    torch.manual_seed(N * H + Cin)
+    x = torch.randn(N, H, H, Cin, device=DEV).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(Cout, k, k, Cin, device=DEV) / (k * k * Cin) ** 0.5).to(torch.bfloat16).requires_grad_()
+    b = (0.1 * torch.randn(Cout, device=DEV)).requires_grad_()
+    y = conv2d(x, w, b, 1, p, act)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = F.conv2d(xr.permute(0, 3, 1, 2), wr.permute(0, 3, 1, 2), br, padding=p)
+    yr = _ref_act(yr, act).permute(0, 2, 3, 1)
+    yr.backward(dy.float())
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+    red = N * H * H
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=5e-2, rtol=3e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=3e-2 * red ** 0.5, rtol=3e-2)
+    torch.testing.assert_close(b.grad, br.grad, atol=3e-2 * red ** 0.5, rtol=3e-2)
+
+
+def test_keras_mnist_cnn_trains_on_native_kernels(monkeypatch):
+    """The reference MNIST CNN (mnist_example_using_fit.py:54-68) under the default
+    (auto -> mixed_bfloat16) policy: the training step never reaches PyTorch's
+    library GEMM / convolution entry points (hipBLASLt / MIOpen)."""
+    import numpy as np
+
+    from cloud_amd import keras
+    from cloud_amd.keras import engine
+
+    monkeypatch.setattr(engine, "_POLICY", None)
+    monkeypatch.delenv("CLOUD_AMD_PRECISION", raising=False)
+    rng = np.random.default_rng(0)
+    x = rng.random((512, 28, 28, 1), dtype=np.float32)
+    y = (x[:, :14].mean(axis=(1, 2, 3)) > x[:, 14:].mean(axis=(1, 2, 3))).astype("int64")
+    model = keras.Sequential([
+        keras.layers.Conv2D(32, 3, activation="relu", input_shape=(28, 28, 1)),
+        keras.layers.MaxPooling2D(),
+        keras.layers.Flatten(),
+        keras.layers.Dense(64, activation="relu"),
+        keras.layers.Dense(10, activation="softmax"),
+    ])
+    model.compile(loss="sparse_categorical_crossentropy", optimizer=keras.optimizers.Adam(), metrics=["accuracy"])
+    assert engine.global_policy().name == "mixed_bfloat16"
+    model.train_on_batch(x[:64], y[:64])  # builds arenas etc. outside the guarded region
+
+    def banned(*a, **k):
+        raise AssertionError("library GEMM/conv reached in the training step")
+
+    for mod, name in ((F, "linear"), (F, "conv2d"), (torch, "mm"), (torch, "matmul"), (torch, "addmm")):
+        monkeypatch.setattr(mod, name, banned)
+    hist = model.fit(x, y, batch_size=64, epochs=4, verbose=0)
+    losses = hist.history["loss"]
+    assert losses[-1] < losses[0], losses
+    monkeypatch.undo()
+    pred = model.predict(x[:8])
+    assert pred.shape == (8, 10) and np.allclose(pred.sum(-1), 1.0, atol=1e-2)
