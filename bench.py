@@ -56,8 +56,6 @@ def parse(argv=None):
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--model", choices=("resnet50", "tiny"), default="resnet50")
     ap.add_argument("--device", choices=("auto", "cpu"), default="auto")
-    ap.add_argument("--graph", type=int, default=int(os.environ.get("CLOUD_AMD_GRAPH", "0")),
-                    help="capture the training step in a HIP graph (1 rank only)")
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--bucket-mb", type=float, default=None,
                     help="gradient all-reduce bucket size (default CLOUD_AMD_BUCKET_MB or 16)")
@@ -129,7 +127,7 @@ def main():
             loss, _ = softmax_cross_entropy(logits, y, denom=B)
         with trace.range("backward"):
             loss.backward()
-        return loss.detach()  # never keep the autograd graph alive across steps (graph capture)
+        return loss.detach()  # never keep the autograd graph alive across steps
 
     def train_step():
         opt.zero_grad()
@@ -147,20 +145,14 @@ def main():
     run_t0 = os.environ.get("CLOUD_AMD_RUN_T0")
     run_to_first = (time.time() - float(run_t0)) if run_t0 else None
 
-    use_graph = bool(args.graph) and on_gpu and (world == 1 or os.environ.get("CLOUD_AMD_GRAPH_FORCE") == "1")
+    # (HIP-graph capture of this step, cloud_amd.runtime.graph, measured slower than eager on
+    # ROCm 7.2 at b256/b512: kernel boundaries cost the same in a graph; not offered here)
     step_fn = train_step
-    if use_graph:
-        loss = None
-        from cloud_amd.runtime.graph import capture_train_step
-
-        step_fn = capture_train_step(fwd_bwd, opt, reducer, warmup=3)
-
     for _ in range(max(args.warmup - 1, 0)):
         loss = step_fn()
     dist_env.barrier()
     sync()
-    if not use_graph:
-        reducer.timing_start()
+    reducer.timing_start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step_fn()
@@ -208,7 +200,7 @@ def main():
             "config": {"model": "resnet50" if args.model == "resnet50" else "tiny_bottleneck_resnet_cpu_test",
                        "global_batch": global_batch, "seq_len": None,
                        "image_size": S, "per_gpu_batch": B, "parallelism": f"dp{world}",
-                       "optimizer": "sgd_momentum0.9_fused", "hip_graph": use_graph},
+                       "optimizer": "sgd_momentum0.9_fused"},
             "device": device.type,
             "backend": backend if world > 1 else None,
             "shared_gpu": os.environ.get("CLOUD_AMD_SHARED_GPU", "0") not in ("", "0", "false"),

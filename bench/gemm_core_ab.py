@@ -49,7 +49,10 @@ def main():
         ref = (a[:256].float() @ w.float().t())
         r["fwd_err"] = float((y[:256].float() - ref).norm() / ref.norm())
         for name, fn in (("fwd", lambda: raw.gemm(a, w)), ("dgrad", lambda: raw.gemm(dy, w, layout=raw.NN)),
-                         ("wgrad", lambda: raw.wgrad_into(dy, a, gw, beta=0.0))):
+                         ("wgrad", lambda: raw.wgrad_into(dy, a, gw, beta=0.0)),
+                         # the library comparator (hipBLASLt through torch.mm) on the same operands
+                         ("blas_fwd", lambda: torch.mm(a, w.t())), ("blas_dgrad", lambda: torch.mm(dy, w)),
+                         ("blas_wgrad", lambda: torch.mm(dy.t(), a))):
             ms = timeit(fn)
             r[name + "_ms"] = round(ms, 4)
             r[name + "_TF"] = round(fl / ms / 1e9, 1)

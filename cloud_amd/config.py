@@ -97,8 +97,6 @@ _VARS = [
     Var("CLOUD_AMD_DATA", str, None, "directory of real .npz datasets (else synthetic)", "data"),
     # benchmarks / examples
     Var("CLOUD_AMD_BENCH_BATCH", int, 512, "per-GPU batch of bench.py (sized for 288 GB HBM)", "bench"),
-    Var("CLOUD_AMD_GRAPH", bool, False, "capture the bench step in a HIP graph", "bench"),
-    Var("CLOUD_AMD_GRAPH_FORCE", bool, False, "allow graph capture with world > 1", "bench"),
     Var("CLOUD_AMD_EXAMPLE_CPU", bool, False, "examples: launch CPU ranks instead of GPUs", "examples"),
     Var("CLOUD_AMD_EXAMPLE_SMALL", bool, False, "examples: tiny datasets (tests)", "examples"),
     Var("CLOUD_AMD_EXAMPLE_OUT", str, None, "examples: output directory", "examples"),
