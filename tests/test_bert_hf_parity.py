@@ -117,8 +117,10 @@ def test_native_bf16_path_matches_hf_fp32_gpu():
     worst = []
     for get, hp in pairs:
         g = _our_grad(ours, get).float()
-        rel = float((g - hp.grad).norm() / hp.grad.norm().clamp_min(1e-12))
+        # the key-projection bias has an exactly-zero true gradient (softmax is invariant to
+        # a per-query constant): |HF| ~ 1e-11, ours ~ 1e-7 of bf16 noise -- hence the floor
+        rel = float((g - hp.grad).norm() / hp.grad.norm().clamp_min(1e-5))
         worst.append(rel)
-        # position rows beyond S and padding-token rows get zero gradient on both sides
-        assert rel < 6e-2, (tuple(hp.shape), rel)
-    assert max(worst) < 6e-2
+        assert rel < 3e-2, (tuple(hp.shape), rel)
+    # measured on MI355X: every other parameter within 1 % of HF-fp32
+    assert max(worst) < 3e-2
