@@ -117,6 +117,11 @@ class GradAllReducer:
             _ACTIVE.add(self)
 
     def _build(self):
+        # An arena is in reverse forward order, so its LAST bucket holds the first layers,
+        # whose gradients exist only when backward ends: that all-reduce is never hidden
+        # behind compute.  Each arena's final bucket is capped at CLOUD_AMD_TAIL_BUCKET_MB
+        # (split off the end of the arena) so the exposed collectives are small ones.
+        tail = int(float(os.environ.get("CLOUD_AMD_TAIL_BUCKET_MB", 1.0)) * (1 << 20))
         for a in self.arenas:
             es = a.grad.element_size()
             cur, lo = [], 0
@@ -127,6 +132,13 @@ class GradAllReducer:
                     self.buckets.append(Bucket(a, lo, end, cur, len(self.buckets)))
                     cur, lo = [], end
             if cur:
+                if tail > 0 and len(cur) > 1 and (a.n - lo) * es > tail:
+                    k = len(cur) - 1  # keep at least one slot in the tail
+                    while k > 1 and (a.n - cur[k - 1].offset) * es <= tail:
+                        k -= 1
+                    cut = cur[k].offset
+                    self.buckets.append(Bucket(a, lo, cut, cur[:k], len(self.buckets)))
+                    cur, lo = cur[k:], cut
                 self.buckets.append(Bucket(a, lo, a.n, cur, len(self.buckets)))
         for b in self.buckets:
             for s in b.slots:

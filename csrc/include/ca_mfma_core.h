@@ -247,13 +247,28 @@ struct DenseNC {
   }
 };
 
+// LDS image of the bf16 C tile staged by the epilogue.  BN = 128: unpadded 256-B rows
+// with a 16-column XOR swizzle by (row >> 2) & 3 -- the 2-byte accumulator stores of one
+// wave-instruction (4 row groups x 16 columns) land in 32 distinct banks, the 16-B row
+// reads stay contiguous, and the tile is exactly 32 KB, so a 32-KB K stage keeps FIVE
+// 128x128 blocks resident per CU instead of four (34.8 KB padded).  Other widths keep
+// the padded layout (the stage, not the C tile, sets their LDS size).
+template <int BN>
+struct EpiLayout {
+  static constexpr bool SWZ = (BN == 128);
+  static constexpr int LD = SWZ ? BN : BN + PAD;
+  __device__ static __forceinline__ int idx(int row, int col) {
+    return SWZ ? row * LD + (col ^ (((row >> 2) & 3) << 4)) : row * LD + col;
+  }
+};
+
 // Shared epilogue: fp32 split-K slab store, or bf16 through LDS with bias /
 // activation / pre-activation / act' / beta-accumulate / BN-statistics options.
 template <int BM, int BN, int WM, int WN, int EPI, int FM = BM / WM / 16, int FN = BN / WN / 16>
 __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM][FN], short* smem, int m0, int n0,
                                               int tm, int tid) {
   constexpr int NT = WM * WN * 64;
-  constexpr int EPI_LD = BN + PAD;
+  using EL = EpiLayout<BN>;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   // C/D layout of mfma_f32_16x16x32: col = lane&15, row = (lane>>4)*4 + r
@@ -290,7 +305,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          Cs[(rbase + i * 16 + r) * EPI_LD + cbase + j * 16] = (short)f2bf(acc[i][j][r]);
+          Cs[EL::idx(rbase + i * 16 + r, cbase + j * 16)] = (short)f2bf(acc[i][j][r]);
     __syncthreads();
     const bool fx = P.act != ACT_NONE || P.dact_src != nullptr || P.preact != nullptr;
     bf16_t* Cg = reinterpret_cast<bf16_t*>(P.C);
@@ -337,7 +352,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
         if (!okr[u]) continue;
         const int row = (tid + (it0 + u) * NT) / (BN / 8);
         const int gm = m0 + row;
-        s8v v = *reinterpret_cast<const s8v*>(Cs + row * EPI_LD + col);
+        s8v v = *reinterpret_cast<const s8v*>(Cs + EL::idx(row, col));
         bf16_t* dst = Cg + orow[u] * P.ldc + gn;
         if (fx) {
           if (P.preact) *reinterpret_cast<s8v*>(P.preact + (long)gm * P.ld_aux + gn) = v;
@@ -358,7 +373,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
             v[j] = (short)f2bf(bf2f((bf16_t)v[j]) + P.beta * o);
           }
         }
-        if (!RSTAT && P.stats && (fx || has_beta)) *reinterpret_cast<s8v*>(Cs + row * EPI_LD + col) = v;
+        if (!RSTAT && P.stats && (fx || has_beta)) *reinterpret_cast<s8v*>(Cs + EL::idx(row, col)) = v;
         *reinterpret_cast<s8v*>(dst) = v;
         if constexpr (STS) {
 #pragma unroll
@@ -411,7 +426,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
       if (rows > BM) rows = BM;
       __syncthreads();
       for (int r = part; r < rows; r += TPC) {
-        const float v = bf2f((bf16_t)Cs[r * EPI_LD + col]);
+        const float v = bf2f((bf16_t)Cs[EL::idx(r, col)]);
         s += v;
         q += v * v;
       }
@@ -445,7 +460,7 @@ __device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
   using GA = TileGeom<BM, A_KC>;
   using GB = TileGeom<BN, B_KC>;
   constexpr int STAGE = GA::ELEMS + GB::ELEMS;
-  constexpr int EPI_LD = BN + PAD;
+  constexpr int EPI_LD = EpiLayout<BN>::LD;
   constexpr int SMEM = (NSTAGE * STAGE > BM * EPI_LD ? NSTAGE * STAGE : BM * EPI_LD);
   constexpr int CPA = GA::CHUNKS / NT, CPB = GB::CHUNKS / NT;
   using LA = LAT<BM, CPA, NT>;
@@ -653,7 +668,7 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
   constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;
   constexpr int STAGE = A_ELEMS + B_ELEMS;
-  constexpr int EPI_LD = BN + PAD;
+  constexpr int EPI_LD = EpiLayout<BN>::LD;
   constexpr int SMEM = (NSTAGE * STAGE > BM * EPI_LD ? NSTAGE * STAGE : BM * EPI_LD);
   constexpr int CPA = A_ELEMS / 8 / NT, CPB = B_ELEMS / 8 / NT;
   using LA = LAT<BM, CPA, NT>;
