@@ -247,20 +247,35 @@ struct DenseNC {
   }
 };
 
-// LDS image of the bf16 C tile staged by the epilogue.  BN = 128: unpadded 256-B rows
-// with a 16-column XOR swizzle by (row >> 2) & 3 -- the 2-byte accumulator stores of one
-// wave-instruction (4 row groups x 16 columns) land in 32 distinct banks, the 16-B row
-// reads stay contiguous, and the tile is exactly 32 KB, so a 32-KB K stage keeps FIVE
-// 128x128 blocks resident per CU instead of four (34.8 KB padded).  Other widths keep
-// the padded layout (the stage, not the C tile, sets their LDS size).
+// LDS image of the bf16 C tile staged by the epilogue.  The accumulators are C^T
+// fragments (see mfma_acc), so a lane owns 4 consecutive columns of one row and writes
+// them as ONE 8-byte ds_write_b64 (16 per thread for a 128x128 tile, not 64 2-byte
+// stores).  BN = 128: unpadded 256-B rows with the 8-column chunks XOR-swizzled by
+// row & 15 -- the 16 rows one ds_write_b64 lane group touches land in 16 distinct
+// 16-B bank slots, and the 16-B row reads of the store phase stay contiguous; the tile
+// is exactly 32 KB (a 32-KB K stage keeps five 128x128 blocks per CU).  Other widths
+// keep the padded layout (row stride 36 banks: conflict-free for the same pattern).
 template <int BN>
 struct EpiLayout {
   static constexpr bool SWZ = (BN == 128);
   static constexpr int LD = SWZ ? BN : BN + PAD;
   __device__ static __forceinline__ int idx(int row, int col) {
-    return SWZ ? row * LD + (col ^ (((row >> 2) & 3) << 4)) : row * LD + col;
+    return SWZ ? row * LD + (col ^ ((row & 15) << 3)) : row * LD + col;
   }
 };
+
+// One K step of a wave's FM x FN fragment grid.  The MFMA is issued with the B
+// fragment as its first operand, so the 16x16 result is the C^T tile: lane l holds
+// C[m = l & 15][n = 4 * (l >> 4) + r], r = 0..3 -- four consecutive columns of one row
+// (vector stores in the epilogue, contiguous float4 split-K slabs).
+template <int FM, int FN>
+__device__ __forceinline__ void mfma_acc(f4v (&acc)[FM][FN], const bf16x8 (&af)[FM], const bf16x8 (&bfr)[FN]) {
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+}
 
 // Shared epilogue: fp32 split-K slab store, or bf16 through LDS with bias /
 // activation / pre-activation / act' / beta-accumulate / BN-statistics options.
@@ -271,41 +286,43 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
   using EL = EpiLayout<BN>;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  // C/D layout of mfma_f32_16x16x32: col = lane&15, row = (lane>>4)*4 + r
-  const int rbase = wm * (BM / WM) + (lane >> 4) * 4;
-  const int cbase = wn * (BN / WN) + (lane & 15);
+  // accumulator layout (mfma_acc): acc[i][j][r] = C[rbase + 16 i][cbase + 16 j + r]
+  const int rbase = wm * (BM / WM) + (lane & 15);
+  const int cbase = wn * (BN / WN) + 4 * (lane >> 4);
   if constexpr (EPI == EPI_F32_PARTIAL) {
+    // N % 8 == 0 and ldc % 4 == 0 (slabs are [M][N]): a column group is whole or absent
     float* Cp = reinterpret_cast<float*>(P.C) + (long)blockIdx.z * P.split_stride;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int gm = m0 + rbase + i * 16 + r, gn = n0 + cbase + j * 16;
-          if (gm < P.M && gn < P.N) Cp[(long)gm * P.ldc + gn] = acc[i][j][r];
-        }
+      for (int j = 0; j < FN; ++j) {
+        const int gm = m0 + rbase + i * 16, gn = n0 + cbase + j * 16;
+        if (gm < P.M && gn < P.N) *reinterpret_cast<f4v*>(Cp + (long)gm * P.ldc + gn) = acc[i][j];
+      }
     return;
   } else {
     short* Cs = smem;
     if (P.bias) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int gn = n0 + cbase + j * 16;
-        const float bv = gn < P.N ? P.bias[gn] : 0.f;
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+        for (int r = 0; r < 4; ++r) {
+          const int gn = n0 + cbase + j * 16 + r;
+          const float bv = gn < P.N ? P.bias[gn] : 0.f;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] += bv;
+          for (int i = 0; i < FM; ++i) acc[i][j][r] += bv;
+        }
       }
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+      for (int j = 0; j < FN; ++j) {
+        s4v pk;
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[EL::idx(rbase + i * 16 + r, cbase + j * 16)] = (short)f2bf(acc[i][j][r]);
+        for (int r = 0; r < 4; ++r) pk[r] = (short)f2bf(acc[i][j][r]);
+        *reinterpret_cast<s4v*>(Cs + EL::idx(rbase + i * 16, cbase + j * 16)) = pk;
+      }
     __syncthreads();
     const bool fx = P.act != ACT_NONE || P.dact_src != nullptr || P.preact != nullptr;
     bf16_t* Cg = reinterpret_cast<bf16_t*>(P.C);
@@ -516,11 +533,7 @@ __device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
       for (int i = 0; i < FM; ++i) af[i] = read_frag<BM, A_KC>(As, wm * (BM / WM) + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < FN; ++j) bfr[j] = read_frag<BN, B_KC>(Bs, wn * (BN / WN) + j * 16, kk, lane);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      mfma_acc<FM, FN>(acc, af, bfr);
     }
   };
   if constexpr (NSTAGE == 1) {
@@ -718,11 +731,7 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
       for (int i = 0; i < FM; ++i) af[i] = read_frag_sw<BM, A_KC>(As, wm * (BM / WM) + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < FN; ++j) bfr[j] = read_frag_sw<BN, B_KC>(Bs, wn * (BN / WN) + j * 16, kk, lane);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      mfma_acc<FM, FN>(acc, af, bfr);
     }
   };
 
