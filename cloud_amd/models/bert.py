@@ -37,6 +37,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import _ext, raw
+from ..ops.dense import dense
 from ..ops.dropout import next_seed
 from ..runtime.side_stream import SideWork
 
@@ -210,21 +211,25 @@ class _LayerFn(torch.autograd.Function):
         side = SideWork(dy2.device)
         deferred = []
 
-        def param_grads(dy, inp, w, b):
+        def param_grads(dy, inp, w, b, bias_done=False):
             def fn():
-                raw.colsum_into(dy, G(b))
+                if not bias_done:
+                    raw.colsum_into(dy, G(b))
                 raw.wgrad_into(dy, inp, G(w))
             side.run(fn, dy, inp)
             if side.enabled:
-                deferred.extend((b, w))
+                deferred.extend((w,) if bias_done else (b, w))
             else:
-                _notify(b), _notify(w)
+                if not bias_done:
+                    _notify(b)
+                _notify(w)
 
-        # LN2 (+ residual y1, + dropout on the FFN output)
+        # LN2 (+ residual y1, + dropout on the FFN output); the same pass sums the
+        # gradient it hands to the FFN output projection into b2's gradient
         dh2, do = raw.ln_bwd(dy2, h2, m2, r2, layer.ln2_w, G(layer.ln2_w), G(layer.ln2_b), p_in=p_hidden, seed_in=s2,
-                             want_dx=True)
-        _notify(layer.ln2_b), _notify(layer.ln2_w)
-        param_grads(do, f, layer.w2, layer.b2)
+                             want_dx=True, dsum=G(layer.b2))
+        _notify(layer.ln2_b), _notify(layer.ln2_w), _notify(layer.b2)
+        param_grads(do, f, layer.w2, layer.b2, bias_done=True)
         dpre = raw.gemm(do, layer.w2, layout=raw.NN, act=cfg.hidden_act, dact_src=pre)
         del do, f
         param_grads(dpre, y1, layer.w1, layer.b1)
@@ -233,10 +238,10 @@ class _LayerFn(torch.autograd.Function):
         dy1 = dh2
         # LN1 (+ residual x, + dropout on the attention output projection)
         dh1, da = raw.ln_bwd(dy1, h1, m1, r1, layer.ln1_w, G(layer.ln1_w), G(layer.ln1_b), p_in=p_hidden, seed_in=s1,
-                             want_dx=True)
-        _notify(layer.ln1_b), _notify(layer.ln1_w)
+                             want_dx=True, dsum=G(layer.bo))
+        _notify(layer.ln1_b), _notify(layer.ln1_w), _notify(layer.bo)
         del dy1
-        param_grads(da, ctx_, layer.wo, layer.bo)
+        param_grads(da, ctx_, layer.wo, layer.bo, bias_done=True)
         dctx = raw.gemm(da, layer.wo, layout=raw.NN)
         del da
         dqkv = raw.attn_bwd(qkv, ctx_, dctx, lse, B, S, H, key_len, p_attn, sa,
@@ -329,8 +334,10 @@ class BertForSequenceClassification(nn.Module):
         for layer in self.layers:
             h = _LayerFn.apply(h, key_len, layer, B, S, ph, pa, *layer.param_list())
         pooled = _PoolerFn.apply(h, self.pool_w, self.pool_b, B, S)
-        pooled = F.dropout(pooled.float(), ph, train)
-        return F.linear(pooled, self.cls_w, self.cls_b)
+        pooled = F.dropout(pooled, ph, train)
+        # classifier on the native dense kernel (num_labels padded to the tile width); the
+        # fp32 weight is rounded to bf16 per step and its gradient flows back through the cast
+        return dense(pooled, self.cls_w.to(torch.bfloat16), self.cls_b).float()
 
     def _torch_forward(self, input_ids, token_type_ids=None, attention_mask=None):
         """Plain PyTorch (fp32 math) -- CPU path and numerics reference."""

@@ -272,9 +272,11 @@ def ln_fwd(x, gamma, beta, eps, residual=None, p_in=0.0, seed_in=0, p_out=0.0, s
 
 
 def ln_bwd(dy, h, mean, rstd, gamma, dgamma=None, dbeta=None, p_in=0.0, seed_in=0, p_out=0.0, seed_out=0,
-           want_dx=False, accumulate=True):
+           want_dx=False, accumulate=True, dsum=None):
     """Returns (dh, dx): dh = grad wrt the pre-norm sum (also the residual grad); dx =
-    drop_in'(dh) when ``want_dx`` (else None)."""
+    drop_in'(dh) when ``want_dx`` (else None).  ``dsum`` (fp32 [C]) receives the column
+    sums of dx (else dh) -- the bias gradient of the layer that fed the LN -- from the
+    same pass (accumulated when ``accumulate``)."""
     ext = _ext.load(required=True)
     C = dy.shape[-1]
     M = dy.numel() // C
@@ -283,7 +285,7 @@ def ln_bwd(dy, h, mean, rstd, gamma, dgamma=None, dbeta=None, p_in=0.0, seed_in=
     ws = torch.empty(ext.ln_workspace_floats(M, C), dtype=torch.float32, device=dy.device)
     ext.ln_bwd(dy.data_ptr(), h.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(), dh.data_ptr(),
                _ext.ptr(dx), _ext.ptr(dgamma), _ext.ptr(dbeta), int(accumulate), ws.data_ptr(), M, C, float(p_in),
-               int(seed_in), float(p_out), int(seed_out), _st(dy.device))
+               int(seed_in), float(p_out), int(seed_out), _st(dy.device), _ext.ptr(dsum))
     return dh, dx
 
 

@@ -68,7 +68,7 @@ long ca_ln_workspace_floats(long, int);
 int ca_ln_fwd(const bf16_t*, const bf16_t*, const float*, const float*, bf16_t*, bf16_t*, float*, float*, long, int,
               float, float, uint64_t, float, uint64_t, hipStream_t);
 int ca_ln_bwd(const bf16_t*, const bf16_t*, const float*, const float*, const float*, bf16_t*, bf16_t*, float*, float*,
-              int, float*, long, int, float, uint64_t, float, uint64_t, hipStream_t);
+              int, float*, long, int, float, uint64_t, float, uint64_t, hipStream_t, float*);
 long ca_colsum_workspace_floats(long, int);
 int ca_colsum(const bf16_t*, long, int, long, float*, int, float*, hipStream_t);
 int ca_embed_sum(const int32_t*, const int32_t*, const float*, const float*, const float*, bf16_t*, long, int, int, int,
@@ -262,11 +262,13 @@ PYBIND11_MODULE(_C, m) {
           "ln_fwd");
   });
   m.def("ln_bwd", [](u64 dy, u64 h, u64 mu, u64 rs, u64 g, u64 dh, u64 dx, u64 dg, u64 db, int acc, u64 ws, long M,
-                     int C, float p_in, u64 seed_in, float p_out, u64 seed_out, u64 s) {
+                     int C, float p_in, u64 seed_in, float p_out, u64 seed_out, u64 s, u64 dsum) {
     check(ca_ln_bwd(P(const bf16_t*, dy), P(const bf16_t*, h), P(const float*, mu), P(const float*, rs),
                     P(const float*, g), P(bf16_t*, dh), P(bf16_t*, dx), P(float*, dg), P(float*, db), acc,
-                    P(float*, ws), M, C, p_in, seed_in, p_out, seed_out, S(s)), "ln_bwd");
-  });
+                    P(float*, ws), M, C, p_in, seed_in, p_out, seed_out, S(s), P(float*, dsum)), "ln_bwd");
+  }, py::arg("dy"), py::arg("h"), py::arg("mu"), py::arg("rs"), py::arg("g"), py::arg("dh"), py::arg("dx"),
+        py::arg("dg"), py::arg("db"), py::arg("acc"), py::arg("ws"), py::arg("M"), py::arg("C"), py::arg("p_in"),
+        py::arg("seed_in"), py::arg("p_out"), py::arg("seed_out"), py::arg("s"), py::arg("dsum") = 0);
   m.def("colsum_workspace_floats", [](long M, int N) { return ca_colsum_workspace_floats(M, N); });
   m.def("colsum", [](u64 x, long M, int N, long ld, u64 out, int acc, u64 ws, u64 s) {
     check(ca_colsum(P(const bf16_t*, x), M, N, ld, P(float*, out), acc, P(float*, ws), S(s)), "colsum");

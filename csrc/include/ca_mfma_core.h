@@ -656,7 +656,9 @@ struct GDenseNC {
     constexpr int CPR = R / 8;  // chunks per k-row
     const int k = tid / CPR, pc = tid % CPR;
     int n = r0 + ((pc ^ nc_swz<R>(k)) << 3);
-    if (n > rlimit - 8) n = rlimit - 8;
+    // launchers guarantee rlimit % 8 == 0 and rlimit >= 8 (N < 8 is refused host-side); the
+    // clamp keeps a fully out-of-range column chunk on the last real one
+    if (n > rlimit - 8) n = rlimit - 8 > 0 ? rlimit - 8 : 0;
     colp = p + n;
     krow0 = k;
   }

@@ -457,7 +457,7 @@ CoreParams conv_params(int Nb, int H, int W, int Cin, int Cout, int KH, int KW, 
 }
 
 bool geom_ok(int Cin, int Cout, long pixels) {
-  return Cin % 8 == 0 && Cout % 8 == 0 && pixels < (1L << 31);
+  return Cin >= 8 && Cout >= 8 && Cin % 8 == 0 && Cout % 8 == 0 && pixels > 0 && pixels < (1L << 31);
 }
 
 }  // namespace

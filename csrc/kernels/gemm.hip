@@ -177,7 +177,7 @@ int ca_splitk_reduce(const float* ws, int splits, long MN, void* out, int out_bf
 // C = A*B (+ beta*C) in bf16.  stats != null -> per-128-row-tile column [sum|sumsq] partials.
 int ca_gemm_bf16(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc,
                  int M, int N, int K, float* stats, float beta, hipStream_t s) {
-  if (N % 8 != 0 || K % 8 != 0 || (layout == 2 && M % 8 != 0)) return -1;
+  if (M <= 0 || N < 8 || N % 8 != 0 || K % 8 != 0 || (layout == 2 && M % 8 != 0)) return -1;
   CoreParams p = base_params(A, lda, B, ldb, C, ldc, M, N, K);
   p.stats = stats;
   p.beta = beta;
@@ -205,7 +205,7 @@ int ca_gemm_bf16_bnstats(int layout, const bf16_t* A, long lda, const bf16_t* B,
 int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N,
                   int K, float beta, const bf16_t* res_src, const uint8_t* res_mask, const bf16_t* bnz,
                   const uint8_t* bnmask, float* stats, hipStream_t s) {
-  if (N % 8 != 0 || K % 8 != 0 || layout != 1 || (bnz && !stats)) return -1;
+  if (M <= 0 || N < 8 || N % 8 != 0 || K % 8 != 0 || layout != 1 || (bnz && !stats)) return -1;
   CoreParams p = base_params(A, lda, B, ldb, C, ldc, M, N, K);
   p.beta = beta;
   p.res_src = res_src;
@@ -226,7 +226,7 @@ int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long l
 int ca_gemm_ex(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N,
                int K, float* stats, float beta, const float* bias, int act, bf16_t* preact, const bf16_t* dact_src,
                long ld_aux, hipStream_t s) {
-  if (N % 8 != 0 || K % 8 != 0 || (layout == 2 && M % 8 != 0)) return -1;
+  if (M <= 0 || N < 8 || N % 8 != 0 || K % 8 != 0 || (layout == 2 && M % 8 != 0)) return -1;
   if ((preact || dact_src) && ld_aux % 8 != 0) return -1;
   CoreParams p = base_params(A, lda, B, ldb, C, ldc, M, N, K);
   p.stats = stats;
@@ -249,7 +249,7 @@ int ca_gemm_splitk_effective(int K, int splits) {
 // `out` (bf16 if out_bf16 else fp32): out = sum + beta*out.
 int ca_gemm_splitk(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, void* out, int out_bf16,
                    float beta, int M, int N, int K, int splits, float* ws, hipStream_t s) {
-  if (N % 8 != 0 || (layout == 2 && M % 8 != 0)) return -1;
+  if (M <= 0 || N < 8 || N % 8 != 0 || (layout == 2 && M % 8 != 0)) return -1;
   int kps = (K / splits + BK - 1) / BK * BK;
   if (kps < BK) kps = BK;
   splits = (K + kps - 1) / kps;

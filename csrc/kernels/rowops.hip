@@ -107,16 +107,19 @@ __global__ void __launch_bounds__(LN_BLK) ln_bwd_kernel(const bf16_t* __restrict
                                                         const float* __restrict__ gamma, bf16_t* __restrict__ dh,
                                                         bf16_t* __restrict__ dx, float* __restrict__ part, long M,
                                                         int C, DropCfg din, DropCfg dout) {
-  extern __shared__ float red[];  // [4 waves][2][C]
+  extern __shared__ float red[];  // [4 waves][3][C]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int C4 = C >> 2;
-  float ag[NV][4], ab[NV][4], g[NV][4];
+  // ag / ab: dgamma / dbeta partials; ax: column sums of the gradient this LN hands on
+  // (dx after the input dropout, else dh) -- the bias gradient of the dense layer whose
+  // output fed the LN (BERT: bo, b2), so no separate column-sum pass re-reads it
+  float ag[NV][4], ab[NV][4], ax[NV][4], g[NV][4];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c4 = lane + 64 * i;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      ag[i][j] = ab[i][j] = 0.f;
+      ag[i][j] = ab[i][j] = ax[i][j] = 0.f;
       g[i][j] = c4 < C4 ? gamma[4 * c4 + j] : 0.f;
     }
   }
@@ -161,6 +164,8 @@ __global__ void __launch_bounds__(LN_BLK) ln_bwd_kernel(const bf16_t* __restrict
         for (int j = 0; j < 4; ++j) o[j] *= din.on ? drop_mul(din, base + 4 * c4 + j) : 1.f;
         store4(dx + base + 4 * c4, o);
       }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ax[i][j] += o[j];
     }
   }
 #pragma unroll
@@ -169,31 +174,32 @@ __global__ void __launch_bounds__(LN_BLK) ln_bwd_kernel(const bf16_t* __restrict
     if (c4 < C4) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        red[(wave * 2 + 0) * C + 4 * c4 + j] = ag[i][j];
-        red[(wave * 2 + 1) * C + 4 * c4 + j] = ab[i][j];
+        red[(wave * 3 + 0) * C + 4 * c4 + j] = ag[i][j];
+        red[(wave * 3 + 1) * C + 4 * c4 + j] = ab[i][j];
+        red[(wave * 3 + 2) * C + 4 * c4 + j] = ax[i][j];
       }
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < 2 * C; c += LN_BLK) {
+  for (int c = threadIdx.x; c < 3 * C; c += LN_BLK) {
     const int k = c / C, col = c - k * C;
     float t = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) t += red[(w * 2 + k) * C + col];
-    part[(long)blockIdx.x * 2 * C + c] = t;
+    for (int w = 0; w < 4; ++w) t += red[(w * 3 + k) * C + col];
+    part[(long)blockIdx.x * 3 * C + c] = t;
   }
 }
 
-// out[c] (+)= sum_p part[p*stride + c], for c < N; out2 (optional) gets columns N..2N-1.
-// Block = 16 columns x 16 part-lanes (enough waves in flight to hide the
-// partial-slab reads; deterministic fixed-order tree).
+// out[c] (+)= sum_p part[p*stride + c], for c < N; out2 / out3 (optional) get columns
+// N..2N-1 / 2N..3N-1.  Block = 16 columns x 16 part-lanes (enough waves in flight to
+// hide the partial-slab reads; deterministic fixed-order tree).
 __global__ void __launch_bounds__(256) col_finalize_kernel(const float* __restrict__ part, int nparts, long stride,
                                                            int N, float* __restrict__ out, float* __restrict__ out2,
-                                                           int accumulate) {
+                                                           int accumulate, float* __restrict__ out3 = nullptr) {
   __shared__ float red[16][17];
   const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
-  const int total = out2 ? 2 * N : N;
+  const int total = out3 ? 3 * N : (out2 ? 2 * N : N);
   float t = 0.f;
   if (c < total) {
 #pragma unroll 4
@@ -205,9 +211,10 @@ __global__ void __launch_bounds__(256) col_finalize_kernel(const float* __restri
   t = 0.f;
 #pragma unroll
   for (int k = 0; k < 16; ++k) t += red[k][cl];
-  float* dst = c < N ? out : out2;
+  const int k = c / N;
+  float* dst = k == 0 ? out : (k == 1 ? out2 : out3);
   if (!dst) return;
-  float* o = dst + (c < N ? c : c - N);
+  float* o = dst + (c - k * N);
   *o = accumulate ? *o + t : t;
 }
 
@@ -348,7 +355,7 @@ int ln_fwd_launch(const bf16_t* x, const bf16_t* res, const float* g, const floa
 template <int NV>
 int ln_bwd_launch(const bf16_t* dy, const bf16_t* h, const float* mu, const float* rs, const float* g, bf16_t* dh,
                   bf16_t* dx, float* part, int nblk, long M, int C, DropCfg din, DropCfg dout, hipStream_t s) {
-  ln_bwd_kernel<NV><<<nblk, LN_BLK, 8 * C * sizeof(float), s>>>(dy, h, mu, rs, g, dh, dx, part, M, C, din, dout);
+  ln_bwd_kernel<NV><<<nblk, LN_BLK, 12 * C * sizeof(float), s>>>(dy, h, mu, rs, g, dh, dx, part, M, C, din, dout);
   return 0;
 }
 
@@ -361,7 +368,7 @@ int ln_nblk(long M) {
 
 extern "C" {
 
-long ca_ln_workspace_floats(long M, int C) { return (long)ln_nblk(M) * 2 * C; }
+long ca_ln_workspace_floats(long M, int C) { return (long)ln_nblk(M) * 3 * C; }
 
 // y = drop_out(LN(res + drop_in(x))); h_out (optional) keeps the pre-norm sum for the backward.
 int ca_ln_fwd(const bf16_t* x, const bf16_t* res, const float* gamma, const float* beta, bf16_t* y, bf16_t* h_out,
@@ -383,11 +390,12 @@ int ca_ln_fwd(const bf16_t* x, const bf16_t* res, const float* gamma, const floa
   return 0;
 }
 
-// dh = LN'(drop_out'(dy)); dx = drop_in'(dh) when dx != null; dgamma/dbeta (+)= column sums.
+// dh = LN'(drop_out'(dy)); dx = drop_in'(dh) when dx != null; dgamma/dbeta (+)= column sums;
+// dsum (optional) (+)= column sums of dx (or dh): the upstream dense layer's bias gradient.
 int ca_ln_bwd(const bf16_t* dy, const bf16_t* h, const float* mean, const float* rstd, const float* gamma, bf16_t* dh,
               bf16_t* dx, float* dgamma, float* dbeta, int accumulate, float* ws, long M, int C, float p_in,
-              uint64_t seed_in, float p_out, uint64_t seed_out, hipStream_t s) {
-  if (C % 4 != 0 || C > 2048) return -1;
+              uint64_t seed_in, float p_out, uint64_t seed_out, hipStream_t s, float* dsum) {
+  if (C % 4 != 0 || C > 1344) return -1;  // 12*C floats of dynamic LDS stay within 64 KB
   const DropCfg din = make_drop(p_in, seed_in), dout = make_drop(p_out, seed_out);
   const int nv = (C / 4 + 63) / 64;
   const int nblk = ln_nblk(M);
@@ -399,8 +407,9 @@ int ca_ln_bwd(const bf16_t* dy, const bf16_t* h, const float* mean, const float*
     default: ln_bwd_launch<8>(dy, h, mean, rstd, gamma, dh, dx, ws, nblk, M, C, din, dout, s); break;
   }
   CA_LAUNCH_CHECK();
-  if (dgamma || dbeta) {
-    col_finalize_kernel<<<ca_cdiv(2 * C, 16), 256, 0, s>>>(ws, nblk, 2L * C, C, dgamma, dbeta, accumulate);
+  if (dgamma || dbeta || dsum) {
+    col_finalize_kernel<<<ca_cdiv((dsum ? 3 : 2) * C, 16), 256, 0, s>>>(ws, nblk, 3L * C, C, dgamma, dbeta,
+                                                                        accumulate, dsum);
     CA_LAUNCH_CHECK();
   }
   return 0;

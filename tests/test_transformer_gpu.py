@@ -64,8 +64,9 @@ def test_layernorm_fwd_bwd(M, C, res, p_in, p_out):
     dg = torch.zeros(C, device=DEV)
     db = torch.ones(C, device=DEV)  # accumulate semantics
     hh = h if h is not None else x
+    dsum = torch.full((C,), 0.5, device=DEV)  # accumulate semantics
     dh, dx = raw.ln_bwd(dy, hh, mu, rs, g, dg, db, p_in=p_in, seed_in=s_in, p_out=p_out, seed_out=s_out,
-                        want_dx=True)
+                        want_dx=True, dsum=dsum)
 
     xr = x.float().requires_grad_()
     gr, br = g.clone().requires_grad_(), b.clone().requires_grad_()
@@ -84,6 +85,7 @@ def test_layernorm_fwd_bwd(M, C, res, p_in, p_out):
     assert rel(dx, xr.grad) < 2e-2
     assert rel(dg, gr.grad) < 1e-2
     assert rel(db - 1, br.grad) < 1e-2
+    assert rel(dsum - 0.5, xr.grad.sum(0)) < 2e-2  # the upstream layer's bias gradient
 
 
 @pytest.mark.parametrize("act", ["gelu", "tanh", "relu", "gelu_tanh"])
