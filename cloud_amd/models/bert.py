@@ -36,6 +36,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import config
 from ..ops import _ext, raw
 from ..ops.dense import dense
 from ..ops.dropout import next_seed
@@ -211,7 +212,10 @@ class _LayerFn(torch.autograd.Function):
         side = SideWork(dy2.device)
         deferred = []
 
+        fuse_bias = config.get("CLOUD_AMD_LN_BIAS_SUM")
+
         def param_grads(dy, inp, w, b, bias_done=False):
+            bias_done = bias_done and fuse_bias
             def fn():
                 if not bias_done:
                     raw.colsum_into(dy, G(b))
@@ -227,8 +231,10 @@ class _LayerFn(torch.autograd.Function):
         # LN2 (+ residual y1, + dropout on the FFN output); the same pass sums the
         # gradient it hands to the FFN output projection into b2's gradient
         dh2, do = raw.ln_bwd(dy2, h2, m2, r2, layer.ln2_w, G(layer.ln2_w), G(layer.ln2_b), p_in=p_hidden, seed_in=s2,
-                             want_dx=True, dsum=G(layer.b2))
-        _notify(layer.ln2_b), _notify(layer.ln2_w), _notify(layer.b2)
+                             want_dx=True, dsum=G(layer.b2) if fuse_bias else None)
+        _notify(layer.ln2_b), _notify(layer.ln2_w)
+        if fuse_bias:
+            _notify(layer.b2)
         param_grads(do, f, layer.w2, layer.b2, bias_done=True)
         dpre = raw.gemm(do, layer.w2, layout=raw.NN, act=cfg.hidden_act, dact_src=pre)
         del do, f
@@ -238,8 +244,10 @@ class _LayerFn(torch.autograd.Function):
         dy1 = dh2
         # LN1 (+ residual x, + dropout on the attention output projection)
         dh1, da = raw.ln_bwd(dy1, h1, m1, r1, layer.ln1_w, G(layer.ln1_w), G(layer.ln1_b), p_in=p_hidden, seed_in=s1,
-                             want_dx=True, dsum=G(layer.bo))
-        _notify(layer.ln1_b), _notify(layer.ln1_w), _notify(layer.bo)
+                             want_dx=True, dsum=G(layer.bo) if fuse_bias else None)
+        _notify(layer.ln1_b), _notify(layer.ln1_w)
+        if fuse_bias:
+            _notify(layer.bo)
         del dy1
         param_grads(da, ctx_, layer.wo, layer.bo, bias_done=True)
         dctx = raw.gemm(da, layer.wo, layout=raw.NN)

@@ -55,6 +55,17 @@ def notify_grad_ready(param):
         r._on_grad(param)
 
 
+def _busy_ms(evs):
+    """Time the collectives of one step kept the (serial) comm path busy: each bucket
+    counts from max(its gradients ready, previous collective done) to its completion."""
+    total, prev_end = 0.0, None
+    for start, end in evs:
+        begin = start if prev_end is None or start.elapsed_time(prev_end) <= 0 else prev_end
+        total += max(begin.elapsed_time(end), 0.0)
+        prev_end = end
+    return total
+
+
 class Bucket:
     __slots__ = ("arena", "lo", "hi", "slots", "pending", "work", "launched", "index", "wire", "ev")
 
@@ -187,12 +198,10 @@ class GradAllReducer:
             ev.record(torch.cuda.current_stream(b.tensor.device))
             self._side.wait_event(ev)
             with torch.cuda.stream(self._side):
-                if self.timing:
+                if self.timing:  # start: the comm stream has caught up with this bucket's gradients
                     b.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                     b.ev[0].record(self._side)
                 b.work = dist.all_reduce(self._wire(b), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
-                if self.timing:
-                    b.ev[1].record(self._side)
         else:
             b.work = dist.all_reduce(self._wire(b), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         b.launched = True
@@ -222,7 +231,9 @@ class GradAllReducer:
             with torch.cuda.stream(self._side):
                 for b in self.buckets:
                     if b.work is not None:
-                        b.work.wait()
+                        b.work.wait()  # the comm stream waits for the collective (RCCL runs it elsewhere)
+                    if b.ev is not None:  # end: the collective has completed
+                        b.ev[1].record(self._side)
                     if b.wire is not None:
                         b.tensor.copy_(b.wire)
             torch.cuda.current_stream(self._side.device).wait_stream(self._side)
@@ -308,7 +319,7 @@ class GradAllReducer:
                 continue
             self._mon.observe(self._mon.EXPOSED_COMM, t_bwd.elapsed_time(t_join))
             if evs:
-                self._mon.observe(self._mon.ALLREDUCE, sum(a.elapsed_time(b) for a, b in evs))
+                self._mon.observe(self._mon.ALLREDUCE, _busy_ms(evs))
         self._timing_log = keep[-64:]
 
     def timing_start(self):
@@ -330,7 +341,7 @@ class GradAllReducer:
                 ar.append(t_join)
                 continue
             ex.append(t_bwd.elapsed_time(t_join))
-            ar.append(sum(s.elapsed_time(e) for s, e in evs) if evs else float("nan"))
+            ar.append(_busy_ms(evs) if evs else float("nan"))
         n = len(ex)
         return {"allreduce_ms": round(sum(ar) / n, 3), "exposed_comm_ms": round(sum(ex) / n, 3), "steps": n}
 
