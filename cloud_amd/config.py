@@ -100,7 +100,7 @@ _VARS = [
     Var("CLOUD_AMD_HBM_GB", float, 288.0, "HBM per GPU used for trial packing", "tuner"),
     Var("CLOUD_AMD_DATA", str, None, "directory of real .npz datasets (else synthetic)", "data"),
     # benchmarks / examples
-    Var("CLOUD_AMD_BENCH_BATCH", int, 512, "per-GPU batch of bench.py (sized for 288 GB HBM)", "bench"),
+    Var("CLOUD_AMD_BENCH_BATCH", int, 1024, "per-GPU batch of bench.py (41 GB of the 288 GB HBM)", "bench"),
     Var("CLOUD_AMD_EXAMPLE_CPU", bool, False, "examples: launch CPU ranks instead of GPUs", "examples"),
     Var("CLOUD_AMD_EXAMPLE_SMALL", bool, False, "examples: tiny datasets (tests)", "examples"),
     Var("CLOUD_AMD_EXAMPLE_OUT", str, None, "examples: output directory", "examples"),
