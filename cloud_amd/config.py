@@ -61,6 +61,8 @@ _VARS = [
     Var("CLOUD_AMD_SHARED_GPU", bool, False, "rehearsal: every local rank uses cuda:0 (pair with "
         "CLOUD_AMD_DIST_BACKEND=gloo on a one-GPU box)", "distributed"),
     Var("CLOUD_AMD_BUCKET_MB", float, 16.0, "gradient bucket size (MB) of the DP engine", "distributed"),
+    Var("CLOUD_AMD_STEM_TAIL", bool, True, "ResNet stem: BN + ReLU + max-pool fused (fwd) and max-pool backward "
+        "fused with the BN-backward statistics", "ops"),
     Var("CLOUD_AMD_LN_BIAS_SUM", bool, True, "BERT: the LayerNorm backward also sums the bias gradient of the "
         "projection that fed it (no separate column-sum pass)", "ops"),
     Var("CLOUD_AMD_TAIL_BUCKET_MB", float, 1.0, "cap on the last gradient bucket (the first layers' gradients, "

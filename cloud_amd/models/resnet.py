@@ -13,7 +13,9 @@ import torch
 import torch.nn as nn
 
 from . import fused_block
+from .. import config
 from ..ops import conv as conv_ops
+from ..ops import pooling as pool_ops
 from .layers import BatchNormAct, Conv2d, GlobalAvgPool, Linear, MaxPool2d
 
 
@@ -78,13 +80,21 @@ class ResNet(nn.Module):
         if self.stem_s2d and x.shape[-1] == self.in_channels and conv_ops.stem_s2d_ok(x, c1.weight, c1.stride,
                                                                                          c1.padding):
             # 7x7/2 stem as a 4x4/1 conv over the space-to-depth input (no channel pad pass)
-            x = self.maxpool(self.bn1(conv_ops.stem_conv_s2d(x, c1.weight, stats=True)))
+            x = self._stem_tail(conv_ops.stem_conv_s2d(x, c1.weight, stats=True))
         else:
             if self.stem_cin != self.in_channels:
                 x = torch.nn.functional.pad(x, (0, self.stem_cin - self.in_channels))
-            x = self.maxpool(self.bn1(self.conv1(x, stats=True)))
+            x = self._stem_tail(self.conv1(x, stats=True))
         x = self.layers(x)
         return self.fc(self.pool(x))
+
+    def _stem_tail(self, out):
+        """maxpool(bn1(conv1 output)): in training, BN + ReLU + max-pool fused into one pass
+        each way (the 112x112x64 BN output is never materialised); else the separate ops."""
+        z, part = out if isinstance(out, tuple) else (out, None)
+        if config.get("CLOUD_AMD_STEM_TAIL") and pool_ops.stem_tail_ok(z, self.bn1, self.maxpool, part):
+            return pool_ops.stem_bn_relu_maxpool(z, self.bn1, part)
+        return self.maxpool(self.bn1((z, part) if part is not None else z))
 
 
 def resnet50(**kw):

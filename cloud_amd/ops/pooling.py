@@ -78,3 +78,59 @@ def global_avg_pool_nhwc(x):
     if x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0 and _ext.use_native(x):
         return _GapFn.apply(x)
     return x.mean(dim=(1, 2))
+
+
+class _StemTailFn(torch.autograd.Function):
+    """maxpool3x3/2/1(relu(BN(z))) for the ResNet stem in one pass each way.
+
+    Forward: the BN statistics come from the stem convolution's epilogue partials
+    (statistics-only finalize), then ``bn_relu_maxpool_s2k3`` applies BN + ReLU while
+    pooling -- the 112x112x64 BN output is never written.  Backward: the max-pool
+    gradient is gated by ``pooled > 0`` (the ReLU derivative at the argmax pixel) and
+    reduced into the BN-backward statistics by the same kernel, so the BN backward
+    runs its apply pass only."""
+
+    @staticmethod
+    def forward(ctx, z, gamma, beta, running_mean, running_var, eps, momentum, partials):
+        from . import raw
+
+        ext = _ext.load(required=True)
+        N, H, W, C = z.shape
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        stats = raw.bn_fwd_stats(z, gamma, beta, running_mean, running_var, eps, momentum, partials)
+        y = torch.empty((N, OH, OW, C), dtype=torch.bfloat16, device=z.device)
+        idx = torch.empty((N, OH, OW, C), dtype=torch.uint8, device=z.device)
+        ext.bn_relu_maxpool_s2k3(z.data_ptr(), stats[2 * C:].data_ptr(), y.data_ptr(), idx.data_ptr(), N, H, W, C,
+                                 OH, OW, _ext.stream_handle(z.device))
+        ctx.save_for_backward(z, stats, y, idx, gamma)
+        ctx.has_beta = beta is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import raw
+
+        ext = _ext.load(required=True)
+        z, stats, y, idx, gamma = ctx.saved_tensors
+        N, H, W, C = z.shape
+        OH, OW = y.shape[1], y.shape[2]
+        dev = z.device
+        g = torch.empty_like(z)
+        parts = torch.empty((ext.maxpool_bnstats_parts(N, H, W, C), 2, C), dtype=torch.float32, device=dev)
+        ext.maxpool_bwd_s2k3_bnstats(dy.contiguous().data_ptr(), y.data_ptr(), idx.data_ptr(), z.data_ptr(),
+                                     g.data_ptr(), parts.data_ptr(), N, H, W, C, OH, OW, _ext.stream_handle(dev))
+        dgamma = torch.empty(C, dtype=torch.float32, device=dev) if gamma is not None else None
+        dbeta = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_beta else None
+        dz, _ = raw.bn_bwd(g, None, z, gamma, stats, False, dgamma=dgamma, dbeta=dbeta, partials=parts)
+        return dz, dgamma, dbeta, None, None, None, None, None
+
+
+def stem_tail_ok(z, bn, pool, partials):
+    return (bn.training and bn.relu and partials is not None and z.is_cuda and z.dtype == torch.bfloat16
+            and z.is_contiguous() and z.shape[-1] % 8 == 0 and 256 % (z.shape[-1] // 8) == 0
+            and (pool.k, pool.stride, pool.padding) == (3, 2, 1) and _ext.use_native(z))
+
+
+def stem_bn_relu_maxpool(z, bn, partials):
+    """The ResNet stem tail ``maxpool(bn1(z))`` of a training step, fused (see _StemTailFn)."""
+    return _StemTailFn.apply(z, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, bn.momentum, partials)

@@ -50,6 +50,10 @@ int ca_gap_fwd(const bf16_t*, void*, int, int, int, int, hipStream_t);
 int ca_gap_bwd(const void*, int, bf16_t*, int, int, int, hipStream_t);
 int ca_gemm_bf16(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float*, float,
                  hipStream_t);
+int ca_bn_relu_maxpool_s2k3(const bf16_t*, const float*, bf16_t*, uint8_t*, int, int, int, int, int, int, hipStream_t);
+int ca_maxpool_bnstats_parts(int, int, int, int);
+int ca_maxpool_bwd_s2k3_bnstats(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, bf16_t*, float*, int, int,
+                                int, int, int, int, hipStream_t);
 int ca_conv_fwd_ex(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int,
                    const float*, int, hipStream_t);
 int ca_conv_fwd(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int, float*,
@@ -220,6 +224,18 @@ PYBIND11_MODULE(_C, m) {
                        int ph, int pw, u64 stats, u64 s) {
     check(ca_conv_fwd(P(const bf16_t*, x), P(const bf16_t*, w), P(bf16_t*, y), Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph,
                       pw, P(float*, stats), S(s)), "conv_fwd");
+  });
+  m.def("bn_relu_maxpool_s2k3", [](u64 z, u64 ss, u64 y, u64 idx, int N, int H, int W, int C, int OH, int OW,
+                                   u64 s) {
+    check(ca_bn_relu_maxpool_s2k3(P(const bf16_t*, z), P(const float*, ss), P(bf16_t*, y), P(uint8_t*, idx), N, H, W,
+                                  C, OH, OW, S(s)), "bn_relu_maxpool_s2k3");
+  });
+  m.def("maxpool_bnstats_parts", [](int N, int H, int W, int C) { return ca_maxpool_bnstats_parts(N, H, W, C); });
+  m.def("maxpool_bwd_s2k3_bnstats", [](u64 dy, u64 yp, u64 idx, u64 z, u64 g, u64 part, int N, int H, int W, int C,
+                                       int OH, int OW, u64 s) {
+    check(ca_maxpool_bwd_s2k3_bnstats(P(const bf16_t*, dy), P(const bf16_t*, yp), P(const uint8_t*, idx),
+                                      P(const bf16_t*, z), P(bf16_t*, g), P(float*, part), N, H, W, C, OH, OW, S(s)),
+          "maxpool_bwd_s2k3_bnstats");
   });
   m.def("conv_fwd_ex", [](u64 x, u64 w, u64 y, int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh,
                           int sw, int ph, int pw, u64 bias, int act, u64 s) {

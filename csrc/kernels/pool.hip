@@ -236,7 +236,187 @@ __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_kernel(const bf16_t* __r
   }
 }
 
+
+// ResNet stem tail, forward: y = maxpool3x3/2/1(relu(z * scale + shift)) in one pass over
+// the stem convolution output z -- the BatchNorm+ReLU output (the largest activation of
+// the network, 64 ch at 112x112) is never written or re-read.  Each window element is
+// rounded to bf16 before the max, exactly as the separate BN-apply + max-pool would see
+// it; the 1-byte argmax per output channel feeds the backward.  ss = [scale C | shift C].
+__global__ void __launch_bounds__(256) bn_relu_maxpool_s2k3_kernel(const bf16_t* __restrict__ z,
+                                                                  const float* __restrict__ ss,
+                                                                  bf16_t* __restrict__ y, uint8_t* __restrict__ idx,
+                                                                  int N, int H, int W, int C, int OH, int OW) {
+  const int CT = C / 8;
+  const long total = (long)N * OH * OW * CT;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int vc = (int)(t % CT);
+    long r = t / CT;
+    const int ow = (int)(r % OW); r /= OW;
+    const int oh = (int)(r % OH);
+    const int n = (int)(r / OH);
+    float sc[8], sh[8], best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = ss[vc * 8 + j];
+      sh[j] = ss[C + vc * 8 + j];
+      best[j] = -INFINITY;
+      bi[j] = 0;
+    }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int h = oh * 2 - 1 + kh;
+      if (h < 0 || h >= H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int w = ow * 2 - 1 + kw;
+        if (w < 0 || w >= W) continue;
+        us8 v = *reinterpret_cast<const us8*>(z + (((long)n * H + h) * W + w) * C + vc * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float f = fmaxf(bf2f(v[j]) * sc[j] + sh[j], 0.f);
+          f = bf2f(f2bf(f));
+          if (f > best[j]) { best[j] = f; bi[j] = (uint8_t)(kh * 3 + kw); }
+        }
+      }
+    }
+    us8 o;
+    uint64_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = f2bf(best[j]);
+      packed |= (uint64_t)bi[j] << (8 * j);
+    }
+    const long oo = (((long)n * OH + oh) * OW + ow) * C + vc * 8;
+    *reinterpret_cast<us8*>(y + oo) = o;
+    *reinterpret_cast<uint64_t*>(idx + oo) = packed;
+  }
+}
+
+// ResNet stem tail, backward of the max-pool fused with the BatchNorm-backward statistics:
+// one thread per 2x2 block of stem pixels (8 channels) as maxpool_bwd_s2k3_kernel, but a
+// window's gradient is gated by its pooled output > 0 (= the ReLU derivative at its argmax
+// pixel, so no ReLU mask exists), and the gated gradient g it writes is also reduced into
+// per-block channel partials [sum g | sum g*z] -- the BN backward skips its statistics
+// pass over g and z.  The grid is fixed (grid-stride loop); 256 % (C/8) == 0 keeps each
+// thread on one channel group.
+__global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnstats_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ ypool, const uint8_t* __restrict__ idx,
+    const bf16_t* __restrict__ z, bf16_t* __restrict__ g, float* __restrict__ part, int N, int H, int W, int C,
+    int OH, int OW) {
+  __shared__ float red[256][17];
+  const int CT = C / 8;
+  const int Hb = (H + 1) / 2, Wb = (W + 1) / 2;
+  const long total = (long)N * Hb * Wb * CT;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (long t = t0; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int vc = (int)(t % CT);
+    long r = t / CT;
+    const int bj = (int)(r % Wb); r /= Wb;
+    const int bi = (int)(r % Hb);
+    const int n = (int)(r / Hb);
+    float acc[2][2][8];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[a][b][j] = 0.f;
+#pragma unroll
+    for (int wy = 0; wy < 2; ++wy) {
+      const int oh = bi + wy;
+      if (oh >= OH) continue;
+#pragma unroll
+      for (int wx = 0; wx < 2; ++wx) {
+        const int ow = bj + wx;
+        if (ow >= OW) continue;
+        const long oo = (((long)n * OH + oh) * OW + ow) * C + vc * 8;
+        const us8 gv = *reinterpret_cast<const us8*>(dy + oo);
+        const us8 yv = *reinterpret_cast<const us8*>(ypool + oo);
+        const uint64_t id = *reinterpret_cast<const uint64_t*>(idx + oo);
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const int kh = a + 1 - 2 * wy;
+          if (kh < 0 || kh > 2) continue;
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int kw = b + 1 - 2 * wx;
+            if (kw < 0 || kw > 2) continue;
+            const uint32_t want = (uint32_t)(kh * 3 + kw);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (((id >> (8 * j)) & 0xff) == want && bf2f(yv[j]) > 0.f) acc[a][b][j] += bf2f(gv[j]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int h = 2 * bi + a;
+      if (h >= H) continue;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int w = 2 * bj + b;
+        if (w >= W) continue;
+        const long off = (((long)n * H + h) * W + w) * C + vc * 8;
+        const us8 zv = *reinterpret_cast<const us8*>(z + off);
+        us8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          o[j] = f2bf(acc[a][b][j]);
+          const float gr = bf2f(o[j]);  // the stored (bf16) gradient, as the BN backward reads it
+          s1[j] += gr;
+          s2[j] += gr * bf2f(zv[j]);
+        }
+        *reinterpret_cast<us8*>(g + off) = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[threadIdx.x][j] = s1[j];
+    red[threadIdx.x][8 + j] = s2[j];
+  }
+  __syncthreads();
+  // channel c = 8*vc + j lives in threads vc, vc + CT, vc + 2CT, ... of this block
+  for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) {
+    const int k = c / C, cc = c - k * C, vc = cc >> 3, j = cc & 7;
+    float tsum = 0.f;
+    for (int th = vc; th < 256; th += CT) tsum += red[th][8 * k + j];
+    part[(long)blockIdx.x * 2 * C + c] = tsum;
+  }
+}
+
 extern "C" {
+
+int ca_bn_relu_maxpool_s2k3(const bf16_t* z, const float* ss, bf16_t* y, uint8_t* idx, int N, int H, int W, int C,
+                            int OH, int OW, hipStream_t st) {
+  if (C % 8 != 0 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
+  const long total = (long)N * OH * OW * (C / 8);
+  const int grid = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  bn_relu_maxpool_s2k3_kernel<<<grid, 256, 0, st>>>(z, ss, y, idx, N, H, W, C, OH, OW);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+// blocks of the fixed grid (= rows of the partials) ca_maxpool_bwd_s2k3_bnstats uses
+int ca_maxpool_bnstats_parts(int N, int H, int W, int C) {
+  const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+  const long b = (total + 255) / 256;
+  return (int)(b < 1024 ? b : 1024);
+}
+
+int ca_maxpool_bwd_s2k3_bnstats(const bf16_t* dy, const bf16_t* ypool, const uint8_t* idx, const bf16_t* z, bf16_t* g,
+                                float* part, int N, int H, int W, int C, int OH, int OW, hipStream_t st) {
+  if (C % 8 != 0 || 256 % (C / 8) != 0 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
+  maxpool_bwd_s2k3_bnstats_kernel<<<ca_maxpool_bnstats_parts(N, H, W, C), 256, 0, st>>>(dy, ypool, idx, z, g, part,
+                                                                                         N, H, W, C, OH, OW);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
 
 int ca_stem_s2d(const bf16_t* x, bf16_t* y, int N, int H, int W, int C, int Hs, int Ws, int pad, hipStream_t st) {
   if (C < 1 || C > 4) return -1;
