@@ -51,21 +51,24 @@ from ..runtime.side_stream import SideWork
 # Cross-block hand-off of bn3 statistics (one slot: blocks run backward one after
 # another).  The parked gradient is held so its memory cannot be reused by another
 # tensor while parked; the consumer checks identity (storage, shape, version).
-_HANDOFF = {"grad": None, "version": -1, "partials": None}
+_HANDOFF = {"grad": None, "version": -1, "partials": None, "partials2": None}
 
 
-def _park(grad, partials):
-    _HANDOFF.update(grad=grad, version=grad._version, partials=partials)
+def _park(grad, partials, partials2=None):
+    _HANDOFF.update(grad=grad, version=grad._version, partials=partials, partials2=partials2)
 
 
 def _take(dout):
-    g, ver, part = _HANDOFF["grad"], _HANDOFF["version"], _HANDOFF["partials"]
-    _HANDOFF.update(grad=None, version=-1, partials=None)
+    """(bn3 partials, projection-shortcut BN partials) parked for this block's output
+    gradient ``dout`` by the next block's conv1 dgrad epilogue, else (None, None)."""
+    g, ver = _HANDOFF["grad"], _HANDOFF["version"]
+    part, part2 = _HANDOFF["partials"], _HANDOFF["partials2"]
+    _HANDOFF.update(grad=None, version=-1, partials=None, partials2=None)
     if g is None or part is None:
-        return None
+        return None, None
     if g.data_ptr() != dout.data_ptr() or g.shape != dout.shape or dout._version != ver:
-        return None
-    return part
+        return None, None
+    return part, part2
 
 
 def _arena_grad(p, dtype):
@@ -144,7 +147,9 @@ class _BottleneckFn(torch.autograd.Function):
         (s1, m1), (s2, m2), (s3, m3) = s1, s2, s3
         ctx.save_for_backward(x, z1, y1, z2, y2, z3, s1, m1, s2, m2, s3, m3,
                               *((zd, sd[0]) if ds is not None else ()))
-        blk._ca_out_src = (z3, m3)
+        # (z3, m3[, zd]): the next block's conv1 dgrad epilogue computes this block's bn3
+        # backward statistics -- and the shortcut BN's, whose input zd sees the same gradient
+        blk._ca_out_src = (z3, m3, zd) if ds is not None else (z3, m3)
         return out
 
     @staticmethod
@@ -174,12 +179,17 @@ class _BottleneckFn(torch.autograd.Function):
             return r
 
         def dgrad(conv, dz, shape, bn_src, out=None, beta=0.0, res=None):
-            """Input gradient; with ``bn_src`` = (z, mask) of the BN that consumes it,
-            also that BN's backward statistics from the epilogue."""
+            """Input gradient; with ``bn_src`` = (z, mask[, z2]) of the BN(s) that consume it,
+            also their backward statistics from the epilogue.  Returns (dx, partials,
+            partials2); z2 is honoured by the residual-gated (``res``) form only."""
             bn = bn_src if (epi and bn_src is not None) else None
+            if bn is not None and res is None:
+                bn = bn[:2]
             r = raw.conv_dgrad(dz, conv.weight, shape, conv.stride, conv.padding, out=out, beta=beta, bn=bn,
                                res=res)
-            return r if bn is not None else (r, None)
+            if bn is None:
+                return r, None, None
+            return (r[0], r[1], r[2] if len(r) > 2 else None)
 
         side = SideWork(x.device)
         deferred = []
@@ -195,14 +205,14 @@ class _BottleneckFn(torch.autograd.Function):
         # the residual gradient dout * relu'(m3) is never materialised: identity blocks gate
         # it in conv1's dgrad epilogue (res=), projection blocks in the shortcut BN backward
         gate_res = m3 is not None
-        dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=not gate_res,
-                            partials=_take(dout) if epi else None)
-        dy2, p2 = dgrad(blk.conv3, dz3, y2.shape, (z2, m2))
+        p3, p_short = _take(dout) if epi else (None, None)
+        dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=not gate_res, partials=p3)
+        dy2, p2, _ = dgrad(blk.conv3, dz3, y2.shape, (z2, m2))
         wgrad(blk.conv3, dz3, y2)
         del dz3
         dz2, _ = bn_back(blk.bn2, dy2, z2, (s2, m2), partials=p2)
         del dy2, p2
-        dy1, p1 = dgrad(blk.conv2, dz2, y1.shape, (z1, m1))
+        dy1, p1, _ = dgrad(blk.conv2, dz2, y1.shape, (z1, m1))
         wgrad(blk.conv2, dz2, y1)
         del dz2
         dz1, _ = bn_back(blk.bn1, dy1, z1, (s1, m1), partials=p1)
@@ -210,7 +220,7 @@ class _BottleneckFn(torch.autograd.Function):
         if ds is not None:
             zd, sd = saved[12], saved[13]
             if gate_res:
-                dzd, _ = bn_back(ds["bn"], dout, zd, (sd, None), gate=m3)
+                dzd, _ = bn_back(ds["bn"], dout, zd, (sd, None), gate=m3, partials=p_short)
             else:
                 dzd, _ = bn_back(ds["bn"], dres, zd, (sd, None))
             del dres
@@ -223,11 +233,11 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             dx = dres  # identity gradient; conv1's input gradient is summed into it below
         # the last write of dx: its epilogue sees the complete block-input gradient
-        _, p_prev = dgrad(blk.conv1, dz1, x.shape, ctx.prev_src, out=dx, beta=1.0,
-                          res=(dout, m3) if (gate_res and ds is None) else None)
+        _, p_prev, p_prev2 = dgrad(blk.conv1, dz1, x.shape, ctx.prev_src, out=dx, beta=1.0,
+                                   res=(dout, m3) if (gate_res and ds is None) else None)
         del dout
         if p_prev is not None:
-            _park(dx, p_prev)
+            _park(dx, p_prev, p_prev2)
         ctx.prev_src = None
         wgrad(blk.conv1, dz1, x)
         # join: later kernels on the main stream (and DDP's bucket events recorded on it)

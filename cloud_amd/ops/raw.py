@@ -67,7 +67,9 @@ def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res
 
     ``res=(src, mask)`` (1x1 convolutions): dx = dgrad + beta * relu'(mask) * src -- a
     residual-path gradient gated on the fly from the block's output gradient instead of
-    being materialised by the BN backward first."""
+    being materialised by the BN backward first.  With ``res``, ``bn`` may carry a third
+    entry ``z2``: the input of a second BN fed by the same gated gradient (a projection
+    shortcut's BN); ``(dx, partials, partials2)`` is then returned."""
     ext = _ext.load(required=True)
     N, H, W, Cin = x_shape
     Cout, KH, KW, _ = w.shape
@@ -76,17 +78,25 @@ def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res
         src, rmask = res
         assert is_gemm_conv(w, stride, padding) and src.shape == dx.shape and src.is_contiguous()
         assert rmask is None or rmask.shape == (N * H * W, Cin // 8)
-        part, zp, mp = None, 0, 0
+        part, part2, zp, mp, z2p = None, None, 0, 0, 0
         if bn is not None:
-            z, mask = bn
+            z, mask = bn[0], bn[1]
             assert z.shape == dx.shape and z.is_contiguous()
             part = torch.empty(((N * H * W + 127) // 128, 2, Cin), dtype=torch.float32, device=dy.device)
             zp, mp = z.data_ptr(), _ext.ptr(mask)
+            if len(bn) > 2 and bn[2] is not None:
+                assert bn[2].shape == dx.shape and bn[2].is_contiguous()
+                part2 = torch.empty_like(part)
+                z2p = bn[2].data_ptr()
         ext.dgrad_gemm(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin, Cout,
-                       float(beta), src.data_ptr(), _ext.ptr(rmask), zp, mp, _ext.ptr(part), _st(dy.device))
-        return (dx, part) if bn is not None else dx
+                       float(beta), src.data_ptr(), _ext.ptr(rmask), zp, mp, _ext.ptr(part), _st(dy.device), z2p,
+                       _ext.ptr(part2))
+        if bn is None:
+            return dx
+        return (dx, part, part2) if len(bn) > 2 else (dx, part)
     if bn is not None:
-        z, mask = bn
+        z, mask = bn[0], bn[1]
+        assert len(bn) == 2 or bn[2] is None, "second-BN statistics need the residual-gated (res=) form"
         assert z.shape == dx.shape and z.is_contiguous() and (mask is None or mask.shape == (N * H * W, Cin // 8))
         if is_gemm_conv(w, stride, padding):
             part = torch.empty(((N * H * W + 127) // 128, 2, Cin), dtype=torch.float32, device=dy.device)

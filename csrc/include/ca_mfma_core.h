@@ -38,7 +38,10 @@ constexpr int PAD = 8;
 // instantiations, so the plain bf16 epilogue carries none of their registers.
 // EPI_BF16_BNR: EPI_BF16_BN that also honours CoreParams::res_src / res_mask (the
 // plain bf16 epilogue always does; the BN-statistics one only in this instantiation).
-enum Epi { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_BF16_BN = 2, EPI_BF16_ST = 3, EPI_BF16_BNR = 4 };
+// EPI_BF16_BNR2: EPI_BF16_BNR that also sums g * z2 for a second BatchNorm fed by the same
+// gradient (CoreParams::bnz2 / stats2: the projection shortcut's BN, whose input is the
+// shortcut convolution output and whose output gradient is the same gated block gradient).
+enum Epi { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_BF16_BN = 2, EPI_BF16_ST = 3, EPI_BF16_BNR = 4, EPI_BF16_BNR2 = 5 };
 
 // Fast unsigned division by a runtime constant (n < 2^31): q = (umulhi(n, m) + n) >> s.
 struct FastDiv {
@@ -69,6 +72,8 @@ struct CoreParams {
   // g = dy * relu'(mask) and z is the BN input (same [rows][ldc] layout as C).
   const bf16_t* bnz;
   const uint8_t* bnmask;  // ReLU bitmask [rows][N/8] (bit j = channel 8c+j active) or null
+  const bf16_t* bnz2;     // EPI_BF16_BNR2: second BN input (same layout as bnz) ...
+  float* stats2;          // ... and its partials [tiles][2][N] = [sum g | sum g*z2]
   // beta source other than C: C = acc + beta * relu'(res_mask) * res_src (same [rows][ldc]
   // layout as C) -- a residual gradient gated on the fly instead of materialised first
   const bf16_t* res_src;
@@ -336,15 +341,24 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
     constexpr int CH = BM * BN / 8;
     static_assert(CH % NT == 0, "epilogue chunks must divide the threads");
     constexpr int IT = CH / NT;
-    constexpr bool BNS = EPI == EPI_BF16_BN || EPI == EPI_BF16_BNR, STS = EPI == EPI_BF16_ST, RSTAT = BNS || STS;
+    constexpr bool Z2 = EPI == EPI_BF16_BNR2;
+    constexpr bool BNS = EPI == EPI_BF16_BN || EPI == EPI_BF16_BNR || Z2, STS = EPI == EPI_BF16_ST;
+    constexpr bool RSTAT = BNS || STS;
+    float bz2sum[Z2 ? 8 : 1];
+#pragma unroll
+    for (int j = 0; j < (Z2 ? 8 : 1); ++j) bz2sum[j] = 0.f;
     constexpr bool RES = EPI != EPI_BF16_BN;  // res_src / res_mask compiled in
+    // the smallest LDS any core gives this tile: max(C staging, one K stage of A + B)
+    static_assert(!Z2 || (3 * (NT / (BN / 8)) * BN * 4 <=
+                          (2 * BM * EL::LD > 2 * (BM + BN) * BK ? 2 * BM * EL::LD : 2 * (BM + BN) * BK)),
+                  "three statistics rows must fit the LDS");
     constexpr int PF = BNS ? (IT < 2 ? IT : 2) : 1;
     const int col = (tid % (BN / 8)) * 8;
     const int gn = n0 + col;
     const bool has_beta = P.beta != 0.f;
 #pragma unroll 1
     for (int it0 = 0; it0 < IT; it0 += PF) {
-      s8v opre[PF], zpre[BNS ? PF : 1];
+      s8v opre[PF], zpre[BNS ? PF : 1], zpre2[Z2 ? PF : 1];
       uint32_t mk[PF];  // bits 0-7: BN ReLU mask (BN-backward statistics), bits 8-15: res_mask
       long orow[PF];
       bool okr[PF];
@@ -363,6 +377,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
           zpre[u] = okr[u] ? *reinterpret_cast<const s8v*>(P.bnz + orow[u] * P.ldc + gn) : zero8();
           mk[u] |= (P.bnmask && okr[u]) ? (uint32_t)P.bnmask[orow[u] * (P.N / 8) + (gn >> 3)] : 0xffu;
         }
+        if constexpr (Z2) zpre2[u] = okr[u] ? *reinterpret_cast<const s8v*>(P.bnz2 + orow[u] * P.ldc + gn) : zero8();
       }
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
@@ -406,6 +421,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
             const float g = ((mk[u] >> j) & 1u) ? bf2f((bf16_t)v[j]) : 0.f;
             bsum[j] += g;
             bzsum[j] += g * bf2f((bf16_t)zpre[u][j]);
+            if constexpr (Z2) bz2sum[j] += g * bf2f((bf16_t)zpre2[u][j]);
           }
         }
       }
@@ -421,18 +437,25 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
       for (int j = 0; j < 8; ++j) {
         sred[part * BN + cg * 8 + j] = bsum[j];
         sred[(PARTS + part) * BN + cg * 8 + j] = bzsum[j];
+        if constexpr (Z2) sred[(2 * PARTS + part) * BN + cg * 8 + j] = bz2sum[j];
       }
       __syncthreads();
       for (int c = tid; c < BN; c += NT) {
         if (n0 + c >= P.N) continue;
-        float ts = 0.f, tq = 0.f;
+        float ts = 0.f, tq = 0.f, t2 = 0.f;
         for (int pp = 0; pp < PARTS; ++pp) {
           ts += sred[pp * BN + c];
           tq += sred[(PARTS + pp) * BN + c];
+          if constexpr (Z2) t2 += sred[(2 * PARTS + pp) * BN + c];
         }
         float* st = P.stats + (long)tm * 2 * P.N;
         st[n0 + c] = ts;
         st[P.N + n0 + c] = tq;
+        if constexpr (Z2) {
+          float* st2 = P.stats2 + (long)tm * 2 * P.N;
+          st2[n0 + c] = ts;
+          st2[P.N + n0 + c] = t2;
+        }
       }
     } else if (P.stats) {
       // per-column sum / sum of squares of the stored bf16 values of this tile

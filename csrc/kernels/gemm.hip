@@ -159,7 +159,7 @@ extern "C" {
 
 int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N,
                   int K, float beta, const bf16_t* res_src, const uint8_t* res_mask, const bf16_t* bnz,
-                  const uint8_t* bnmask, float* stats, hipStream_t s);
+                  const uint8_t* bnmask, float* stats, hipStream_t s, const bf16_t* bnz2, float* stats2);
 
 int ca_splitk_reduce(const float* ws, int splits, long MN, void* out, int out_bf16, float beta, hipStream_t s) {
   if (MN % 4) return -3;
@@ -194,18 +194,21 @@ int ca_gemm_bf16(int layout, const bf16_t* A, long lda, const bf16_t* B, long ld
 int ca_gemm_bf16_bnstats(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc,
                          int M, int N, int K, float beta, const bf16_t* bnz, const uint8_t* bnmask, float* stats,
                          hipStream_t s) {
-  return ca_dgrad_gemm(layout, A, lda, B, ldb, C, ldc, M, N, K, beta, nullptr, nullptr, bnz, bnmask, stats, s);
+  return ca_dgrad_gemm(layout, A, lda, B, ldb, C, ldc, M, N, K, beta, nullptr, nullptr, bnz, bnmask, stats, s, nullptr,
+                       nullptr);
 }
 
 // Input-gradient GEMM (NN) with the two backward epilogue options of a ResNet block:
 //   res_src [+ res_mask]: C = A*B + beta * relu'(res_mask) * res_src -- the block's
 //                         identity-path gradient gated from the output gradient on the
 //                         fly (never materialised);
-//   bnz / bnmask / stats: BN-backward statistics of C for the BN that consumes it.
+//   bnz / bnmask / stats: BN-backward statistics of C for the BN that consumes it;
+//   bnz2 / stats2 (with res_src): the same for a second BN fed by the same gated gradient.
 int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N,
                   int K, float beta, const bf16_t* res_src, const uint8_t* res_mask, const bf16_t* bnz,
-                  const uint8_t* bnmask, float* stats, hipStream_t s) {
+                  const uint8_t* bnmask, float* stats, hipStream_t s, const bf16_t* bnz2, float* stats2) {
   if (M <= 0 || N < 8 || N % 8 != 0 || K % 8 != 0 || layout != 1 || (bnz && !stats)) return -1;
+  if (bnz2 && (!bnz || !stats2 || !res_src)) return -1;
   CoreParams p = base_params(A, lda, B, ldb, C, ldc, M, N, K);
   p.beta = beta;
   p.res_src = res_src;
@@ -214,6 +217,12 @@ int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long l
   p.stats = stats;
   p.bnz = bnz;
   p.bnmask = bnmask;
+  if (bnz2) {
+    p.bnz2 = bnz2;
+    p.stats2 = stats2;
+    return want_small_n(p, 1) ? launch<128, 64, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI_BF16_BNR2>(p, 1, s)
+                              : launch<128, 128, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI_BF16_BNR2>(p, 1, s);
+  }
   if (res_src)
     return want_small_n(p, 1) ? launch<128, 64, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI_BF16_BNR>(p, 1, s)
                               : launch<128, 128, DenseKC, DenseNC, GDenseKC, GDenseNC, EPI_BF16_BNR>(p, 1, s);

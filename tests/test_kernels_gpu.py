@@ -386,8 +386,9 @@ def test_dgrad_bn_backward_stats_epilogue(k, s, p, beta, Cin):
 
 
 def test_fused_bottleneck_chain_hands_off_bn_statistics(monkeypatch):
-    """Two consecutive fused blocks: block 2's conv1 dgrad computes block 1's bn3
-    backward statistics (cross-block hand-off); gradients match the op-by-op path."""
+    """Consecutive fused blocks: block i+1's conv1 dgrad computes block i's bn3 backward
+    statistics (cross-block hand-off) -- and, when block i is a projection block, its
+    shortcut BN's statistics too; gradients match the op-by-op path."""
     from cloud_amd.models import fused_block
     from cloud_amd.models.resnet import Bottleneck
     from cloud_amd.ops import raw
@@ -396,8 +397,8 @@ def test_fused_bottleneck_chain_hands_off_bn_statistics(monkeypatch):
     torch.manual_seed(13)
     net = torch.nn.Sequential(
         Bottleneck(64, 16, 1, dtype=torch.bfloat16, device=DEV, zero_init_residual=False),
-        Bottleneck(64, 16, 1, dtype=torch.bfloat16, device=DEV, zero_init_residual=False),
-        Bottleneck(64, 32, 2, dtype=torch.bfloat16, device=DEV, zero_init_residual=False))
+        Bottleneck(64, 32, 2, dtype=torch.bfloat16, device=DEV, zero_init_residual=False),
+        Bottleneck(128, 32, 1, dtype=torch.bfloat16, device=DEV, zero_init_residual=False))
     opt = SGD(net, learning_rate=0.0)
     x = torch.randn(4, 16, 16, 64, device=DEV).to(torch.bfloat16)
     dy = torch.randn(4, 8, 8, 128, device=DEV).to(torch.bfloat16)
@@ -406,7 +407,7 @@ def test_fused_bottleneck_chain_hands_off_bn_statistics(monkeypatch):
 
     def spy(dout):
         r = orig_take(dout)
-        taken.append(r is not None)
+        taken.append((r[0] is not None, r[1] is not None))
         return r
 
     monkeypatch.setattr(fused_block, "_take", spy)
@@ -422,7 +423,9 @@ def test_fused_bottleneck_chain_hands_off_bn_statistics(monkeypatch):
         return xi.grad.float(), {n: p.grad.detach().float().clone() for n, p in net.named_parameters()}
 
     dx_e, g_e = run(True, True)
-    assert taken == [False, True, True], taken  # last block has no producer; blocks 2 and 1 take
+    # the last block has no producer; the projection block takes bn3 AND shortcut-BN
+    # statistics; the first block takes its bn3 statistics
+    assert taken == [(False, False), (True, True), (True, False)], taken
     dx_n, g_n = run(True, False)
     dx_u, g_u = run(False, False)
 

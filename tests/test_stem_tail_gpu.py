@@ -33,7 +33,11 @@ def test_stem_tail_matches_separate_ops(N, H, W):
     ya = stem_bn_relu_maxpool(za, bns[0], part)
     zb = z0.clone().requires_grad_()
     yb = pool(bns[1]((zb, part)))
-    assert torch.equal(ya, yb)  # same statistics, same bf16 rounding before the max
+    # same statistics; the apply arithmetic may differ in the last fp32 bit before the bf16
+    # rounding (scale/shift FMA vs normalise-then-affine): at most 1 bf16 ulp, rarely
+    d = (ya.float() - yb.float()).abs()
+    assert float(d.max()) <= 1e-2 * float(yb.float().abs().max()) + 1e-6, float(d.max())
+    assert float((d > 0).float().mean()) < 1e-2, float((d > 0).float().mean())
     dy = torch.randn_like(ya)
     ya.backward(dy)
     yb.backward(dy)
