@@ -70,7 +70,7 @@ _VARS = [
     Var("CLOUD_AMD_GRAD_REDUCE_DTYPE", str, "bf16", "wire dtype of the gradient all-reduce of bf16 layers: "
         "'bf16' (native, half the bytes) or 'fp32' (reduce an fp32 copy)", "distributed"),
     Var("CLOUD_AMD_RCCL_ENV", bool, True, "launcher sets the xGMI RCCL defaults (NCCL_MIN_NCHANNELS, "
-        "HSA_NO_SCRATCH_RECLAIM, NCCL_DEBUG) for multi-GPU jobs", "distributed"),
+        "HSA_NO_SCRATCH_RECLAIM) for multi-GPU jobs", "distributed"),
     Var("CLOUD_AMD_RCCL_CHANNELS", int, 0, "NCCL_MIN_NCHANNELS the launcher sets (0 = one per xGMI link)",
         "distributed"),
     Var("CLOUD_AMD_KFD_ROOT", str, "/sys/class/kfd/kfd/topology/nodes", "KFD topology root read by the "

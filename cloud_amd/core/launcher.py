@@ -94,8 +94,8 @@ def rccl_env(world, links):
       per direction).  RCCL may pick more channels by itself; this is a floor.
       ``CLOUD_AMD_RCCL_CHANNELS`` overrides the value.
     * ``HSA_NO_SCRATCH_RECLAIM=1``: keeps the ROCr scratch pool of the RCCL kernels
-      resident instead of reclaiming it after every launch.
-    * ``NCCL_DEBUG=WARN`` surfaces transport problems in the rank logs.
+      resident instead of reclaiming it after every launch (read at HIP start-up, so
+      only ranks this launcher starts get it).
 
     Gradient buckets are sized separately (``CLOUD_AMD_BUCKET_MB``, bench
     ``--bucket-mb``).  These values are a starting point that the driver's 8-GPU runs
@@ -103,7 +103,7 @@ def rccl_env(world, links):
     if world <= 1 or os.environ.get("CLOUD_AMD_RCCL_ENV", "1") == "0":
         return {}
     ch = os.environ.get("CLOUD_AMD_RCCL_CHANNELS") or str(max(links, 1))
-    return {"NCCL_MIN_NCHANNELS": ch, "HSA_NO_SCRATCH_RECLAIM": "1", "NCCL_DEBUG": "WARN"}
+    return {"NCCL_MIN_NCHANNELS": ch, "HSA_NO_SCRATCH_RECLAIM": "1"}
 
 
 def _print_logs_info(job_id, job_dir):

@@ -49,6 +49,8 @@ def init_distributed(backend=None, timeout_s=None, device=None):
         os.environ.setdefault("MASTER_PORT", "29500")
         backend = backend or os.environ.get("CLOUD_AMD_DIST_BACKEND") or (
             "nccl" if device.type == "cuda" else "gloo")
+        if backend == "nccl":
+            _rccl_defaults(w)
         timeout = datetime.timedelta(seconds=timeout_s or env_int("CLOUD_AMD_PG_TIMEOUT_S", 600))
         kw = {"device_id": device} if (backend == "nccl" and device.type == "cuda") else {}
         try:
@@ -57,6 +59,20 @@ def init_distributed(backend=None, timeout_s=None, device=None):
             dist.init_process_group(backend, rank=r, world_size=w, timeout=timeout)
         atexit.register(_shutdown)
     return r, w, device
+
+
+def _rccl_defaults(world):
+    """The launcher's xGMI RCCL defaults (``core.launcher.rccl_env``) for ranks started by
+    another launcher (torchrun): the NCCL_* variables are read when the communicator is
+    created, so setting them here (unless exported) still applies."""
+    try:
+        from ..core import launcher, topology
+
+        for k, v in launcher.rccl_env(world, topology.xgmi_links_per_gpu(world)).items():
+            if k.startswith("NCCL_"):
+                os.environ.setdefault(k, v)
+    except Exception:  # noqa: BLE001 - defaults only
+        pass
 
 
 def _shutdown():
