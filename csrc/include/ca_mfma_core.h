@@ -284,7 +284,7 @@ __device__ __forceinline__ void mfma_acc(f4v (&acc)[FM][FN], const bf16x8 (&af)[
 
 // Shared epilogue: fp32 split-K slab store, or bf16 through LDS with bias /
 // activation / pre-activation / act' / beta-accumulate / BN-statistics options.
-template <int BM, int BN, int WM, int WN, int EPI, int FM = BM / WM / 16, int FN = BN / WN / 16>
+template <int BM, int BN, int WM, int WN, int EPI, int SMEM_SHORTS, int FM = BM / WM / 16, int FN = BN / WN / 16>
 __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM][FN], short* smem, int m0, int n0,
                                               int tm, int tid) {
   constexpr int NT = WM * WN * 64;
@@ -348,10 +348,8 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
 #pragma unroll
     for (int j = 0; j < (Z2 ? 8 : 1); ++j) bz2sum[j] = 0.f;
     constexpr bool RES = EPI != EPI_BF16_BN;  // res_src / res_mask compiled in
-    // the smallest LDS any core gives this tile: max(C staging, one K stage of A + B)
-    static_assert(!Z2 || (3 * (NT / (BN / 8)) * BN * 4 <=
-                          (2 * BM * EL::LD > 2 * (BM + BN) * BK ? 2 * BM * EL::LD : 2 * (BM + BN) * BK)),
-                  "three statistics rows must fit the LDS");
+    // the calling core's LDS (SMEM_SHORTS bf16 slots) must hold the three statistics rows
+    static_assert(!Z2 || 3 * (NT / (BN / 8)) * BN * 4 <= 2 * SMEM_SHORTS, "three statistics rows must fit the LDS");
     constexpr int PF = BNS ? (IT < 2 ? IT : 2) : 1;
     const int col = (tid % (BN / 8)) * 8;
     const int gn = n0 + col;
@@ -585,7 +583,7 @@ __device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
     }
   }
 
-  gemm_epilogue<BM, BN, WM, WN, EPI>(P, acc, smem, m0, n0, tm, tid);
+  gemm_epilogue<BM, BN, WM, WN, EPI, SMEM>(P, acc, smem, m0, n0, tm, tid);
 }
 
 // ======================================================= LDS-DMA (glds) core --
@@ -783,7 +781,7 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
       __builtin_amdgcn_s_barrier();
     }
   }
-  gemm_epilogue<BM, BN, WM, WN, EPI>(P, acc, smem, m0, n0, tm, tid);
+  gemm_epilogue<BM, BN, WM, WN, EPI, SMEM>(P, acc, smem, m0, n0, tm, tid);
 }
 
 }  // namespace ca

@@ -13,4 +13,7 @@ for i in 1 2; do
   CLOUD_AMD_STEM_TAIL=0 $S 200 r2s10_off_$i.log python bench.py --via-run 0 || exit 1
 done
 CLOUD_AMD_WGRAD_STREAM=0 $S 300 r2s10_prof.log rocprofv3 --kernel-trace --stats -d gpurun_out/r2s10_prof -o run -- python bench.py --via-run 0 --steps 5 --warmup 3 || exit 1
+for b in 64 128 256; do
+  $S 200 r2s10_bert_b$b.log python bench/bert_base_synth.py --via-run 0 --batch $b || exit 1
+done
 echo SESSION_DONE
