@@ -48,6 +48,12 @@ def main():
         y = raw.gemm(a, w)
         ref = (a[:256].float() @ w.float().t())
         r["fwd_err"] = float((y[:256].float() - ref).norm() / ref.norm())
+        yd = raw.gemm(dy, w, layout=raw.NN)
+        refd = dy[:256].float() @ w.float()
+        r["dgrad_err"] = float((yd[:256].float() - refd).norm() / refd.norm())
+        raw.wgrad_into(dy, a, gw, beta=0.0)
+        refw = dy.t().float() @ a.float()
+        r["wgrad_err"] = float((gw.float() - refw).norm() / refw.norm())
         for name, fn in (("fwd", lambda: raw.gemm(a, w)), ("dgrad", lambda: raw.gemm(dy, w, layout=raw.NN)),
                          ("wgrad", lambda: raw.wgrad_into(dy, a, gw, beta=0.0)),
                          # the library comparator (hipBLASLt through torch.mm) on the same operands

@@ -50,6 +50,7 @@ int ca_gap_fwd(const bf16_t*, void*, int, int, int, int, hipStream_t);
 int ca_gap_bwd(const void*, int, bf16_t*, int, int, int, hipStream_t);
 int ca_gemm_bf16(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float*, float,
                  hipStream_t);
+int ca_gemm_set_core(int);
 int ca_bn_relu_maxpool_s2k3(const bf16_t*, const float*, bf16_t*, uint8_t*, int, int, int, int, int, int, hipStream_t);
 int ca_maxpool_bnstats_parts(int, int, int, int);
 int ca_maxpool_bwd_s2k3_bnstats(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, bf16_t*, float*, int, int,
@@ -232,6 +233,7 @@ PYBIND11_MODULE(_C, m) {
     check(ca_bn_relu_maxpool_s2k3(P(const bf16_t*, z), P(const float*, ss), P(bf16_t*, y), P(uint8_t*, idx), N, H, W,
                                   C, OH, OW, S(s)), "bn_relu_maxpool_s2k3");
   });
+  m.def("gemm_set_core", [](int kind) { return ca_gemm_set_core(kind); });
   m.def("maxpool_bnstats_parts", [](int N, int H, int W, int C) { return ca_maxpool_bnstats_parts(N, H, W, C); });
   m.def("maxpool_bwd_s2k3_bnstats", [](u64 dy, u64 yp, u64 idx, u64 z, u64 g, u64 part, int N, int H, int W, int C,
                                        int OH, int OW, u64 s) {

@@ -34,15 +34,24 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) d
   mfma_gemm_glds<BM, BN, 2, 4, LA, LB, EPI, 2>(P);
 }
 
-// CLOUD_AMD_GEMM_CORE=reg selects the register-staged core (A/B comparisons).
-// 0 = register-staged, 1 = glds single stage (4 waves), 2 = glds double-buffered (8 waves)
+// The 256 x 256 ping-pong core (mfma_gemm_pp256): CLOUD_AMD_GEMM_CORE=pp256.
+template <template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
+__global__ void __launch_bounds__(512) dense_gemm_pp256_kernel(CoreParams P) {
+  mfma_gemm_pp256<LA, LB, EPI>(P);
+}
+
+// CLOUD_AMD_GEMM_CORE selects the core (A/B comparisons; ca_gemm_set_core overrides it):
+// 0 "reg" = register-staged, 1 (default) = glds single stage (4 waves), 2 "glds8" = glds
+// double-buffered (8 waves), 4 "pp256" = 1 plus the 256 x 256 ping-pong core for large
+// plain-epilogue GEMMs (measured: +10-15 % at 4096^3 / 8192^3, slower on the BERT / ResNet
+// shapes -- docs/performance.md).
+int g_core_kind = -1;
 int core_kind() {
-  static int v = -1;
-  if (v < 0) {
+  if (g_core_kind < 0) {
     const char* e = getenv("CLOUD_AMD_GEMM_CORE");
-    v = !e ? 1 : (e[0] == 'r' ? 0 : (strcmp(e, "glds8") == 0 ? 2 : 1));
+    g_core_kind = !e ? 1 : (e[0] == 'r' ? 0 : (strcmp(e, "glds8") == 0 ? 2 : (strcmp(e, "pp256") == 0 ? 4 : 1)));
   }
-  return v;
+  return g_core_kind;
 }
 bool use_glds() { return core_kind() != 0; }
 
@@ -88,6 +97,14 @@ template <int BM, int BN, template <int, int, int> class LA, template <int, int,
           template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
 int launch(const CoreParams& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  if constexpr (BM == 128 && BN == 128 && (EPI == EPI_BF16 || EPI == EPI_F32_PARTIAL)) {
+    if (core_kind() == 4 && p.M >= 256 && p.N >= 256) {
+      const int t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+      dense_gemm_pp256_kernel<GA, GB, EPI><<<dim3(t256, 1, splits), 512, 0, s>>>(p);
+      CA_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   if (BN == 128 && core_kind() == 2) {
     dense_gemm_glds8_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 512, 0, s>>>(p);
     CA_LAUNCH_CHECK();
@@ -160,6 +177,14 @@ extern "C" {
 int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N,
                   int K, float beta, const bf16_t* res_src, const uint8_t* res_mask, const bf16_t* bnz,
                   const uint8_t* bnmask, float* stats, hipStream_t s, const bf16_t* bnz2, float* stats2);
+
+// Select the GEMM core for this process (values as CLOUD_AMD_GEMM_CORE above); returns
+// the previous one.
+int ca_gemm_set_core(int kind) {
+  const int prev = core_kind();
+  if (kind == 0 || kind == 1 || kind == 2 || kind == 4) g_core_kind = kind;
+  return prev;
+}
 
 int ca_splitk_reduce(const float* ws, int splits, long MN, void* out, int out_bf16, float beta, hipStream_t s) {
   if (MN % 4) return -3;
