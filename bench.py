@@ -91,6 +91,7 @@ def main():
         return via_run(args)
     import torch
 
+    from cloud_amd import config
     from cloud_amd.models import resnet50
     from cloud_amd.models.resnet import resnet18_like_small
     from cloud_amd.ops import softmax_cross_entropy
@@ -208,7 +209,7 @@ def main():
                        "optimizer": "sgd_momentum0.9_fused"},
             "device": device.type,
             "backend": backend if world > 1 else None,
-            "shared_gpu": os.environ.get("CLOUD_AMD_SHARED_GPU", "0") not in ("", "0", "false"),
+            "shared_gpu": bool(config.get("CLOUD_AMD_SHARED_GPU")),
             "comm": dict(reducer.describe(), allreduce_ms=comm["allreduce_ms"],
                          exposed_comm_ms=comm["exposed_comm_ms"]),
             "first_step_latency_s": round(first_lat, 3),

@@ -68,8 +68,10 @@ def main():
     if args.via_run and not benchlaunch.inside_launched_rank():
         return benchlaunch.launch_via_run(os.path.abspath(__file__), args.gpus, tag="bert")
     import torch
+    import torch.distributed as dist
     import torch.nn.functional as F
 
+    from cloud_amd import config
     from cloud_amd.utils import dist_env
 
     rank, world, device = dist_env.init_distributed()
@@ -159,6 +161,8 @@ def main():
             "impl": impl, "first_step_latency_s": round(first, 3),
             "run_to_first_step_s": round(run_to_first, 3) if run_to_first is not None else None,
             "launched_via": benchlaunch.launched_via(), "comm": comm,
+            "backend": dist.get_backend() if world > 1 else None,
+            "shared_gpu": bool(config.get("CLOUD_AMD_SHARED_GPU")),
             "tokens_per_sec": round(sps * S, 1), "final_loss": round(float(loss.detach().float()), 4)}), flush=True)
     if world > 1:
         import torch.distributed as dist

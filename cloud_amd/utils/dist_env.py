@@ -40,7 +40,9 @@ def init_distributed(backend=None, timeout_s=None, device=None):
         # CLOUD_AMD_SHARED_GPU=1 maps every local rank onto cuda:0: a rehearsal of the
         # multi-rank path on a one-GPU box (with CLOUD_AMD_DIST_BACKEND=gloo; RCCL
         # refuses two ranks on one device).
-        ordinal = 0 if os.environ.get("CLOUD_AMD_SHARED_GPU") == "1" else lr
+        from .. import config
+
+        ordinal = 0 if config.get("CLOUD_AMD_SHARED_GPU") else lr
         device = torch.device("cuda", ordinal) if torch.cuda.is_available() else torch.device("cpu")
     if device.type == "cuda":
         torch.cuda.set_device(device)
