@@ -9,11 +9,30 @@ parameter gradients written straight into the flat gradient arena).
 """
 from __future__ import annotations
 
+import json
+import os
+
 import torch
 
 from . import _ext
 
 NT, NN, TN = 0, 1, 2
+
+# Shape log for roofline analysis (scripts/gemm_roofline.py): with CLOUD_AMD_SHAPE_LOG=<path>,
+# every GEMM / convolution launch appends one JSON line (kind, M, N, K, minimum HBM bytes) in
+# launch order, to be aligned with a serialized rocprofv3 kernel trace.
+_SHAPE_LOG = os.environ.get("CLOUD_AMD_SHAPE_LOG") or None
+
+
+def _log(kind, M, N, K, nbytes, **kw):
+    if _SHAPE_LOG is None:
+        return
+    with open(_SHAPE_LOG, "a") as f:
+        f.write(json.dumps(dict(kind=kind, M=int(M), N=int(N), K=int(K), bytes=int(nbytes), **kw)) + "\n")
+
+
+def _nb(*ts):
+    return sum(t.numel() * t.element_size() for t in ts if t is not None)
 
 
 def _st(dev):
@@ -48,11 +67,13 @@ def conv_fwd(x, w, stride, padding, stats=None):
         y = torch.empty((N, H, W, Cout), dtype=torch.bfloat16, device=x.device)
         ext.gemm_bf16(NT, x.data_ptr(), Cin, w.data_ptr(), Cin, y.data_ptr(), Cout, N * H * W, Cout, Cin,
                       _ext.ptr(stats), 0.0, _st(x.device))
+        _log("fwd1x1", N * H * W, Cout, Cin, _nb(x, w, y))
         return y
     OH, OW = out_hw(H, KH, stride, padding), out_hw(W, KW, stride, padding)
     y = torch.empty((N, OH, OW, Cout), dtype=torch.bfloat16, device=x.device)
     ext.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), N, H, W, Cin, Cout, KH, KW, stride, stride, padding,
                  padding, _ext.ptr(stats), _st(x.device))
+    _log("fwd%dx%ds%d" % (KH, KW, stride), N * OH * OW, Cout, KH * KW * Cin, _nb(x, w, y))
     return y
 
 
@@ -91,6 +112,7 @@ def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res
         ext.dgrad_gemm(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin, Cout,
                        float(beta), src.data_ptr(), _ext.ptr(rmask), zp, mp, _ext.ptr(part), _st(dy.device), z2p,
                        _ext.ptr(part2))
+        _log("dgrad1x1_res", N * H * W, Cin, Cout, _nb(dy, w, dx, src, rmask, *(bn or ())) + (2 * _nb(dx) if beta else 0))
         if bn is None:
             return dx
         return (dx, part, part2) if len(bn) > 2 else (dx, part)
@@ -102,19 +124,24 @@ def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res
             part = torch.empty(((N * H * W + 127) // 128, 2, Cin), dtype=torch.float32, device=dy.device)
             ext.gemm_bf16_bnstats(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin, Cout,
                                   float(beta), z.data_ptr(), _ext.ptr(mask), part.data_ptr(), _st(dy.device))
+            _log("dgrad1x1_bn", N * H * W, Cin, Cout, _nb(dy, w, dx, z, mask) + (_nb(dx) if beta else 0))
         else:
             rows = ext.conv_dgrad_stat_tiles(N, H, W, stride, stride)
             part = torch.empty((rows, 2, Cin), dtype=torch.float32, device=dy.device)
             ext.conv_dgrad_bnstats(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, KH, KW, stride,
                                    stride, padding, padding, float(beta), z.data_ptr(), _ext.ptr(mask),
                                    part.data_ptr(), _st(dy.device))
+            _log("dgrad%dx%ds%d_bn" % (KH, KW, stride), N * H * W, Cin, Cout * KH * KW, _nb(dy, w, dx, z, mask),
+                 launches=stride * stride)
         return dx, part
     if is_gemm_conv(w, stride, padding):
         ext.gemm_bf16(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin, Cout, 0,
                       float(beta), _st(dy.device))
+        _log("dgrad1x1", N * H * W, Cin, Cout, _nb(dy, w, dx) + (_nb(dx) if beta else 0))
         return dx
     ext.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, KH, KW, stride, stride, padding,
                    padding, float(beta), _st(dy.device))
+    _log("dgrad%dx%ds%d" % (KH, KW, stride), N * H * W, Cin, Cout * KH * KW, _nb(dy, w, dx), launches=stride * stride)
     return dx
 
 
@@ -135,6 +162,8 @@ def conv_wgrad(dy, x, w_shape, stride, padding, out, beta=1.0):
     else:
         ext.conv_wgrad(dy.data_ptr(), x.data_ptr(), out.data_ptr(), obf, float(beta), N, H, W, Cin, Cout, KH, KW,
                        stride, stride, padding, padding, splits, ws.data_ptr(), _st(x.device))
+    _log("wgrad%dx%ds%d" % (KH, KW, stride), Cout, ncols, kred, _nb(dy, x, out) + (2 * _nb(ws) if splits > 1 else 0),
+         splits=splits)
     return out
 
 
@@ -238,6 +267,7 @@ def gemm(a, w, bias=None, act=None, preact=None, out=None, beta=0.0, layout=NT, 
     ext.gemm_ex(layout, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0), M, N, K,
                 _ext.ptr(stats), float(beta), _ext.ptr(bias), ACT[act], _ext.ptr(preact), _ext.ptr(dact_src), ld_aux,
                 _st(a.device))
+    _log("dense", M, N, K, _nb(a, w, out, bias, preact, dact_src))
     return out
 
 
@@ -252,6 +282,7 @@ def wgrad_into(dy, x, out, beta=1.0):
     ext.gemm_splitk(TN, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
                     int(out.dtype == torch.bfloat16), float(beta), n_out, k_in, M, splits, ws.data_ptr(),
                     _st(dy.device))
+    _log("dense_wgrad", n_out, k_in, M, _nb(dy, x, out) + (2 * _nb(ws) if splits > 1 else 0), splits=splits)
     return out
 
 

@@ -607,6 +607,16 @@ static __device__ __attribute__((aligned(16))) bf16_t ca_zero16[8];
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// Branch-free choice between a chunk's source address and the zero page.  Written as a
+// mask on the address bits: a plain `ok ? a : zero` lets the compiler sink the address
+// arithmetic into an exec-masked branch per chunk (measured: 2 branches + ~20 SALU per
+// chunk in the DMA issue sequence of the gather loaders).
+__device__ __forceinline__ const bf16_t* sel_src(bool ok, const bf16_t* a) {
+  const uint64_t m = 0 - (uint64_t)ok;
+  return reinterpret_cast<const bf16_t*>((reinterpret_cast<uint64_t>(a) & m) |
+                                         (reinterpret_cast<uint64_t>(ca_zero16) & ~m));
+}
+
 template <int R>
 __device__ __forceinline__ int nc_swz(int k) {
   if constexpr (R >= 128) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
@@ -657,7 +667,7 @@ struct GDenseKC {
     int gr = row0 + i * (NT / 8);
     gr = gr > rlast ? rlast : gr;
     const int k = k0 + col;
-    return k < K ? p + (long)gr * ld + k : ca_zero16;
+    return sel_src(k < K, p + (long)gr * ld + k);
   }
 };
 
@@ -685,7 +695,7 @@ struct GDenseNC {
   }
   __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
     const int k = k0 + krow0 + i * (NT * 8 / R);
-    return k < K ? colp + (long)k * ld : ca_zero16;
+    return sel_src(k < K, colp + (long)k * ld);
   }
 };
 

@@ -324,6 +324,134 @@ struct GConvWgradB {
   }
 };
 
+// ---- tap-mask gather loaders (K tile = one tap x 64 channels) ----------------
+// When the gathered operand's channel count is a multiple of BK, a K tile is one
+// filter tap and one 64-channel slice, so the tap (kh, kw) and the channel offset are
+// wave-uniform: the per-tile address work moves to the scalar unit.  Each chunk keeps a
+// 64-bit pointer to its centre pixel and a bitmask of the taps that land inside the image
+// (computed once); per K tile a lane only tests one bit and adds the uniform tap offset,
+// selecting the zero page without a branch.  The general loaders above spend ~25 VALU
+// and two divergent branches per chunk per K tile, which on the 64-channel layers costs
+// more issue time than the tile's 16 MFMAs.  Needs KH*KW (taps per class) <= 32.
+struct TapOff {
+  int tap;  // filter tap (kh * KW + kw) of the K tile
+  int c;    // channel offset of the K tile within the tap
+  long sp;  // (kh * pitch + kw) * C: spatial part of the element offset
+};
+__device__ __forceinline__ TapOff tap_offset(int k0, const FastDiv& dc, int C, const FastDiv& dkw, int KW, int pitch) {
+  TapOff t;
+  t.tap = (int)fdiv((uint32_t)k0, dc);
+  t.c = k0 - t.tap * C;
+  const int kh = (int)fdiv((uint32_t)t.tap, dkw), kw = t.tap - kh * KW;
+  t.sp = ((long)kh * pitch + kw) * C;
+  return t;
+}
+
+// forward A: X[n, oy*s - p + kh, ox*s - p + kw, c]; Cin % BK == 0.
+template <int R, int CPT, int NT>
+struct GConvFwdAT {
+  static constexpr bool KC = true;
+  const CoreParams& P;
+  const bf16_t* base[CPT];  // &X[n, oy*s - p, ox*s - p, col] (may point outside X; only used when valid)
+  uint32_t vm[CPT];         // bit kh*KW + kw: that tap is inside the image
+  __device__ GConvFwdAT(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    const int row_t = tid >> 3;
+    const int col = ((tid & 7) ^ (row_t & 7)) << 3;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int m = r0 + row_t + i * (NT / 8);
+      uint32_t mask = 0;
+      long off = 0;
+      if (m < P.M) {
+        const Pix o = decode((uint32_t)m, P.div_ow, P.div_oh);
+        const int iy0 = o.y * P.sh - P.ph, ix0 = o.x * P.sw - P.pw;
+        off = (((long)o.n * P.H + iy0) * P.W + ix0) * P.Cin + col;
+        for (int kh = 0; kh < P.KH; ++kh) {
+          if ((unsigned)(iy0 + kh) >= (unsigned)P.H) continue;
+          for (int kw = 0; kw < P.KW; ++kw)
+            if ((unsigned)(ix0 + kw) < (unsigned)P.W) mask |= 1u << (kh * P.KW + kw);
+        }
+      }
+      base[i] = P.A + off;
+      vm[i] = mask;
+    }
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const TapOff t = tap_offset(k0, P.div_cin, P.Cin, P.div_kw, P.KW, P.W);
+    return sel_src((vm[i] >> t.tap) & 1u, base[i] + (t.sp + t.c));
+  }
+};
+
+// stride-1 dgrad A: dY[n, iy + p - kh, ix + p - kw, co]; Cout % BK == 0.
+template <int R, int CPT, int NT>
+struct GConvDgradAT {
+  static constexpr bool KC = true;
+  const CoreParams& P;
+  const bf16_t* base[CPT];  // &dY[n, iy + p, ix + p, col]
+  uint32_t vm[CPT];
+  __device__ GConvDgradAT(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    const int row_t = tid >> 3;
+    const int col = ((tid & 7) ^ (row_t & 7)) << 3;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int m = r0 + row_t + i * (NT / 8);
+      uint32_t mask = 0;
+      long off = 0;
+      if (m < P.M) {
+        const Pix q = decode((uint32_t)m, P.div_w, P.div_h);
+        const int oy0 = q.y + P.ph, ox0 = q.x + P.pw;
+        off = (((long)q.n * P.OH + oy0) * P.OW + ox0) * P.Cout + col;
+        for (int kh = 0; kh < P.KH; ++kh) {
+          if ((unsigned)(oy0 - kh) >= (unsigned)P.OH) continue;
+          for (int kw = 0; kw < P.KW; ++kw)
+            if ((unsigned)(ox0 - kw) < (unsigned)P.OW) mask |= 1u << (kh * P.KW + kw);
+        }
+      }
+      base[i] = P.A + off;
+      vm[i] = mask;
+    }
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const TapOff t = tap_offset(k0, P.div_cout, P.Cout, P.div_kw, P.KW, P.OW);
+    return sel_src((vm[i] >> t.tap) & 1u, base[i] + (t.c - t.sp));  // the gather walks back by the tap
+  }
+};
+
+// Branch-free form of GConvWgradB: one pixel decode per chunk, the validity test folded
+// into sel_src.  For a stride-1 "same" convolution (OH == H, OW == W) the source address is
+// linear in the pixel index: X + (k + (kh - p) * W + (kw - p)) * Cin + ci.
+template <int R, int CPT, int NT>
+struct GConvWgradBT {
+  static constexpr bool KC = false;
+  const CoreParams& P;
+  const bf16_t* tbase;  // X + ((kh - ph) * W + (kw - pw)) * Cin + ci
+  int krow0, dh, dw, ci;
+  bool lin;
+  __device__ GConvWgradBT(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    constexpr int CPR = R / 8;
+    const int k = tid / CPR, pc = tid % CPR;
+    int j = r0 + ((pc ^ nc_swz<R>(k)) << 3);
+    if (j > P.N - 8) j = P.N - 8;
+    int tap, cc;
+    tap_split(j, 0, P.Cin, P.div_cin, false, tap, cc);
+    const int kh = (int)fdiv((uint32_t)tap, P.div_kw);
+    dh = kh - P.ph;
+    dw = tap - kh * P.KW - P.pw;
+    ci = cc;
+    krow0 = k;
+    tbase = P.B + ((long)dh * P.W + dw) * P.Cin + ci;
+    lin = P.sh == 1 && P.sw == 1 && P.OH == P.H && P.OW == P.W;
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const int k = k0 + krow0 + i * (NT * 8 / R);
+    const Pix o = decode((uint32_t)k, P.div_ow, P.div_oh);
+    const int ih = o.y * P.sh + dh, iw = o.x * P.sw + dw;
+    const bool ok = k < P.K && (unsigned)ih < (unsigned)P.H && (unsigned)iw < (unsigned)P.W;
+    const bf16_t* a = lin ? tbase + (long)k * P.Cin : P.B + (((long)o.n * P.H + ih) * P.W + iw) * P.Cin + ci;
+    return sel_src(ok, a);
+  }
+};
+
 // ---- strided dgrad by output-parity class (sub-pixel decomposition) ----------
 // For stride s the input pixels with (iy % s, ix % s) = (py, px) only receive
 // taps kh = kh0 + s*th (kh0 = (py + ph) % s), kw likewise, from dY row
@@ -365,6 +493,41 @@ struct GConvDgradSA {
     const int oy = qy[i] - th, ox = qx[i] - tw;
     if ((unsigned)oy >= (unsigned)P.OH || (unsigned)ox >= (unsigned)P.OW) return ca_zero16;
     return nbase[i] + ((long)oy * P.OW + ox) * P.Cout + co;
+  }
+};
+
+// tap-mask form of GConvDgradSA (Cout % BK == 0, nh*nw <= 32): dY[n, qy + dy0 - th, qx + dx0 - tw, co].
+template <int R, int CPT, int NT>
+struct GConvDgradSAT {
+  static constexpr bool KC = true;
+  const CoreParams& P;
+  const bf16_t* base[CPT];  // &dY[n, qy + dy0, qx + dx0, col]
+  uint32_t vm[CPT];         // bit th*nw + tw
+  __device__ GConvDgradSAT(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    const int row_t = tid >> 3;
+    const int col = ((tid & 7) ^ (row_t & 7)) << 3;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int m = r0 + row_t + i * (NT / 8);
+      uint32_t mask = 0;
+      long off = 0;
+      if (m < P.M) {
+        const Pix q = decode((uint32_t)m, P.div_wq, P.div_hq);
+        const int oy0 = q.y + P.dg_dy0, ox0 = q.x + P.dg_dx0;
+        off = (((long)q.n * P.OH + oy0) * P.OW + ox0) * P.Cout + col;
+        for (int th = 0; th < P.dg_nh; ++th) {
+          if ((unsigned)(oy0 - th) >= (unsigned)P.OH) continue;
+          for (int tw = 0; tw < P.dg_nw; ++tw)
+            if ((unsigned)(ox0 - tw) < (unsigned)P.OW) mask |= 1u << (th * P.dg_nw + tw);
+        }
+      }
+      base[i] = P.A + off;
+      vm[i] = mask;
+    }
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const TapOff t = tap_offset(k0, P.div_cout, P.Cout, P.div_nw, P.dg_nw, P.OW);
+    return sel_src((vm[i] >> t.tap) & 1u, base[i] + (t.c - t.sp));
   }
 };
 
@@ -417,6 +580,16 @@ int core_kind() {
   return v;
 }
 bool use_glds() { return core_kind() != 0; }
+
+// CLOUD_AMD_TAPMASK=0 keeps the general gather loaders on every convolution (A/B runs).
+bool tapmask_loaders() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_TAPMASK");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
+}
 
 template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
 __global__ void __launch_bounds__(256) conv_gemm_kernel(CoreParams P) {
@@ -474,6 +647,14 @@ int ca_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   p.A = x; p.B = w; p.lda = Cin; p.ldb = (long)KH * KW * Cin; p.C = y; p.ldc = Cout;
   p.M = Nb * p.OH * p.OW; p.N = Cout; p.K = KH * KW * Cin; p.k_per_split = p.K;
   p.stats = stats;
+  if (p.cin_tile && KH * KW <= 32 && tapmask_loaders()) {
+    if (stats) {
+      if (Cout <= 64) return launch<128, 64, ConvFwdA, DenseKC, GConvFwdAT, GDenseKC, EPI_BF16_ST>(p, 1, s);
+      return launch<128, 128, ConvFwdA, DenseKC, GConvFwdAT, GDenseKC, EPI_BF16_ST>(p, 1, s);
+    }
+    if (Cout <= 64) return launch<128, 64, ConvFwdA, DenseKC, GConvFwdAT, GDenseKC, EPI_BF16>(p, 1, s);
+    return launch<128, 128, ConvFwdA, DenseKC, GConvFwdAT, GDenseKC, EPI_BF16>(p, 1, s);
+  }
   if (stats) {
     if (Cout <= 64) return launch<128, 64, ConvFwdA, DenseKC, GConvFwdA, GDenseKC, EPI_BF16_ST>(p, 1, s);
     return launch<128, 128, ConvFwdA, DenseKC, GConvFwdA, GDenseKC, EPI_BF16_ST>(p, 1, s);
@@ -513,6 +694,10 @@ long ca_conv_dgrad_stat_tiles(int Nb, int H, int W, int sh, int sw) {
 
 template <int EPI>
 static int launch_dgrad(const CoreParams& p, int Cin, hipStream_t s) {
+  if (p.cout_tile && p.sh == 1 && p.sw == 1 && p.KH * p.KW <= 32 && tapmask_loaders()) {
+    if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradAT, GConvDgradB, EPI>(p, 1, s);
+    return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradAT, GConvDgradB, EPI>(p, 1, s);
+  }
   if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI>(p, 1, s);
   return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI>(p, 1, s);
 }
@@ -520,6 +705,10 @@ static int launch_dgrad(const CoreParams& p, int Cin, hipStream_t s) {
 // one output-parity class of a strided dgrad (row map on)
 template <int EPI>
 static int launch_dgrad_s(const CoreParams& q, int Cin, hipStream_t s) {
+  if (q.cout_tile && q.dg_nh * q.dg_nw <= 32 && tapmask_loaders()) {
+    if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradSAT, GConvDgradSB, EPI>(q, 1, s);
+    return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradSAT, GConvDgradSB, EPI>(q, 1, s);
+  }
   if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradSA, GConvDgradSB, EPI>(q, 1, s);
   return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradSA, GConvDgradSB, EPI>(q, 1, s);
 }
@@ -602,6 +791,16 @@ int ca_conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, floa
   p.k_per_split = kps;
   p.C = ws; p.ldc = p.N; p.split_stride = (long)p.M * p.N;
   int rc;
+  if (tapmask_loaders()) {
+    if (Cout <= 64)
+      rc = (p.N <= 64) ? launch<64, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradBT, EPI_F32_PARTIAL>(p, splits, s)
+                       : launch<64, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradBT, EPI_F32_PARTIAL>(p, splits, s);
+    else
+      rc = (p.N <= 64) ? launch<128, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradBT, EPI_F32_PARTIAL>(p, splits, s)
+                       : launch<128, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradBT, EPI_F32_PARTIAL>(p, splits, s);
+    if (rc) return rc;
+    return ca_splitk_reduce(ws, splits, (long)p.M * p.N, dw, dw_bf16, beta, s);
+  }
   if (Cout <= 64)  // 64 output channels: 64-row tiles (no MFMA rows past Cout)
     rc = (p.N <= 64) ? launch<64, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s)
                      : launch<64, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s);

@@ -235,7 +235,10 @@ def test_linear_autograd_writes_arena_grad():
 
 @pytest.mark.parametrize("N,H,Cin,Cout,k,s,p", [
     (2, 14, 64, 64, 3, 1, 1), (2, 15, 64, 128, 3, 2, 1), (2, 16, 8, 64, 7, 2, 3),
-    (2, 14, 128, 256, 1, 2, 0), (1, 9, 24, 40, 3, 1, 1), (2, 8, 256, 64, 1, 1, 0)])
+    (2, 14, 128, 256, 1, 2, 0), (1, 9, 24, 40, 3, 1, 1), (2, 8, 256, 64, 1, 1, 0),
+    # tap-mask loaders: two 64-channel slices per tap, 7x7 maps (every row touches a border),
+    # even-sized strided input, 3 images (pixel decode across image boundaries)
+    (3, 7, 128, 64, 3, 1, 1), (2, 10, 64, 128, 3, 2, 1), (3, 5, 64, 192, 3, 1, 1)])
 def test_conv_fwd_dgrad_wgrad_vs_fp32(N, H, Cin, Cout, k, s, p):
     from cloud_amd.ops import conv2d_nhwc
 
