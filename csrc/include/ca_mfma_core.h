@@ -644,30 +644,38 @@ __device__ __forceinline__ bf16x8 read_frag_sw(const short* lds, int r0, int k0,
   }
 }
 
+// Loader address rule (all glds loaders): everything that varies per lane is folded into
+// per-chunk pointers in the constructor, so a K tile adds only a wave-uniform offset
+// (computed on the scalar unit) -- no per-tile integer multiplies, which are quarter-rate
+// on the VALU.  Measured before this rule (counter pass, ResNet-50): 140-210 VALU per K tile
+// per wave in the convolution loaders against 16-32 MFMAs, i.e. the SIMD's issue slots, not
+// the matrix pipe, bounded the implicit-GEMM kernels.
+
 // Dense K-contiguous operand for the glds core: X[r][k] at p[r*ld + k].
 // Chunk i of thread tid covers tile row (tid>>3) + i*(NT/8) and the swizzled
-// column slot (tid&7) ^ (row&7) -- the XOR term is the same for every i, so the
-// loader keeps one base row and one column (few VGPRs -> more blocks per CU).
+// column slot (tid&7) ^ (row&7) -- the XOR term is the same for every i.
 template <int R, int CPT, int NT>
 struct GDenseKC {
   static constexpr bool KC = true;
-  const bf16_t* p;
+  const bf16_t* rp;  // &X[row_0][col]; chunk i is NT/8 rows further (a uniform step)
   long ld;
-  int row0, col, rlast, K;
+  int col, K;
+  uint32_t rowok;  // bit i: chunk i's row is inside the operand
   __device__ GDenseKC(const CoreParams& P, bool isA, int r0, int tid) {
-    p = isA ? P.A : P.B;
+    const bf16_t* p = isA ? P.A : P.B;
     ld = isA ? P.lda : P.ldb;
-    rlast = (isA ? P.M : P.N) - 1;
+    const int rows = isA ? P.M : P.N;
     K = P.K;
     const int row = tid >> 3;
-    row0 = r0 + row;
     col = ((tid & 7) ^ (row & 7)) << 3;
+    rowok = 0;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) rowok |= (uint32_t)(r0 + row + i * (NT / 8) < rows) << i;
+    rp = p + (long)(r0 + row) * ld + col;
   }
   __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
-    int gr = row0 + i * (NT / 8);
-    gr = gr > rlast ? rlast : gr;
-    const int k = k0 + col;
-    return sel_src(k < K, p + (long)gr * ld + k);
+    const bool ok = ((rowok >> i) & 1u) & (k0 + col < K);
+    return sel_src(ok, rp + ((long)i * (NT / 8) * ld + k0));
   }
 };
 
@@ -676,7 +684,8 @@ struct GDenseKC {
 template <int R, int CPT, int NT>
 struct GDenseNC {
   static constexpr bool KC = false;
-  const bf16_t* colp;
+  static constexpr int KSTEP = NT * 8 / R;
+  const bf16_t* cp;  // &X[krow0][col]; chunk i and tile k0 add the uniform (k0 + i*KSTEP) rows
   long ld;
   int krow0, K;
   __device__ GDenseNC(const CoreParams& P, bool isA, int r0, int tid) {
@@ -690,13 +699,23 @@ struct GDenseNC {
     // launchers guarantee rlimit % 8 == 0 and rlimit >= 8 (N < 8 is refused host-side); the
     // clamp keeps a fully out-of-range column chunk on the last real one
     if (n > rlimit - 8) n = rlimit - 8 > 0 ? rlimit - 8 : 0;
-    colp = p + n;
     krow0 = k;
+    cp = p + n + (long)k * ld;
   }
   __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
-    const int k = k0 + krow0 + i * (NT * 8 / R);
-    return sel_src(k < K, colp + (long)k * ld);
+    return sel_src(k0 + krow0 + i * KSTEP < K, cp + (long)(k0 + i * KSTEP) * ld);
   }
+};
+
+// Loaders that keep per-chunk state walked forward one K tile at a time define advance();
+// the cores call it after issuing each tile of that operand (tiles are issued in order).
+template <class L, class = void>
+struct loader_stateful {
+  static constexpr bool value = false;
+};
+template <class L>
+struct loader_stateful<L, decltype((void)&L::advance)> {
+  static constexpr bool value = true;
 };
 
 template <int BM, int BN, int WM, int WN, template <int, int, int> class LAT, template <int, int, int> class LBT,
@@ -735,8 +754,8 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
   if (kend > P.K) kend = P.K;
   const int nk = (kend - kbeg + BK - 1) / BK;
 
-  const LA la(P, true, m0, tid);
-  const LB lb(P, false, n0, tid);
+  LA la(P, true, m0, tid);
+  LB lb(P, false, n0, tid);
 
   f4v acc[FM][FN];
 #pragma unroll
@@ -754,6 +773,8 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
     for (int i = 0; i < CPB; ++i)
       __builtin_amdgcn_global_load_lds((const void*)lb.src(i, k0),
                                        (lds_void*)(base + A_ELEMS + (i * NT + wave * 64) * 8), 16, 0, 0);
+    if constexpr (loader_stateful<LA>::value) la.advance();
+    if constexpr (loader_stateful<LB>::value) lb.advance();
   };
   auto compute = [&](const short* As) {
     const short* Bs = As + A_ELEMS;
@@ -844,8 +865,8 @@ __device__ __forceinline__ void mfma_gemm_pp256(const CoreParams& P) {
   if (kend > P.K) kend = P.K;
   const int nk = (kend - kbeg + BK - 1) / BK;
 
-  const LA la(P, true, m0, tid);
-  const LB lb(P, false, n0, tid);
+  LA la(P, true, m0, tid);
+  LB lb(P, false, n0, tid);
 
   f4v acc[FM][FN];
 #pragma unroll
@@ -860,6 +881,7 @@ __device__ __forceinline__ void mfma_gemm_pp256(const CoreParams& P) {
     for (int i = 0; i < CPA; ++i)
       __builtin_amdgcn_global_load_lds((const void*)la.src(i, k0), (lds_void*)(base + (i * NT + wave * 64) * 8), 16,
                                        0, 0);
+    if constexpr (loader_stateful<LA>::value) la.advance();
   };
   auto issue_b = [&](int t) {
     short* base = smem + (t & 1) * STAGE + A_ELEMS;
@@ -868,6 +890,7 @@ __device__ __forceinline__ void mfma_gemm_pp256(const CoreParams& P) {
     for (int i = 0; i < CPB; ++i)
       __builtin_amdgcn_global_load_lds((const void*)lb.src(i, k0), (lds_void*)(base + (i * NT + wave * 64) * 8), 16,
                                        0, 0);
+    if constexpr (loader_stateful<LB>::value) lb.advance();
   };
   const int ar0 = wm * (BM / WM), bc0 = wn * (BN / WN);
   bf16x8 af[2][2][4], bq[2][2][2];  // af[qm][kk][i], bq[qn][kk][j]

@@ -452,6 +452,95 @@ struct GConvWgradBT {
   }
 };
 
+// dgrad B with Cout % BK == 0: W[co][tap][ci], co = c0 + krow (c0, tap uniform per K tile).
+template <int R, int CPT, int NT>
+struct GConvDgradBT {
+  static constexpr bool KC = false;
+  static constexpr int KSTEP = NT * 8 / R;
+  const CoreParams& P;
+  const bf16_t* wp;  // &W[krow0][0][ci]; chunk i is i*KSTEP output channels further
+  int krow0;
+  __device__ GConvDgradBT(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    constexpr int CPR = R / 8;
+    const int k = tid / CPR, pc = tid % CPR;
+    int n = r0 + ((pc ^ nc_swz<R>(k)) << 3);
+    if (n > P.N - 8) n = P.N - 8;
+    krow0 = k;
+    wp = P.B + n + (long)k * (P.KH * P.KW) * P.Cin;
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const int tap = (int)fdiv((uint32_t)k0, P.div_cout), c0 = k0 - tap * P.Cout;
+    const long off = ((long)(c0 + i * KSTEP) * (P.KH * P.KW) + tap) * P.Cin;
+    return sel_src(k0 + krow0 + i * KSTEP < P.K, wp + off);
+  }
+};
+
+// Weight-gradient B walked incrementally: each chunk keeps its pixel (oy, ox) and source
+// pointer and steps them BK pixels per K tile with uniform deltas (no per-tile division or
+// 64-bit multiply).  One row carry and one image carry per step are enough when
+// OH * OW >= 2 * BK (host-checked); smaller maps use GConvWgradBT.
+template <int R, int CPT, int NT>
+struct GConvWgradBI {
+  static constexpr bool KC = false;
+  static constexpr int KSTEP = NT * 8 / R;
+  const CoreParams& P;
+  const bf16_t* ptr[CPT];  // &X[n, oy*s + dh, ox*s + dw, ci] of the chunk's current pixel
+  int oy[CPT], ox[CPT];
+  int krow0, dh, dw;
+  long dpa, dcx, dcy;  // pointer step per tile, extra on a row carry, extra on an image carry
+  int dxa, dya;
+  __device__ GConvWgradBI(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    constexpr int CPR = R / 8;
+    const int k = tid / CPR, pc = tid % CPR;
+    int j = r0 + ((pc ^ nc_swz<R>(k)) << 3);
+    if (j > P.N - 8) j = P.N - 8;
+    int tap, ci;
+    tap_split(j, 0, P.Cin, P.div_cin, false, tap, ci);
+    const int kh = (int)fdiv((uint32_t)tap, P.div_kw);
+    dh = kh - P.ph;
+    dw = tap - kh * P.KW - P.pw;
+    krow0 = k;
+    dya = BK / P.OW;
+    dxa = BK - dya * P.OW;
+    const long rowp = (long)P.sh * P.W * P.Cin, colp = (long)P.sw * P.Cin;
+    dpa = dya * rowp + dxa * colp;
+    dcx = rowp - (long)P.OW * colp;
+    dcy = (long)P.H * P.W * P.Cin - (long)P.OH * rowp;
+    const int kbeg = blockIdx.z * P.k_per_split;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const Pix o = decode((uint32_t)(kbeg + k + i * KSTEP), P.div_ow, P.div_oh);
+      oy[i] = o.y;
+      ox[i] = o.x;
+      ptr[i] = P.B + (((long)o.n * P.H + o.y * P.sh + dh) * P.W + o.x * P.sw + dw) * P.Cin + ci;
+    }
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const int ih = __umul24(oy[i], P.sh) + dh, iw = __umul24(ox[i], P.sw) + dw;
+    const bool ok = (k0 + krow0 + i * KSTEP < P.K) & ((unsigned)ih < (unsigned)P.H) & ((unsigned)iw < (unsigned)P.W);
+    return sel_src(ok, ptr[i]);
+  }
+  __device__ __forceinline__ void advance() {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      int x = ox[i] + dxa, y = oy[i] + dya;
+      long d = dpa;
+      if (x >= P.OW) {
+        x -= P.OW;
+        y += 1;
+        d += dcx;
+      }
+      if (y >= P.OH) {
+        y -= P.OH;
+        d += dcy;
+      }
+      ox[i] = x;
+      oy[i] = y;
+      ptr[i] += d;
+    }
+  }
+};
+
 // ---- strided dgrad by output-parity class (sub-pixel decomposition) ----------
 // For stride s the input pixels with (iy % s, ix % s) = (py, px) only receive
 // taps kh = kh0 + s*th (kh0 = (py + ph) % s), kw likewise, from dY row
@@ -553,6 +642,31 @@ struct GConvDgradSB {
     const int th = (int)fdiv((uint32_t)t, P.div_nw), tw = t - th * P.dg_nw;
     const int kh = P.dg_kh0 + P.sh * th, kw = P.dg_kw0 + P.sw * tw;
     return P.B + ((long)co * (P.KH * P.KW) + kh * P.KW + kw) * P.Cin + ci;
+  }
+};
+
+// class dgrad B with Cout % BK == 0: W[co][kh0 + s*th][kw0 + s*tw][ci], (t, c0) uniform per K tile.
+template <int R, int CPT, int NT>
+struct GConvDgradSBT {
+  static constexpr bool KC = false;
+  static constexpr int KSTEP = NT * 8 / R;
+  const CoreParams& P;
+  const bf16_t* wp;
+  int krow0;
+  __device__ GConvDgradSBT(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    constexpr int CPR = R / 8;
+    const int k = tid / CPR, pc = tid % CPR;
+    int n = r0 + ((pc ^ nc_swz<R>(k)) << 3);
+    if (n > P.N - 8) n = P.N - 8;
+    krow0 = k;
+    wp = P.B + n + (long)k * (P.KH * P.KW) * P.Cin;
+  }
+  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+    const int t = (int)fdiv((uint32_t)k0, P.div_cout), c0 = k0 - t * P.Cout;
+    const int th = (int)fdiv((uint32_t)t, P.div_nw), tw = t - th * P.dg_nw;
+    const int kh = P.dg_kh0 + P.sh * th, kw = P.dg_kw0 + P.sw * tw;
+    const long off = ((long)(c0 + i * KSTEP) * (P.KH * P.KW) + kh * P.KW + kw) * P.Cin;
+    return sel_src(k0 + krow0 + i * KSTEP < P.K, wp + off);
   }
 };
 
@@ -695,8 +809,8 @@ long ca_conv_dgrad_stat_tiles(int Nb, int H, int W, int sh, int sw) {
 template <int EPI>
 static int launch_dgrad(const CoreParams& p, int Cin, hipStream_t s) {
   if (p.cout_tile && p.sh == 1 && p.sw == 1 && p.KH * p.KW <= 32 && tapmask_loaders()) {
-    if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradAT, GConvDgradB, EPI>(p, 1, s);
-    return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradAT, GConvDgradB, EPI>(p, 1, s);
+    if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradAT, GConvDgradBT, EPI>(p, 1, s);
+    return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradAT, GConvDgradBT, EPI>(p, 1, s);
   }
   if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI>(p, 1, s);
   return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI>(p, 1, s);
@@ -706,8 +820,8 @@ static int launch_dgrad(const CoreParams& p, int Cin, hipStream_t s) {
 template <int EPI>
 static int launch_dgrad_s(const CoreParams& q, int Cin, hipStream_t s) {
   if (q.cout_tile && q.dg_nh * q.dg_nw <= 32 && tapmask_loaders()) {
-    if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradSAT, GConvDgradSB, EPI>(q, 1, s);
-    return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradSAT, GConvDgradSB, EPI>(q, 1, s);
+    if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradSAT, GConvDgradSBT, EPI>(q, 1, s);
+    return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradSAT, GConvDgradSBT, EPI>(q, 1, s);
   }
   if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradSA, GConvDgradSB, EPI>(q, 1, s);
   return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradSA, GConvDgradSB, EPI>(q, 1, s);
@@ -791,6 +905,16 @@ int ca_conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, floa
   p.k_per_split = kps;
   p.C = ws; p.ldc = p.N; p.split_stride = (long)p.M * p.N;
   int rc;
+  if (tapmask_loaders() && (long)p.OH * p.OW >= 2 * BK) {  // incremental pixel walk (GConvWgradBI)
+    if (Cout <= 64)
+      rc = (p.N <= 64) ? launch<64, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradBI, EPI_F32_PARTIAL>(p, splits, s)
+                       : launch<64, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradBI, EPI_F32_PARTIAL>(p, splits, s);
+    else
+      rc = (p.N <= 64) ? launch<128, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradBI, EPI_F32_PARTIAL>(p, splits, s)
+                       : launch<128, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradBI, EPI_F32_PARTIAL>(p, splits, s);
+    if (rc) return rc;
+    return ca_splitk_reduce(ws, splits, (long)p.M * p.N, dw, dw_bf16, beta, s);
+  }
   if (tapmask_loaders()) {
     if (Cout <= 64)
       rc = (p.N <= 64) ? launch<64, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradBT, EPI_F32_PARTIAL>(p, splits, s)
