@@ -94,6 +94,8 @@ static void check(int rc, const char* what) {
   if (rc != 0) {
     std::string msg = std::string(what) + " failed: ";
     if (rc > 0) msg += hipGetErrorString(static_cast<hipError_t>(rc));
+    else if (rc == -3)
+      msg += "an operand window of one GEMM block exceeds the 2 GiB reach of the buffer loads (split the batch or K)";
     else msg += "invalid arguments (code " + std::to_string(rc) + ")";
     throw std::runtime_error(msg);
   }

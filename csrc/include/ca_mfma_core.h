@@ -617,6 +617,45 @@ __device__ __forceinline__ const bf16_t* sel_src(bool ok, const bf16_t* a) {
                                          (reinterpret_cast<uint64_t>(ca_zero16) & ~m));
 }
 
+// Buffer-mode loaders (static constexpr bool BUF = true): a block-uniform base `sbase`, a
+// byte range `nrec`, and per chunk a 32-bit byte offset from off(i, k0).  The DMA is a
+// buffer_load_dwordx4 ... lds through a resource built once per operand; a lane whose
+// offset is >= nrec (loaders return nrec itself for padding taps, K tails and rows past the
+// operand) gets ZEROS in its LDS slot from the hardware range check -- probed on gfx950,
+// scripts/debug/buffer_lds_oob_probe.hip -- so there is no zero page, no 64-bit address
+// arithmetic and no select on 64-bit pointers in the issue sequence.
+constexpr uint32_t BUF_CAP = 0x7fffffc0u;  // byte range of one resource (offsets stay < 2 GiB)
+
+__device__ __forceinline__ uint32_t buf_span(long bytes) {
+  return bytes <= 0 ? 0u : (bytes >= (long)BUF_CAP ? BUF_CAP : (uint32_t)bytes);
+}
+
+template <class L, class = void>
+struct loader_buf {
+  static constexpr bool value = false;
+};
+template <class L>
+struct loader_buf<L, decltype((void)L::BUF)> {
+  static constexpr bool value = L::BUF;
+};
+
+template <class L>
+__device__ __forceinline__ auto loader_rsrc(const L& l) {
+  if constexpr (loader_buf<L>::value)
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(l.sbase), (short)0, (int)l.nrec, 0x00020000);
+  else
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(ca_zero16), (short)0, 0, 0x00020000);
+}
+
+// one 16-B chunk per lane into the lane-linear LDS slot at dst (buffer- or pointer-mode loader)
+#define CA_DMA_CHUNK(L, l, r, i, k0, dst)                                                           \
+  do {                                                                                              \
+    if constexpr (loader_buf<L>::value)                                                             \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds((r), (lds_void*)(dst), 16, (l).off((i), (k0)), 0, 0, 0); \
+    else                                                                                            \
+      __builtin_amdgcn_global_load_lds((const void*)(l).src((i), (k0)), (lds_void*)(dst), 16, 0, 0);  \
+  } while (0)
+
 template <int R>
 __device__ __forceinline__ int nc_swz(int k) {
   if constexpr (R >= 128) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
@@ -656,26 +695,28 @@ __device__ __forceinline__ bf16x8 read_frag_sw(const short* lds, int r0, int k0,
 // column slot (tid&7) ^ (row&7) -- the XOR term is the same for every i.
 template <int R, int CPT, int NT>
 struct GDenseKC {
-  static constexpr bool KC = true;
-  const bf16_t* rp;  // &X[row_0][col]; chunk i is NT/8 rows further (a uniform step)
-  long ld;
+  static constexpr bool KC = true, BUF = true;
+  const bf16_t* sbase;  // &X[r0][0] (block-uniform)
+  uint32_t nrec;        // bytes from sbase to the end of the operand's last row
+  uint32_t roff;        // (row * ld + col) * 2 of chunk 0
+  uint32_t ldb2;        // ld * 2
   int col, K;
-  uint32_t rowok;  // bit i: chunk i's row is inside the operand
   __device__ GDenseKC(const CoreParams& P, bool isA, int r0, int tid) {
     const bf16_t* p = isA ? P.A : P.B;
-    ld = isA ? P.lda : P.ldb;
+    const long ld = isA ? P.lda : P.ldb;
     const int rows = isA ? P.M : P.N;
     K = P.K;
     const int row = tid >> 3;
     col = ((tid & 7) ^ (row & 7)) << 3;
-    rowok = 0;
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) rowok |= (uint32_t)(r0 + row + i * (NT / 8) < rows) << i;
-    rp = p + (long)(r0 + row) * ld + col;
+    sbase = p + (long)r0 * ld;
+    // rows at or past `rows` start at byte (rows - r0) * ld * 2 >= nrec: read as zeros
+    nrec = buf_span((long)(rows - r0) * ld * 2);
+    ldb2 = (uint32_t)(ld * 2);
+    roff = (uint32_t)((row * ld + col) * 2);
   }
-  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
-    const bool ok = ((rowok >> i) & 1u) & (k0 + col < K);
-    return sel_src(ok, rp + ((long)i * (NT / 8) * ld + k0));
+  __device__ __forceinline__ uint32_t off(int i, int k0) const {
+    const uint32_t o = roff + (uint32_t)(i * (NT / 8)) * ldb2 + (uint32_t)k0 * 2u;
+    return (k0 + col < K) ? o : nrec;
   }
 };
 
@@ -683,14 +724,16 @@ struct GDenseKC {
 // Chunk i covers k-row (tid / (R/8)) + i * (NT*8/R); its swizzle term is i-invariant.
 template <int R, int CPT, int NT>
 struct GDenseNC {
-  static constexpr bool KC = false;
+  static constexpr bool KC = false, BUF = true;
   static constexpr int KSTEP = NT * 8 / R;
-  const bf16_t* cp;  // &X[krow0][col]; chunk i and tile k0 add the uniform (k0 + i*KSTEP) rows
-  long ld;
-  int krow0, K;
+  const bf16_t* sbase;  // &X[kbeg][0]: the block's first reduction row (split-K start)
+  uint32_t nrec;
+  uint32_t coff;  // (krow0 * ld + n) * 2
+  uint32_t ldb2;
+  int krow0, kbeg, K;
   __device__ GDenseNC(const CoreParams& P, bool isA, int r0, int tid) {
     const bf16_t* p = isA ? P.A : P.B;
-    ld = isA ? P.lda : P.ldb;
+    const long ld = isA ? P.lda : P.ldb;
     const int rlimit = isA ? P.M : P.N;
     K = P.K;
     constexpr int CPR = R / 8;  // chunks per k-row
@@ -700,10 +743,15 @@ struct GDenseNC {
     // clamp keeps a fully out-of-range column chunk on the last real one
     if (n > rlimit - 8) n = rlimit - 8 > 0 ? rlimit - 8 : 0;
     krow0 = k;
-    cp = p + n + (long)k * ld;
+    kbeg = blockIdx.z * P.k_per_split;
+    sbase = p + (long)kbeg * ld;
+    nrec = buf_span(((long)(K - kbeg - 1) * ld + rlimit) * 2);
+    ldb2 = (uint32_t)(ld * 2);
+    coff = (uint32_t)((k * ld + n) * 2);
   }
-  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
-    return sel_src(k0 + krow0 + i * KSTEP < K, cp + (long)(k0 + i * KSTEP) * ld);
+  __device__ __forceinline__ uint32_t off(int i, int k0) const {
+    const uint32_t o = coff + (uint32_t)(k0 - kbeg + i * KSTEP) * ldb2;
+    return (k0 + krow0 + i * KSTEP < K) ? o : nrec;
   }
 };
 
@@ -763,16 +811,14 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
+  const auto ra = loader_rsrc(la);
+  const auto rb = loader_rsrc(lb);
   auto issue = [&](int t, short* base) {
     const int k0 = kbeg + t * BK;
 #pragma unroll
-    for (int i = 0; i < CPA; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)la.src(i, k0), (lds_void*)(base + (i * NT + wave * 64) * 8), 16,
-                                       0, 0);
+    for (int i = 0; i < CPA; ++i) CA_DMA_CHUNK(LA, la, ra, i, k0, base + (i * NT + wave * 64) * 8);
 #pragma unroll
-    for (int i = 0; i < CPB; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)lb.src(i, k0),
-                                       (lds_void*)(base + A_ELEMS + (i * NT + wave * 64) * 8), 16, 0, 0);
+    for (int i = 0; i < CPB; ++i) CA_DMA_CHUNK(LB, lb, rb, i, k0, base + A_ELEMS + (i * NT + wave * 64) * 8);
     if constexpr (loader_stateful<LA>::value) la.advance();
     if constexpr (loader_stateful<LB>::value) lb.advance();
   };
@@ -874,22 +920,20 @@ __device__ __forceinline__ void mfma_gemm_pp256(const CoreParams& P) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
+  const auto ra = loader_rsrc(la);
+  const auto rb = loader_rsrc(lb);
   auto issue_a = [&](int t) {
     short* base = smem + (t & 1) * STAGE;
     const int k0 = kbeg + t * BK;
 #pragma unroll
-    for (int i = 0; i < CPA; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)la.src(i, k0), (lds_void*)(base + (i * NT + wave * 64) * 8), 16,
-                                       0, 0);
+    for (int i = 0; i < CPA; ++i) CA_DMA_CHUNK(LA, la, ra, i, k0, base + (i * NT + wave * 64) * 8);
     if constexpr (loader_stateful<LA>::value) la.advance();
   };
   auto issue_b = [&](int t) {
     short* base = smem + (t & 1) * STAGE + A_ELEMS;
     const int k0 = kbeg + t * BK;
 #pragma unroll
-    for (int i = 0; i < CPB; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)lb.src(i, k0), (lds_void*)(base + (i * NT + wave * 64) * 8), 16,
-                                       0, 0);
+    for (int i = 0; i < CPB; ++i) CA_DMA_CHUNK(LB, lb, rb, i, k0, base + (i * NT + wave * 64) * 8);
     if constexpr (loader_stateful<LB>::value) lb.advance();
   };
   const int ar0 = wm * (BM / WM), bc0 = wn * (BN / WN);

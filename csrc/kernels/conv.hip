@@ -350,13 +350,19 @@ __device__ __forceinline__ TapOff tap_offset(int k0, const FastDiv& dc, int C, c
 // forward A: X[n, oy*s - p + kh, ox*s - p + kw, c]; Cin % BK == 0.
 template <int R, int CPT, int NT>
 struct GConvFwdAT {
-  static constexpr bool KC = true;
+  static constexpr bool KC = true, BUF = true;
   const CoreParams& P;
-  const bf16_t* base[CPT];  // &X[n, oy*s - p, ox*s - p, col] (may point outside X; only used when valid)
-  uint32_t vm[CPT];         // bit kh*KW + kw: that tap is inside the image
+  const bf16_t* sbase;  // &X[n0] (image of the tile's first row)
+  uint32_t nrec;
+  int32_t cofs[CPT];  // byte offset of X[n, oy*s - p, ox*s - p, col] from sbase (may be < 0)
+  uint32_t vm[CPT];   // bit kh*KW + kw: that tap is inside the image
   __device__ GConvFwdAT(const CoreParams& p, bool, int r0, int tid) : P(p) {
     const int row_t = tid >> 3;
     const int col = ((tid & 7) ^ (row_t & 7)) << 3;
+    const long img = (long)P.H * P.W * P.Cin;
+    const int n0 = (int)fdiv(fdiv((uint32_t)r0, P.div_ow), P.div_oh);
+    sbase = P.A + n0 * img;
+    nrec = buf_span((P.Nb - n0) * img * 2);
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int m = r0 + row_t + i * (NT / 8);
@@ -365,33 +371,40 @@ struct GConvFwdAT {
       if (m < P.M) {
         const Pix o = decode((uint32_t)m, P.div_ow, P.div_oh);
         const int iy0 = o.y * P.sh - P.ph, ix0 = o.x * P.sw - P.pw;
-        off = (((long)o.n * P.H + iy0) * P.W + ix0) * P.Cin + col;
+        off = (((long)(o.n - n0) * P.H + iy0) * P.W + ix0) * P.Cin + col;
         for (int kh = 0; kh < P.KH; ++kh) {
           if ((unsigned)(iy0 + kh) >= (unsigned)P.H) continue;
           for (int kw = 0; kw < P.KW; ++kw)
             if ((unsigned)(ix0 + kw) < (unsigned)P.W) mask |= 1u << (kh * P.KW + kw);
         }
       }
-      base[i] = P.A + off;
+      cofs[i] = (int32_t)(off * 2);
       vm[i] = mask;
     }
   }
-  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+  __device__ __forceinline__ uint32_t off(int i, int k0) const {
     const TapOff t = tap_offset(k0, P.div_cin, P.Cin, P.div_kw, P.KW, P.W);
-    return sel_src((vm[i] >> t.tap) & 1u, base[i] + (t.sp + t.c));
+    const uint32_t o = (uint32_t)cofs[i] + (uint32_t)((t.sp + t.c) * 2);
+    return ((vm[i] >> t.tap) & 1u) ? o : nrec;
   }
 };
 
 // stride-1 dgrad A: dY[n, iy + p - kh, ix + p - kw, co]; Cout % BK == 0.
 template <int R, int CPT, int NT>
 struct GConvDgradAT {
-  static constexpr bool KC = true;
+  static constexpr bool KC = true, BUF = true;
   const CoreParams& P;
-  const bf16_t* base[CPT];  // &dY[n, iy + p, ix + p, col]
+  const bf16_t* sbase;  // &dY[n0]
+  uint32_t nrec;
+  int32_t cofs[CPT];  // byte offset of dY[n, iy + p, ix + p, col] from sbase
   uint32_t vm[CPT];
   __device__ GConvDgradAT(const CoreParams& p, bool, int r0, int tid) : P(p) {
     const int row_t = tid >> 3;
     const int col = ((tid & 7) ^ (row_t & 7)) << 3;
+    const long img = (long)P.OH * P.OW * P.Cout;
+    const int n0 = (int)fdiv(fdiv((uint32_t)r0, P.div_w), P.div_h);
+    sbase = P.A + n0 * img;
+    nrec = buf_span((P.Nb - n0) * img * 2);
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int m = r0 + row_t + i * (NT / 8);
@@ -400,20 +413,21 @@ struct GConvDgradAT {
       if (m < P.M) {
         const Pix q = decode((uint32_t)m, P.div_w, P.div_h);
         const int oy0 = q.y + P.ph, ox0 = q.x + P.pw;
-        off = (((long)q.n * P.OH + oy0) * P.OW + ox0) * P.Cout + col;
+        off = (((long)(q.n - n0) * P.OH + oy0) * P.OW + ox0) * P.Cout + col;
         for (int kh = 0; kh < P.KH; ++kh) {
           if ((unsigned)(oy0 - kh) >= (unsigned)P.OH) continue;
           for (int kw = 0; kw < P.KW; ++kw)
             if ((unsigned)(ox0 - kw) < (unsigned)P.OW) mask |= 1u << (kh * P.KW + kw);
         }
       }
-      base[i] = P.A + off;
+      cofs[i] = (int32_t)(off * 2);
       vm[i] = mask;
     }
   }
-  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+  __device__ __forceinline__ uint32_t off(int i, int k0) const {
     const TapOff t = tap_offset(k0, P.div_cout, P.Cout, P.div_kw, P.KW, P.OW);
-    return sel_src((vm[i] >> t.tap) & 1u, base[i] + (t.c - t.sp));  // the gather walks back by the tap
+    const uint32_t o = (uint32_t)cofs[i] + (uint32_t)((t.c - t.sp) * 2);  // the gather walks back by the tap
+    return ((vm[i] >> t.tap) & 1u) ? o : nrec;
   }
 };
 
@@ -455,10 +469,12 @@ struct GConvWgradBT {
 // dgrad B with Cout % BK == 0: W[co][tap][ci], co = c0 + krow (c0, tap uniform per K tile).
 template <int R, int CPT, int NT>
 struct GConvDgradBT {
-  static constexpr bool KC = false;
+  static constexpr bool KC = false, BUF = true;
   static constexpr int KSTEP = NT * 8 / R;
   const CoreParams& P;
-  const bf16_t* wp;  // &W[krow0][0][ci]; chunk i is i*KSTEP output channels further
+  const bf16_t* sbase;  // W
+  uint32_t nrec;
+  uint32_t wofs;  // byte offset of W[krow0][0][ci]
   int krow0;
   __device__ GConvDgradBT(const CoreParams& p, bool, int r0, int tid) : P(p) {
     constexpr int CPR = R / 8;
@@ -466,12 +482,14 @@ struct GConvDgradBT {
     int n = r0 + ((pc ^ nc_swz<R>(k)) << 3);
     if (n > P.N - 8) n = P.N - 8;
     krow0 = k;
-    wp = P.B + n + (long)k * (P.KH * P.KW) * P.Cin;
+    sbase = P.B;
+    nrec = buf_span((long)P.Cout * P.KH * P.KW * P.Cin * 2);
+    wofs = (uint32_t)((n + (long)k * (P.KH * P.KW) * P.Cin) * 2);
   }
-  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+  __device__ __forceinline__ uint32_t off(int i, int k0) const {
     const int tap = (int)fdiv((uint32_t)k0, P.div_cout), c0 = k0 - tap * P.Cout;
-    const long off = ((long)(c0 + i * KSTEP) * (P.KH * P.KW) + tap) * P.Cin;
-    return sel_src(k0 + krow0 + i * KSTEP < P.K, wp + off);
+    const uint32_t o = wofs + (uint32_t)((((long)(c0 + i * KSTEP) * (P.KH * P.KW) + tap) * P.Cin) * 2);
+    return (k0 + krow0 + i * KSTEP < P.K) ? o : nrec;
   }
 };
 
@@ -481,13 +499,15 @@ struct GConvDgradBT {
 // OH * OW >= 2 * BK (host-checked); smaller maps use GConvWgradBT.
 template <int R, int CPT, int NT>
 struct GConvWgradBI {
-  static constexpr bool KC = false;
+  static constexpr bool KC = false, BUF = true;
   static constexpr int KSTEP = NT * 8 / R;
   const CoreParams& P;
-  const bf16_t* ptr[CPT];  // &X[n, oy*s + dh, ox*s + dw, ci] of the chunk's current pixel
+  const bf16_t* sbase;  // &X[n0]: image of the block's first pixel (split-K start)
+  uint32_t nrec;
+  uint32_t ofs[CPT];    // byte offset of X[n, oy*s + dh, ox*s + dw, ci] for the chunk's current pixel
   int oy[CPT], ox[CPT];
   int krow0, dh, dw;
-  long dpa, dcx, dcy;  // pointer step per tile, extra on a row carry, extra on an image carry
+  uint32_t dpa, dcx, dcy;  // byte steps: per tile, extra on a row carry, extra on an image carry
   int dxa, dya;
   __device__ GConvWgradBI(const CoreParams& p, bool, int r0, int tid) : P(p) {
     constexpr int CPR = R / 8;
@@ -502,29 +522,32 @@ struct GConvWgradBI {
     krow0 = k;
     dya = BK / P.OW;
     dxa = BK - dya * P.OW;
-    const long rowp = (long)P.sh * P.W * P.Cin, colp = (long)P.sw * P.Cin;
-    dpa = dya * rowp + dxa * colp;
-    dcx = rowp - (long)P.OW * colp;
-    dcy = (long)P.H * P.W * P.Cin - (long)P.OH * rowp;
+    const long rowp = (long)P.sh * P.W * P.Cin, colp = (long)P.sw * P.Cin, img = (long)P.H * P.W * P.Cin;
+    dpa = (uint32_t)((dya * rowp + dxa * colp) * 2);
+    dcx = (uint32_t)((rowp - (long)P.OW * colp) * 2);
+    dcy = (uint32_t)((img - (long)P.OH * rowp) * 2);
     const int kbeg = blockIdx.z * P.k_per_split;
+    const int n0 = (int)fdiv(fdiv((uint32_t)kbeg, P.div_ow), P.div_oh);
+    sbase = P.B + n0 * img;
+    nrec = buf_span((P.Nb - n0) * img * 2);
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const Pix o = decode((uint32_t)(kbeg + k + i * KSTEP), P.div_ow, P.div_oh);
       oy[i] = o.y;
       ox[i] = o.x;
-      ptr[i] = P.B + (((long)o.n * P.H + o.y * P.sh + dh) * P.W + o.x * P.sw + dw) * P.Cin + ci;
+      ofs[i] = (uint32_t)(((((long)(o.n - n0) * P.H + o.y * P.sh + dh) * P.W + o.x * P.sw + dw) * P.Cin + ci) * 2);
     }
   }
-  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+  __device__ __forceinline__ uint32_t off(int i, int k0) const {
     const int ih = __umul24(oy[i], P.sh) + dh, iw = __umul24(ox[i], P.sw) + dw;
     const bool ok = (k0 + krow0 + i * KSTEP < P.K) & ((unsigned)ih < (unsigned)P.H) & ((unsigned)iw < (unsigned)P.W);
-    return sel_src(ok, ptr[i]);
+    return ok ? ofs[i] : nrec;
   }
   __device__ __forceinline__ void advance() {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       int x = ox[i] + dxa, y = oy[i] + dya;
-      long d = dpa;
+      uint32_t d = dpa;
       if (x >= P.OW) {
         x -= P.OW;
         y += 1;
@@ -536,7 +559,7 @@ struct GConvWgradBI {
       }
       ox[i] = x;
       oy[i] = y;
-      ptr[i] += d;
+      ofs[i] += d;
     }
   }
 };
@@ -588,13 +611,19 @@ struct GConvDgradSA {
 // tap-mask form of GConvDgradSA (Cout % BK == 0, nh*nw <= 32): dY[n, qy + dy0 - th, qx + dx0 - tw, co].
 template <int R, int CPT, int NT>
 struct GConvDgradSAT {
-  static constexpr bool KC = true;
+  static constexpr bool KC = true, BUF = true;
   const CoreParams& P;
-  const bf16_t* base[CPT];  // &dY[n, qy + dy0, qx + dx0, col]
-  uint32_t vm[CPT];         // bit th*nw + tw
+  const bf16_t* sbase;  // &dY[n0]
+  uint32_t nrec;
+  int32_t cofs[CPT];  // byte offset of dY[n, qy + dy0, qx + dx0, col] from sbase
+  uint32_t vm[CPT];   // bit th*nw + tw
   __device__ GConvDgradSAT(const CoreParams& p, bool, int r0, int tid) : P(p) {
     const int row_t = tid >> 3;
     const int col = ((tid & 7) ^ (row_t & 7)) << 3;
+    const long img = (long)P.OH * P.OW * P.Cout;
+    const int n0 = (int)fdiv(fdiv((uint32_t)r0, P.div_wq), P.div_hq);
+    sbase = P.A + n0 * img;
+    nrec = buf_span((P.Nb - n0) * img * 2);
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int m = r0 + row_t + i * (NT / 8);
@@ -603,20 +632,21 @@ struct GConvDgradSAT {
       if (m < P.M) {
         const Pix q = decode((uint32_t)m, P.div_wq, P.div_hq);
         const int oy0 = q.y + P.dg_dy0, ox0 = q.x + P.dg_dx0;
-        off = (((long)q.n * P.OH + oy0) * P.OW + ox0) * P.Cout + col;
+        off = (((long)(q.n - n0) * P.OH + oy0) * P.OW + ox0) * P.Cout + col;
         for (int th = 0; th < P.dg_nh; ++th) {
           if ((unsigned)(oy0 - th) >= (unsigned)P.OH) continue;
           for (int tw = 0; tw < P.dg_nw; ++tw)
             if ((unsigned)(ox0 - tw) < (unsigned)P.OW) mask |= 1u << (th * P.dg_nw + tw);
         }
       }
-      base[i] = P.A + off;
+      cofs[i] = (int32_t)(off * 2);
       vm[i] = mask;
     }
   }
-  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+  __device__ __forceinline__ uint32_t off(int i, int k0) const {
     const TapOff t = tap_offset(k0, P.div_cout, P.Cout, P.div_nw, P.dg_nw, P.OW);
-    return sel_src((vm[i] >> t.tap) & 1u, base[i] + (t.c - t.sp));
+    const uint32_t o = (uint32_t)cofs[i] + (uint32_t)((t.c - t.sp) * 2);
+    return ((vm[i] >> t.tap) & 1u) ? o : nrec;
   }
 };
 
@@ -648,10 +678,12 @@ struct GConvDgradSB {
 // class dgrad B with Cout % BK == 0: W[co][kh0 + s*th][kw0 + s*tw][ci], (t, c0) uniform per K tile.
 template <int R, int CPT, int NT>
 struct GConvDgradSBT {
-  static constexpr bool KC = false;
+  static constexpr bool KC = false, BUF = true;
   static constexpr int KSTEP = NT * 8 / R;
   const CoreParams& P;
-  const bf16_t* wp;
+  const bf16_t* sbase;
+  uint32_t nrec;
+  uint32_t wofs;
   int krow0;
   __device__ GConvDgradSBT(const CoreParams& p, bool, int r0, int tid) : P(p) {
     constexpr int CPR = R / 8;
@@ -659,14 +691,16 @@ struct GConvDgradSBT {
     int n = r0 + ((pc ^ nc_swz<R>(k)) << 3);
     if (n > P.N - 8) n = P.N - 8;
     krow0 = k;
-    wp = P.B + n + (long)k * (P.KH * P.KW) * P.Cin;
+    sbase = P.B;
+    nrec = buf_span((long)P.Cout * P.KH * P.KW * P.Cin * 2);
+    wofs = (uint32_t)((n + (long)k * (P.KH * P.KW) * P.Cin) * 2);
   }
-  __device__ __forceinline__ const bf16_t* src(int i, int k0) const {
+  __device__ __forceinline__ uint32_t off(int i, int k0) const {
     const int t = (int)fdiv((uint32_t)k0, P.div_cout), c0 = k0 - t * P.Cout;
     const int th = (int)fdiv((uint32_t)t, P.div_nw), tw = t - th * P.dg_nw;
     const int kh = P.dg_kh0 + P.sh * th, kw = P.dg_kw0 + P.sw * tw;
-    const long off = ((long)(c0 + i * KSTEP) * (P.KH * P.KW) + kh * P.KW + kw) * P.Cin;
-    return sel_src(k0 + krow0 + i * KSTEP < P.K, wp + off);
+    const uint32_t o = wofs + (uint32_t)((((long)(c0 + i * KSTEP) * (P.KH * P.KW) + kh * P.KW + kw) * P.Cin) * 2);
+    return (k0 + krow0 + i * KSTEP < P.K) ? o : nrec;
   }
 };
 

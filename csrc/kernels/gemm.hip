@@ -97,6 +97,10 @@ template <int BM, int BN, template <int, int, int> class LA, template <int, int,
           template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
 int launch(const CoreParams& p, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  // buffer-mode loaders address one block's operand window with 32-bit offsets
+  // (ca_mfma_core.h BUF_CAP): rows of a tile (KC) or one split's K range (NC)
+  const long span = (long)(p.k_per_split + BK > 256 ? p.k_per_split + BK : 256) * (p.lda > p.ldb ? p.lda : p.ldb) * 2;
+  if (use_glds() && span >= (long)BUF_CAP) return -3;
   if constexpr (BM == 128 && BN == 128 && (EPI == EPI_BF16 || EPI == EPI_F32_PARTIAL)) {
     if (core_kind() == 4 && p.M >= 256 && p.N >= 256) {
       const int t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
