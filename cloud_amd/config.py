@@ -42,6 +42,8 @@ _VARS = [
     Var("CLOUD_AMD_GEMM", str, "native", "dense GEMMs: 'native' or 'torch'", "ops"),
     Var("CLOUD_AMD_CONV", str, "native", "convolutions: 'native' or 'torch'", "ops"),
     Var("CLOUD_AMD_GEMM_CORE", str, "glds", "GEMM/conv staging core: 'glds' (LDS-DMA) or 'reg' (register)", "ops"),
+    Var("CLOUD_AMD_WGRAD_BLOCKS", int, 512, "convolution weight gradients: split-K so that about this many "
+        "workgroups run (tiles x splits); fewer splits = less fp32 slab traffic, more = fuller CUs", "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "
         "second HIP stream, overlapping the memory-bound BN/LN/dgrad chain", "ops"),
     Var("CLOUD_AMD_BN_BWD_EPILOGUE", bool, True, "ResNet block backward: BatchNorm-backward statistics from the "

@@ -51,6 +51,9 @@ def stats_buffer(rows, channels, device):
     return torch.empty(((rows + 127) // 128, 2, channels), dtype=torch.float32, device=device)
 
 
+_WGRAD_BLOCKS = None
+
+
 def wgrad_splits(m, n, kred, target_blocks=1024, min_k=512):
     bn = 64 if n <= 64 else 128
     tiles = ((m + 127) // 128) * ((n + bn - 1) // bn)
@@ -147,13 +150,18 @@ def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res
 
 def conv_wgrad(dy, x, w_shape, stride, padding, out, beta=1.0):
     """out (bf16 or fp32, shape of w) = wgrad + beta * out, split-K over N*OH*OW."""
+    global _WGRAD_BLOCKS
     ext = _ext.load(required=True)
+    if _WGRAD_BLOCKS is None:
+        from .. import config
+
+        _WGRAD_BLOCKS = config.get("CLOUD_AMD_WGRAD_BLOCKS")
     N, H, W, Cin = x.shape
     Cout, KH, KW, _ = w_shape
     OH, OW = dy.shape[1], dy.shape[2]
     kred = N * OH * OW
     ncols = KH * KW * Cin
-    splits = ext.gemm_splitk_effective(kred, wgrad_splits(Cout, ncols, kred))
+    splits = ext.gemm_splitk_effective(kred, wgrad_splits(Cout, ncols, kred, target_blocks=_WGRAD_BLOCKS))
     ws = torch.empty(splits * Cout * ncols, dtype=torch.float32, device=x.device)
     obf = int(out.dtype == torch.bfloat16)
     if KH == 1 and KW == 1 and stride == 1 and padding == 0:
