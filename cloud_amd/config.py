@@ -44,6 +44,12 @@ _VARS = [
     Var("CLOUD_AMD_GEMM_CORE", str, "glds", "GEMM/conv staging core: 'glds' (LDS-DMA) or 'reg' (register)", "ops"),
     Var("CLOUD_AMD_WGRAD_BLOCKS", int, 512, "convolution weight gradients: split-K so that about this many "
         "workgroups run (tiles x splits); fewer splits = less fp32 slab traffic, more = fuller CUs", "ops"),
+    Var("CLOUD_AMD_DENSE_WGRAD_BLOCKS", int, 512, "dense-layer weight gradients (BERT): split-K workgroup target",
+        "ops"),
+    Var("CLOUD_AMD_TAPMASK", bool, True, "convolutions: tap-mask / incremental buffer-mode gather loaders; 0 keeps "
+        "the general per-chunk decode loaders (A/B runs)", "ops"),
+    Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "
+        "K, minimum HBM bytes) to this file, for scripts/gemm_roofline.py", "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "
         "second HIP stream, overlapping the memory-bound BN/LN/dgrad chain", "ops"),
     Var("CLOUD_AMD_BN_BWD_EPILOGUE", bool, True, "ResNet block backward: BatchNorm-backward statistics from the "

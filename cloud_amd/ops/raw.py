@@ -52,6 +52,7 @@ def stats_buffer(rows, channels, device):
 
 
 _WGRAD_BLOCKS = None
+_DENSE_WGRAD_BLOCKS = None
 
 
 def wgrad_splits(m, n, kred, target_blocks=1024, min_k=512):
@@ -275,17 +276,23 @@ def gemm(a, w, bias=None, act=None, preact=None, out=None, beta=0.0, layout=NT, 
     ext.gemm_ex(layout, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0), M, N, K,
                 _ext.ptr(stats), float(beta), _ext.ptr(bias), ACT[act], _ext.ptr(preact), _ext.ptr(dact_src), ld_aux,
                 _st(a.device))
-    _log("dense", M, N, K, _nb(a, w, out, bias, preact, dact_src))
+    _log("dense_nt" if layout == NT else "dense_nn", M, N, K, _nb(a, w, out, bias, preact, dact_src) +
+         (_nb(out) if beta else 0))
     return out
 
 
 def wgrad_into(dy, x, out, beta=1.0):
     """out[N_out, K_in] (+)= dy[M, N_out]^T @ x[M, K_in] (split-K over M), bf16 or fp32 out."""
+    global _DENSE_WGRAD_BLOCKS
     ext = _ext.load(required=True)
+    if _DENSE_WGRAD_BLOCKS is None:
+        from .. import config
+
+        _DENSE_WGRAD_BLOCKS = config.get("CLOUD_AMD_DENSE_WGRAD_BLOCKS")
     M, n_out = dy.shape
     k_in = x.shape[1]
     # dense layers: K = tokens is moderate, so fewer/larger K slices (less slab traffic)
-    splits = ext.gemm_splitk_effective(M, wgrad_splits(n_out, k_in, M, target_blocks=512, min_k=1024))
+    splits = ext.gemm_splitk_effective(M, wgrad_splits(n_out, k_in, M, target_blocks=_DENSE_WGRAD_BLOCKS, min_k=1024))
     ws = torch.empty(splits * n_out * k_in, dtype=torch.float32, device=dy.device)
     ext.gemm_splitk(TN, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
                     int(out.dtype == torch.bfloat16), float(beta), n_out, k_in, M, splits, ws.data_ptr(),

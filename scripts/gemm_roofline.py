@@ -54,6 +54,8 @@ def role(name):
 
 def lrole(kind):
     fam = "dense" if (kind.startswith("dense") or kind.endswith("1x1") or "1x1s1" in kind or "1x1_" in kind) else "conv"
+    if kind == "dense_nn":
+        return "dgrad", fam
     return ("wgrad" if "wgrad" in kind else ("dgrad" if "dgrad" in kind else "fwd")), fam
 
 
