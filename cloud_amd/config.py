@@ -48,6 +48,8 @@ _VARS = [
         "ops"),
     Var("CLOUD_AMD_TAPMASK", bool, True, "convolutions: tap-mask / incremental buffer-mode gather loaders; 0 keeps "
         "the general per-chunk decode loaders (A/B runs)", "ops"),
+    Var("CLOUD_AMD_SPLIT_XCD", bool, True, "split-K GEMM/conv grids: give each XCD contiguous (split, tile) "
+        "ranges so the tiles of one K chunk share an L2; 0 remaps tiles only (A/B runs)", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "
         "K, minimum HBM bytes) to this file, for scripts/gemm_roofline.py", "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "

@@ -98,6 +98,7 @@ struct CoreParams {
   int rowmap;
   int dg_py, dg_px, dg_kh0, dg_kw0, dg_nh, dg_nw, dg_dy0, dg_dx0, Hq, Wq;
   FastDiv div_wq, div_hq, div_nw;
+  int split_xcd;  // split-K grids: deal (split, tile) ranges to XCDs split-major (blk_pos)
 };
 
 // output row of GEMM row gm (identity unless the parity-class row map is on)
@@ -183,6 +184,33 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   return base + (bid >> 3);
 }
+
+// Block -> (output tile, K split).  Workgroups go to the 8 XCDs round-robin by linear
+// id (x fastest, then z).  A split-K grid's tiles of one K chunk read the same K rows
+// of both operands (a conv weight gradient's 5-9 column tiles all gather the same dY
+// and X pixels), so with split_xcd each XCD gets a contiguous range of the
+// split-major (split, tile) order and those re-reads hit its own L2 instead of
+// being fetched once per XCD.  Without it the tiles of a split land on different XCDs.
+// host: CLOUD_AMD_SPLIT_XCD=0 keeps the tile-only XCD remap on split-K grids (A/B runs)
+inline int split_xcd_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_SPLIT_XCD");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v;
+}
+
+struct BlkPos {
+  int tile, split;
+};
+__device__ __forceinline__ BlkPos blk_pos(const CoreParams& P) {
+  const int nt = gridDim.x;
+  if (gridDim.z == 1 || !P.split_xcd) return {xcd_remap(blockIdx.x, nt), (int)blockIdx.z};
+  const int lid = xcd_remap(blockIdx.x + nt * blockIdx.z, nt * gridDim.z);
+  return {lid % nt, lid / nt};
+}
+__device__ __forceinline__ int blk_split(const CoreParams& P) { return blk_pos(P).split; }
 
 __device__ __forceinline__ s8v zero8() { return s8v{0, 0, 0, 0, 0, 0, 0, 0}; }
 __device__ __forceinline__ s8v ld16(const bf16_t* p) { return *reinterpret_cast<const s8v*>(p); }
@@ -296,7 +324,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
   const int cbase = wn * (BN / WN) + 4 * (lane >> 4);
   if constexpr (EPI == EPI_F32_PARTIAL) {
     // N % 8 == 0 and ldc % 4 == 0 (slabs are [M][N]): a column group is whole or absent
-    float* Cp = reinterpret_cast<float*>(P.C) + (long)blockIdx.z * P.split_stride;
+    float* Cp = reinterpret_cast<float*>(P.C) + (long)blk_split(P) * P.split_stride;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -509,10 +537,10 @@ __device__ __forceinline__ void mfma_gemm_body(const CoreParams& P) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int tiles_m = (P.M + BM - 1) / BM, tiles_n = (P.N + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const BlkPos bp = blk_pos(P);
+  const int tm = bp.tile / tiles_n, tn = bp.tile % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.z * P.k_per_split;
+  const int kbeg = bp.split * P.k_per_split;
   int kend = kbeg + P.k_per_split;
   if (kend > P.K) kend = P.K;
   const int nk = (kend - kbeg + BK - 1) / BK;
@@ -743,7 +771,7 @@ struct GDenseNC {
     // clamp keeps a fully out-of-range column chunk on the last real one
     if (n > rlimit - 8) n = rlimit - 8 > 0 ? rlimit - 8 : 0;
     krow0 = k;
-    kbeg = blockIdx.z * P.k_per_split;
+    kbeg = blk_split(P) * P.k_per_split;
     sbase = p + (long)kbeg * ld;
     nrec = buf_span(((long)(K - kbeg - 1) * ld + rlimit) * 2);
     ldb2 = (uint32_t)(ld * 2);
@@ -794,10 +822,10 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int tiles_m = (P.M + BM - 1) / BM, tiles_n = (P.N + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const BlkPos bp = blk_pos(P);
+  const int tm = bp.tile / tiles_n, tn = bp.tile % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.z * P.k_per_split;
+  const int kbeg = bp.split * P.k_per_split;
   int kend = kbeg + P.k_per_split;
   if (kend > P.K) kend = P.K;
   const int nk = (kend - kbeg + BK - 1) / BK;
@@ -903,10 +931,10 @@ __device__ __forceinline__ void mfma_gemm_pp256(const CoreParams& P) {
   const int wm = wave / WN, wn = wave % WN;
   const int grp = __builtin_amdgcn_readfirstlane(wave) >> 2;  // == wm, provably wave-uniform
   const int tiles_m = (P.M + BM - 1) / BM, tiles_n = (P.N + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const BlkPos bp = blk_pos(P);
+  const int tm = bp.tile / tiles_n, tn = bp.tile % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.z * P.k_per_split;
+  const int kbeg = bp.split * P.k_per_split;
   int kend = kbeg + P.k_per_split;
   if (kend > P.K) kend = P.K;
   const int nk = (kend - kbeg + BK - 1) / BK;

@@ -526,7 +526,7 @@ struct GConvWgradBI {
     dpa = (uint32_t)((dya * rowp + dxa * colp) * 2);
     dcx = (uint32_t)((rowp - (long)P.OW * colp) * 2);
     dcy = (uint32_t)((img - (long)P.OH * rowp) * 2);
-    const int kbeg = blockIdx.z * P.k_per_split;
+    const int kbeg = blk_split(P) * P.k_per_split;
     const int n0 = (int)fdiv(fdiv((uint32_t)kbeg, P.div_ow), P.div_oh);
     sbase = P.B + n0 * img;
     nrec = buf_span((P.Nb - n0) * img * 2);
@@ -746,7 +746,9 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(CoreParams P) {
 
 template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB,
           template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
-int launch(const CoreParams& p, int splits, hipStream_t s) {
+int launch(const CoreParams& p0, int splits, hipStream_t s) {
+  CoreParams p = p0;
+  p.split_xcd = split_xcd_enabled();
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   if (BN == 128 && core_kind() == 2) {
     conv_glds8_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 512, 0, s>>>(p);

@@ -95,7 +95,9 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
 
 template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB,
           template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
-int launch(const CoreParams& p, int splits, hipStream_t s) {
+int launch(const CoreParams& p0, int splits, hipStream_t s) {
+  CoreParams p = p0;
+  p.split_xcd = split_xcd_enabled();
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   // buffer-mode loaders address one block's operand window with 32-bit offsets
   // (ca_mfma_core.h BUF_CAP): rows of a tile (KC) or one split's K range (NC)
