@@ -44,12 +44,18 @@ _VARS = [
     Var("CLOUD_AMD_GEMM_CORE", str, "glds", "GEMM/conv staging core: 'glds' (LDS-DMA) or 'reg' (register)", "ops"),
     Var("CLOUD_AMD_WGRAD_BLOCKS", int, 512, "convolution weight gradients: split-K so that about this many "
         "workgroups run (tiles x splits); fewer splits = less fp32 slab traffic, more = fuller CUs", "ops"),
+    Var("CLOUD_AMD_WGRAD_BLOCKS_SMALLM", int, 512, "convolution weight gradients with <= 128 output channels "
+        "(ResNet stem, layers 1-2): split-K workgroup target", "ops"),
     Var("CLOUD_AMD_DENSE_WGRAD_BLOCKS", int, 512, "dense-layer weight gradients (BERT): split-K workgroup target",
         "ops"),
     Var("CLOUD_AMD_TAPMASK", bool, True, "convolutions: tap-mask / incremental buffer-mode gather loaders; 0 keeps "
         "the general per-chunk decode loaders (A/B runs)", "ops"),
     Var("CLOUD_AMD_SPLIT_XCD", bool, True, "split-K GEMM/conv grids: give each XCD contiguous (split, tile) "
         "ranges so the tiles of one K chunk share an L2; 0 remaps tiles only (A/B runs)", "ops"),
+    Var("CLOUD_AMD_BN_APPLY_BLOCKS", int, 0, "BatchNorm apply passes (fwd y/mask, bwd dz): total workgroups of "
+        "the HBM stream; 0 = the reduction kernels' tiling", "ops"),
+    Var("CLOUD_AMD_BN_APPLY_ILV", bool, False, "BatchNorm apply passes: 1 = RP-row groups dealt round-robin to "
+        "the workgroups (one contiguous sweep); 0 = one contiguous row chunk per workgroup", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "
         "K, minimum HBM bytes) to this file, for scripts/gemm_roofline.py", "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "

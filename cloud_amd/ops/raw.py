@@ -52,6 +52,7 @@ def stats_buffer(rows, channels, device):
 
 
 _WGRAD_BLOCKS = None
+_WGRAD_BLOCKS_SMALLM = None
 _DENSE_WGRAD_BLOCKS = None
 
 
@@ -151,18 +152,22 @@ def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res
 
 def conv_wgrad(dy, x, w_shape, stride, padding, out, beta=1.0):
     """out (bf16 or fp32, shape of w) = wgrad + beta * out, split-K over N*OH*OW."""
-    global _WGRAD_BLOCKS
+    global _WGRAD_BLOCKS, _WGRAD_BLOCKS_SMALLM
     ext = _ext.load(required=True)
     if _WGRAD_BLOCKS is None:
         from .. import config
 
         _WGRAD_BLOCKS = config.get("CLOUD_AMD_WGRAD_BLOCKS")
+        _WGRAD_BLOCKS_SMALLM = config.get("CLOUD_AMD_WGRAD_BLOCKS_SMALLM")
     N, H, W, Cin = x.shape
     Cout, KH, KW, _ = w_shape
     OH, OW = dy.shape[1], dy.shape[2]
     kred = N * OH * OW
     ncols = KH * KW * Cin
-    splits = ext.gemm_splitk_effective(kred, wgrad_splits(Cout, ncols, kred, target_blocks=_WGRAD_BLOCKS))
+    # <= 128 output channels: one row of tiles, so the grid is mostly K splits; the fp32
+    # slabs stay small next to the pixel operands, and more splits fill the CUs
+    target = _WGRAD_BLOCKS_SMALLM if Cout <= 128 else _WGRAD_BLOCKS
+    splits = ext.gemm_splitk_effective(kred, wgrad_splits(Cout, ncols, kred, target_blocks=target))
     ws = torch.empty(splits * Cout * ncols, dtype=torch.float32, device=x.device)
     obf = int(out.dtype == torch.bfloat16)
     if KH == 1 and KW == 1 and stride == 1 and padding == 0:

@@ -22,24 +22,46 @@ constexpr int BLK = 256;
 struct Tiling {
   int CT, TW, RP, ncol, nchunks;
   long rows_per_chunk;
+  int ilv;  // apply passes: row groups of RP rows dealt round-robin to the blocks (grid stride)
 };
 
-__host__ __device__ inline Tiling make_tiling(long M, int C) {
+// total: workgroups wanted over all column blocks; cap: row chunks at most.  The
+// reduction kernels keep (2048, 1024): their partials are [nchunks][C].
+__host__ __device__ inline Tiling make_tiling(long M, int C, int total = 2048, int cap = 1024) {
   Tiling t;
   t.CT = C / 8;
   t.TW = t.CT < 64 ? t.CT : 64;
   t.RP = BLK / t.TW;
   t.ncol = (t.CT + t.TW - 1) / t.TW;
   long maxchunks = (M + t.RP - 1) / t.RP;
-  long want = 2048 / t.ncol;
+  long want = total / t.ncol;
   if (want < 1) want = 1;
   if (want > maxchunks) want = maxchunks;
-  if (want > 1024) want = 1024;
+  if (want > cap) want = cap;
   t.nchunks = (int)want;
   long rpc = (M + t.nchunks - 1) / t.nchunks;
   rpc = ((rpc + t.RP - 1) / t.RP) * t.RP;
   t.rows_per_chunk = rpc;
+  t.ilv = 0;
   t.nchunks = (int)((M + rpc - 1) / rpc);
+  return t;
+}
+
+// Elementwise apply passes need no partials, so their grid is sized for the HBM stream
+// alone: CLOUD_AMD_BN_APPLY_BLOCKS workgroups in total (0 = the reduction tiling);
+// CLOUD_AMD_BN_APPLY_ILV=1 deals RP-row groups round-robin (A/B runs; default: one
+// contiguous row chunk per block).
+inline Tiling apply_tiling(long M, int C) {
+  static int blocks = -1, ilv = 0;
+  if (blocks < 0) {
+    const char* e = getenv("CLOUD_AMD_BN_APPLY_BLOCKS");
+    blocks = e ? atoi(e) : 0;
+    if (blocks < 0) blocks = 0;
+    const char* f = getenv("CLOUD_AMD_BN_APPLY_ILV");
+    ilv = (f && f[0] == '1') ? 1 : 0;
+  }
+  Tiling t = blocks ? make_tiling(M, C, blocks, blocks) : make_tiling(M, C);
+  t.ilv = ilv;
   return t;
 }
 
@@ -210,19 +232,22 @@ template <bool RELU, bool RES>
 __global__ void __launch_bounds__(BLK) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                       const float* __restrict__ scale, const float* __restrict__ shift,
                                                       bf16_t* __restrict__ y, uint8_t* __restrict__ mask, long M,
-                                                      int C) {
-  const Tiling t = make_tiling(M, C);
+                                                      int C, const Tiling tl) {
+  const Tiling& t = tl;
   const int tx = threadIdx.x % t.TW, ty = threadIdx.x / t.TW;
   const int vc = blockIdx.x * t.TW + tx;
   if (vc >= t.CT) return;
   float sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { sc[j] = scale[vc * 8 + j]; sh[j] = shift[vc * 8 + j]; }
-  const long r0 = (long)blockIdx.y * t.rows_per_chunk;
-  long r1 = r0 + t.rows_per_chunk;
+  // contiguous row chunk per block, or (ilv) RP-row groups dealt round-robin so that the
+  // blocks in flight sweep one contiguous span instead of ~nchunks far-apart streams
+  const long step = t.ilv ? (long)gridDim.y * t.RP : t.RP;
+  const long r0 = t.ilv ? (long)blockIdx.y * t.RP : (long)blockIdx.y * t.rows_per_chunk;
+  long r1 = t.ilv ? M : r0 + t.rows_per_chunk;
   if (r1 > M) r1 = M;
   const long off0 = (long)vc * 8;
-  for (long r = r0 + ty; r < r1; r += t.RP) {
+  for (long r = r0 + ty; r < r1; r += step) {
     const long o = r * C + off0;
     float v[8];
     ld8bf(x + o, v);
@@ -254,8 +279,8 @@ __global__ void __launch_bounds__(BLK) bn_apply_resbn_kernel(const bf16_t* __res
                                                             const float* __restrict__ shift,
                                                             const float* __restrict__ rscale,
                                                             const float* __restrict__ rshift, bf16_t* __restrict__ y,
-                                                            uint8_t* __restrict__ mask, long M, int C) {
-  const Tiling t = make_tiling(M, C);
+                                                            uint8_t* __restrict__ mask, long M, int C, const Tiling tl) {
+  const Tiling& t = tl;
   const int tx = threadIdx.x % t.TW, ty = threadIdx.x / t.TW;
   const int vc = blockIdx.x * t.TW + tx;
   if (vc >= t.CT) return;
@@ -267,11 +292,12 @@ __global__ void __launch_bounds__(BLK) bn_apply_resbn_kernel(const bf16_t* __res
     rs[j] = rscale[vc * 8 + j];
     rh[j] = rshift[vc * 8 + j];
   }
-  const long r0 = (long)blockIdx.y * t.rows_per_chunk;
-  long r1 = r0 + t.rows_per_chunk;
+  const long step = t.ilv ? (long)gridDim.y * t.RP : t.RP;
+  const long r0 = t.ilv ? (long)blockIdx.y * t.RP : (long)blockIdx.y * t.rows_per_chunk;
+  long r1 = t.ilv ? M : r0 + t.rows_per_chunk;
   if (r1 > M) r1 = M;
   const long off0 = (long)vc * 8;
-  for (long rr = r0 + ty; rr < r1; rr += t.RP) {
+  for (long rr = r0 + ty; rr < r1; rr += step) {
     const long o = rr * C + off0;
     float v[8], rv[8];
     ld8bf(x + o, v);
@@ -395,8 +421,8 @@ __global__ void __launch_bounds__(BLK) bn_bwd_apply_kernel(const bf16_t* __restr
                                                           const uint8_t* __restrict__ mask,
                                                           const bf16_t* __restrict__ x, const float* __restrict__ coef,
                                                           bf16_t* __restrict__ dx, bf16_t* __restrict__ dres,
-                                                          long M, int C) {
-  const Tiling t = make_tiling(M, C);
+                                                          long M, int C, const Tiling tl) {
+  const Tiling& t = tl;
   const int tx = threadIdx.x % t.TW, ty = threadIdx.x / t.TW;
   const int vc = blockIdx.x * t.TW + tx;
   if (vc >= t.CT) return;
@@ -407,11 +433,14 @@ __global__ void __launch_bounds__(BLK) bn_bwd_apply_kernel(const bf16_t* __restr
     B[j] = coef[C + vc * 8 + j];
     D[j] = coef[2 * C + vc * 8 + j];
   }
-  const long r0 = (long)blockIdx.y * t.rows_per_chunk;
-  long r1 = r0 + t.rows_per_chunk;
+  // contiguous row chunk per block, or (ilv) RP-row groups dealt round-robin so that the
+  // blocks in flight sweep one contiguous span instead of ~nchunks far-apart streams
+  const long step = t.ilv ? (long)gridDim.y * t.RP : t.RP;
+  const long r0 = t.ilv ? (long)blockIdx.y * t.RP : (long)blockIdx.y * t.rows_per_chunk;
+  long r1 = t.ilv ? M : r0 + t.rows_per_chunk;
   if (r1 > M) r1 = M;
   const long off0 = (long)vc * 8;
-  for (long r = r0 + ty; r < r1; r += t.RP) {
+  for (long r = r0 + ty; r < r1; r += step) {
     const long o = r * C + off0;
     float d[8], xv[8];
     ld8bf(dy + o, d);
@@ -441,6 +470,8 @@ int ca_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
   if (C % 8 != 0) return -1;
   Tiling t = make_tiling(M, C);
   dim3 grid(t.ncol, t.nchunks);
+  const Tiling ta = apply_tiling(M, C);
+  const dim3 agrid(ta.ncol, ta.nchunks);
   bn_stats_kernel<<<grid, BLK, 0, s>>>(x, M, C, ws);
   CA_LAUNCH_CHECK();
   bn_fwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(ws, t.nchunks, (long)C, (long)t.nchunks * C, M, C, gamma,
@@ -448,10 +479,10 @@ int ca_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
                                                          run_mean, run_var, save_mean, save_rstd,
                                                          scale_shift, scale_shift + C);
   CA_LAUNCH_CHECK();
-  if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
-  else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
-  else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
-  else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  if (relu && res) bn_apply_kernel<true, true><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
+  else if (relu) bn_apply_kernel<true, false><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
+  else if (res) bn_apply_kernel<false, true><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
+  else bn_apply_kernel<false, false><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
   CA_LAUNCH_CHECK();
   return 0;
 }
@@ -466,6 +497,8 @@ int ca_bn_fwd_partials(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, in
   if (C % 8 != 0) return -1;
   Tiling t = make_tiling(M, C);
   dim3 grid(t.ncol, t.nchunks);
+  const Tiling ta = apply_tiling(M, C);
+  const dim3 agrid(ta.ncol, ta.nchunks);
   const float* fin = partials;
   int nfin = nparts;
   if (nparts > 64 && gws) {
@@ -479,10 +512,10 @@ int ca_bn_fwd_partials(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, in
                                                          momentum, run_mean, run_var, save_mean, save_rstd,
                                                          scale_shift, scale_shift + C);
   CA_LAUNCH_CHECK();
-  if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
-  else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
-  else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
-  else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  if (relu && res) bn_apply_kernel<true, true><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
+  else if (relu) bn_apply_kernel<true, false><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
+  else if (res) bn_apply_kernel<false, true><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
+  else bn_apply_kernel<false, false><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
   CA_LAUNCH_CHECK();
   return 0;
 }
@@ -501,6 +534,8 @@ int ca_bn_fwd_partials_ex(const bf16_t* x, const bf16_t* res, const float* res_s
                               save_mean, save_rstd, scale_shift, relu, mask, gws, s);
   Tiling t = make_tiling(M, C);
   dim3 grid(t.ncol, t.nchunks);
+  const Tiling ta = apply_tiling(M, C);
+  const dim3 agrid(ta.ncol, ta.nchunks);
   const float* fin = partials;
   int nfin = nparts;
   if (nparts > 64 && gws) {
@@ -516,11 +551,11 @@ int ca_bn_fwd_partials_ex(const bf16_t* x, const bf16_t* res, const float* res_s
   CA_LAUNCH_CHECK();
   if (!y) return 0;
   if (relu)
-    bn_apply_resbn_kernel<true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, res_ss, res_ss + C, y,
-                                                     mask, M, C);
+    bn_apply_resbn_kernel<true><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, res_ss, res_ss + C, y,
+                                                     mask, M, C, ta);
   else
-    bn_apply_resbn_kernel<false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, res_ss, res_ss + C, y,
-                                                      mask, M, C);
+    bn_apply_resbn_kernel<false><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, res_ss, res_ss + C, y,
+                                                      mask, M, C, ta);
   CA_LAUNCH_CHECK();
   return 0;
 }
@@ -532,10 +567,12 @@ int ca_bn_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
   if (C % 8 != 0) return -1;
   Tiling t = make_tiling(M, C);
   dim3 grid(t.ncol, t.nchunks);
-  if (relu && res) bn_apply_kernel<true, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
-  else if (relu) bn_apply_kernel<true, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
-  else if (res) bn_apply_kernel<false, true><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
-  else bn_apply_kernel<false, false><<<grid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C);
+  const Tiling ta = apply_tiling(M, C);
+  const dim3 agrid(ta.ncol, ta.nchunks);
+  if (relu && res) bn_apply_kernel<true, true><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
+  else if (relu) bn_apply_kernel<true, false><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
+  else if (res) bn_apply_kernel<false, true><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
+  else bn_apply_kernel<false, false><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
   CA_LAUNCH_CHECK();
   return 0;
 }
@@ -550,6 +587,8 @@ int ca_bn_bwd(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16
   relu &= 1;
   Tiling t = make_tiling(M, C);
   dim3 grid(t.ncol, t.nchunks);
+  const Tiling ta = apply_tiling(M, C);
+  const dim3 agrid(ta.ncol, ta.nchunks);
   if (relu) bn_bwd_reduce_kernel<true><<<grid, BLK, 0, s>>>(dy, y, mask, x, save_mean, save_rstd, M, C, ws);
   else bn_bwd_reduce_kernel<false><<<grid, BLK, 0, s>>>(dy, y, mask, x, save_mean, save_rstd, M, C, ws);
   CA_LAUNCH_CHECK();
@@ -562,10 +601,10 @@ int ca_bn_bwd(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16
   bn_bwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(gws, G, 2L * C, (long)C, M, C, gamma, save_mean, save_rstd,
                                                          dgamma, dbeta, coef, accum, 0);
   CA_LAUNCH_CHECK();
-  if (relu && dres) bn_bwd_apply_kernel<true, true><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
-  else if (relu) bn_bwd_apply_kernel<true, false><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
-  else if (dres) bn_bwd_apply_kernel<false, true><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
-  else bn_bwd_apply_kernel<false, false><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
+  if (relu && dres) bn_bwd_apply_kernel<true, true><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
+  else if (relu) bn_bwd_apply_kernel<true, false><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
+  else if (dres) bn_bwd_apply_kernel<false, true><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
+  else bn_bwd_apply_kernel<false, false><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
   CA_LAUNCH_CHECK();
   return 0;
 }
@@ -582,6 +621,8 @@ int ca_bn_bwd_partials(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, c
   relu &= 1;
   Tiling t = make_tiling(M, C);
   dim3 grid(t.ncol, t.nchunks);
+  const Tiling ta = apply_tiling(M, C);
+  const dim3 agrid(ta.ncol, ta.nchunks);
   const float* fin = partials;
   int nfin = nparts;
   if (nparts > 64) {
@@ -594,10 +635,10 @@ int ca_bn_bwd_partials(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, c
   bn_bwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(fin, nfin, 2L * C, (long)C, M, C, gamma, save_mean, save_rstd,
                                                          dgamma, dbeta, coef, accum, 1);
   CA_LAUNCH_CHECK();
-  if (relu && dres) bn_bwd_apply_kernel<true, true><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
-  else if (relu) bn_bwd_apply_kernel<true, false><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
-  else if (dres) bn_bwd_apply_kernel<false, true><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
-  else bn_bwd_apply_kernel<false, false><<<grid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C);
+  if (relu && dres) bn_bwd_apply_kernel<true, true><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
+  else if (relu) bn_bwd_apply_kernel<true, false><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
+  else if (dres) bn_bwd_apply_kernel<false, true><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
+  else bn_bwd_apply_kernel<false, false><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
   CA_LAUNCH_CHECK();
   return 0;
 }

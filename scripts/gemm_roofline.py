@@ -95,6 +95,19 @@ print("matched %d calls; measured %.2f ms, floor %.2f ms (PF %.2f, BW %.1f TB/s)
 print("%-18s %6s %10s %10s %8s %8s" % ("kind", "calls", "ms", "floor_ms", "x_floor", "TF/s"))
 for k, (c, t, f, fl) in sorted(agg.items(), key=lambda kv: -(kv[1][1] - kv[1][2])):
     print("%-18s %6d %10.2f %10.2f %8.2f %8.0f" % (k, c, t / 1e3, f / 1e3, t / max(f, 1e-9), fl / t / 1e6))
+print("\nby shape (mean per call, all calls):")
+shp = defaultdict(lambda: [0, 0.0, 0.0, 0.0])
+for ex, t, f, e, name, red in per:
+    a = shp[(e["kind"], e["M"], e["N"], e["K"], e.get("splits", 0))]
+    a[0] += 1
+    a[1] += t
+    a[2] += f
+    a[3] += red
+print("%-14s %8s %6s %9s %6s %6s %9s %9s %7s %8s" % ("kind", "M", "N", "K", "splits", "calls", "us", "floor_us", "x_flr",
+                                                     "over_ms"))
+for (kind, m, nn, kk, sp), (c, t, f, red) in sorted(shp.items(), key=lambda kv: -(kv[1][1] - kv[1][2])):
+    print("%-14s %8d %6d %9d %6d %6d %9.1f %9.1f %7.2f %8.2f" % (kind, m, nn, kk, sp, c, t / c, f / c, t / f,
+                                                                (t - f) / 1e3))
 print("\ntop calls by time above floor:")
 for ex, t, f, e, name, red in sorted(per, key=lambda p: -p[0])[:40]:
     print("%7.1f us over (%7.1f vs floor %7.1f, reduce %5.1f) %-14s M=%d N=%d K=%d %s %s" % (
