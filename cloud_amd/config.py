@@ -54,7 +54,7 @@ _VARS = [
         "ranges so the tiles of one K chunk share an L2; 0 remaps tiles only (A/B runs)", "ops"),
     Var("CLOUD_AMD_BN_APPLY_BLOCKS", int, 0, "BatchNorm apply passes (fwd y/mask, bwd dz): total workgroups of "
         "the HBM stream; 0 = the reduction kernels' tiling", "ops"),
-    Var("CLOUD_AMD_BN_APPLY_ILV", bool, False, "BatchNorm apply passes: 1 = RP-row groups dealt round-robin to "
+    Var("CLOUD_AMD_BN_APPLY_ILV", bool, True, "BatchNorm apply passes: 1 = RP-row groups dealt round-robin to "
         "the workgroups (one contiguous sweep); 0 = one contiguous row chunk per workgroup", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "
         "K, minimum HBM bytes) to this file, for scripts/gemm_roofline.py", "ops"),

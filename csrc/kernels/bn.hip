@@ -49,16 +49,17 @@ __host__ __device__ inline Tiling make_tiling(long M, int C, int total = 2048, i
 
 // Elementwise apply passes need no partials, so their grid is sized for the HBM stream
 // alone: CLOUD_AMD_BN_APPLY_BLOCKS workgroups in total (0 = the reduction tiling);
-// CLOUD_AMD_BN_APPLY_ILV=1 deals RP-row groups round-robin (A/B runs; default: one
-// contiguous row chunk per block).
+// RP-row groups are dealt round-robin (one contiguous sweep by the blocks in flight:
+// bwd apply 4.8-5.1 -> 5.5-5.6 TB/s on the ResNet-50 shapes, bench/bn_apply_bw.py);
+// CLOUD_AMD_BN_APPLY_ILV=0 keeps one contiguous row chunk per block (A/B runs).
 inline Tiling apply_tiling(long M, int C) {
-  static int blocks = -1, ilv = 0;
+  static int blocks = -1, ilv = 1;
   if (blocks < 0) {
     const char* e = getenv("CLOUD_AMD_BN_APPLY_BLOCKS");
     blocks = e ? atoi(e) : 0;
     if (blocks < 0) blocks = 0;
     const char* f = getenv("CLOUD_AMD_BN_APPLY_ILV");
-    ilv = (f && f[0] == '1') ? 1 : 0;
+    ilv = (f && f[0] == '0') ? 0 : 1;
   }
   Tiling t = blocks ? make_tiling(M, C, blocks, blocks) : make_tiling(M, C);
   t.ilv = ilv;
