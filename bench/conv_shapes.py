@@ -31,8 +31,10 @@ def timeit(fn, iters=10, warm=2):
 
 
 def main():
-    only = sys.argv[1] if len(sys.argv) > 1 else None
+    only = sys.argv[1] if len(sys.argv) > 1 and sys.argv[1] != "all" else None
+    batch = int(sys.argv[2]) if len(sys.argv) > 2 else None  # override the per-shape batch
     for N, H, Cin, Cout, k, s, p, tag in SHAPES:
+        N = batch or N
         if only and tag != only:
             continue
         x = torch.randn(N, H, H, Cin, device="cuda").to(torch.bfloat16)

@@ -56,6 +56,8 @@ _VARS = [
         "the HBM stream; 0 = the reduction kernels' tiling", "ops"),
     Var("CLOUD_AMD_BN_APPLY_ILV", bool, True, "BatchNorm apply passes: 1 = RP-row groups dealt round-robin to "
         "the workgroups (one contiguous sweep); 0 = one contiguous row chunk per workgroup", "ops"),
+    Var("CLOUD_AMD_CONV_TALL", bool, True, "<= 64-channel 3x3 convolutions (fwd, stride-1 dgrad): 256 x 64 tiles "
+        "with 4 x 1 waves; 0 = 128 x 64 with 2 x 2 waves", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "
         "K, minimum HBM bytes) to this file, for scripts/gemm_roofline.py", "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "

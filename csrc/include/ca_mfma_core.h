@@ -474,13 +474,25 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
           tq += sred[(PARTS + pp) * BN + c];
           if constexpr (Z2) t2 += sred[(2 * PARTS + pp) * BN + c];
         }
-        float* st = P.stats + (long)tm * 2 * P.N;
+        // partial rows are per 128 GEMM rows (host-sized): a 256-row tile writes its sums
+        // into the first of its two rows and zeros into the second (when it exists)
+        constexpr int SR = BM >= 128 ? BM / 128 : 1;
+        const bool zrow = SR == 2 && (long)(tm * 2 + 1) * 128 < P.M;
+        float* st = P.stats + (long)tm * SR * 2 * P.N;
         st[n0 + c] = ts;
         st[P.N + n0 + c] = tq;
+        if (zrow) {
+          st[2 * P.N + n0 + c] = 0.f;
+          st[3 * P.N + n0 + c] = 0.f;
+        }
         if constexpr (Z2) {
-          float* st2 = P.stats2 + (long)tm * 2 * P.N;
+          float* st2 = P.stats2 + (long)tm * SR * 2 * P.N;
           st2[n0 + c] = ts;
           st2[P.N + n0 + c] = t2;
+          if (zrow) {
+            st2[2 * P.N + n0 + c] = 0.f;
+            st2[3 * P.N + n0 + c] = 0.f;
+          }
         }
       }
     } else if (P.stats) {
@@ -508,9 +520,14 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
           ts += sred[pp * BN + col];
           tq += sred[(TPC + pp) * BN + col];
         }
-        float* st = P.stats + (long)tm * 2 * P.N;
+        constexpr int SR = BM >= 128 ? BM / 128 : 1;
+        float* st = P.stats + (long)tm * SR * 2 * P.N;
         st[n0 + col] = ts;
         st[P.N + n0 + col] = tq;
+        if (SR == 2 && (long)(tm * 2 + 1) * 128 < P.M) {
+          st[2 * P.N + n0 + col] = 0.f;
+          st[3 * P.N + n0 + col] = 0.f;
+        }
       }
     }
   }

@@ -717,6 +717,26 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
   mfma_gemm_glds<BM, BN, 2, 4, LA, LB, EPI, 2>(P);
 }
 
+// Tall tiles for the <= 64-channel implicit-GEMM convolutions (ResNet layer-1 3x3 fwd and
+// dgrad): 256 x 64 with 4 x 1 waves (64 x 64 wave tiles) -- twice the MFMAs per K-tile
+// barrier of the 128 x 64 / 2 x 2 tile and one B-operand fetch per 256 rows.
+template <int BM, int BN, int WM, int WN, template <int, int, int> class LA, template <int, int, int> class LB,
+          int EPI>
+__global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(4)))
+conv_glds_w_kernel(CoreParams P) {
+  mfma_gemm_glds<BM, BN, WM, WN, LA, LB, EPI>(P);
+}
+
+// CLOUD_AMD_CONV_TALL=0 keeps 128 x 64 tiles on those convolutions (A/B runs).
+bool tall_tiles() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_CONV_TALL");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
+}
+
 // CLOUD_AMD_GEMM_CORE=reg selects the register-staged core (A/B comparisons).
 // 0 = register-staged, 1 = glds single stage (4 waves), 2 = glds double-buffered (8 waves)
 int core_kind() {
@@ -765,6 +785,19 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
   return 0;
 }
 
+// 128 x 64 launch of an N <= 64 convolution, as 256 x 64 / 4 x 1 waves when enabled
+template <template <int, int, int> class LA, template <int, int, int> class LB,
+          template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
+int launch_n64(const CoreParams& p0, hipStream_t s) {
+  if (!(tall_tiles() && core_kind() == 1)) return launch<128, 64, LA, LB, GA, GB, EPI>(p0, 1, s);
+  CoreParams p = p0;
+  p.split_xcd = split_xcd_enabled();
+  const int tiles = (p.M + 255) / 256;
+  conv_glds_w_kernel<256, 64, 4, 1, GA, GB, EPI><<<dim3(tiles, 1, 1), 256, 0, s>>>(p);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
 CoreParams conv_params(int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw) {
   CoreParams p{};
   p.Nb = Nb; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout; p.KH = KH; p.KW = KW;
@@ -799,10 +832,10 @@ int ca_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   p.stats = stats;
   if (p.cin_tile && KH * KW <= 32 && tapmask_loaders()) {
     if (stats) {
-      if (Cout <= 64) return launch<128, 64, ConvFwdA, DenseKC, GConvFwdAT, GDenseKC, EPI_BF16_ST>(p, 1, s);
+      if (Cout <= 64) return launch_n64<ConvFwdA, DenseKC, GConvFwdAT, GDenseKC, EPI_BF16_ST>(p, s);
       return launch<128, 128, ConvFwdA, DenseKC, GConvFwdAT, GDenseKC, EPI_BF16_ST>(p, 1, s);
     }
-    if (Cout <= 64) return launch<128, 64, ConvFwdA, DenseKC, GConvFwdAT, GDenseKC, EPI_BF16>(p, 1, s);
+    if (Cout <= 64) return launch_n64<ConvFwdA, DenseKC, GConvFwdAT, GDenseKC, EPI_BF16>(p, s);
     return launch<128, 128, ConvFwdA, DenseKC, GConvFwdAT, GDenseKC, EPI_BF16>(p, 1, s);
   }
   if (stats) {
@@ -845,7 +878,7 @@ long ca_conv_dgrad_stat_tiles(int Nb, int H, int W, int sh, int sw) {
 template <int EPI>
 static int launch_dgrad(const CoreParams& p, int Cin, hipStream_t s) {
   if (p.cout_tile && p.sh == 1 && p.sw == 1 && p.KH * p.KW <= 32 && tapmask_loaders()) {
-    if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradAT, GConvDgradBT, EPI>(p, 1, s);
+    if (Cin <= 64) return launch_n64<ConvDgradA, ConvDgradB, GConvDgradAT, GConvDgradBT, EPI>(p, s);
     return launch<128, 128, ConvDgradA, ConvDgradB, GConvDgradAT, GConvDgradBT, EPI>(p, 1, s);
   }
   if (Cin <= 64) return launch<128, 64, ConvDgradA, ConvDgradB, GConvDgradA, GConvDgradB, EPI>(p, 1, s);
