@@ -46,6 +46,8 @@ _VARS = [
         "workgroups run (tiles x splits); fewer splits = less fp32 slab traffic, more = fuller CUs", "ops"),
     Var("CLOUD_AMD_WGRAD_BLOCKS_SMALLM", int, 512, "convolution weight gradients with <= 128 output channels "
         "(ResNet stem, layers 1-2): split-K workgroup target", "ops"),
+    Var("CLOUD_AMD_STEM_WGRAD_BLOCKS", int, 2048, "space-to-depth stem weight gradient (the last kernel of the "
+        "backward pass): split-K workgroup target", "ops"),
     Var("CLOUD_AMD_DENSE_WGRAD_BLOCKS", int, 512, "dense-layer weight gradients (BERT): split-K workgroup target",
         "ops"),
     Var("CLOUD_AMD_TAPMASK", bool, True, "convolutions: tap-mask / incremental buffer-mode gather loaders; 0 keeps "

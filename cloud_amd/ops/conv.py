@@ -22,6 +22,7 @@ import os
 import torch
 import torch.nn.functional as F
 
+from .. import config
 from . import _ext, gemm
 
 
@@ -148,7 +149,9 @@ class _StemS2DFn(torch.autograd.Function):
         dy = dy.contiguous()
         Cout = dy.shape[-1]
         g = torch.zeros((Cout, 4, 4, 16), dtype=torch.float32, device=dy.device)
-        raw.conv_wgrad(dy, xs, g.shape, 1, 0, out=g, beta=0.0)
+        # the last kernel of the backward pass (nothing left to overlap it with): a wide
+        # split-K grid (b1024: 869 -> 651 us at 2048 vs 512 workgroups, bench/wgrad_sweep.py)
+        raw.conv_wgrad(dy, xs, g.shape, 1, 0, out=g, beta=0.0, blocks=config.get("CLOUD_AMD_STEM_WGRAD_BLOCKS"))
         gw = _s2d_weight_grad(g, ctx.cx)
         param = ctx.param
         sink = gemm._grad_sink(param) if param is not None else None

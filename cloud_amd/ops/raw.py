@@ -150,8 +150,9 @@ def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res
     return dx
 
 
-def conv_wgrad(dy, x, w_shape, stride, padding, out, beta=1.0):
-    """out (bf16 or fp32, shape of w) = wgrad + beta * out, split-K over N*OH*OW."""
+def conv_wgrad(dy, x, w_shape, stride, padding, out, beta=1.0, blocks=None):
+    """out (bf16 or fp32, shape of w) = wgrad + beta * out, split-K over N*OH*OW.
+    ``blocks``: split-K workgroup target overriding the configured one."""
     global _WGRAD_BLOCKS, _WGRAD_BLOCKS_SMALLM
     ext = _ext.load(required=True)
     if _WGRAD_BLOCKS is None:
@@ -166,7 +167,7 @@ def conv_wgrad(dy, x, w_shape, stride, padding, out, beta=1.0):
     ncols = KH * KW * Cin
     # <= 128 output channels: one row of tiles, so the grid is mostly K splits; the fp32
     # slabs stay small next to the pixel operands, and more splits fill the CUs
-    target = _WGRAD_BLOCKS_SMALLM if Cout <= 128 else _WGRAD_BLOCKS
+    target = blocks or (_WGRAD_BLOCKS_SMALLM if Cout <= 128 else _WGRAD_BLOCKS)
     splits = ext.gemm_splitk_effective(kred, wgrad_splits(Cout, ncols, kred, target_blocks=target))
     ws = torch.empty(splits * Cout * ncols, dtype=torch.float32, device=x.device)
     obf = int(out.dtype == torch.bfloat16)
