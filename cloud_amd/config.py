@@ -60,6 +60,8 @@ _VARS = [
         "the workgroups (one contiguous sweep); 0 = one contiguous row chunk per workgroup", "ops"),
     Var("CLOUD_AMD_CONV_TALL", bool, True, "<= 64-channel 3x3 convolutions (fwd, stride-1 dgrad): 256 x 64 tiles "
         "with 4 x 1 waves; 0 = 128 x 64 with 2 x 2 waves", "ops"),
+    Var("CLOUD_AMD_BN_GROUPS_MAX", int, 512, "BatchNorm statistics: most groups of the first-level reduction of the "
+        "per-tile partial rows (1..512; ~64 rows per group)", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "
         "K, minimum HBM bytes) to this file, for scripts/gemm_roofline.py", "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "

@@ -52,6 +52,7 @@ def stats_buffer(rows, channels, device):
 
 
 _WGRAD_BLOCKS = None
+_GWS_ROWS = 512  # BN statistics group workspace rows (bn.hip group_count)
 _WGRAD_BLOCKS_SMALLM = None
 _DENSE_WGRAD_BLOCKS = None
 
@@ -191,7 +192,7 @@ def bn_fwd_stats(x, gamma, beta, running_mean, running_var, eps, momentum, parti
     M = x.numel() // C
     dev = x.device
     stats = torch.empty(4 * C, dtype=torch.float32, device=dev)
-    gws = torch.empty(64 * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
+    gws = torch.empty(_GWS_ROWS * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
     sp = stats.data_ptr()
     ext.bn_fwd_partials_ex(x.data_ptr(), 0, 0, 0, M, C, partials.data_ptr(), partials.shape[0], _ext.ptr(gamma),
                            _ext.ptr(beta), float(eps), float(momentum), _ext.ptr(running_mean),
@@ -214,14 +215,14 @@ def bn_fwd(x, gamma, beta, running_mean, running_var, eps, momentum, relu, resid
     sp = stats.data_ptr()
     if residual_ss is not None:  # residual = input of another BN with [scale | shift] = residual_ss
         assert partials is not None and residual is not None and residual_ss.numel() == 2 * C
-        gws = torch.empty(64 * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
+        gws = torch.empty(_GWS_ROWS * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
         ext.bn_fwd_partials_ex(x.data_ptr(), residual.data_ptr(), residual_ss.data_ptr(), y.data_ptr(), M, C,
                                partials.data_ptr(), partials.shape[0], _ext.ptr(gamma), _ext.ptr(beta), float(eps),
                                float(momentum), _ext.ptr(running_mean), _ext.ptr(running_var), sp, sp + 4 * C,
                                sp + 8 * C, int(relu), _ext.ptr(mask), _ext.ptr(gws), _st(dev))
         return y, stats, mask
     if partials is not None:
-        gws = torch.empty(64 * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
+        gws = torch.empty(_GWS_ROWS * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
         ext.bn_fwd_partials(x.data_ptr(), _ext.ptr(residual), y.data_ptr(), M, C, partials.data_ptr(),
                             partials.shape[0], _ext.ptr(gamma), _ext.ptr(beta), float(eps), float(momentum),
                             _ext.ptr(running_mean), _ext.ptr(running_var), sp, sp + 4 * C, sp + 8 * C, int(relu),
@@ -251,7 +252,7 @@ def bn_bwd(dy, y, x, gamma, stats, relu, dgamma=None, dbeta=None, want_dres=Fals
     sp = stats.data_ptr()
     if partials is not None:
         assert partials.shape[1:] == (2, C)
-        gws = torch.empty(64 * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
+        gws = torch.empty(_GWS_ROWS * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
         ext.bn_bwd_partials(dy.data_ptr(), _ext.ptr(y), _ext.ptr(mask), x.data_ptr(), M, C, partials.data_ptr(),
                             partials.shape[0], _ext.ptr(gamma), sp, sp + 4 * C, dx.data_ptr(), _ext.ptr(dres),
                             _ext.ptr(dgamma), _ext.ptr(dbeta), coef.data_ptr(), _ext.ptr(gws),

@@ -153,9 +153,18 @@ __global__ void __launch_bounds__(256) chunk_group_reduce_kernel(const float* __
   out[(long)g * 2 * C + C + c] = (rb[0][cl] + rb[1][cl]) + (rb[2][cl] + rb[3][cl]);
 }
 
+// ~64 partial rows per group, at most 512 groups (the [512][2][C] group workspace the
+// callers pass).  A 56x56 layer at batch 1024 has 25,088 tile rows: 64 groups left 64
+// workgroups walking 392 rows each (18-22 us, latency-bound); 392 groups take ~5 us.
 int group_count(int nchunks) {
+  static int cap = -1;
+  if (cap < 0) {  // CLOUD_AMD_BN_GROUPS_MAX (A/B runs; 64 = the earlier fixed cap)
+    const char* e = getenv("CLOUD_AMD_BN_GROUPS_MAX");
+    cap = e ? atoi(e) : 512;
+    if (cap < 1 || cap > 512) cap = 512;
+  }
   int g = (nchunks + 63) / 64;
-  return g < 1 ? 1 : (g > 64 ? 64 : g);
+  return g < 1 ? 1 : (g > cap ? cap : g);
 }
 
 __global__ void __launch_bounds__(BLK) bn_stats_kernel(const bf16_t* __restrict__ x, long M, int C,
@@ -493,7 +502,7 @@ int ca_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
 int ca_bn_fwd_partials(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C, const float* partials,
                        int nparts, const float* gamma, const float* beta, float eps, float momentum,
                        float* run_mean, float* run_var, float* save_mean, float* save_rstd,
-                       float* scale_shift, int relu, uint8_t* mask, float* gws /* [64][2][C] or null */,
+                       float* scale_shift, int relu, uint8_t* mask, float* gws /* [512][2][C] or null */,
                        hipStream_t s) {
   if (C % 8 != 0) return -1;
   Tiling t = make_tiling(M, C);
@@ -616,7 +625,7 @@ int ca_bn_bwd(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16
 int ca_bn_bwd_partials(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16_t* x, long M, int C,
                        const float* partials, int nparts, const float* gamma, const float* save_mean,
                        const float* save_rstd, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta,
-                       float* coef /* [3C] */, float* gws /* [64][2][C] */, int relu, hipStream_t s) {
+                       float* coef /* [3C] */, float* gws /* [512][2][C] */, int relu, hipStream_t s) {
   if (C % 8 != 0 || (nparts > 64 && !gws)) return -1;
   const int accum = (relu >> 1) & 1;
   relu &= 1;
