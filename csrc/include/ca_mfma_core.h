@@ -312,7 +312,11 @@ __device__ __forceinline__ void mfma_acc(f4v (&acc)[FM][FN], const bf16x8 (&af)[
 
 // Shared epilogue: fp32 split-K slab store, or bf16 through LDS with bias /
 // activation / pre-activation / act' / beta-accumulate / BN-statistics options.
-template <int BM, int BN, int WM, int WN, int EPI, int SMEM_SHORTS, int FM = BM / WM / 16, int FN = BN / WN / 16>
+// EPF > 1: plain / statistics bf16 epilogues read EPF staged rows from LDS before
+// storing any (batched LDS latency; dense GEMMs only -- the conv loaders' registers leave
+// no room, see docs/performance.md)
+template <int BM, int BN, int WM, int WN, int EPI, int SMEM_SHORTS, int EPF = 1, int FM = BM / WM / 16,
+          int FN = BN / WN / 16>
 __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM][FN], short* smem, int m0, int n0,
                                               int tm, int tid) {
   constexpr int NT = WM * WN * 64;
@@ -378,7 +382,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
     constexpr bool RES = EPI != EPI_BF16_BN;  // res_src / res_mask compiled in
     // the calling core's LDS (SMEM_SHORTS bf16 slots) must hold the three statistics rows
     static_assert(!Z2 || 3 * (NT / (BN / 8)) * BN * 4 <= 2 * SMEM_SHORTS, "three statistics rows must fit the LDS");
-    constexpr int PF = BNS ? (IT < 2 ? IT : 2) : 1;
+    constexpr int PF = BNS ? (IT < 2 ? IT : 2) : (IT < EPF ? IT : EPF);
     const int col = (tid % (BN / 8)) * 8;
     const int gn = n0 + col;
     const bool has_beta = P.beta != 0.f;
@@ -812,7 +816,7 @@ struct loader_stateful<L, decltype((void)&L::advance)> {
 };
 
 template <int BM, int BN, int WM, int WN, template <int, int, int> class LAT, template <int, int, int> class LBT,
-          int EPI, int NSTAGE = 1>
+          int EPI, int NSTAGE = 1, int EPF = 1>
 __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
   // Measured on MI355X (bench/conv_shapes.py, bench/gemm_core_ab.py): NSTAGE 1 at
   // 4 blocks/CU beats NSTAGE 2 at 2 blocks/CU by 10-15% on every ResNet/BERT shape.
@@ -903,7 +907,7 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
       __builtin_amdgcn_s_barrier();
     }
   }
-  gemm_epilogue<BM, BN, WM, WN, EPI, SMEM>(P, acc, smem, m0, n0, tm, tid);
+  gemm_epilogue<BM, BN, WM, WN, EPI, SMEM, EPF>(P, acc, smem, m0, n0, tm, tid);
 }
 
 // ============================================== 256 x 256 ping-pong core --

@@ -26,6 +26,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) d
   mfma_gemm_glds<BM, BN, 2, 2, LA, LB, EPI>(P);
 }
 
+// same, with the plain / statistics epilogues reading 4 staged rows ahead of their stores
+template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) dense_gemm_glds_pf_kernel(CoreParams P) {
+  mfma_gemm_glds<BM, BN, 2, 2, LA, LB, EPI, 1, 4>(P);
+}
+
+// CLOUD_AMD_EPI_PF=1: dense bf16 GEMMs without BN-backward statistics use the batched epilogue
+bool epi_pf() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_EPI_PF");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v != 0;
+}
+
 // 8 waves (2 x 4, wave tile 64 x BN/4) with a double-buffered LDS-DMA pipeline:
 // same 16 waves/CU occupancy as the 4-wave single-stage kernel, but the next K
 // tile's DMA overlaps this tile's MFMAs (CLOUD_AMD_GEMM_CORE=glds8).
@@ -115,6 +131,15 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
     dense_gemm_glds8_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 512, 0, s>>>(p);
     CA_LAUNCH_CHECK();
     return 0;
+  }
+  // K-contiguous operands only (forward GEMMs): the N-contiguous loaders' extra registers
+  // make the batched epilogue spill (448-480 B/lane of scratch)
+  if constexpr ((EPI == EPI_BF16 || EPI == EPI_BF16_ST) && GA<BM, 1, 256>::KC && GB<BN, 1, 256>::KC) {
+    if (use_glds() && epi_pf()) {
+      dense_gemm_glds_pf_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
+      CA_LAUNCH_CHECK();
+      return 0;
+    }
   }
   if (use_glds()) {
     dense_gemm_glds_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
