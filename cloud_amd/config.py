@@ -62,8 +62,8 @@ _VARS = [
         "with 4 x 1 waves; 0 = 128 x 64 with 2 x 2 waves", "ops"),
     Var("CLOUD_AMD_BN_GROUPS_MAX", int, 512, "BatchNorm statistics: most groups of the first-level reduction of the "
         "per-tile partial rows (1..512; ~64 rows per group)", "ops"),
-    Var("CLOUD_AMD_EPI_PF", bool, False, "dense forward GEMMs (K-contiguous operands, plain / BN-statistics "
-        "epilogue): read 4 staged output rows from LDS before storing any", "ops"),
+    Var("CLOUD_AMD_EPI_PF", bool, True, "dense forward GEMMs with the BN-statistics epilogue (ResNet 1x1 convs): "
+        "read 4 staged output rows from LDS before storing any", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "
         "K, minimum HBM bytes) to this file, for scripts/gemm_roofline.py", "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "
