@@ -64,6 +64,8 @@ _VARS = [
         "per-tile partial rows (1..512; ~64 rows per group)", "ops"),
     Var("CLOUD_AMD_EPI_PF", bool, True, "dense forward GEMMs with the BN-statistics epilogue (ResNet 1x1 convs): "
         "read 4 staged output rows from LDS before storing any", "ops"),
+    Var("CLOUD_AMD_CONV_EPI_PF", bool, True, "implicit-GEMM forward convolutions with the BN-statistics epilogue: "
+        "read 2 staged output rows from LDS before storing", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "
         "K, minimum HBM bytes) to this file, for scripts/gemm_roofline.py", "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "

@@ -704,9 +704,12 @@ struct GConvDgradSBT {
   }
 };
 
-template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
+// EPF: rows the BN-statistics epilogue reads from LDS before storing (2 fits the gather
+// loaders' registers without scratch; 4 spills 480-512 B/lane)
+template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB, int EPI,
+          int EPF = 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) conv_glds_kernel(CoreParams P) {
-  mfma_gemm_glds<BM, BN, 2, 2, LA, LB, EPI>(P);
+  mfma_gemm_glds<BM, BN, 2, 2, LA, LB, EPI, 1, EPF>(P);
 }
 
 // 8 waves (2 x 4, wave tile 64 x BN/4) with a double-buffered LDS-DMA pipeline:
@@ -721,10 +724,22 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) c
 // dgrad): 256 x 64 with 4 x 1 waves (64 x 64 wave tiles) -- twice the MFMAs per K-tile
 // barrier of the 128 x 64 / 2 x 2 tile and one B-operand fetch per 256 rows.
 template <int BM, int BN, int WM, int WN, template <int, int, int> class LA, template <int, int, int> class LB,
-          int EPI>
+          int EPI, int EPF = 1>
 __global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(4)))
 conv_glds_w_kernel(CoreParams P) {
-  mfma_gemm_glds<BM, BN, WM, WN, LA, LB, EPI>(P);
+  mfma_gemm_glds<BM, BN, WM, WN, LA, LB, EPI, 1, EPF>(P);
+}
+
+// Forward convolutions with the BN-statistics epilogue read 2 staged rows per epilogue trip
+// (fwd3x3 -2..-5 % per call, end-to-end neutral: 14,148 vs 14,137 img/s same box);
+// CLOUD_AMD_CONV_EPI_PF=0 restores one row per trip (A/B runs).
+bool conv_epi_pf() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_CONV_EPI_PF");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
 }
 
 // CLOUD_AMD_CONV_TALL=0 keeps 128 x 64 tiles on those convolutions (A/B runs).
@@ -775,6 +790,13 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
     CA_LAUNCH_CHECK();
     return 0;
   }
+  if constexpr (EPI == EPI_BF16_ST) {
+    if (use_glds() && conv_epi_pf()) {
+      conv_glds_kernel<BM, BN, GA, GB, EPI, 2><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
+      CA_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   if (use_glds()) {
     conv_glds_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
     CA_LAUNCH_CHECK();
@@ -793,6 +815,13 @@ int launch_n64(const CoreParams& p0, hipStream_t s) {
   CoreParams p = p0;
   p.split_xcd = split_xcd_enabled();
   const int tiles = (p.M + 255) / 256;
+  if constexpr (EPI == EPI_BF16_ST) {
+    if (conv_epi_pf()) {
+      conv_glds_w_kernel<256, 64, 4, 1, GA, GB, EPI, 2><<<dim3(tiles, 1, 1), 256, 0, s>>>(p);
+      CA_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   conv_glds_w_kernel<256, 64, 4, 1, GA, GB, EPI><<<dim3(tiles, 1, 1), 256, 0, s>>>(p);
   CA_LAUNCH_CHECK();
   return 0;
