@@ -48,7 +48,8 @@ _VARS = [
         "(ResNet stem, layers 1-2): split-K workgroup target", "ops"),
     Var("CLOUD_AMD_STEM_WGRAD_BLOCKS", int, 2048, "space-to-depth stem weight gradient (the last kernel of the "
         "backward pass): split-K workgroup target", "ops"),
-    Var("CLOUD_AMD_DENSE_WGRAD_BLOCKS", int, 512, "dense-layer weight gradients (BERT): split-K workgroup target",
+    Var("CLOUD_AMD_DENSE_WGRAD_BLOCKS", int, 1024, "dense-layer weight gradients (BERT): split-K workgroup target "
+        "(1024 with the split-major XCD mapping: 6,210 / 6,231 vs 6,153 / 6,131 seq/s at 512)",
         "ops"),
     Var("CLOUD_AMD_TAPMASK", bool, True, "convolutions: tap-mask / incremental buffer-mode gather loaders; 0 keeps "
         "the general per-chunk decode loaders (A/B runs)", "ops"),
