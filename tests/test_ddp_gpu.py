@@ -14,6 +14,16 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+
+def _free_port():
+    """An unused TCP port on 127.0.0.1 (bind to 0): fixed pid-based formulas collide across
+    test cases and pytest-xdist workers."""
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
 def _worker(rank, world, port, out_dir, use_fused=True, emulate=1):
     """``emulate`` > 1 (with world 1): one process runs every replica's half-batch
     through forward/backward into the same arena (gradient accumulation) -- the
@@ -76,7 +86,7 @@ def _worker(rank, world, port, out_dir, use_fused=True, emulate=1):
 @pytest.mark.parametrize("use_fused", [True, False])
 def test_ddp_two_ranks_through_fused_blocks(tmp_path, use_fused):
     world = 2
-    port = 29700 + os.getpid() % 1000 + (0 if use_fused else 7)
+    port = _free_port()
     mp.spawn(_worker, args=(world, port, str(tmp_path), use_fused), nprocs=world, join=True)
     r = [torch.load(tmp_path / f"r{i}.pt", weights_only=True) for i in range(world)]
     assert r[0]["fused"] == use_fused and r[1]["fused"] == use_fused

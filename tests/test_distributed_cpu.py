@@ -13,6 +13,16 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+
+def _free_port():
+    """An unused TCP port on 127.0.0.1 (bind to 0): fixed pid-based formulas collide across
+    test cases and pytest-xdist workers."""
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
 def _worker(rank, world, port, out_dir):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
@@ -48,7 +58,7 @@ def _worker(rank, world, port, out_dir):
 
 def test_ddp_matches_single_process(tmp_path):
     world = 2
-    port = 29000 + os.getpid() % 1000
+    port = _free_port()
     mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
     r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
@@ -124,7 +134,7 @@ def _desync_worker(rank, world, port, out_dir):
 
 def test_grad_desync_detector(tmp_path):
     world = 2
-    port = 29500 + os.getpid() % 1000
+    port = _free_port()
     mp.spawn(_desync_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
     assert [open(tmp_path / f"desync{r}").read() for r in range(world)] == ["caught", "caught"]
 

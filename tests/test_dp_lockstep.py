@@ -75,6 +75,16 @@ def _train(mode, n, strategy=None):
     return [w.copy() for w in m.get_weights()], {"loss": losses}
 
 
+def _free_port():
+    """An unused TCP port on 127.0.0.1 (bind to 0): fixed formulas collide across
+    parametrised cases and pytest-xdist workers."""
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
 def _worker(rank, port, mode, n, out_dir):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), CLOUD_AMD_DEVICE="cpu", CLOUD_AMD_JOB_ID="lockstep-test")
@@ -92,7 +102,7 @@ def _worker(rank, port, mode, n, out_dir):
 @pytest.mark.parametrize("mode,n", [("fit_array", 70), ("fit_array", 65), ("fit_dataset", 65),
                                     ("ctl", 70), ("ctl", 65)])
 def test_two_replicas_match_single_process(tmp_path, mode, n):
-    port = 29700 + (os.getpid() + n + len(mode)) % 200
+    port = _free_port()
     mp.spawn(_worker, args=(port, mode, n, str(tmp_path)), nprocs=WORLD, join=True)
     sys.path.insert(0, ROOT)
     os.environ.pop("WORLD_SIZE", None)

@@ -16,6 +16,16 @@ WORLD = 8
 N = 1 << 16
 
 
+
+def _free_port():
+    """An unused TCP port on 127.0.0.1 (bind to 0): fixed pid-based formulas collide across
+    test cases and pytest-xdist workers."""
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
 def _grads(rank):
     g = torch.Generator().manual_seed(100 + rank)
     # a shared signal plus per-rank noise (replica gradients are correlated), plus a few
@@ -51,7 +61,7 @@ def _worker(rank, port, out_dir):
 
 
 def test_bf16_vs_fp32_wire_error_at_8_ranks(tmp_path):
-    port = 29300 + os.getpid() % 500
+    port = _free_port()
     mp.spawn(_worker, args=(port, str(tmp_path)), nprocs=WORLD, join=True)
     res = json.load(open(tmp_path / "sums.json"))
     exact = sum(_grads(r).double() for r in range(WORLD))
