@@ -1,0 +1,16 @@
+#!/usr/bin/env bash
+# 128x64 tiles for all forward 1x1 GEMMs with BN statistics (reverted FWD_N64 switch, gemm.hip): tests, A/B, profile.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+S=scripts/gpu_step.sh
+FWD_N64=1 $S 600 r2s42_pytest_gpu.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread || exit 1
+grep -q " passed" gpurun_out/r2s42_pytest_gpu.log && ! grep -q " failed" gpurun_out/r2s42_pytest_gpu.log || { echo "GPU tests failed"; exit 1; }
+for i in 1 2 3; do
+  FWD_N64=0 $S 200 r2s42_bench_n0_$i.log python bench.py --via-run 0 || exit 1
+  FWD_N64=1 $S 200 r2s42_bench_n1_$i.log python bench.py --via-run 0 || exit 1
+done
+rm -f gpurun_out/r2s42_shapes.jsonl
+FWD_N64=1 CLOUD_AMD_WGRAD_STREAM=0 CLOUD_AMD_SHAPE_LOG=gpurun_out/r2s42_shapes.jsonl $S 300 r2s42_prof.log \
+  rocprofv3 --kernel-trace --stats -d gpurun_out/r2s42_prof -o run -- python bench.py --via-run 0 --steps 5 --warmup 3 || exit 1
+echo SESSION_DONE
