@@ -34,12 +34,20 @@ def family(name):
 def main(dirs):
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = collections.defaultdict(dict)
+    seen = collections.defaultdict(set)  # counter -> passes that collected it
     for d in dirs:
         with open(os.path.join(d, "run_counter_collection.csv")) as f:
             for r in csv.DictReader(f):
                 k = family(r["Kernel_Name"])
                 acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                seen[r["Counter_Name"]].add(d)
                 dur[k][(d, r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    # a counter collected in several passes (GRBM_GUI_ACTIVE as the clock reference) is the
+    # per-pass mean, so it stays comparable with counters collected once
+    for k in acc:
+        for cn, ds in seen.items():
+            if len(ds) > 1 and cn in acc[k]:
+                acc[k][cn] /= len(ds)
     rows = []
     for k, c in acc.items():
         t = sum(dur[k].values()) / max(1, len(dirs))  # each pass re-runs the same dispatches
