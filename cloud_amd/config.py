@@ -67,6 +67,8 @@ _VARS = [
         "read 4 staged output rows from LDS before storing any", "ops"),
     Var("CLOUD_AMD_CONV_EPI_PF", bool, True, "implicit-GEMM forward convolutions with the BN-statistics epilogue: "
         "read 2 staged output rows from LDS before storing", "ops"),
+    Var("CLOUD_AMD_CONV_HALO", bool, False, "stride-1 3x3 forward convolutions (W <= 63, Cin % 64 == 0): flattened-"
+        "halo kernel (one LDS fill of the input rows per 64-channel chunk, 9 taps read shifted)", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "
         "K, minimum HBM bytes) to this file, for scripts/gemm_roofline.py", "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "
