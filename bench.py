@@ -72,6 +72,17 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def _finite(o):
+    """NaN / inf -> None: the JSON line must be strict JSON (json.dumps allow_nan=False)."""
+    if isinstance(o, float):
+        return o if o == o and o not in (float("inf"), float("-inf")) else None
+    if isinstance(o, dict):
+        return {k: _finite(v) for k, v in o.items()}
+    if isinstance(o, (list, tuple)):
+        return [_finite(v) for v in o]
+    return o
+
+
 def via_run(args):
     """Stage this script and launch ``--gpus`` ranks through ``cloud_amd.run()``.
     This process never initialises HIP; rank 0's log (ending in the JSON line) is
@@ -96,11 +107,17 @@ def main():
     from cloud_amd.models.resnet import resnet18_like_small
     from cloud_amd.ops import softmax_cross_entropy
     from cloud_amd.optim import SGD
-    from cloud_amd.parallel.ddp import GradAllReducer
+    from cloud_amd.parallel import strategy as strategy_mod
     from cloud_amd.utils import dist_env, trace
 
-    dev_arg = torch.device("cpu") if args.device == "cpu" else None
-    rank, world, device = dist_env.init_distributed(device=dev_arg)
+    if args.device == "cpu":
+        os.environ.setdefault("CLOUD_AMD_DEVICE", "cpu")
+    # The DP engine comes from the distribution strategy: the one run()'s generated wrapper
+    # installed (distribution_strategy="auto": MirroredStrategy at N > 1, OneDeviceStrategy at
+    # 1 -- reference TFC/core/preprocess.py:137-146), or the default for a torchrun rank.
+    strategy = strategy_mod.get_strategy()
+    device = strategy.device
+    rank, world = strategy.rank, strategy.num_replicas_in_sync
     benchlaunch.check_world(args.gpus, world)
     on_gpu = device.type == "cuda"
     if not on_gpu and args.model == "resnet50" and os.environ.get("CLOUD_AMD_BENCH_ALLOW_CPU") != "1":
@@ -114,7 +131,7 @@ def main():
     model = build(num_classes=args.classes, dtype=dtype, device=device)
     # mean over the GLOBAL batch: every rank holds B samples, so 1/world folds into the optimizer
     opt = SGD(model, learning_rate=args.lr, momentum=0.9, weight_decay=5e-5, grad_scale=1.0 / world)
-    reducer = GradAllReducer(opt.arenas, bucket_mb=args.bucket_mb, reduce_dtype=args.grad_reduce_dtype)
+    reducer = strategy.gradient_reducer(opt.arenas, bucket_mb=args.bucket_mb, reduce_dtype=args.grad_reduce_dtype)
     reducer.broadcast_parameters()
 
     gen = torch.Generator(device=device)
@@ -151,11 +168,20 @@ def main():
     run_t0 = os.environ.get("CLOUD_AMD_RUN_T0")
     run_to_first = (time.time() - float(run_t0)) if run_t0 else None
 
-    # (HIP-graph capture of this step, cloud_amd.runtime.graph, measured slower than eager on
-    # ROCm 7.2 at b256/b512: kernel boundaries cost the same in a graph; not offered here)
+    # (HIP-graph capture of this step measured slower than eager on ROCm 7.2 at b256/b512:
+    # kernel boundaries cost the same in a graph; not offered here -- docs/performance.md)
     step_fn = train_step
     for _ in range(max(args.warmup - 1, 0)):
         loss = step_fn()
+    # desync check once after warmup (world > 1): every replica must hold identical
+    # all-reduced gradients (fp64 fingerprint over all arenas, all-gathered)
+    replicas_consistent = None
+    if world > 1:
+        try:
+            replicas_consistent = bool(reducer.check_consistency())
+        except RuntimeError as e:
+            replicas_consistent = False
+            print("[bench] %s" % e, file=sys.stderr, flush=True)
     dist_env.barrier()
     sync()
     reducer.timing_start()
@@ -166,8 +192,10 @@ def main():
     dist_env.barrier()
     t1 = time.perf_counter()
     comm = reducer.timing_summary()
+    per_rank_ms = [v / args.steps * 1000.0 for v in dist_env.all_gather_floats(t1 - t0, device)]
     elapsed = dist_env.all_reduce_max(t1 - t0, device)
     ms = elapsed / args.steps * 1000.0
+    busbw = dist_env.allreduce_busbw(device) if world > 1 else None  # after the timed steps
     ips = global_batch * args.steps / elapsed
     first_lat = dist_env.all_reduce_max(first_step_latency, device)
     if run_to_first is not None:
@@ -210,15 +238,19 @@ def main():
             "device": device.type,
             "backend": backend if world > 1 else None,
             "shared_gpu": bool(config.get("CLOUD_AMD_SHARED_GPU")),
+            "strategy": strategy.name,
             "comm": dict(reducer.describe(), allreduce_ms=comm["allreduce_ms"],
-                         exposed_comm_ms=comm["exposed_comm_ms"]),
+                         exposed_comm_ms=comm["exposed_comm_ms"], timing=comm.get("timing"),
+                         busbw_gbs=busbw),
+            "replicas_consistent": replicas_consistent,
+            "rank_ms_per_step": {"min": round(min(per_rank_ms), 3), "max": round(max(per_rank_ms), 3)},
             "first_step_latency_s": round(first_lat, 3),
             "run_to_first_step_s": round(run_to_first, 3) if run_to_first is not None else None,
             "launched_via": launched,
             "final_loss": round(final_loss, 4),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2) if on_gpu else None,
         }
-        line = json.dumps(out)
+        line = json.dumps(_finite(out), allow_nan=False)
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:

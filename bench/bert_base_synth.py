@@ -61,6 +61,17 @@ def synthetic_glue(B, S, device, seed):
     return ids, tts, am, labels
 
 
+def _finite(o):
+    """NaN / inf -> None (the result line is strict JSON)."""
+    if isinstance(o, float):
+        return o if o == o and o not in (float("inf"), float("-inf")) else None
+    if isinstance(o, dict):
+        return {k: _finite(v) for k, v in o.items()}
+    if isinstance(o, (list, tuple)):
+        return [_finite(v) for v in o]
+    return o
+
+
 def main():
     args = parse()
     from cloud_amd.utils import benchlaunch
@@ -72,9 +83,14 @@ def main():
     import torch.nn.functional as F
 
     from cloud_amd import config
+    from cloud_amd.parallel import strategy as strategy_mod
     from cloud_amd.utils import dist_env
 
-    rank, world, device = dist_env.init_distributed()
+    # DP engine from the strategy run()'s wrapper installed (auto: Mirrored at N > 1,
+    # OneDevice at 1), or the default strategy of a torchrun rank
+    strategy = strategy_mod.get_strategy()
+    device = strategy.device
+    rank, world = strategy.rank, strategy.num_replicas_in_sync
     benchlaunch.check_world(args.gpus, world, tag="bert")
     reducer = None
     torch.manual_seed(1234)
@@ -104,12 +120,12 @@ def main():
         from cloud_amd.models.bert import BertConfig, BertForSequenceClassification
         from cloud_amd.ops import softmax_cross_entropy
         from cloud_amd.optim import AdamW
-        from cloud_amd.parallel.ddp import GradAllReducer
 
         cfg = BertConfig.base(num_hidden_layers=args.layers, num_labels=2)
         model = BertForSequenceClassification(cfg, device=device)
         opt = AdamW(model, learning_rate=args.lr, weight_decay=0.01, grad_scale=1.0 / world)
-        reducer = GradAllReducer(opt.arenas, bucket_mb=args.bucket_mb, reduce_dtype=args.grad_reduce_dtype)
+        reducer = strategy.gradient_reducer(opt.arenas, bucket_mb=args.bucket_mb,
+                                            reduce_dtype=args.grad_reduce_dtype)
         reducer.broadcast_parameters()
 
         def train_step():
@@ -129,6 +145,13 @@ def main():
     run_to_first = (time.time() - float(run_t0)) if run_t0 else None
     for _ in range(max(args.warmup - 1, 0)):
         loss = train_step()
+    replicas_consistent = None
+    if world > 1 and reducer is not None:
+        try:
+            replicas_consistent = bool(reducer.check_consistency())
+        except RuntimeError as e:
+            replicas_consistent = False
+            print("[bert] %s" % e, file=sys.stderr, flush=True)
     dist_env.barrier()
     torch.cuda.synchronize()
     if reducer is not None:
@@ -138,7 +161,10 @@ def main():
         loss = train_step()
     torch.cuda.synchronize()
     dist_env.barrier()
-    elapsed = dist_env.all_reduce_max(time.perf_counter() - t0, device)
+    dt = time.perf_counter() - t0
+    per_rank = [v / args.steps * 1000.0 for v in dist_env.all_gather_floats(dt, device)]
+    elapsed = dist_env.all_reduce_max(dt, device)
+    busbw = dist_env.allreduce_busbw(device) if world > 1 else None
     sps = B * world * args.steps / elapsed
     first = dist_env.all_reduce_max(first, device)
     if run_to_first is not None:
@@ -147,9 +173,10 @@ def main():
     if reducer is not None:
         t = reducer.timing_summary()
         comm = dict(reducer.describe(), allreduce_ms=dist_env.all_reduce_max(t["allreduce_ms"], device),
-                    exposed_comm_ms=dist_env.all_reduce_max(t["exposed_comm_ms"], device))
+                    exposed_comm_ms=dist_env.all_reduce_max(t["exposed_comm_ms"], device), timing=t.get("timing"),
+                    busbw_gbs=busbw)
     if rank == 0:
-        print(json.dumps({
+        print(json.dumps(_finite({
             "metric": "sequences/sec BERT-base fine-tune synthetic GLUE (seq %d)" % S,
             "value": round(sps, 2), "unit": "sequences/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000, 3), "higher_is_better": True,
@@ -163,7 +190,10 @@ def main():
             "launched_via": benchlaunch.launched_via(), "comm": comm,
             "backend": dist.get_backend() if world > 1 else None,
             "shared_gpu": bool(config.get("CLOUD_AMD_SHARED_GPU")),
-            "tokens_per_sec": round(sps * S, 1), "final_loss": round(float(loss.detach().float()), 4)}), flush=True)
+            "tokens_per_sec": round(sps * S, 1), "final_loss": round(float(loss.detach().float()), 4),
+            "strategy": strategy.name, "replicas_consistent": replicas_consistent,
+            "rank_ms_per_step": {"min": round(min(per_rank), 3), "max": round(max(per_rank), 3)}}),
+            allow_nan=False), flush=True)
     if world > 1:
         import torch.distributed as dist
 

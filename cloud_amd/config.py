@@ -24,6 +24,8 @@ class Var:
 _VARS = [
     # launcher / run()
     Var("CLOUD_AMD_JOBS_DIR", str, "./jobs", "where run() stages job directories", "launcher"),
+    Var("CLOUD_AMD_STAGE_COPY", bool, False, "stage the entry directory by copying instead of hard-linking "
+        "(a running job then never sees in-place edits of its sources)", "launcher"),
     Var("CLOUD_AMD_NUM_GPUS", int, None, "override the visible-GPU count (0 = CPU node)", "launcher"),
     Var("CLOUD_AMD_RUNNING_REMOTELY", str, "", "set by the launcher inside job ranks (remote() is True)", "launcher"),
     Var("CLOUD_AMD_JOB_ID", str, "", "job id (set in every rank)", "launcher"),

@@ -14,7 +14,10 @@ but the "cluster" is the local node:
   ``logs/<role>-<index>[-gpu<k>].log``;
 * a watchdog: if any rank exits non-zero the rest of the group is terminated,
   exit codes go to ``job.json`` and the job is marked FAILED;
-* ``stream_logs=True`` tails the chief log (rank 0) to stdout until the job ends.
+* ``stream_logs=True`` tails every rank's log to stdout until the job ends (reference
+  ``deploy.py:187-211`` streams the whole job); with more than one rank each line is
+  prefixed ``[chief-0]`` / ``[worker-1]`` / ``[chief-0-gpu3]`` (the log file's stem);
+* when the job fails, the failing rank and the last 50 lines of its log are printed.
 
 The launcher process never initialises the GPU: it sizes the job from the KFD
 topology in sysfs (:mod:`cloud_amd.core.topology`) and never calls into HIP, so
@@ -132,10 +135,11 @@ class Job:
         first_failure = None
         while True:
             codes = [p.poll() for p in self.procs]
-            bad = [c for c in codes if c not in (None, 0)]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
             if bad and failed_at is None:
                 failed_at = time.time()
-                first_failure = bad[0]  # the rank that failed, before the watchdog kills the rest
+                # the rank that failed, before the watchdog kills the rest
+                self.meta["failed_rank"], first_failure = bad[0]
                 for p in self.procs:
                     if p.poll() is None:
                         try:
@@ -170,26 +174,79 @@ class Job:
     def log_path(self, rank=0):
         return os.path.join(self.job_dir, "logs", log_name(self.ranks[rank]))
 
-    def stream(self, rank=0, out=None):
-        """Tail one rank's log to ``out`` until the job finishes."""
+    def stream(self, ranks=None, out=None, prefix=None):
+        """Tail the logs of ``ranks`` (default: every rank) to ``out`` until the job
+        finishes.  ``prefix`` (default: on when more than one log is streamed) starts each
+        line with ``[<role>-<index>]``; a line is only written once it is complete."""
         out = out or sys.stdout
-        path = self.log_path(rank)
-        while not os.path.exists(path) and not self.done():
-            time.sleep(0.05)
-        with open(path, "r", errors="replace") as f:
-            while True:
-                line = f.readline()
-                if line:
-                    out.write(line.replace("\x08", ""))
-                    out.flush()
+        if ranks is None:
+            ranks = list(range(len(self.ranks)))
+        elif isinstance(ranks, int):
+            ranks = [ranks]
+        if prefix is None:
+            prefix = len(ranks) > 1
+        tails = []  # [rank, file or None, partial line]
+        for r in ranks:
+            tails.append([r, None, ""])
+
+        def pump(final=False):
+            wrote = False
+            for t in tails:
+                r, f, part = t
+                if f is None:
+                    path = self.log_path(r)
+                    if not os.path.exists(path):
+                        continue
+                    f = t[1] = open(path, "r", errors="replace")
+                chunk = f.read()
+                if not chunk and not (final and part):
                     continue
-                if self.done():
-                    rest = f.read()
-                    if rest:
-                        out.write(rest)
-                        out.flush()
-                    break
-                time.sleep(0.05)
+                data = part + chunk
+                lines = data.split("\n")
+                t[2] = lines.pop()  # incomplete tail (no newline yet)
+                if final and t[2]:
+                    lines.append(t[2])
+                    t[2] = ""
+                tag = "[%s] " % log_name(self.ranks[r])[:-4] if prefix else ""
+                for ln in lines:
+                    out.write(tag + ln.replace("\x08", "") + "\n")
+                wrote = wrote or bool(lines)
+            if wrote:
+                out.flush()
+            return wrote
+
+        try:
+            while not self.done():
+                if not pump():
+                    time.sleep(0.05)
+            pump(final=True)
+        finally:
+            for t in tails:
+                if t[1] is not None:
+                    t[1].close()
+
+    def log_tail(self, rank, n=50):
+        """Last ``n`` lines of one rank's log."""
+        try:
+            with open(self.log_path(rank), "r", errors="replace") as f:
+                return f.read().splitlines()[-n:]
+        except OSError:
+            return []
+
+    def failure_report(self, n=50):
+        """Text naming the rank that failed first, its exit code and its last ``n`` log lines
+        (None if the job did not fail)."""
+        if self.returncode in (None, 0):
+            return None
+        r = self.meta.get("failed_rank")
+        if r is None:
+            codes = self.meta.get("exit_codes") or []
+            r = next((i for i, c in enumerate(codes) if c not in (None, 0)), 0)
+        code = (self.meta.get("exit_codes") or [None] * (r + 1))[r]
+        lines = ["[cloud_amd] job %s FAILED: rank %d (%s) exited with code %s; last %d lines of %s:"
+                 % (self.job_id, r, log_name(self.ranks[r])[:-4], code, n, self.log_path(r))]
+        lines += ["    " + ln for ln in self.log_tail(r, n)]
+        return "\n".join(lines)
 
 
 def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, entry_point_args=None,
@@ -200,7 +257,9 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
     port = free_port()
     app_dir = os.path.dirname(target)
     python = python or sys.executable
-    any_gpu = any(r["gpu"] is not None for r in ranks)
+    # CLOUD_AMD_DEVICE=cpu (validate.cpu_rehearsal): GPU-shaped job, CPU ranks over gloo
+    rehearsal = os.environ.get("CLOUD_AMD_DEVICE") == "cpu"
+    any_gpu = any(r["gpu"] is not None for r in ranks) and not rehearsal
     node = topology.describe_node()
     n_gpu_ranks = sum(1 for r in ranks if r["gpu"] is not None)
     comm_env = rccl_env(n_gpu_ranks, topology.xgmi_links_per_gpu(n_gpu_ranks)) if any_gpu else {}
@@ -209,7 +268,7 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
         "chief_config": chief_config.to_dict(), "worker_count": worker_count,
         "worker_config": worker_config.to_dict() if worker_config is not None and worker_count > 0 else None,
         "labels": dict(job_labels or {}), "args": list(entry_point_args or []),
-        "backend": "nccl(rccl)" if any_gpu else "gloo", "master_port": port,
+        "backend": "nccl(rccl)" if any_gpu else "gloo", "master_port": port, "cpu_rehearsal": rehearsal,
         "ranks": ranks, "node": node, "comm_env": {k: os.environ.get(k, v) for k, v in comm_env.items()},
     }
     procs = []
@@ -265,7 +324,10 @@ def deploy_job(job_id, job_dir, target, chief_config, worker_count, worker_confi
     _print_logs_info(job_id, job_dir)
     if enable_stream_logs:
         print("Streaming job logs: ")
-        job.stream(0)
+        job.stream()
     if wait or (wait is None and enable_stream_logs):
         job.wait()
+        report = job.failure_report()
+        if report:
+            print(report, file=sys.stderr, flush=True)
     return job

@@ -57,6 +57,20 @@ def run(entry_point=None, requirements_txt=None, distribution_strategy="auto", d
                       called_from_notebook, job_labels=job_labels, docker_base_image=docker_base_image,
                       check_node=True)
 
+    if entry_point is None and called_from_notebook:
+        # run() inside a notebook with no entry point: the reference pulled the live notebook
+        # from Colab (TFC/core/preprocess.py:166-167,196-212); here the notebook file the
+        # kernel serves is located and converted like an .ipynb entry point
+        nb = current_notebook_path()
+        if nb is None:
+            raise RuntimeError("run() was called from a notebook with entry_point=None, but the notebook file "
+                               "could not be located (no JPY_SESSION_NAME / __session__); pass "
+                               "entry_point='<notebook>.ipynb'.")
+        entry_point = os.path.relpath(nb) if not os.path.relpath(nb).startswith("..") else nb
+        validate.validate(entry_point, requirements_txt, distribution_strategy, chief_config, worker_config,
+                          worker_count, region, entry_point_args, stream_logs, docker_image_bucket_name,
+                          called_from_notebook, job_labels=job_labels, docker_base_image=docker_base_image)
+
     job_id = launcher.generate_job_id()
     root = os.path.abspath(jobs_dir) if jobs_dir else stage.jobs_root()
     os.makedirs(root, exist_ok=True)
@@ -82,6 +96,33 @@ def run(entry_point=None, requirements_txt=None, distribution_strategy="auto", d
         rc = job.wait() if (wait or stream_logs) else 0
         sys.exit(rc or 0)
     return job
+
+
+def current_notebook_path(user_ns=None, environ=None):
+    """Path of the notebook this kernel is running, or None.
+
+    Two mechanisms, in order: ``JPY_SESSION_NAME`` (jupyter_server >= 2 exports the
+    notebook's path into the kernel's environment) and the ``__session__`` global that
+    ipykernel puts into the user namespace.  Relative paths are taken against the
+    kernel's working directory; only an existing ``.ipynb`` counts."""
+    environ = os.environ if environ is None else environ
+    cands = [environ.get("JPY_SESSION_NAME")]
+    if user_ns is None:
+        try:
+            import IPython
+
+            ip = IPython.get_ipython()
+            user_ns = getattr(ip, "user_ns", None) or {}
+        except Exception:  # noqa: BLE001 - no IPython
+            user_ns = {}
+    cands.append(user_ns.get("__session__"))
+    for c in cands:
+        if not c or not isinstance(c, str):
+            continue
+        path = c if os.path.isabs(c) else os.path.abspath(c)
+        if path.endswith(".ipynb") and os.path.isfile(path):
+            return path
+    return None
 
 
 def _called_from_notebook():

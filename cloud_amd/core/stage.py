@@ -14,6 +14,17 @@ generated a Dockerfile and built/pushed an image.  On an MI355X node the
 
 Requirements are installed best-effort with ``pip install --user`` only when
 ``CLOUD_AMD_PIP_INSTALL=1`` (GPU boxes have no package index).
+
+Staging is part of ``run()`` -> first-step latency, so it stays cheap:
+
+* the entry directory is *hard-linked* file by file into ``app/`` (a copy only across
+  filesystems, or with ``CLOUD_AMD_STAGE_COPY=1``).  A hard link shares the bytes: an
+  in-place edit of a source file while its job runs is visible to that job (editors that
+  save by rename are not), which ``CLOUD_AMD_STAGE_COPY=1`` avoids;
+* build trees and results that no rank reads are skipped (``build/``, ``profiles/``,
+  ``gpurun_out/``, ``jobs/``, ``*.o``, VCS and cache directories);
+* the framework stamp reads package metadata and never imports torch (a cold
+  ``import torch`` costs ~2 s in the launching process, which never needs it).
 """
 from __future__ import annotations
 
@@ -26,7 +37,8 @@ import time
 
 from ..version import ARCH, __version__
 
-IGNORE = shutil.ignore_patterns("__pycache__", "*.pyc", ".git", "jobs", ".ipynb_checkpoints", "gpurun_out")
+IGNORE = shutil.ignore_patterns("__pycache__", "*.pyc", ".git", "jobs", ".ipynb_checkpoints", "gpurun_out",
+                                "build", "profiles", "*.o", ".pytest_cache", ".hypothesis")
 
 
 def _ignore(root):
@@ -58,15 +70,37 @@ def file_path_map(entry_point, preprocessed_entry_point, requirements_txt=None, 
 
 
 def _framework_stamp():
+    """cloud_amd / torch / HIP / arch versions from package metadata and torch's generated
+    ``version.py`` text -- without importing torch."""
     stamp = {"cloud_amd": __version__, "arch": ARCH, "python": sys.version.split()[0]}
     try:
-        import torch
+        import importlib.metadata as md
 
-        stamp["torch"] = torch.__version__
-        stamp["hip"] = getattr(torch.version, "hip", None)
+        stamp["torch"] = md.version("torch")
+    except Exception:  # pragma: no cover - torch not installed
+        return stamp
+    try:
+        import importlib.util
+        import re
+
+        spec = importlib.util.find_spec("torch")  # locates the package, does not import it
+        if spec is not None and spec.submodule_search_locations:
+            vfile = os.path.join(list(spec.submodule_search_locations)[0], "version.py")
+            with open(vfile) as f:
+                m = re.search(r"^hip\s*(?::\s*[^=]+)?=\s*['\"]([^'\"]+)['\"]", f.read(), re.M)
+            stamp["hip"] = m.group(1) if m else None
     except Exception:  # pragma: no cover
         pass
     return stamp
+
+
+def _link_or_copy(src, dst):
+    """Hard link (cheap, same filesystem); fall back to a copy."""
+    try:
+        os.link(src, dst)
+    except OSError:
+        shutil.copy2(src, dst)
+    return dst
 
 
 def stage_job(job_id, entry_point, preprocessed_entry_point, requirements_txt=None, entry_point_args=None,
@@ -82,10 +116,16 @@ def stage_job(job_id, entry_point, preprocessed_entry_point, requirements_txt=No
         if os.path.isdir(src):
             if os.path.abspath(src).startswith(os.path.abspath(job_dir)):
                 raise ValueError("entry-point directory is inside the job directory")
-            shutil.copytree(src, dst, ignore=_ignore(root), dirs_exist_ok=True, symlinks=False)
+            copy = shutil.copy2 if os.environ.get("CLOUD_AMD_STAGE_COPY") == "1" else _link_or_copy
+            shutil.copytree(src, dst, ignore=_ignore(root), dirs_exist_ok=True, symlinks=False,
+                            copy_function=copy)
         else:
             os.makedirs(os.path.dirname(dst), exist_ok=True)
-            shutil.copy2(src, dst)
+            if os.path.exists(dst):
+                if os.path.samefile(src, dst):  # already linked in with the entry directory
+                    continue
+                os.remove(dst)
+            _link_or_copy(src, dst)
     if preprocessed_entry_point is not None:
         target = os.path.join(app, os.path.basename(preprocessed_entry_point))
     else:

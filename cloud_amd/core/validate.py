@@ -82,10 +82,17 @@ def cluster_gpu_count(chief_config, worker_config, worker_count):
     return n
 
 
+def cpu_rehearsal():
+    """``CLOUD_AMD_DEVICE=cpu`` exported by the caller: a GPU-shaped job (same machine
+    configs, same strategy auto-selection) whose ranks train on the CPU over gloo -- the
+    multi-rank launch path rehearsed on a host without GPUs."""
+    return os.environ.get("CLOUD_AMD_DEVICE") == "cpu"
+
+
 def validate_node_capacity(chief_config, worker_config, worker_count, available=None):
     """All ranks of a single-node job must map onto distinct local GPUs."""
     need = cluster_gpu_count(chief_config, worker_config, worker_count)
-    if need == 0:
+    if need == 0 or cpu_rehearsal():
         return
     have = topology.visible_gpu_count() if available is None else available
     if need > have:

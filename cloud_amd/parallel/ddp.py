@@ -23,6 +23,13 @@ RCCL communicator (:mod:`cloud_amd.parallel.comm`, ``CLOUD_AMD_COMM=rccl``) whos
 collectives run on a dedicated high-priority stream joined once before the
 optimizer step.
 
+Timing (bench JSON ``comm`` / monitoring): every transport records, per bucket, when
+its collective started (gradients ready and the comm path free) and when it completed --
+GPU events on the comm stream for RCCL (torch.distributed or the native communicator),
+host clocks from the work's completion future for gloo / CPU.  ``allreduce_ms`` is the
+time the (serial) comm path was busy, ``exposed_comm_ms`` the time from the end of
+backward to the last bucket joined; both are finite on every transport.
+
 Bucket size: xGMI on MI355X is 7 point-to-point links per GPU; a ring
 all-reduce moves 2(N-1)/N of the bucket per link, so ~25-64 MB buckets keep
 RCCL's multi-channel rings busy while leaving enough buckets (>= 4-8 for
@@ -66,8 +73,29 @@ def _busy_ms(evs):
     return total
 
 
+def _busy_host_ms(spans):
+    """Host-clock version of :func:`_busy_ms` over (start_s, end_s) pairs."""
+    total, prev_end = 0.0, None
+    for start, end in spans:
+        begin = start if prev_end is None else max(start, prev_end)
+        total += max(end - begin, 0.0)
+        prev_end = end if prev_end is None else max(prev_end, end)
+    return total * 1e3
+
+
+class _TorchTransport:
+    """``torch.distributed`` all-reduce (RCCL on GPU, gloo on CPU); a fake with the same
+    ``all_reduce(tensor) -> work`` contract can be injected (tests)."""
+
+    def __init__(self, pg):
+        self.pg = pg
+
+    def all_reduce(self, t):
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+
+
 class Bucket:
-    __slots__ = ("arena", "lo", "hi", "slots", "pending", "work", "launched", "index", "wire", "ev")
+    __slots__ = ("arena", "lo", "hi", "slots", "pending", "work", "launched", "index", "wire", "ev", "span")
 
     def __init__(self, arena, lo, hi, slots, index):
         self.arena, self.lo, self.hi, self.slots, self.index = arena, lo, hi, slots, index
@@ -75,7 +103,8 @@ class Bucket:
         self.work = None
         self.launched = False
         self.wire = None   # reduce-dtype copy on the wire (fp32 reduction of bf16 grads)
-        self.ev = None     # (start, end) timing events of this step's collective
+        self.ev = None     # (start, end) timing events of this step's collective (GPU)
+        self.span = None   # [start_s, end_s] host clock of this step's collective (gloo / CPU)
 
     @property
     def tensor(self):
@@ -83,10 +112,13 @@ class Bucket:
 
 
 class GradAllReducer:
-    def __init__(self, arenas, process_group=None, bucket_mb=None, overlap=True, reduce_dtype=None):
+    def __init__(self, arenas, process_group=None, bucket_mb=None, overlap=True, reduce_dtype=None,
+                 transport=None, world=None):
         self.arenas = arenas
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        if world is None:
+            world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.world = world
         mb = float(bucket_mb if bucket_mb is not None else os.environ.get("CLOUD_AMD_BUCKET_MB", 16))
         self.bucket_mb = mb
         self.bucket_bytes = int(mb * (1 << 20))
@@ -110,12 +142,26 @@ class GradAllReducer:
         self._steps = 0
         self.comm = None
         self._side = None
+        self._comm_stream = None
         on_gpu = bool(self.arenas) and self.arenas[0].grad.is_cuda
-        if self.world > 1 and on_gpu and _comm.backend() != "rccl" and _DDP_ORDER != "backend":
+        self.transport = transport
+        injected = transport is not None
+        if transport is None and self.world > 1:
+            self.transport = _TorchTransport(process_group)
+        # GPU-event timing needs a collective that the comm stream can wait on without
+        # blocking the host: RCCL.  gloo (CPU tensors, or the shared-GPU rehearsal) is timed
+        # on the host clock from each work's completion future.
+        backend = dist.get_backend(process_group) if (dist.is_initialized() and not injected) else "fake"
+        self._device_timed = on_gpu and backend == "nccl"
+        if (self.world > 1 and on_gpu and not injected and _comm.backend() != "rccl"
+                and _DDP_ORDER != "backend"):
             self._side = torch.cuda.Stream(self.arenas[0].grad.device, priority=-1)
-        if self.world > 1 and _comm.backend() == "rccl" and self.arenas and self.arenas[0].grad.is_cuda:
+        if (self.world > 1 and not injected and _comm.backend() == "rccl" and self.arenas
+                and self.arenas[0].grad.is_cuda):
             self.comm = _comm.RcclComm()  # native communicator: side stream + events
             self.comm.start_watchdog()
+            self._comm_stream = torch.cuda.ExternalStream(self.comm.c.stream, device=self.arenas[0].grad.device)
+            self._device_timed = True
         self.buckets = []
         self._param_bucket = {}
         self._next = 0
@@ -185,7 +231,22 @@ class GradAllReducer:
     def _launch(self, b):
         trace.mark("bucket%d" % b.index)
         if self.comm is not None:
-            self.comm.all_reduce(b.tensor)
+            # native communicator: the copy to the wire dtype, the collective and the copy
+            # back all run on the communicator's stream, after the gradients' producers
+            dev = b.tensor.device
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(dev))
+            self._comm_stream.wait_event(ready)
+            with torch.cuda.stream(self._comm_stream):
+                if self.timing:
+                    b.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    b.ev[0].record(self._comm_stream)
+                wire = self._wire(b)
+                self.comm.all_reduce(wire)
+                if b.wire is not None:
+                    b.tensor.copy_(b.wire)
+                if self.timing:
+                    b.ev[1].record(self._comm_stream)
         elif self._side is not None:
             # Explicit ordering: the collective is issued from a dedicated comm stream that
             # first waits on an event recorded on the compute stream (where the kernels that
@@ -198,13 +259,38 @@ class GradAllReducer:
             ev.record(torch.cuda.current_stream(b.tensor.device))
             self._side.wait_event(ev)
             with torch.cuda.stream(self._side):
-                if self.timing:  # start: the comm stream has caught up with this bucket's gradients
+                if self.timing and self._device_timed:
+                    # start: the comm stream has caught up with this bucket's gradients
                     b.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                     b.ev[0].record(self._side)
-                b.work = dist.all_reduce(self._wire(b), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                b.work = self.transport.all_reduce(self._wire(b))
+                if self._device_timed:
+                    # RCCL: the side stream waits for the collective's stream (no host block),
+                    # so the end event marks its completion and the copy back follows it
+                    b.work.wait()
+                    b.work = None
+                    if b.wire is not None:
+                        b.tensor.copy_(b.wire)
+                    if b.ev is not None:
+                        b.ev[1].record(self._side)
+                elif self.timing:
+                    self._host_span(b)
         else:
-            b.work = dist.all_reduce(self._wire(b), op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            b.work = self.transport.all_reduce(self._wire(b))
+            if self.timing:
+                self._host_span(b)
         b.launched = True
+
+    def _host_span(self, b):
+        """Host-clock span of a gloo / fake collective: launch -> completion future."""
+        b.span = [time.perf_counter(), None]
+        fut = b.work.get_future() if hasattr(b.work, "get_future") else None
+        if fut is not None:
+            def done(_f, span=b.span):
+                span[1] = time.perf_counter()
+                return None
+
+            fut.then(done)
 
     def _launch_ready(self):
         while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
@@ -215,9 +301,9 @@ class GradAllReducer:
         """Launch remaining buckets in order and join them onto the compute stream."""
         if self.world <= 1:
             return
-        on_gpu = self._side is not None or self.comm is not None
+        dev_timed = self.timing and self._device_timed
         if self.timing:  # backward done (compute stream) -> comm joined = exposed communication
-            if on_gpu:
+            if dev_timed:
                 t_bwd = torch.cuda.Event(enable_timing=True)
                 t_bwd.record(torch.cuda.current_stream(self.arenas[0].grad.device))
             else:
@@ -226,37 +312,43 @@ class GradAllReducer:
             self._launch(self.buckets[self._next])
             self._next += 1
         if self.comm is not None:
-            self.comm.join()
-        if self._side is not None:
+            self.comm.join()  # compute stream waits for the comm stream (collectives + copies)
+        elif self._side is not None:
             with torch.cuda.stream(self._side):
                 for b in self.buckets:
-                    if b.work is not None:
-                        b.work.wait()  # the comm stream waits for the collective (RCCL runs it elsewhere)
-                    if b.ev is not None:  # end: the collective has completed
-                        b.ev[1].record(self._side)
-                    if b.wire is not None:
-                        b.tensor.copy_(b.wire)
+                    if b.work is not None:  # gloo on device tensors: a host-side wait
+                        b.work.wait()
+                        self._close_span(b)
+                        if b.wire is not None:
+                            b.tensor.copy_(b.wire)
             torch.cuda.current_stream(self._side.device).wait_stream(self._side)
         else:
             for b in self.buckets:
                 if b.work is not None:
                     b.work.wait()
+                    self._close_span(b)
                 if b.wire is not None:
                     b.tensor.copy_(b.wire)
         if self.timing:
-            if on_gpu:
+            if dev_timed:
                 t_join = torch.cuda.Event(enable_timing=True)
                 t_join.record(torch.cuda.current_stream(self.arenas[0].grad.device))
                 self._timing_log.append((t_bwd, t_join, [b.ev for b in self.buckets if b.ev is not None]))
             else:
-                dt = (time.perf_counter() - t_bwd) * 1e3
-                self._timing_log.append((dt, dt, []))
+                t_join = time.perf_counter()
+                spans = [tuple(b.span) for b in self.buckets if b.span is not None]
+                self._timing_log.append(((t_join - t_bwd) * 1e3, _busy_host_ms(spans), None))
             if self._mon is not None:
                 self._drain_to_monitoring()
         self.reset()
         self._steps += 1
         if self.check_every and self._steps % self.check_every == 0:
             self.check_consistency()
+
+    @staticmethod
+    def _close_span(b):
+        if b.span is not None and b.span[1] is None:  # no completion callback ran (fake work)
+            b.span[1] = time.perf_counter()
 
     def no_sync(self):
         """Gradient accumulation: backward passes inside this context only accumulate into
@@ -303,6 +395,7 @@ class GradAllReducer:
             b.launched = False
             b.wire = None
             b.ev = None
+            b.span = None
         self._next = 0
 
     def _drain_to_monitoring(self):
@@ -310,7 +403,7 @@ class GradAllReducer:
         keep = []
         for entry in self._timing_log:
             t_bwd, t_join, evs = entry
-            if isinstance(t_bwd, float):
+            if evs is None:  # host-timed: (exposed_ms, allreduce_ms, None)
                 self._mon.observe(self._mon.ALLREDUCE, t_join)
                 self._mon.observe(self._mon.EXPOSED_COMM, t_bwd)
                 continue
@@ -318,8 +411,7 @@ class GradAllReducer:
                 keep.append(entry)
                 continue
             self._mon.observe(self._mon.EXPOSED_COMM, t_bwd.elapsed_time(t_join))
-            if evs:
-                self._mon.observe(self._mon.ALLREDUCE, _busy_ms(evs))
+            self._mon.observe(self._mon.ALLREDUCE, _busy_ms(evs) if evs else 0.0)
         self._timing_log = keep[-64:]
 
     def timing_start(self):
@@ -328,22 +420,26 @@ class GradAllReducer:
         self._timing_log = []
 
     def timing_summary(self):
-        """Mean per-step ``allreduce_ms`` (sum of bucket collective times on the comm
-        stream) and ``exposed_comm_ms`` (end of backward on the compute stream -> all
-        buckets joined).  Call after a device synchronize."""
+        """Mean per-step ``allreduce_ms`` (time the serial comm path was busy with this
+        step's collectives) and ``exposed_comm_ms`` (end of backward on the compute stream
+        -> all buckets joined).  Call after a device synchronize.  Always finite."""
         self.timing = self._mon is not None
         if self.world <= 1 or not self._timing_log:
-            return {"allreduce_ms": 0.0, "exposed_comm_ms": 0.0, "steps": len(self._timing_log)}
+            return {"allreduce_ms": 0.0, "exposed_comm_ms": 0.0, "steps": len(self._timing_log),
+                    "timing": "none"}
         ar, ex = [], []
+        host = False
         for t_bwd, t_join, evs in self._timing_log:
-            if isinstance(t_bwd, float):
+            if evs is None:
+                host = True
                 ex.append(t_bwd)
                 ar.append(t_join)
                 continue
             ex.append(t_bwd.elapsed_time(t_join))
-            ar.append(_busy_ms(evs) if evs else float("nan"))
+            ar.append(_busy_ms(evs) if evs else 0.0)
         n = len(ex)
-        return {"allreduce_ms": round(sum(ar) / n, 3), "exposed_comm_ms": round(sum(ex) / n, 3), "steps": n}
+        return {"allreduce_ms": round(sum(ar) / n, 3), "exposed_comm_ms": round(sum(ex) / n, 3), "steps": n,
+                "timing": "host_clock" if host else "device_events"}
 
     def describe(self):
         """Bucket layout for reports: count, target size, wire dtype, transport."""

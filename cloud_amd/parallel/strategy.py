@@ -119,6 +119,18 @@ class Strategy:
         if dist.is_initialized():
             dist.barrier()
 
+    # -- the data-parallel engine ----------------------------------------------
+    def gradient_reducer(self, arenas, **kwargs):
+        """The strategy's gradient all-reduce engine over the optimizer's flat arenas
+        (:class:`cloud_amd.parallel.ddp.GradAllReducer`: buckets overlapped with backward
+        on a side stream).  With one replica it is a no-op, so training code is the same
+        under every strategy."""
+        from .ddp import GradAllReducer
+
+        if self.num_replicas_in_sync <= 1:
+            kwargs["world"] = 1
+        return GradAllReducer(arenas, **kwargs)
+
     # -- data -----------------------------------------------------------------
     def experimental_distribute_dataset(self, dataset):
         """Shard a dataset across replicas (C4): rank-strided, no communication."""
@@ -154,6 +166,8 @@ def _parse_device(device):
         return None
     if isinstance(device, torch.device):
         return device
+    if os.environ.get("CLOUD_AMD_DEVICE") == "cpu":  # CPU rehearsal of a GPU-shaped job
+        return torch.device("cpu")
     d = str(device).lower().strip("/")
     if d.startswith("device:"):
         d = d[len("device:"):]
@@ -193,8 +207,9 @@ class MirroredStrategy(Strategy):
     def __init__(self, devices=None, cross_device_ops=None):
         forced = os.environ.get("CLOUD_AMD_DEVICE")
         use_gpu = torch.cuda.is_available() and forced != "cpu"
-        dev = torch.device("cuda", dist_env.local_rank()) if use_gpu else torch.device("cpu")
-        _, _, dev = dist_env.init_distributed(device=dev)
+        # GPU: init_distributed picks cuda:LOCAL_RANK (cuda:0 for every rank of the
+        # CLOUD_AMD_SHARED_GPU rehearsal on a one-GPU box)
+        _, _, dev = dist_env.init_distributed(device=None if use_gpu else torch.device("cpu"))
         super().__init__(dev)
         self.cross_device_ops = cross_device_ops
 
@@ -274,7 +289,12 @@ def has_strategy():
 
 
 def _default_strategy():
-    if dist_env.world_size() > 1:
+    """No strategy installed (a rank started by torchrun, or a plain script): Mirrored
+    when every rank is on this node, MultiWorkerMirrored across nodes, else OneDevice."""
+    w = dist_env.world_size()
+    if w > 1:
+        if dist_env.env_int("LOCAL_WORLD_SIZE", w) == w:
+            return MirroredStrategy()
         return MultiWorkerMirroredStrategy()
     forced = os.environ.get("CLOUD_AMD_DEVICE")
     return OneDeviceStrategy(forced if forced else None)

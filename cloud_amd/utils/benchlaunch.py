@@ -29,29 +29,38 @@ def strip_flag(argv, flag):
 
 def launch_via_run(script, gpus, device="auto", argv=None, tag="bench"):
     """Stage ``script`` (its directory is the app) and run it on ``gpus`` ranks via
-    ``cloud_amd.run()``; stream rank 0's log; exit with the job's code."""
+    ``cloud_amd.run(distribution_strategy="auto")`` -- the generated wrapper installs
+    MirroredStrategy (N > 1) or OneDeviceStrategy (N = 1) exactly as the reference's
+    auto path does (``TFC/core/preprocess.py:137-146``) and the bench takes its DP engine
+    from that strategy.  Streams every rank's log; with several ranks the streamed lines
+    carry ``[chief-0]``-style prefixes, so rank 0's JSON result line is printed once more
+    verbatim at the end.  Exits with the job's code."""
     import cloud_amd as tfc
     from cloud_amd.core.machine_config import AcceleratorType, MachineConfig
 
     argv = strip_flag(sys.argv[1:] if argv is None else argv, "--via-run")
     if device == "cpu":
-        cpu = tfc.COMMON_MACHINE_CONFIGS["CPU"]
-        chief, workers, wcfg = cpu, gpus - 1, cpu  # one process per CPU "machine", gloo
-    else:
-        chief = tfc.COMMON_MACHINE_CONFIGS.get("MI355X_%dX" % gpus) or MachineConfig(
-            cpu_cores=16 * gpus, memory=256 * gpus, accelerator_type=AcceleratorType.AMD_INSTINCT_MI355X,
-            accelerator_count=gpus)
-        workers, wcfg = 0, "auto"
+        # the same GPU-shaped job (MI355X_<N>X chief: MirroredStrategy at N > 1), its ranks
+        # on CPU over gloo (validate.cpu_rehearsal)
+        os.environ["CLOUD_AMD_DEVICE"] = "cpu"
+    chief = tfc.COMMON_MACHINE_CONFIGS.get("MI355X_%dX" % gpus) or MachineConfig(
+        cpu_cores=16 * gpus, memory=256 * gpus, accelerator_type=AcceleratorType.AMD_INSTINCT_MI355X,
+        accelerator_count=gpus)
+    workers, wcfg = 0, "auto"
     script = os.path.abspath(script)
     os.chdir(os.path.dirname(script))
     try:
-        job = tfc.run(entry_point=os.path.basename(script), distribution_strategy=None, chief_config=chief,
+        job = tfc.run(entry_point=os.path.basename(script), distribution_strategy="auto", chief_config=chief,
                       worker_config=wcfg, worker_count=workers, entry_point_args=argv, stream_logs=True,
                       exit=False, wait=True)
     except ValueError as e:
         print("[%s] cannot launch %d rank(s) through cloud_amd.run(): %s" % (tag, gpus, e), file=sys.stderr)
         sys.exit(2)
     rc = job.returncode or 0
+    if len(job.ranks) > 1:
+        result = [ln for ln in job.log_tail(0, 200) if ln.startswith('{"metric"')]
+        if result:
+            print(result[-1], flush=True)
     if rc:
         print("[%s] job %s failed (exit codes %s); logs: %s" % (
             tag, job.job_id, job.meta.get("exit_codes"), os.path.join(job.job_dir, "logs")), file=sys.stderr)

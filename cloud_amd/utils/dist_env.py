@@ -100,3 +100,41 @@ def all_reduce_max(x: float, device) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def all_gather_floats(x: float, device) -> list:
+    """Every rank's value of ``x`` (rank order); ``[x]`` without a process group."""
+    if not dist.is_initialized():
+        return [x]
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(o.item()) for o in out]
+
+
+def allreduce_busbw(device, nbytes=64 << 20, iters=5, dtype=torch.float32):
+    """One-shot all-reduce bus bandwidth in GB/s over the default group (nccl-tests
+    convention: busbw = bytes * 2(n-1)/n / time; the slowest rank's time).  On an 8-GPU
+    MI355X node this shows whether RCCL spreads a collective over the 7 xGMI links of a
+    GPU (~150 GB/s per link) or rides one ring.  None without a multi-rank group."""
+    if not dist.is_initialized() or dist.get_world_size() < 2:
+        return None
+    import time
+
+    n = dist.get_world_size()
+    t = torch.ones(max(nbytes // torch.tensor([], dtype=dtype).element_size(), 1), dtype=dtype, device=device)
+
+    def sync():
+        if t.is_cuda:
+            torch.cuda.synchronize(t.device)
+
+    dist.all_reduce(t)  # warm the communicator / channels
+    sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(t)
+    sync()
+    dt = all_reduce_max((time.perf_counter() - t0) / iters, device)
+    size = t.numel() * t.element_size()
+    return round(size * 2.0 * (n - 1) / n / dt / 1e9, 2)

@@ -1,0 +1,226 @@
+// Standalone GEMM core benchmark + numerics check (no Python, no torch): the fast
+// edit -> measure loop for the MFMA cores in csrc/include.  Every variant is timed in the
+// same process on the same random operands (uniform [-1, 1), cdna_hip_programming.md
+// §5.4 rules 24/25) and checked against an fp32 reference GEMM computed on the GPU.
+//
+//   build:  python scripts/build_gemm_bench.py        (-> bin/gemm_bench)
+//   run:    bin/gemm_bench [iters] M,N,K,layout ...   layout 0 = NT (fwd), 1 = NN (dgrad), 2 = TN (wgrad)
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "ca_gemm256.h"
+
+using namespace ca;
+
+#define CHECK(x)                                                                       \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      exit(1);                                                                         \
+    }                                                                                  \
+  } while (0)
+
+__global__ void init_uniform(bf16_t* p, long n, uint32_t seed) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (long)gridDim.x * blockDim.x) {
+    uint32_t x = (uint32_t)i * 2654435761u ^ seed;
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    const float u = (float)(x >> 8) * (1.0f / 16777216.0f) * 2.f - 1.f;
+    p[i] = f2bf(u);
+  }
+}
+
+// reference: C[m][n] = sum_k A(m,k) B(k,n) in fp32, rows m = r * row_step only
+__global__ void ref_gemm(const bf16_t* A, long lda, const bf16_t* B, long ldb, int layout, float* C, int M, int N, int K,
+                         int row_step, int rows) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int r = blockIdx.y;
+  if (n >= N || r >= rows) return;
+  const int m = r * row_step;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float a = layout == 2 ? bf2f(A[(long)k * lda + m]) : bf2f(A[(long)m * lda + k]);
+    const float b = layout == 0 ? bf2f(B[(long)n * ldb + k]) : bf2f(B[(long)k * ldb + n]);
+    s += a * b;
+  }
+  C[(long)r * N + n] = s;
+}
+
+template <template <int, int, int> class GA, template <int, int, int> class GB>
+__global__ void __launch_bounds__(512) k256(CoreParams P) {
+  mfma_gemm_256<GA, GB, EPI_BF16>(P);
+}
+
+template <template <int, int, int> class GA, template <int, int, int> class GB>
+__global__ void __launch_bounds__(512) k256s(CoreParams P) {
+  mfma_gemm_256<GA, GB, EPI_BF16, true>(P);
+}
+
+template <template <int, int, int> class GA, template <int, int, int> class GB>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k128(CoreParams P) {
+  mfma_gemm_glds<128, 128, 2, 2, GA, GB, EPI_BF16>(P);
+}
+
+template <template <int, int, int> class GA, template <int, int, int> class GB>
+__global__ void __launch_bounds__(512) kpp(CoreParams P) {
+  mfma_gemm_pp256<GA, GB, EPI_BF16>(P);
+}
+
+struct Variant {
+  const char* name;
+  int bm, bn;
+  void (*launch)(const CoreParams&, int layout, dim3 grid, hipStream_t);
+};
+
+static void launch256(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) k256<GDenseKC, GDenseKC><<<g, 512, 0, s>>>(p);
+  else if (layout == 1) k256<GDenseKC, GDenseNC><<<g, 512, 0, s>>>(p);
+  else k256<GDenseNC, GDenseNC><<<g, 512, 0, s>>>(p);
+}
+static void launch256s(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) k256s<GDenseKC, GDenseKC><<<g, 512, 0, s>>>(p);
+  else if (layout == 1) k256s<GDenseKC, GDenseNC><<<g, 512, 0, s>>>(p);
+  else k256s<GDenseNC, GDenseNC><<<g, 512, 0, s>>>(p);
+}
+
+// per-segment cycle medians of the stamped K tile (k256s): segments R(q) / M(q) per wave
+// group, each as work cycles (start -> arrival at the closing barrier) + barrier wait
+static void stamp_report(const CoreParams& p0, int layout, dim3 g, hipStream_t s) {
+  CoreParams p = p0;
+  const long n = (long)g.x * 8 * 17;
+  CHECK(hipMalloc(&p.stamps, n * 8));
+  CHECK(hipMemsetAsync(p.stamps, 0, n * 8, s));
+  for (int w = 0; w < 3; ++w) launch256s(p, layout, g, s);
+  CHECK(hipStreamSynchronize(s));
+  std::vector<unsigned long long> h(n);
+  CHECK(hipMemcpy(h.data(), p.stamps, n * 8, hipMemcpyDeviceToHost));
+  CHECK(hipFree(p.stamps));
+  for (int grp = 0; grp < 2; ++grp) {
+    printf("{\"stamps_group\": %d, \"segments\": [", grp);
+    for (int seg = 0; seg < 8; ++seg) {
+      std::vector<long> work, wait;
+      for (unsigned b = 0; b < g.x; ++b)
+        for (int w = grp * 4; w < grp * 4 + 4; ++w) {
+          const unsigned long long* st = h.data() + ((long)b * 8 + w) * 17;
+          work.push_back((long)(st[2 * seg + 1] - st[2 * seg]));
+          wait.push_back((long)(st[2 * seg + 2] - st[2 * seg + 1]));
+        }
+      std::sort(work.begin(), work.end());
+      std::sort(wait.begin(), wait.end());
+      printf("%s{\"%s%d\": [%ld, %ld]}", seg ? ", " : "", (seg & 1) ? "M" : "R", seg / 2, work[work.size() / 2],
+             wait[wait.size() / 2]);
+    }
+    printf("]}\n");
+  }
+}
+
+static void launch128(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) k128<GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
+  else if (layout == 1) k128<GDenseKC, GDenseNC><<<g, 256, 0, s>>>(p);
+  else k128<GDenseNC, GDenseNC><<<g, 256, 0, s>>>(p);
+}
+static void launchpp(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) kpp<GDenseKC, GDenseKC><<<g, 512, 0, s>>>(p);
+  else if (layout == 1) kpp<GDenseKC, GDenseNC><<<g, 512, 0, s>>>(p);
+  else kpp<GDenseNC, GDenseNC><<<g, 512, 0, s>>>(p);
+}
+
+int main(int argc, char** argv) {
+  int iters = 20;
+  int a0 = 1;
+  if (argc > 1 && !strchr(argv[1], ',')) {
+    iters = atoi(argv[1]);
+    a0 = 2;
+  }
+  std::vector<int> shapes;
+  for (int a = a0; a < argc; ++a) {
+    int M, N, K, L;
+    if (sscanf(argv[a], "%d,%d,%d,%d", &M, &N, &K, &L) == 4) shapes.insert(shapes.end(), {M, N, K, L});
+  }
+  if (shapes.empty()) shapes = {4096, 4096, 4096, 0};
+  const char* only = getenv("GB_VARIANTS");  // e.g. "v3,glds"
+  Variant vars[] = {{"v3_256", 256, 256, launch256}, {"glds128", 128, 128, launch128}, {"pp256", 256, 256, launchpp}};
+  hipStream_t s;
+  CHECK(hipStreamCreate(&s));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  for (size_t si = 0; si < shapes.size(); si += 4) {
+    const int M = shapes[si], N = shapes[si + 1], K = shapes[si + 2], L = shapes[si + 3];
+    bf16_t *A, *B, *C;
+    const long na = (long)M * K, nb = (long)N * K, nc = (long)M * N;
+    CHECK(hipMalloc(&A, na * 2));
+    CHECK(hipMalloc(&B, nb * 2));
+    CHECK(hipMalloc(&C, nc * 2));
+    init_uniform<<<2048, 256, 0, s>>>(A, na, 0x1234u);
+    init_uniform<<<2048, 256, 0, s>>>(B, nb, 0x9876u);
+    const long lda = L == 2 ? M : K;  // TN: A stored [K][M]
+    const long ldb = L == 0 ? K : N;  // NT: B [N][K]; NN/TN: B [K][N]
+    const int row_step = M > 512 ? M / 509 : 1;
+    const int rows = (M + row_step - 1) / row_step;
+    float* R;
+    CHECK(hipMalloc(&R, (long)rows * N * 4));
+    ref_gemm<<<dim3((N + 255) / 256, rows), 256, 0, s>>>(A, lda, B, ldb, L, R, M, N, K, row_step, rows);
+    std::vector<float> ref((long)rows * N);
+    CHECK(hipMemcpyAsync(ref.data(), R, ref.size() * 4, hipMemcpyDeviceToHost, s));
+    CHECK(hipStreamSynchronize(s));
+    for (const Variant& v : vars) {
+      if (only && !strstr(only, v.name)) continue;
+      CoreParams p{};
+      p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.C = C; p.ldc = N;
+      p.M = M; p.N = N; p.K = K; p.k_per_split = K; p.split_xcd = 1;
+      const int tiles = ((M + v.bm - 1) / v.bm) * ((N + v.bn - 1) / v.bn);
+      const dim3 g(tiles, 1, 1);
+      CHECK(hipMemsetAsync(C, 0xff, nc * 2, s));
+      v.launch(p, L, g, s);
+      CHECK(hipGetLastError());
+      CHECK(hipStreamSynchronize(s));
+      std::vector<bf16_t> out((long)rows * N);
+      for (int r = 0; r < rows; ++r)
+        CHECK(hipMemcpy(out.data() + (long)r * N, C + (long)r * row_step * N, (long)N * 2, hipMemcpyDeviceToHost));
+      double num = 0, den = 0, maxe = 0;
+      long bad = 0;
+      for (long i = 0; i < (long)rows * N; ++i) {
+        uint32_t ob = ((uint32_t)out[i]) << 16;
+        float of;
+        memcpy(&of, &ob, 4);
+        const double o = of, r = ref[i];
+        const double d = o - r;
+        num += d * d;
+        den += r * r;
+        const double e = fabs(d) / (1.0 + fabs(r));
+        if (!(e <= 0.05)) ++bad;
+        if (e > maxe || e != e) maxe = e;
+      }
+      for (int w = 0; w < 3; ++w) v.launch(p, L, g, s);
+      CHECK(hipEventRecord(e0, s));
+      for (int it = 0; it < iters; ++it) v.launch(p, L, g, s);
+      CHECK(hipEventRecord(e1, s));
+      CHECK(hipEventSynchronize(e1));
+      float ms = 0;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= iters;
+      printf("{\"variant\": \"%s\", \"M\": %d, \"N\": %d, \"K\": %d, \"layout\": %d, \"us\": %.1f, \"TF\": %.1f, "
+             "\"rel_l2\": %.3e, \"max_err\": %.3e, \"bad\": %ld}\n",
+             v.name, M, N, K, L, ms * 1e3, 2.0 * M * N * K / ms / 1e9, sqrt(num / (den + 1e-30)), maxe, bad);
+      fflush(stdout);
+      if (getenv("GB_STAMP") && v.launch == launch256) stamp_report(p, L, g, s);
+    }
+    CHECK(hipFree(A));
+    CHECK(hipFree(B));
+    CHECK(hipFree(C));
+    CHECK(hipFree(R));
+  }
+  return 0;
+}

@@ -210,3 +210,130 @@ def test_launcher_never_touches_hip_and_sets_rccl_env(tmp_path, monkeypatch):
     meta = json.load(open(job_dir / "job.json"))
     assert meta["node"]["source"] == "kfd" and meta["node"]["gpus"] == 2
     assert meta["comm_env"]["NCCL_MIN_NCHANNELS"] == "1"
+
+
+# ---- launcher fidelity -------------------------------------------
+
+def test_stream_logs_all_ranks_prefixed_and_failure_tail(tmp_path, monkeypatch, capsys):
+    """stream_logs=True tails EVERY rank (reference deploy.py:187-211 streams the job), each
+    line tagged with its role; a failing rank 1 is named with the tail of its log."""
+    app = _stage_script(tmp_path)
+    monkeypatch.chdir(app)
+    monkeypatch.setenv("CLOUD_AMD_NUM_GPUS", "0")
+    monkeypatch.setenv("FAIL_RANK", "1")
+    job = run_mod.run(entry_point="train.py", chief_config=CPU, worker_config=CPU, worker_count=2,
+                      jobs_dir=str(tmp_path / "jobs"), exit=False, wait=True, stream_logs=True)
+    assert job.wait(120) == 3
+    cap = capsys.readouterr()
+    out_lines = cap.out.splitlines()
+    for tag in ("[chief-0] RESULT ", "[worker-0] RESULT ", "[worker-1] RESULT "):
+        assert any(ln.startswith(tag) for ln in out_lines), cap.out
+    assert job.meta["failed_rank"] == 1
+    assert "rank 1 (worker-0) exited with code 3" in cap.err
+    tail_lines = [ln for ln in cap.err.splitlines() if ln.startswith("    ")]
+    assert any("RESULT" in ln for ln in tail_lines) and len(tail_lines) <= 50
+
+
+def test_stream_single_rank_unprefixed(tmp_path, monkeypatch, capsys):
+    app = _stage_script(tmp_path)
+    monkeypatch.chdir(app)
+    monkeypatch.setenv("CLOUD_AMD_NUM_GPUS", "0")
+    job = run_mod.run(entry_point="train.py", chief_config=CPU, jobs_dir=str(tmp_path / "jobs"), exit=False,
+                      wait=True, stream_logs=True)
+    assert job.wait(120) == 0
+    out = capsys.readouterr().out
+    assert any(ln.startswith("RESULT ") for ln in out.splitlines()), out
+
+
+def test_launcher_process_never_imports_torch(tmp_path):
+    """run() -> stage -> deploy in the launching process must not import torch (a cold
+    import costs ~2 s of run() -> first-step latency); the ranks import it themselves."""
+    import subprocess
+
+    app = _stage_script(tmp_path)
+    code = (
+        "import sys, os\n"
+        "import cloud_amd as tfc\n"
+        "job = tfc.run(entry_point='train.py', chief_config=tfc.COMMON_MACHINE_CONFIGS['CPU'],\n"
+        "              jobs_dir=%r, exit=False, wait=True)\n"
+        "assert job.returncode == 0, job.meta\n"
+        "print('TORCH_IMPORTED', 'torch' in sys.modules)\n" % str(tmp_path / "jobs"))
+    env = dict(os.environ, CLOUD_AMD_NUM_GPUS="0", PYTHONPATH=os.path.dirname(HERE))
+    for k in ("WORLD_SIZE", "RANK", "CLOUD_AMD_RUNNING_REMOTELY", "TF_KERAS_RUNNING_REMOTELY", "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", code], cwd=str(app), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "TORCH_IMPORTED False" in r.stdout, r.stdout
+
+
+def test_stage_hardlinks_and_skips_build_artifacts(tmp_path):
+    proj = tmp_path / "proj"
+    (proj / "build").mkdir(parents=True)
+    (proj / "profiles").mkdir()
+    (proj / "pkg").mkdir()
+    (proj / "train.py").write_text("print('hi')\n")
+    (proj / "pkg" / "mod.py").write_text("x = 1\n")
+    (proj / "pkg" / "obj.o").write_text("object")
+    (proj / "build" / "big.o").write_text("object")
+    (proj / "profiles" / "p.txt").write_text("x")
+    cwd = os.getcwd()
+    os.chdir(proj)
+    try:
+        job_dir, target = stage.stage_job("j1", "train.py", None, root=str(tmp_path / "jobs"))
+    finally:
+        os.chdir(cwd)
+    app = os.path.join(job_dir, "app")
+    assert os.path.isfile(os.path.join(app, "pkg", "mod.py"))
+    assert not os.path.exists(os.path.join(app, "build"))
+    assert not os.path.exists(os.path.join(app, "profiles"))
+    assert not os.path.exists(os.path.join(app, "pkg", "obj.o"))
+    # hard links: same inode as the source
+    assert os.stat(os.path.join(app, "pkg", "mod.py")).st_ino == os.stat(proj / "pkg" / "mod.py").st_ino
+    man = json.load(open(os.path.join(job_dir, "manifest.json")))
+    assert man["framework"]["torch"] and "hip" in man["framework"]
+
+
+def _write_nb(path):
+    nb = {"cells": [{"cell_type": "code", "source": ["import json\n", "print('NB_RAN', 6 * 7)\n"]},
+                    {"cell_type": "markdown", "source": ["text"]}],
+          "metadata": {}, "nbformat": 4, "nbformat_minor": 4}
+    path.write_text(json.dumps(nb))
+
+
+@pytest.mark.parametrize("mechanism", ["JPY_SESSION_NAME", "__session__"])
+def test_run_in_notebook_without_entry_point(tmp_path, monkeypatch, mechanism, capsys):
+    """run(entry_point=None) inside a notebook kernel locates the notebook file (reference
+    preprocess.py:166-167,196-212 fetched the live Colab notebook) and runs its cells."""
+    proj = tmp_path / "nbproj"
+    proj.mkdir()
+    nb = proj / "analysis.ipynb"
+    _write_nb(nb)
+    monkeypatch.chdir(proj)
+    monkeypatch.setenv("CLOUD_AMD_NUM_GPUS", "0")
+    monkeypatch.delenv("JPY_SESSION_NAME", raising=False)
+    monkeypatch.setattr(run_mod, "_called_from_notebook", lambda: True)
+    if mechanism == "JPY_SESSION_NAME":
+        monkeypatch.setenv("JPY_SESSION_NAME", str(nb))
+    else:
+        fake_ns = {"__session__": "analysis.ipynb"}
+
+        class _IP:
+            user_ns = fake_ns
+
+        import types
+
+        fake_ipython = types.SimpleNamespace(get_ipython=lambda: _IP())
+        monkeypatch.setitem(sys.modules, "IPython", fake_ipython)
+    job = run_mod.run(entry_point=None, chief_config=CPU, jobs_dir=str(tmp_path / "jobs"), exit=False, wait=True)
+    assert job.wait(120) == 0
+    log = open(job.log_path(0)).read()
+    assert "NB_RAN 42" in log, log
+
+
+def test_run_in_notebook_not_found_is_clear_error(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.delenv("JPY_SESSION_NAME", raising=False)
+    monkeypatch.setattr(run_mod, "_called_from_notebook", lambda: True)
+    monkeypatch.setattr(run_mod, "current_notebook_path", lambda *a, **k: None)
+    with pytest.raises(RuntimeError, match="could not be located"):
+        run_mod.run(entry_point=None, chief_config=CPU, jobs_dir=str(tmp_path / "jobs"), exit=False)

@@ -1,0 +1,178 @@
+"""The DP engine's transport contract and communication accounting.
+
+* A fake asynchronous communicator (``all_reduce(tensor) -> work``) is driven through a
+  real backward: buckets must launch strictly in index order, each only after every
+  parameter gradient it holds was produced, and ``finish()`` must join every outstanding
+  collective before the optimizer could read the arena.
+* Under gloo (2 CPU ranks) the per-step ``allreduce_ms`` / ``exposed_comm_ms`` must be
+  finite, the comm time positive and the exposed time no longer than the step.
+"""
+import math
+import os
+import sys
+import time
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from cloud_amd.optim import SGD  # noqa: E402
+from cloud_amd.parallel.ddp import GradAllReducer  # noqa: E402
+
+
+class FakeWork:
+    def __init__(self, log, idx, tensor):
+        self.log, self.idx, self.tensor = log, idx, tensor
+        self.done = False
+
+    def wait(self):
+        # the collective "completes": a sum over 2 identical replicas
+        self.tensor.mul_(2.0)
+        self.done = True
+        self.log.append(("wait", self.idx))
+        return True
+
+
+class FakeComm:
+    """Records launches (with the set of gradients that existed at launch time)."""
+
+    def __init__(self, reducer_ref):
+        self.log = []
+        self.reducer_ref = reducer_ref
+        self.works = []
+
+    def all_reduce(self, t):
+        red = self.reducer_ref[0]
+        b = next(b for b in red.buckets if b.tensor.data_ptr() == t.data_ptr() or b.wire is t)
+        ready = {id(s.param) for s in b.slots if id(s.param) in red._seen}
+        self.log.append(("launch", b.index, len(ready) == len(b.slots)))
+        w = FakeWork(self.log, b.index, t)
+        self.works.append(w)
+        return w
+
+
+def _model():
+    torch.manual_seed(0)
+    return torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.ReLU(), torch.nn.Linear(64, 64), torch.nn.ReLU(),
+                               torch.nn.Linear(64, 8))
+
+
+def test_fake_comm_bucket_order_and_join():
+    model = _model()
+    opt = SGD(model, learning_rate=0.1)
+    ref = [None]
+    fake = FakeComm(ref)
+    red = GradAllReducer(opt.arenas, bucket_mb=0.002, transport=fake, world=2)
+    ref[0] = red
+    assert len(red.buckets) >= 3
+    x = torch.randn(4, 16)
+    for step in range(2):
+        fake.log.clear()
+        opt.zero_grad()
+        model(x).square().sum().backward()
+        launched_in_backward = [e for e in fake.log if e[0] == "launch"]
+        # overlap: at least the early buckets go out while backward is still running
+        assert len(launched_in_backward) >= 1
+        red.finish()
+        launches = [e for e in fake.log if e[0] == "launch"]
+        waits = [e for e in fake.log if e[0] == "wait"]
+        # every bucket exactly once, strictly in index order, each with all its gradients
+        assert [e[1] for e in launches] == list(range(len(red.buckets)))
+        assert all(e[2] for e in launches), launches
+        # join: every launched collective was waited for by finish(), in order
+        assert [e[1] for e in waits] == list(range(len(red.buckets)))
+        assert all(w.done for w in fake.works)
+        fake.works.clear()
+        # the reducer is reset for the next step
+        assert red._next == 0 and not red._seen
+
+
+def test_fake_comm_grads_reduced_before_optimizer():
+    model = _model()
+    opt = SGD(model, learning_rate=0.0)
+    ref = [None]
+    red = GradAllReducer(opt.arenas, bucket_mb=0.002, transport=FakeComm(ref), world=2)
+    ref[0] = red
+    x = torch.randn(4, 16)
+    model(x).square().sum().backward()
+    before = [a.grad.clone() for a in opt.arenas]
+    red.finish()
+    for a, b in zip(opt.arenas, before):
+        torch.testing.assert_close(a.grad, 2.0 * b)
+
+
+def test_fake_comm_host_timing_finite():
+    model = _model()
+    opt = SGD(model, learning_rate=0.1)
+    ref = [None]
+    red = GradAllReducer(opt.arenas, bucket_mb=0.002, transport=FakeComm(ref), world=2)
+    ref[0] = red
+    red.timing_start()
+    x = torch.randn(4, 16)
+    for _ in range(3):
+        opt.zero_grad()
+        model(x).square().sum().backward()
+        red.finish()
+    t = red.timing_summary()
+    assert t["steps"] == 3 and t["timing"] == "host_clock"
+    assert math.isfinite(t["allreduce_ms"]) and math.isfinite(t["exposed_comm_ms"])
+    assert t["allreduce_ms"] >= 0 and t["exposed_comm_ms"] >= 0
+
+
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def _gloo_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(*[torch.nn.Linear(256, 256) for _ in range(6)])
+    opt = SGD(model, learning_rate=0.01, grad_scale=1.0 / world)
+    red = GradAllReducer(opt.arenas, bucket_mb=0.25)
+    red.broadcast_parameters()
+    x = torch.randn(32, 256)
+    red.timing_start()
+    steps = []
+    for _ in range(4):
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        model(x).square().mean().backward()
+        red.finish()
+        opt.step()
+        steps.append((time.perf_counter() - t0) * 1e3)
+    t = red.timing_summary()
+    ok = red.check_consistency()
+    q.put((rank, t, sum(steps) / len(steps), ok))
+    dist.destroy_process_group()
+
+
+def test_gloo_comm_accounting_consistent():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, t, step_ms, ok in res:
+        assert ok is True
+        assert t["timing"] == "host_clock"
+        assert math.isfinite(t["allreduce_ms"]) and math.isfinite(t["exposed_comm_ms"])
+        assert t["allreduce_ms"] > 0, t
+        assert t["exposed_comm_ms"] <= step_ms, (t, step_ms)

@@ -90,7 +90,10 @@ def test_keras_job_via_run_two_workers(tmp_path):
                        capture_output=True, text=True, timeout=600, cwd=os.path.join(ROOT, "examples"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Job submitted successfully." in r.stdout
-    res = [json.loads(ln[7:]) for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]
+    # stream_logs tails every rank, lines tagged with the rank's role (the chief's first)
+    res = [json.loads(ln[len("[chief-0] RESULT "):]) for ln in r.stdout.splitlines()
+           if ln.startswith("[chief-0] RESULT ")]
+    assert any(ln.startswith("[worker-0] ") for ln in r.stdout.splitlines())
     assert res and res[0]["replicas"] == 2 and res[0]["strategy"] == "MultiWorkerMirroredStrategy"
     assert res[0]["loss"][-1] < res[0]["loss"][0] and res[0]["test_acc"] > 0.8
     logs = os.listdir(os.path.join(tmp_path, os.listdir(tmp_path)[0], "logs"))
