@@ -43,7 +43,9 @@ _VARS = [
     Var("CLOUD_AMD_OPS", str, "native", "'native' HIP kernels or 'torch' stock ops", "ops"),
     Var("CLOUD_AMD_GEMM", str, "native", "dense GEMMs: 'native' or 'torch'", "ops"),
     Var("CLOUD_AMD_CONV", str, "native", "convolutions: 'native' or 'torch'", "ops"),
-    Var("CLOUD_AMD_GEMM_CORE", str, "glds", "GEMM/conv staging core: 'glds' (LDS-DMA) or 'reg' (register)", "ops"),
+    Var("CLOUD_AMD_GEMM_CORE", str, "auto", "GEMM core: 'auto' (128x128 LDS-DMA core plus the 256x256 ring core "
+        "for large GEMMs), 'glds' (128 core only), 'v256' (256 core whenever M, N >= 256), 'glds8', 'reg' "
+        "(register staging)", "ops"),
     Var("CLOUD_AMD_WGRAD_BLOCKS", int, 512, "convolution weight gradients: split-K so that about this many "
         "workgroups run (tiles x splits); fewer splits = less fp32 slab traffic, more = fuller CUs", "ops"),
     Var("CLOUD_AMD_WGRAD_BLOCKS_SMALLM", int, 512, "convolution weight gradients with <= 128 output channels "
@@ -69,8 +71,6 @@ _VARS = [
         "read 4 staged output rows from LDS before storing any", "ops"),
     Var("CLOUD_AMD_CONV_EPI_PF", bool, True, "implicit-GEMM forward convolutions with the BN-statistics epilogue: "
         "read 2 staged output rows from LDS before storing", "ops"),
-    Var("CLOUD_AMD_CONV_HALO", bool, False, "stride-1 3x3 forward convolutions (W <= 63, Cin % 64 == 0): flattened-"
-        "halo kernel (one LDS fill of the input rows per 64-channel chunk, 9 taps read shifted)", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "
         "K, minimum HBM bytes) to this file, for scripts/gemm_roofline.py", "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "

@@ -911,150 +911,4 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
   gemm_epilogue<BM, BN, WM, WN, EPI, SMEM, EPF>(P, acc, smem, m0, n0, tm, tid);
 }
 
-// ============================================== 256 x 256 ping-pong core --
-// 8 waves as 2 (M) x 4 (N), wave tile 128 x 64 (8 x 4 fragments), BK = 64, two LDS stages
-// of [A 256 x 64 | B 256 x 64] (128 KB, one block per CU, two waves per SIMD: wave w and
-// w + 4 share a SIMD).  Each K tile runs as four phases of one 64 x 32 accumulator quadrant
-// (16 MFMAs) each: a phase is {LDS reads or LDS-DMA issue} -> s_barrier -> {MFMAs} ->
-// s_barrier, and the wave group M = 1 starts one barrier late, so on every SIMD one wave
-// multiplies while its partner reads / issues (the two-waves-per-SIMD ping-pong,
-// MI355X_MICROARCH.md §Two waves per SIMD; cdna_hip_programming.md T3-T5).
-//   phase 0: read A rows 0-63 + B cols 0-31 of the wave tile (12 reads)   -> Q00
-//   phase 1: read A rows 64-127 + B cols 32-63 (12 reads; the whole tile is now in
-//            registers and this stage is free once the phase's barrier is passed) -> Q01
-//   phase 2: LDS-DMA of tile t+2's A into this stage (4 pieces)            -> Q11
-//   phase 3: LDS-DMA of tile t+2's B (4 pieces); vmcnt(8) retires tile t+1 and leaves
-//            tile t+2 in flight                                            -> Q10
-// The DMA issue cost (60-185 cycles per piece, MI355X_MICROARCH.md constants) is spread
-// over two phases behind the partner's MFMAs; loads never drain to zero in the loop and
-// stay in flight across the raw barriers.  Barrier balance: the late group's extra barrier
-// at the start is matched by the early group's at the end.
-__device__ __forceinline__ void pp_bar() {
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");  // no LDS access is moved across the barrier
-}
-
-template <template <int, int, int> class LAT, template <int, int, int> class LBT, int EPI>
-__device__ __forceinline__ void mfma_gemm_pp256(const CoreParams& P) {
-  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NT = 512;
-  constexpr int FM = 8, FN = 4;
-  constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;
-  constexpr int STAGE = A_ELEMS + B_ELEMS;
-  constexpr int EPI_LD = EpiLayout<BN>::LD;
-  constexpr int SMEM = (2 * STAGE > BM * EPI_LD ? 2 * STAGE : BM * EPI_LD);
-  constexpr int CPA = A_ELEMS / 8 / NT, CPB = B_ELEMS / 8 / NT;
-  using LA = LAT<BM, CPA, NT>;
-  using LB = LBT<BN, CPB, NT>;
-  constexpr bool A_KC = LA::KC, B_KC = LB::KC;
-  static_assert(CPA == 4 && CPB == 4, "vmcnt counts below assume 4 + 4 pieces per tile");
-  __shared__ __attribute__((aligned(16))) short smem[SMEM];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int grp = __builtin_amdgcn_readfirstlane(wave) >> 2;  // == wm, provably wave-uniform
-  const int tiles_m = (P.M + BM - 1) / BM, tiles_n = (P.N + BN - 1) / BN;
-  const BlkPos bp = blk_pos(P);
-  const int tm = bp.tile / tiles_n, tn = bp.tile % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = bp.split * P.k_per_split;
-  int kend = kbeg + P.k_per_split;
-  if (kend > P.K) kend = P.K;
-  const int nk = (kend - kbeg + BK - 1) / BK;
-
-  LA la(P, true, m0, tid);
-  LB lb(P, false, n0, tid);
-
-  f4v acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
-
-  const auto ra = loader_rsrc(la);
-  const auto rb = loader_rsrc(lb);
-  auto issue_a = [&](int t) {
-    short* base = smem + (t & 1) * STAGE;
-    const int k0 = kbeg + t * BK;
-#pragma unroll
-    for (int i = 0; i < CPA; ++i) CA_DMA_CHUNK(LA, la, ra, i, k0, base + (i * NT + wave * 64) * 8);
-    if constexpr (loader_stateful<LA>::value) la.advance();
-  };
-  auto issue_b = [&](int t) {
-    short* base = smem + (t & 1) * STAGE + A_ELEMS;
-    const int k0 = kbeg + t * BK;
-#pragma unroll
-    for (int i = 0; i < CPB; ++i) CA_DMA_CHUNK(LB, lb, rb, i, k0, base + (i * NT + wave * 64) * 8);
-    if constexpr (loader_stateful<LB>::value) lb.advance();
-  };
-  const int ar0 = wm * (BM / WM), bc0 = wn * (BN / WN);
-  bf16x8 af[2][2][4], bq[2][2][2];  // af[qm][kk][i], bq[qn][kk][j]
-  auto read_q = [&](const short* As, const short* Bs, int q) {  // A rows q*64.. and B cols q*32..
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bq[q][kk][j] = read_frag_sw<BN, B_KC>(Bs, bc0 + (q * 2 + j) * 16, kk * 32, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[q][kk][i] = read_frag_sw<BM, A_KC>(As, ar0 + (q * 4 + i) * 16, kk * 32, lane);
-    }
-  };
-  auto mma = [&](int qm, int qn) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[qm * 4 + i][qn * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[qn][kk][j], af[qm][kk][i],
-                                                                                acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  // prologue: tiles 0 and 1 in flight, tile 0 retired
-  if (nk > 0) {
-    issue_a(0);
-    issue_b(0);
-  }
-  if (nk > 1) {
-    issue_a(1);
-    issue_b(1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  pp_bar();
-  if (grp == 1) pp_bar();
-  for (int t = 0; t < nk; ++t) {
-    const short* As = smem + (t & 1) * STAGE;
-    const short* Bs = As + A_ELEMS;
-    const bool more = t + 2 < nk;
-    read_q(As, Bs, 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    pp_bar();
-    mma(0, 0);
-    pp_bar();
-    read_q(As, Bs, 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // stage t&1 read out before the next barrier
-    pp_bar();
-    mma(0, 1);
-    pp_bar();
-    if (more) issue_a(t + 2);
-    pp_bar();
-    mma(1, 1);
-    pp_bar();
-    if (more) {
-      issue_b(t + 2);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile t+1 landed, tile t+2 in flight
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    pp_bar();
-    mma(1, 0);
-    pp_bar();
-  }
-  if (grp == 0) pp_bar();
-  __syncthreads();
-  gemm_epilogue<BM, BN, WM, WN, EPI, SMEM>(P, acc, smem, m0, n0, tm, tid);
-}
-
 }  // namespace ca

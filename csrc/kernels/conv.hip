@@ -752,135 +752,6 @@ bool tall_tiles() {
   return v != 0;
 }
 
-// ---- flattened-halo 3x3 / stride 1 / pad 1 forward convolution -----------------------
-// The BM output pixels of a tile are consecutive in the flattened (n, y, x) order, and with
-// stride 1 every tap (dy, dx) reads the same pixel range shifted by dy * W + dx.  So the A
-// operand of one 64-channel chunk is ONE dense LDS-DMA of input rows [m0 - W - 1,
-// m0 + BM + W + 1) (the halo), read by all 9 taps at a row offset; a per-lane test
-// (0 <= y + dy < H, 0 <= x + dx < W) zeroes the fragments of out-of-image taps.  The
-// weights stream per tap, double-buffered (the next tap's DMA overlaps this tap's MFMAs).
-// LDS fill per 128-row tile: 31 KB of A + 9 x BN x 128 B of B, against 9 x (16 KB + B) for
-// the per-tap implicit GEMM.  W <= 63 (halo rows fit HROWS), Cin % 64 == 0.
-constexpr int HROWS = 256;  // >= BM + 2 * (W + 1) for BM = 128, W <= 63
-
-template <int BN, int EPI>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) conv3x3_halo_kernel(CoreParams P) {
-  constexpr int BM = 128, WM = 2, WN = 2, NT = 256;
-  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
-  constexpr int A_ELEMS = HROWS * BK, B_ELEMS = BN * BK;
-  constexpr int CPA = A_ELEMS / 8 / NT, CPB = B_ELEMS / 8 / NT;
-  constexpr int EPI_LD = EpiLayout<BN>::LD;
-  constexpr int SMEM = (A_ELEMS + 2 * B_ELEMS > BM * EPI_LD) ? A_ELEMS + 2 * B_ELEMS : BM * EPI_LD;
-  static_assert(CPA + CPB < 64, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) short smem[SMEM];
-  short* As = smem;
-  short* Bs = smem + A_ELEMS;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int tiles_n = (P.N + BN - 1) / BN;
-  const BlkPos bp = blk_pos(P);
-  const int tm = bp.tile / tiles_n, tn = bp.tile % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int W = P.W, H = P.H, Cin = P.Cin, halo = W + 1;
-
-  // A (halo rows): chunk i of thread tid = LDS row (tid >> 3) + 32 i, 16-B slot tid & 7,
-  // holding input channels c0 + 8 * ((tid & 7) ^ (row & 7)) (the reader's KC swizzle)
-  const int arow = tid >> 3;
-  const int acol = ((tid & 7) ^ (arow & 7)) << 3;
-  const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(P.A), (short)0,
-                                                    (int)buf_span((long)P.M * Cin * 2), 0x00020000);
-  const uint32_t a_oob = 0x7fffffc0u;
-  // B (weights [Cout][3][3][Cin]): chunk i = output channel n0 + (tid >> 3) + 32 i
-  const int brow = tid >> 3;
-  const int bcol = ((tid & 7) ^ (brow & 7)) << 3;
-  const long ldw = 9L * Cin;
-  const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(P.B), (short)0,
-                                                    (int)buf_span((long)P.N * ldw * 2), 0x00020000);
-
-  // output pixel (y, x) of this lane's fragment rows (the same for every tap and chunk)
-  int py[FM], px[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
-    const Pix o = decode((uint32_t)(m < P.M ? m : 0), P.div_w, P.div_h);
-    py[i] = m < P.M ? o.y : -(1 << 20);
-    px[i] = o.x;
-  }
-
-  f4v acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
-
-  auto issue_a = [&](int c0) {
-#pragma unroll
-    for (int i = 0; i < CPA; ++i) {
-      const int g = m0 - halo + arow + i * (NT / 8);  // input pixel of this LDS row
-      const uint32_t o = ((unsigned)g < (unsigned)P.M) ? (uint32_t)(((long)g * Cin + c0 + acol) * 2) : a_oob;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(As + (i * NT + wave * 64) * 8), 16, o, 0, 0, 0);
-    }
-  };
-  auto issue_b = [&](int tap, int c0, short* dst) {
-#pragma unroll
-    for (int i = 0; i < CPB; ++i) {
-      const int co = n0 + brow + i * (NT / 8);
-      const uint32_t o = co < P.N ? (uint32_t)((co * ldw + (long)tap * Cin + c0 + bcol) * 2) : a_oob;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(dst + (i * NT + wave * 64) * 8), 16, o, 0, 0, 0);
-    }
-  };
-
-  const int nchunk = Cin / BK;
-  for (int ch = 0; ch < nchunk; ++ch) {
-    const int c0 = ch * BK;
-    issue_a(c0);
-    issue_b(0, c0, Bs);
-    for (int tap = 0; tap < 9; ++tap) {
-      if (tap + 1 < 9) {
-        issue_b(tap + 1, c0, Bs + ((tap + 1) & 1) * B_ELEMS);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CPB) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-      const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-      const int shift = halo + dy * W + dx;
-      bool ok[FM];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-        ok[i] = ((unsigned)(py[i] + dy) < (unsigned)H) & ((unsigned)(px[i] + dx) < (unsigned)W);
-      const short* Bt = Bs + (tap & 1) * B_ELEMS;
-#pragma unroll
-      for (int kk = 0; kk < BK; kk += 32) {
-        bf16x8 af[FM], bfr[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const bf16x8 v = read_frag_sw<HROWS, true>(As, wm * (BM / WM) + i * 16 + shift, kk, lane);
-          af[i] = ok[i] ? v : bf16x8{};
-        }
-#pragma unroll
-        for (int j = 0; j < FN; ++j) bfr[j] = read_frag_sw<BN, true>(Bt, wn * (BN / WN) + j * 16, kk, lane);
-        mfma_acc<FM, FN>(acc, af, bfr);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  }
-  gemm_epilogue<BM, BN, WM, WN, EPI, SMEM, (EPI == EPI_BF16_ST ? 2 : 1)>(P, acc, smem, m0, n0, tm, tid);
-}
-
-// CLOUD_AMD_CONV_HALO=1: stride-1 3x3 forward convolutions (W <= 63, Cin % 64 == 0) on the
-// flattened-halo kernel (A/B runs)
-bool conv_halo() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CLOUD_AMD_CONV_HALO");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v != 0;
-}
-
 // CLOUD_AMD_GEMM_CORE=reg selects the register-staged core (A/B comparisons).
 // 0 = register-staged, 1 = glds single stage (4 waves), 2 = glds double-buffered (8 waves)
 int core_kind() {
@@ -988,19 +859,6 @@ int ca_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   p.A = x; p.B = w; p.lda = Cin; p.ldb = (long)KH * KW * Cin; p.C = y; p.ldc = Cout;
   p.M = Nb * p.OH * p.OW; p.N = Cout; p.K = KH * KW * Cin; p.k_per_split = p.K;
   p.stats = stats;
-  if (conv_halo() && use_glds() && KH == 3 && KW == 3 && sh == 1 && sw == 1 && ph == 1 && pw == 1 && Cin % BK == 0 &&
-      W <= 63 && (long)p.M * Cin * 2 < (long)BUF_CAP && (long)Cout * 9 * Cin * 2 < (long)BUF_CAP) {
-    p.split_xcd = split_xcd_enabled();
-    // 64-wide N tiles at every width: 48 KB of LDS keeps 3 blocks per CU (128-wide tiles
-    // need 64 KB, 2 blocks per CU, and measured 14-17 % slower at 128-512 channels)
-    const dim3 grid(((p.M + 127) / 128) * ((Cout + 63) / 64), 1, 1);
-    if (stats)
-      conv3x3_halo_kernel<64, EPI_BF16_ST><<<grid, 256, 0, s>>>(p);
-    else
-      conv3x3_halo_kernel<64, EPI_BF16><<<grid, 256, 0, s>>>(p);
-    CA_LAUNCH_CHECK();
-    return 0;
-  }
   if (p.cin_tile && KH * KW <= 32 && tapmask_loaders()) {
     if (stats) {
       if (Cout <= 64) return launch_n64<ConvFwdA, DenseKC, GConvFwdAT, GDenseKC, EPI_BF16_ST>(p, s);

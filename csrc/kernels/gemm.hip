@@ -11,7 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "ca_mfma_core.h"
+#include "ca_gemm256.h"
 
 namespace {
 using namespace ca;
@@ -53,22 +53,27 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) d
   mfma_gemm_glds<BM, BN, 2, 4, LA, LB, EPI, 2>(P);
 }
 
-// The 256 x 256 ping-pong core (mfma_gemm_pp256): CLOUD_AMD_GEMM_CORE=pp256.
+// The 256 x 256 ring core (csrc/include/ca_gemm256.h) for large GEMMs: one 512-thread
+// workgroup per CU.  K-contiguous operands use the 32-deep KC32 loader, N-contiguous ones
+// the same GDenseNC loader as the 128 cores.
 template <template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
-__global__ void __launch_bounds__(512) dense_gemm_pp256_kernel(CoreParams P) {
-  mfma_gemm_pp256<LA, LB, EPI>(P);
+__global__ void __launch_bounds__(512) dense_gemm_256_kernel(CoreParams P) {
+  mfma_gemm_256<LA, LB, EPI>(P);
 }
 
 // CLOUD_AMD_GEMM_CORE selects the core (A/B comparisons; ca_gemm_set_core overrides it):
-// 0 "reg" = register-staged, 1 (default) = glds single stage (4 waves), 2 "glds8" = glds
-// double-buffered (8 waves), 4 "pp256" = 1 plus the 256 x 256 ping-pong core for large
-// plain-epilogue GEMMs (measured: +10-15 % at 4096^3 / 8192^3, slower on the BERT / ResNet
-// shapes -- docs/performance.md).
+// 0 "reg" = register-staged, 1 "glds" = glds single stage (4 waves) only, 2 "glds8" = glds
+// double-buffered (8 waves), 3 (default) = glds plus the 256 x 256 ring core for large
+// GEMMs (use_256 below; 4096^3: 904 -> 1126-1148 TF/s, 8192^3: 845 -> 1166-1175), 4 "v256"
+// = the 256 core for every GEMM with M, N >= 256 (tests).
 int g_core_kind = -1;
 int core_kind() {
   if (g_core_kind < 0) {
     const char* e = getenv("CLOUD_AMD_GEMM_CORE");
-    g_core_kind = !e ? 1 : (e[0] == 'r' ? 0 : (strcmp(e, "glds8") == 0 ? 2 : (strcmp(e, "pp256") == 0 ? 4 : 1)));
+    g_core_kind = !e ? 3
+                     : (e[0] == 'r' ? 0
+                                    : (strcmp(e, "glds8") == 0 ? 2
+                                                              : (strcmp(e, "glds") == 0 ? 1 : (strcmp(e, "v256") == 0 ? 4 : 3))));
   }
   return g_core_kind;
 }
@@ -112,6 +117,26 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
+// Fraction of CU-slots doing work when `tiles` equal blocks are spread over the
+// 256 CUs in rounds (wave quantisation).
+static double tile_balance(long tiles) {
+  const long cus = 256;
+  const long rounds = (tiles + cus - 1) / cus;
+  return (double)tiles / (double)(rounds * cus);
+}
+
+// The 256 core pays when its grid fills the chip in (nearly) whole rounds and every block
+// has enough K tiles to amortise its 3-tile prologue and its 128-KB epilogue: >= 2 rounds
+// at >= 85 % slot use, or exactly whole rounds, and >= 16 K tiles of 32 per block.  (BERT's
+// M = 8192 GEMMs get 96-384 tiles -- 1.1-1.5 rounds -- and stay on the 128 core, whose 4
+// co-resident blocks per CU absorb the quantisation.)
+static bool use_256(const CoreParams& p, int splits) {
+  if (core_kind() == 4) return p.M >= 256 && p.N >= 256;
+  if (core_kind() != 3 || p.M < 256 || p.N < 256 || p.k_per_split < 512) return false;
+  const long t = (long)((p.M + 255) / 256) * ((p.N + 255) / 256) * splits;
+  return t >= 256 && (tile_balance(t) >= 0.999 || (t >= 512 && tile_balance(t) >= 0.85));
+}
+
 template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB,
           template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
 int launch(const CoreParams& p0, int splits, hipStream_t s) {
@@ -122,10 +147,18 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
   // (ca_mfma_core.h BUF_CAP): rows of a tile (KC) or one split's K range (NC)
   const long span = (long)(p.k_per_split + BK > 256 ? p.k_per_split + BK : 256) * (p.lda > p.ldb ? p.lda : p.ldb) * 2;
   if (use_glds() && span >= (long)BUF_CAP) return -3;
-  if constexpr (BM == 128 && BN == 128 && (EPI == EPI_BF16 || EPI == EPI_F32_PARTIAL)) {
-    if (core_kind() == 4 && p.M >= 256 && p.N >= 256) {
+  if constexpr (BM == 128 && BN == 128 && (EPI == EPI_BF16 || EPI == EPI_F32_PARTIAL || EPI == EPI_BF16_ST)) {
+    if (use_256(p, splits)) {
       const int t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
-      dense_gemm_pp256_kernel<GA, GB, EPI><<<dim3(t256, 1, splits), 512, 0, s>>>(p);
+      constexpr bool AK = GA<BM, 1, 256>::KC, BKC = GB<BN, 1, 256>::KC;
+      if constexpr (AK && BKC)
+        dense_gemm_256_kernel<GDenseKC32, GDenseKC32, EPI><<<dim3(t256, 1, splits), 512, 0, s>>>(p);
+      else if constexpr (AK && !BKC)
+        dense_gemm_256_kernel<GDenseKC32, GDenseNC, EPI><<<dim3(t256, 1, splits), 512, 0, s>>>(p);
+      else if constexpr (!AK && !BKC)
+        dense_gemm_256_kernel<GDenseNC, GDenseNC, EPI><<<dim3(t256, 1, splits), 512, 0, s>>>(p);
+      else
+        return -2;
       CA_LAUNCH_CHECK();
       return 0;
     }
@@ -158,13 +191,6 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
   return 0;
 }
 
-// Fraction of CU-slots doing work when `tiles` equal blocks are spread over the
-// 256 CUs in rounds (wave quantisation).
-static double tile_balance(long tiles) {
-  const long cus = 256;
-  const long rounds = (tiles + cus - 1) / cus;
-  return (double)tiles / (double)(rounds * cus);
-}
 
 // 128-wide N tiles unless N is small, or the 128-wide grid would leave a badly
 // filled last round (e.g. M=8192, N=768: 384 tiles -> 1.5 rounds) and halving
@@ -216,7 +242,7 @@ int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long l
 // the previous one.
 int ca_gemm_set_core(int kind) {
   const int prev = core_kind();
-  if (kind == 0 || kind == 1 || kind == 2 || kind == 4) g_core_kind = kind;
+  if (kind >= 0 && kind <= 4) g_core_kind = kind;
   return prev;
 }
 

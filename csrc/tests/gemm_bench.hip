@@ -57,24 +57,14 @@ __global__ void ref_gemm(const bf16_t* A, long lda, const bf16_t* B, long ldb, i
   C[(long)r * N + n] = s;
 }
 
-template <template <int, int, int> class GA, template <int, int, int> class GB>
+template <template <int, int, int> class GA, template <int, int, int> class GB, bool ST>
 __global__ void __launch_bounds__(512) k256(CoreParams P) {
-  mfma_gemm_256<GA, GB, EPI_BF16>(P);
-}
-
-template <template <int, int, int> class GA, template <int, int, int> class GB>
-__global__ void __launch_bounds__(512) k256s(CoreParams P) {
-  mfma_gemm_256<GA, GB, EPI_BF16, true>(P);
+  mfma_gemm_256<GA, GB, EPI_BF16, ST>(P);
 }
 
 template <template <int, int, int> class GA, template <int, int, int> class GB>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k128(CoreParams P) {
   mfma_gemm_glds<128, 128, 2, 2, GA, GB, EPI_BF16>(P);
-}
-
-template <template <int, int, int> class GA, template <int, int, int> class GB>
-__global__ void __launch_bounds__(512) kpp(CoreParams P) {
-  mfma_gemm_pp256<GA, GB, EPI_BF16>(P);
 }
 
 struct Variant {
@@ -83,57 +73,47 @@ struct Variant {
   void (*launch)(const CoreParams&, int layout, dim3 grid, hipStream_t);
 };
 
-static void launch256(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
-  if (layout == 0) k256<GDenseKC, GDenseKC><<<g, 512, 0, s>>>(p);
-  else if (layout == 1) k256<GDenseKC, GDenseNC><<<g, 512, 0, s>>>(p);
-  else k256<GDenseNC, GDenseNC><<<g, 512, 0, s>>>(p);
+template <bool ST>
+static void launch256_t(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) k256<GDenseKC32, GDenseKC32, ST><<<g, 512, 0, s>>>(p);
+  else if (layout == 1) k256<GDenseKC32, GDenseNC, ST><<<g, 512, 0, s>>>(p);
+  else k256<GDenseNC, GDenseNC, ST><<<g, 512, 0, s>>>(p);
 }
-static void launch256s(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
-  if (layout == 0) k256s<GDenseKC, GDenseKC><<<g, 512, 0, s>>>(p);
-  else if (layout == 1) k256s<GDenseKC, GDenseNC><<<g, 512, 0, s>>>(p);
-  else k256s<GDenseNC, GDenseNC><<<g, 512, 0, s>>>(p);
-}
-
-// per-segment cycle medians of the stamped K tile (k256s): segments R(q) / M(q) per wave
-// group, each as work cycles (start -> arrival at the closing barrier) + barrier wait
-static void stamp_report(const CoreParams& p0, int layout, dim3 g, hipStream_t s) {
-  CoreParams p = p0;
-  const long n = (long)g.x * 8 * 17;
-  CHECK(hipMalloc(&p.stamps, n * 8));
-  CHECK(hipMemsetAsync(p.stamps, 0, n * 8, s));
-  for (int w = 0; w < 3; ++w) launch256s(p, layout, g, s);
-  CHECK(hipStreamSynchronize(s));
-  std::vector<unsigned long long> h(n);
-  CHECK(hipMemcpy(h.data(), p.stamps, n * 8, hipMemcpyDeviceToHost));
-  CHECK(hipFree(p.stamps));
-  for (int grp = 0; grp < 2; ++grp) {
-    printf("{\"stamps_group\": %d, \"segments\": [", grp);
-    for (int seg = 0; seg < 8; ++seg) {
-      std::vector<long> work, wait;
-      for (unsigned b = 0; b < g.x; ++b)
-        for (int w = grp * 4; w < grp * 4 + 4; ++w) {
-          const unsigned long long* st = h.data() + ((long)b * 8 + w) * 17;
-          work.push_back((long)(st[2 * seg + 1] - st[2 * seg]));
-          wait.push_back((long)(st[2 * seg + 2] - st[2 * seg + 1]));
-        }
-      std::sort(work.begin(), work.end());
-      std::sort(wait.begin(), wait.end());
-      printf("%s{\"%s%d\": [%ld, %ld]}", seg ? ", " : "", (seg & 1) ? "M" : "R", seg / 2, work[work.size() / 2],
-             wait[wait.size() / 2]);
-    }
-    printf("]}\n");
-  }
-}
+static void launch256(const CoreParams& p, int layout, dim3 g, hipStream_t s) { launch256_t<false>(p, layout, g, s); }
 
 static void launch128(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
   if (layout == 0) k128<GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
   else if (layout == 1) k128<GDenseKC, GDenseNC><<<g, 256, 0, s>>>(p);
   else k128<GDenseNC, GDenseNC><<<g, 256, 0, s>>>(p);
 }
-static void launchpp(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
-  if (layout == 0) kpp<GDenseKC, GDenseKC><<<g, 512, 0, s>>>(p);
-  else if (layout == 1) kpp<GDenseKC, GDenseNC><<<g, 512, 0, s>>>(p);
-  else kpp<GDenseNC, GDenseNC><<<g, 512, 0, s>>>(p);
+
+// per-phase shader-cycle medians of the 256 core (GB_STAMP=1): R work, R -> barrier wait,
+// M work, per wave group, for the K tile in the middle of each block's loop
+static void stamp_report(const CoreParams& p0, int layout, dim3 g, hipStream_t s) {
+  CoreParams p = p0;
+  const long n = (long)g.x * 8 * 17;
+  CHECK(hipMalloc(&p.stamps, n * 8));
+  CHECK(hipMemsetAsync(p.stamps, 0, n * 8, s));
+  for (int w = 0; w < 3; ++w) launch256_t<true>(p, layout, g, s);
+  CHECK(hipStreamSynchronize(s));
+  std::vector<unsigned long long> h(n);
+  CHECK(hipMemcpy(h.data(), p.stamps, n * 8, hipMemcpyDeviceToHost));
+  CHECK(hipFree(p.stamps));
+  for (int grp = 0; grp < 2; ++grp) {
+    std::vector<long> r, w, m;
+    for (unsigned b = 0; b < g.x; ++b)
+      for (int wv = grp * 4; wv < grp * 4 + 4; ++wv) {
+        const unsigned long long* st = h.data() + ((long)b * 8 + wv) * 17;
+        r.push_back((long)(st[1] - st[0]));
+        w.push_back((long)(st[2] - st[1]));
+        m.push_back((long)(st[3] - st[2]));
+      }
+    std::sort(r.begin(), r.end());
+    std::sort(w.begin(), w.end());
+    std::sort(m.begin(), m.end());
+    printf("{\"stamps_group\": %d, \"R\": %ld, \"R_wait\": %ld, \"M\": %ld}\n", grp, r[r.size() / 2],
+           w[w.size() / 2], m[m.size() / 2]);
+  }
 }
 
 int main(int argc, char** argv) {
@@ -149,8 +129,8 @@ int main(int argc, char** argv) {
     if (sscanf(argv[a], "%d,%d,%d,%d", &M, &N, &K, &L) == 4) shapes.insert(shapes.end(), {M, N, K, L});
   }
   if (shapes.empty()) shapes = {4096, 4096, 4096, 0};
-  const char* only = getenv("GB_VARIANTS");  // e.g. "v3,glds"
-  Variant vars[] = {{"v3_256", 256, 256, launch256}, {"glds128", 128, 128, launch128}, {"pp256", 256, 256, launchpp}};
+  const char* only = getenv("GB_VARIANTS");  // comma list of full variant names, e.g. "v256,glds128"
+  Variant vars[] = {{"v256", 256, 256, launch256}, {"glds128", 128, 128, launch128}};
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
   hipEvent_t e0, e1;

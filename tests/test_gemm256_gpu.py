@@ -1,0 +1,89 @@
+"""The 256 x 256 ring GEMM core (csrc/include/ca_gemm256.h mfma_gemm_256; forced on every
+GEMM with M, N >= 256 by core kind 4 = CLOUD_AMD_GEMM_CORE=v256) against a plain PyTorch fp32
+GEMM of the same bf16 operands: forward (NT), input grad (NN), weight grad (TN, split-K fp32
+slabs), the fused bias + activation and BN-statistics epilogues, ragged M / N / K (partial
+tiles, K tails read as zeros through the buffer range check), one to many K tiles -- plus
+the default dispatch (core kind 3) on a shape that selects the 256 core by itself."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def core256():
+    from cloud_amd.ops import _ext
+
+    ext = _ext.load(required=True)
+    prev = ext.gemm_set_core(4)  # v256: force the 256 core
+    yield
+    ext.gemm_set_core(prev)
+
+
+def _rel(a, b):
+    return float((a.float() - b).norm() / b.norm())
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 512, 64), (1024, 768, 2048), (300, 264, 200), (4096, 256, 1024),
+                                   (777, 1032, 4104)])
+def test_256_forward_and_input_grad(core256, M, N, K):
+    from cloud_amd.ops import raw
+
+    torch.manual_seed(M + N + K)
+    a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+    y = raw.gemm(a, w)
+    assert _rel(y, a.float() @ w.float().t()) < 5e-3
+    dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    dx = raw.gemm(dy, w, layout=raw.NN)
+    assert _rel(dx, dy.float() @ w.float()) < 5e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(8192, 512, 256), (2000, 1024, 512)])
+def test_256_weight_grad_splitk(core256, M, N, K):
+    from cloud_amd.ops import raw
+
+    torch.manual_seed(M + N)
+    dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    gw = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
+    raw.wgrad_into(dy, x, gw, beta=0.0)
+    assert _rel(gw, dy.float().t() @ x.float()) < 5e-3
+
+
+def test_256_bias_act_and_stats_epilogues(core256):
+    from cloud_amd.ops import raw
+
+    torch.manual_seed(7)
+    M, N, K = 1024, 512, 320
+    a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda")
+    ref = a.float() @ w.float().t() + bias
+    y = raw.gemm(a, w, bias=bias, act="relu")
+    assert _rel(y, torch.relu(ref)) < 5e-3
+    st = raw.stats_buffer(M, N, a.device)
+    y2 = raw.gemm(a, w, stats=st)
+    z = (a.float() @ w.float().t())
+    s_sum = st.view(-1, 2, N)[:, 0].sum(0)
+    s_sq = st.view(-1, 2, N)[:, 1].sum(0)
+    assert _rel(y2, z) < 5e-3
+    assert _rel(s_sum, y2.float().sum(0)) < 1e-3
+    assert _rel(s_sq, (y2.float() ** 2).sum(0)) < 1e-3
+
+
+def test_default_dispatch_selects_256_on_large_gemm():
+    """8192 x 2048 x 1024: 256 tiles of 256 x 256 (one full round), 32 K tiles -> kind 3 uses
+    the 256 core; result checked against fp32."""
+    from cloud_amd.ops import _ext, raw
+
+    ext = _ext.load(required=True)
+    prev = ext.gemm_set_core(3)
+    try:
+        torch.manual_seed(3)
+        a = torch.randn(8192, 1024, device="cuda").to(torch.bfloat16)
+        w = torch.randn(2048, 1024, device="cuda").to(torch.bfloat16)
+        y = raw.gemm(a, w)
+        assert _rel(y[:1024], a[:1024].float() @ w.float().t()) < 5e-3
+    finally:
+        ext.gemm_set_core(prev)
