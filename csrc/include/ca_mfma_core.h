@@ -114,9 +114,31 @@ __device__ __forceinline__ long out_row(const CoreParams& P, int gm) {
 
 enum Act { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2, ACT_TANH = 3, ACT_GELU_TANH = 4, ACT_ELU = 5 };
 
+// Phi(x) = 0.5 (1 + erf(x / sqrt 2)) for the erf-GELU epilogues, without erff: erfc(z) =
+// t exp(-z^2 + P(t)), t = 1 / (1 + z / 2) (the Chebyshev-fitted form with fractional error
+// < 1.2e-7 over all z, Numerical Recipes "erfcc"), log2(e) folded into P so the exponential
+// is one v_exp_f32.  1 rcp + 1 exp + 11 FMA-class ops per element against ocml erff's two
+// branchy polynomials: the epilogue of a K = 768 GEMM (BERT FFN) is VALU-bound, so this
+// sets its cost (docs/performance.md, "BERT step, round 3").
+__device__ __forceinline__ float gelu_cdf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.f));
+  float q = fmaf(t, 2.465172979e-01f, -1.186114945e+00f);
+  q = fmaf(t, q, 2.147474464e+00f);
+  q = fmaf(t, q, -1.637753152e+00f);
+  q = fmaf(t, q, 4.023215817e-01f);
+  q = fmaf(t, q, -2.687568603e-01f);
+  q = fmaf(t, q, 1.396300565e-01f);
+  q = fmaf(t, q, 5.397006155e-01f);
+  q = fmaf(t, q, 1.442729204e+00f);
+  q = fmaf(t, q, -1.825748218e+00f);
+  const float h = 0.5f * t * __builtin_amdgcn_exp2f(fmaf(x, x * -0.72134752044448170f, q));  // erfc(z) / 2
+  return x >= 0.f ? 1.f - h : h;
+}
+
 __device__ __forceinline__ float act_fwd(int act, float x) {
   switch (act) {
-    case ACT_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case ACT_GELU: return x * gelu_cdf(x);
     case ACT_RELU: return x > 0.f ? x : 0.f;
     case ACT_TANH: return tanhf(x);
     case ACT_GELU_TANH: {
@@ -132,7 +154,7 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
 __device__ __forceinline__ float act_grad(int act, float x) {
   switch (act) {
     case ACT_GELU:
-      return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+      return fmaf(x * 0.3989422804014327f, __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f), gelu_cdf(x));
     case ACT_RELU: return x > 0.f ? 1.f : 0.f;
     case ACT_TANH: {
       const float t = tanhf(x);
@@ -389,7 +411,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
     const bool has_beta = P.beta != 0.f;
 #pragma unroll 1
     for (int it0 = 0; it0 < IT; it0 += PF) {
-      s8v opre[PF], zpre[BNS ? PF : 1], zpre2[Z2 ? PF : 1];
+      s8v opre[PF], zpre[BNS ? PF : 1], zpre2[Z2 ? PF : 1], dsrc[RSTAT ? 1 : PF];
       uint32_t mk[PF];  // bits 0-7: BN ReLU mask (BN-backward statistics), bits 8-15: res_mask
       long orow[PF];
       bool okr[PF];
@@ -401,6 +423,10 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
         const bf16_t* bsrc = (RES && P.res_src) ? P.res_src : Cg;
         opre[u] = (has_beta && okr[u]) ? *reinterpret_cast<const s8v*>(bsrc + orow[u] * P.ldc + gn) : zero8();
         mk[u] = 0xff00u;
+        if constexpr (!RSTAT) {
+          dsrc[u] = (P.dact_src && okr[u]) ? *reinterpret_cast<const s8v*>(P.dact_src + (long)gm * P.ld_aux + gn)
+                                           : zero8();
+        }
         if constexpr (RES) {
           if (has_beta && P.res_mask && okr[u]) mk[u] = (uint32_t)P.res_mask[orow[u] * (P.N / 8) + (gn >> 3)] << 8;
         }
@@ -420,7 +446,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
         if (fx) {
           if (P.preact) *reinterpret_cast<s8v*>(P.preact + (long)gm * P.ld_aux + gn) = v;
           if (P.dact_src) {
-            const s8v src = *reinterpret_cast<const s8v*>(P.dact_src + (long)gm * P.ld_aux + gn);
+            const s8v src = RSTAT ? *reinterpret_cast<const s8v*>(P.dact_src + (long)gm * P.ld_aux + gn) : dsrc[RSTAT ? 0 : u];
 #pragma unroll
             for (int j = 0; j < 8; ++j)
               v[j] = (short)f2bf(bf2f((bf16_t)v[j]) * act_grad(P.act, bf2f((bf16_t)src[j])));

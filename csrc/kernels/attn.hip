@@ -101,6 +101,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
   const bf16x8 qf0 = gfrag(qrow, 0, lane), qf1 = gfrag(qrow, 1, lane);
   const float c2 = a.scale * LOG2E;
   const long bh = (long)b * H + h;
+  const uint64_t bhss = (uint64_t)bh * S * S;  // dropout index of element (q, key): bhss + q*S + key
 
   f4v o[4];
   float m[4], l[4];
@@ -155,9 +156,9 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a) {
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const long q = q0 + (lane >> 4) * 4 + r;
-          const long key = k0 + t * 16 + (lane & 15);
-          s[t][r] *= drop_mul(a.drop, (bh * S + q) * S + key);
+          const int q = q0 + (lane >> 4) * 4 + r;
+          const int key = k0 + t * 16 + (lane & 15);
+          s[t][r] *= drop_mul(a.drop, bhss + (uint32_t)(q * S + key));
         }
     }
 #pragma unroll
@@ -235,6 +236,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
   int klen = a.key_len ? a.key_len[b] : S;
   klen = klen < 1 ? 1 : (klen > S ? S : klen);
   const long bh = (long)b * H + h;
+  const uint64_t bhss = (uint64_t)bh * S * S;  // dropout index of element (q, key): bhss + q*S + key
   const bf16_t* base = a.qkv + (long)b * S * ldq;
   const bf16_t* krow = base + (long)(k0 + (lane & 15)) * ldq + C + h * D;
   const bf16_t* vrow = base + (long)(k0 + (lane & 15)) * ldq + 2 * C + h * D;
@@ -278,7 +280,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dkv_kernel(AttnArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + (lane >> 4) * 4 + r;
         const float pr = key < klen ? exp2f(p[t][r] * c2 - ls) : 0.f;
-        const float mul = a.drop.on ? drop_mul(a.drop, (bh * S + q0 + qi) * S + key) : 1.f;
+        const float mul = a.drop.on ? drop_mul(a.drop, bhss + (uint32_t)((q0 + qi) * S + key)) : 1.f;
         pd[t][r] = pr * mul;
         ds[t][r] = pr * (dp[t][r] * mul - dvq);
       }
@@ -329,6 +331,7 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   int klen = a.key_len ? a.key_len[b] : S;
   klen = klen < 1 ? 1 : (klen > S ? S : klen);
   const long bh = (long)b * H + h;
+  const uint64_t bhss = (uint64_t)bh * S * S;  // dropout index of element (q, key): bhss + q*S + key
   const bf16_t* base = a.qkv + (long)b * S * ldq;
   const bf16_t* qrow = base + (long)(q0 + (lane & 15)) * ldq + h * D;
   const bf16_t* grow = a.dout + ((long)b * S + q0 + (lane & 15)) * C + h * D;
@@ -368,9 +371,9 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
       const int key = k0 + t * 16 + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const long q = q0 + (lane >> 4) * 4 + r;
+        const int q = q0 + (lane >> 4) * 4 + r;
         const float pr = key < klen ? exp2f(s[t][r] * c2 - ls[r]) : 0.f;
-        const float mul = a.drop.on ? drop_mul(a.drop, (bh * S + q) * S + key) : 1.f;
+        const float mul = a.drop.on ? drop_mul(a.drop, bhss + (uint32_t)(q * S + key)) : 1.f;
         s[t][r] = pr * (dp[t][r] * mul - dvq[r]);
       }
     }

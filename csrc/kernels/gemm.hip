@@ -170,8 +170,13 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
   }
   // K-contiguous operands only (forward GEMMs): the N-contiguous loaders' extra registers
   // make the batched epilogue spill (448-480 B/lane of scratch)
-  if constexpr (EPI == EPI_BF16_ST && GA<BM, 1, 256>::KC && GB<BN, 1, 256>::KC) {
-    if (use_glds() && epi_pf()) {
+  // Dense-layer epilogues that read memory (act' source, old C for beta) or run the
+  // activation: 4 rows' loads in flight per trip instead of one (BERT FFN2 dgrad with
+  // GELU': one HBM round trip per staged row otherwise)
+  constexpr bool PLAIN = EPI == EPI_BF16;
+  if constexpr (PLAIN || (EPI == EPI_BF16_ST && GA<BM, 1, 256>::KC && GB<BN, 1, 256>::KC)) {
+    const bool want = !PLAIN || p.dact_src || p.act || p.beta != 0.f;
+    if (want && use_glds() && epi_pf()) {
       dense_gemm_glds_pf_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 256, 0, s>>>(p);
       CA_LAUNCH_CHECK();
       return 0;
