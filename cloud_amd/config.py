@@ -67,8 +67,13 @@ _VARS = [
         "with 4 x 1 waves; 0 = 128 x 64 with 2 x 2 waves", "ops"),
     Var("CLOUD_AMD_BN_GROUPS_MAX", int, 512, "BatchNorm statistics: most groups of the first-level reduction of the "
         "per-tile partial rows (1..512; ~64 rows per group)", "ops"),
-    Var("CLOUD_AMD_EPI_PF", bool, True, "dense forward GEMMs with the BN-statistics epilogue (ResNet 1x1 convs): "
-        "read 4 staged output rows from LDS before storing any", "ops"),
+    Var("CLOUD_AMD_EPI_PF", bool, True, "GEMM epilogues that read memory or run an activation (BN-statistics "
+        "forward 1x1 convs, BERT bias/GELU/GELU'/beta dense layers): 4 staged output rows in flight per trip", "ops"),
+    Var("CLOUD_AMD_SPLITK_INLAUNCH", bool, False, "split-K weight gradients (dense and conv): 1 = the last-arriving "
+        "split of each tile sums the fp32 slabs inside the GEMM launch (measured slower on BERT/ResNet: "
+        "4,791 vs 6,414 seq/s); default keeps the separate reduce kernel", "ops"),
+    Var("CLOUD_AMD_ATTN_FUSED_BWD", bool, True, "attention at S = 64 / 128: one workgroup per (batch, head) for "
+        "the forward and a single fused backward kernel; 0 keeps the 64-query-block kernels", "ops"),
     Var("CLOUD_AMD_CONV_EPI_PF", bool, True, "implicit-GEMM forward convolutions with the BN-statistics epilogue: "
         "read 2 staged output rows from LDS before storing", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "

@@ -363,11 +363,13 @@ def embed_sum(ids, tts, word, pos, type_, seq_len, pos_offset=0):
 
 
 def embed_bwd(dh, ids, tts, dword, dpos, dtype_, seq_len, n_types, pos_offset=0, pad_id=-1):
-    """Scatter-add (fp32 atomics) into dword, skipping ``pad_id`` rows; dpos/dtype_ reduced."""
+    """Scatter-add into dword (deterministic owner-row kernel; ids outside [0, vocab) and
+    ``pad_id`` get nothing), dpos / dtype_ reduced."""
     ext = _ext.load(required=True)
     M, C = dh.shape
+    V = dword.shape[0] if dword is not None else 0
     ext.embed_bwd(dh.data_ptr(), ids.data_ptr(), _ext.ptr(tts), _ext.ptr(dword), _ext.ptr(dpos), _ext.ptr(dtype_), M,
-                  seq_len, C, n_types, pos_offset, int(pad_id), _st(dh.device))
+                  seq_len, C, n_types, pos_offset, int(pad_id), int(V), _st(dh.device))
 
 
 def attn_fwd(qkv, B, S, H, key_len=None, p_drop=0.0, seed=0, scale=None):

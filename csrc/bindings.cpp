@@ -79,7 +79,7 @@ int ca_colsum(const bf16_t*, long, int, long, float*, int, float*, hipStream_t);
 int ca_embed_sum(const int32_t*, const int32_t*, const float*, const float*, const float*, bf16_t*, long, int, int, int,
                  hipStream_t);
 int ca_embed_bwd(const bf16_t*, const int32_t*, const int32_t*, float*, float*, float*, long, int, int, int, int, int,
-                 hipStream_t);
+                 int, hipStream_t);
 int ca_dropout(const bf16_t*, bf16_t*, long, float, uint64_t, hipStream_t);
 int ca_dropout_mask(uint8_t*, long, long, float, uint64_t, hipStream_t);
 int ca_attn_fwd(const bf16_t*, bf16_t*, float*, const int*, int, int, int, float, float, uint64_t, hipStream_t);
@@ -300,9 +300,9 @@ PYBIND11_MODULE(_C, m) {
                        P(const float*, type), P(bf16_t*, h), M, S_, C, po, S(s)), "embed_sum");
   });
   m.def("embed_bwd", [](u64 dh, u64 ids, u64 tts, u64 dw, u64 dp, u64 dt, long M, int S_, int C, int T, int po,
-                        int pad_id, u64 s) {
+                        int pad_id, int V, u64 s) {
     check(ca_embed_bwd(P(const bf16_t*, dh), P(const int32_t*, ids), P(const int32_t*, tts), P(float*, dw),
-                       P(float*, dp), P(float*, dt), M, S_, C, T, po, pad_id, S(s)), "embed_bwd");
+                       P(float*, dp), P(float*, dt), M, S_, C, T, po, pad_id, V, S(s)), "embed_bwd");
   });
   m.def("dropout", [](u64 x, u64 y, long n, float p, u64 seed, u64 s) {
     check(ca_dropout(P(const bf16_t*, x), P(bf16_t*, y), n, p, seed, S(s)), "dropout");

@@ -12,11 +12,11 @@
 // the tests.  The host picks a fresh seed per call (cloud_amd/ops/dropout.py).
 //
 // Cost: every element of an attention-probability matrix and of every BERT hidden
-// state draws one hash per pass (forward and each backward kernel regenerate it), so
-// the hash is sized for the VALU: 3 quarter-rate 32-bit multiplies + 1 full-rate 24-bit
-// one and ~8 single-cycle ops.  The first version (64-bit splitmix64 per element: nine
-// 32-bit multiply pieces plus 64-bit shifts) made the attention kernels and the
-// dropout LayerNorms VALU-bound (docs/performance.md, "BERT step, round 3").
+// state draws one hash per pass (forward and backward regenerate it), so the hash is
+// sized for the VALU: 3 quarter-rate 32-bit multiplies + 1 full-rate 24-bit one and ~8
+// single-cycle ops, against nine 32-bit multiply pieces plus 64-bit shifts for the
+// splitmix64-per-element form it replaced (the attention / LayerNorm kernels were not
+// bound by it: attention forward 24.2 -> 24.0 us, docs/performance.md "BERT step, round 3").
 #pragma once
 #include <stdint.h>
 

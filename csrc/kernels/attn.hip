@@ -402,7 +402,280 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused backward for short sequences (S = 64 or 128, BERT fine-tuning): ONE workgroup per
+// (batch, head) holds the whole head in LDS, so the three-kernel path's prep pass, its
+// second recomputation of P / dP / the dropout hash (dQ kernel) and its per-block reloads
+// of Q / dO / K / V all disappear:
+//   load   Q, dO, K -> LDS; this wave's 16 K / V rows -> A fragments; Dv = rowsum(dO * O)
+//   A      (wave w = keys 16w..16w+15, all S queries)
+//          S^T = K Q^T, dP^T = V dO^T  ->  P, dS = P (dP * mask - Dv)  -> LDS [q][key]
+//          dV = P^T dO, dK = dS^T Q    (P^T / dS^T as transposed reads of the [q][key] arrays)
+//   B      (wave w = queries 16w..16w+15)  dQ = dS K   (dS rows straight from LDS)
+// Every P / dS element is computed (and its dropout bit hashed) once instead of twice.
+// LDS: 3 x [S][72] + 2 x [S][S + 8] bf16 = 124 KB at S = 128 (one 8-wave block per CU).
+template <int LD>
+__device__ __forceinline__ bf16x8 frag_kc(const short* lds, int r0, int k0, int lane) {
+  s8v v = *reinterpret_cast<const s8v*>(lds + (r0 + (lane & 15)) * LD + k0 + 8 * (lane >> 4));
+  return __builtin_bit_cast(bf16x8, v);
+}
+// element (r, k) at lds[k * LD + r] (r contiguous): the transposed read
+template <int LD>
+__device__ __forceinline__ bf16x8 frag_nc(const short* lds, int r0, int k0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const short* b0 = lds + (k0 + 8 * g + q) * LD + r0 + 4 * p;
+  s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b0));
+  s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b0 + 4 * LD));
+  s8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// C-layout 16 x 64 fp32 (4 column tiles, lane l: row 4 (l >> 4) + r, column 16 t + (l & 15))
+// -> bf16 [16][LDT] slab, then 16-B row stores to dst rows (pitch ld)
+__device__ __forceinline__ void stage_store(short* slab, const f4v (&v)[4], bf16_t* dst, long ld, int lane) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) slab[((lane >> 4) * 4 + r) * LDT + t * 16 + (lane & 15)] = (short)f2bf(v[t][r]);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = lane + i * 64;
+    const int r = c >> 3, col = (c & 7) * 8;
+    *reinterpret_cast<s8v*>(dst + (long)r * ld + col) = *reinterpret_cast<const s8v*>(slab + r * LDT + col);
+  }
+}
+
+template <int SQ>
+__global__ void __launch_bounds__(SQ * 4) attn_bwd_fused_kernel(AttnArgs a) {
+  constexpr int NW = SQ / 16, NT = NW * 64, TQ = SQ / 16, PL = SQ + 8;
+  __shared__ __attribute__((aligned(16))) short Qs[SQ * LDT];
+  __shared__ __attribute__((aligned(16))) short Gs[SQ * LDT];  // dO
+  __shared__ __attribute__((aligned(16))) short Ks[SQ * LDT];
+  __shared__ __attribute__((aligned(16))) short Ps[SQ * PL];   // P  [q][key]
+  __shared__ __attribute__((aligned(16))) short Ds[SQ * PL];   // dS [q][key]
+  __shared__ float lse_s[SQ], dv_s[SQ];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bh = blockIdx.x;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int H = a.H, C = H * D;
+  const long ldq = 3L * C;
+  int klen = a.key_len ? a.key_len[b] : SQ;
+  klen = klen < 1 ? 1 : (klen > SQ ? SQ : klen);
+  const uint64_t bhss = (uint64_t)bh * SQ * SQ;
+  const bf16_t* base = a.qkv + (long)b * SQ * ldq;
+  const bf16_t* gbase = a.dout + (long)b * SQ * C + h * D;
+  const bf16_t* obase = a.out + (long)b * SQ * C + h * D;
+
+  // ---- loads: Q / dO / K tiles, Dv = rowsum(dO * O) from the same dO chunks
+#pragma unroll
+  for (int i = 0; i < SQ * 8 / NT; ++i) {
+    const int c = tid + i * NT;
+    const int r = c >> 3, col = (c & 7) * 8;
+    const s8v qv = *reinterpret_cast<const s8v*>(base + (long)r * ldq + h * D + col);
+    const s8v kv = *reinterpret_cast<const s8v*>(base + (long)r * ldq + C + h * D + col);
+    const us8 gv = *reinterpret_cast<const us8*>(gbase + (long)r * C + col);
+    const us8 ov = *reinterpret_cast<const us8*>(obase + (long)r * C + col);
+    *reinterpret_cast<s8v*>(Qs + r * LDT + col) = qv;
+    *reinterpret_cast<s8v*>(Ks + r * LDT + col) = kv;
+    *reinterpret_cast<us8*>(Gs + r * LDT + col) = gv;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += bf2f(gv[j]) * bf2f(ov[j]);
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if ((c & 7) == 0) dv_s[r] = s;
+  }
+  if (tid < SQ) lse_s[tid] = a.lse[(long)bh * SQ + tid];
+  const int k0 = wave * 16;
+  const bf16_t* krow = base + (long)(k0 + (lane & 15)) * ldq + C + h * D;
+  const bf16_t* vrow = krow + C;
+  const bf16x8 kf0 = gfrag(krow, 0, lane), kf1 = gfrag(krow, 1, lane);
+  const bf16x8 vf0 = gfrag(vrow, 0, lane), vf1 = gfrag(vrow, 1, lane);
+  const float c2 = a.scale * LOG2E;
+  __syncthreads();
+
+  // ---- phase A: this wave's 16 keys against all queries
+  {
+    f4v p[TQ], dp[TQ];
+#pragma unroll
+    for (int t = 0; t < TQ; ++t) {
+      p[t] = f4v{0.f, 0.f, 0.f, 0.f};
+      p[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf0, frag_kc<LDT>(Qs, t * 16, 0, lane), p[t], 0, 0, 0);
+      p[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf1, frag_kc<LDT>(Qs, t * 16, 32, lane), p[t], 0, 0, 0);
+      dp[t] = f4v{0.f, 0.f, 0.f, 0.f};
+      dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf0, frag_kc<LDT>(Gs, t * 16, 0, lane), dp[t], 0, 0, 0);
+      dp[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf1, frag_kc<LDT>(Gs, t * 16, 32, lane), dp[t], 0, 0, 0);
+    }
+    // p[t][r] = S^T[key = k0 + 4 (l >> 4) + r][q = 16 t + (l & 15)]
+    const int kr = k0 + (lane >> 4) * 4;
+#pragma unroll
+    for (int t = 0; t < TQ; ++t) {
+      const int qi = t * 16 + (lane & 15);
+      const float ls = lse_s[qi], dvq = dv_s[qi];
+      s4v pk, dk4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kr + r;
+        const float pr = key < klen ? exp2f(p[t][r] * c2 - ls) : 0.f;
+        const float mul = a.drop.on ? drop_mul(a.drop, bhss + (uint32_t)(qi * SQ + key)) : 1.f;
+        pk[r] = (short)f2bf(pr * mul);
+        dk4[r] = (short)f2bf(pr * (dp[t][r] * mul - dvq));
+      }
+      *reinterpret_cast<s4v*>(Ps + qi * PL + kr) = pk;
+      *reinterpret_cast<s4v*>(Ds + qi * PL + kr) = dk4;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  f4v dk[4], dv[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) dk[t] = dv[t] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < SQ / 32; ++kk) {
+    const bf16x8 pa = frag_nc<PL>(Ps, k0, kk * 32, lane);  // P^T: row = key, k = query
+    const bf16x8 da = frag_nc<PL>(Ds, k0, kk * 32, lane);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      dv[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, frag_nc<LDT>(Gs, t * 16, kk * 32, lane), dv[t], 0, 0, 0);
+      dk[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, frag_nc<LDT>(Qs, t * 16, kk * 32, lane), dk[t], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dk[t][r] *= a.scale;
+  __syncthreads();  // every wave's dS columns written; P / dO no longer read
+
+  // dK, dV out through this wave's slabs in the (now free) P and dO regions
+  bf16_t* drow = a.dqkv + ((long)b * SQ + k0) * ldq + h * D;
+  stage_store(Ps + wave * 16 * LDT, dk, drow + C, ldq, lane);
+  stage_store(Gs + wave * 16 * LDT, dv, drow + 2 * C, ldq, lane);
+
+  // ---- phase B: dQ for this wave's 16 queries
+  const int q0 = wave * 16;
+  f4v dq[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) dq[t] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int nkk = (klen + 31) / 32;
+  for (int kk = 0; kk < nkk; ++kk) {
+    const bf16x8 da = frag_kc<PL>(Ds, q0, kk * 32, lane);  // dS: row = query, k = key
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      dq[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, frag_nc<LDT>(Ks, t * 16, kk * 32, lane), dq[t], 0, 0, 0);
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dq[t][r] *= a.scale;
+  stage_store(Qs + wave * 16 * LDT, dq, a.dqkv + ((long)b * SQ + q0) * ldq + h * D, ldq, lane);
+}
+
+// Forward for S = 64 / 128: one workgroup per (batch, head), all S keys' K and V issued
+// to LDS up front (one memory round trip instead of one per 64-key block), then each
+// wave's 16 query rows take an exact (not online) softmax over the whole key row.
+// LDS: 2 x [S][72] + per-wave P slabs [16][S + 8] = 72 KB at S = 128 (two blocks per CU).
+template <int SQ>
+__global__ void __launch_bounds__(SQ * 4) attn_fwd_short_kernel(AttnArgs a) {
+  constexpr int NW = SQ / 16, NT = NW * 64, TK = SQ / 16, PL = SQ + 8;
+  __shared__ __attribute__((aligned(16))) short Ks[SQ * LDT];
+  __shared__ __attribute__((aligned(16))) short Vs[SQ * LDT];
+  __shared__ __attribute__((aligned(16))) short Ps[NW][16 * PL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int bh = blockIdx.x;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int C = a.H * D;
+  const long ldq = 3L * C;
+  int klen = a.key_len ? a.key_len[b] : SQ;
+  klen = klen < 1 ? 1 : (klen > SQ ? SQ : klen);
+  const uint64_t bhss = (uint64_t)bh * SQ * SQ;
+  const bf16_t* base = a.qkv + (long)b * SQ * ldq;
+#pragma unroll
+  for (int i = 0; i < SQ * 8 / NT; ++i) {
+    const int c = tid + i * NT;
+    const int r = c >> 3, col = (c & 7) * 8;
+    const s8v kv = *reinterpret_cast<const s8v*>(base + (long)r * ldq + C + h * D + col);
+    const s8v vv = *reinterpret_cast<const s8v*>(base + (long)r * ldq + 2 * C + h * D + col);
+    *reinterpret_cast<s8v*>(Ks + r * LDT + col) = kv;
+    *reinterpret_cast<s8v*>(Vs + r * LDT + col) = vv;
+  }
+  const int q0 = wave * 16;
+  const bf16_t* qrow = base + (long)(q0 + (lane & 15)) * ldq + h * D;
+  const bf16x8 qf0 = gfrag(qrow, 0, lane), qf1 = gfrag(qrow, 1, lane);
+  const float c2 = a.scale * LOG2E;
+  __syncthreads();
+  // s[t][r] = S[q = q0 + 4 (l >> 4) + r][key = 16 t + (l & 15)]
+  f4v s[TK];
+#pragma unroll
+  for (int t = 0; t < TK; ++t) {
+    s[t] = f4v{0.f, 0.f, 0.f, 0.f};
+    s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf0, frag_kc<LDT>(Ks, t * 16, 0, lane), s[t], 0, 0, 0);
+    s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf1, frag_kc<LDT>(Ks, t * 16, 32, lane), s[t], 0, 0, 0);
+  }
+  float m[4], l[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < TK; ++t) {
+      const int key = t * 16 + (lane & 15);
+      const float v = key < klen ? s[t][r] * c2 : -INFINITY;
+      s[t][r] = v;
+      mx = fmaxf(mx, v);
+    }
+    m[r] = grp16_max(mx);
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < TK; ++t) {
+      const float p = exp2f(s[t][r] - m[r]);
+      ls += p;
+      s[t][r] = p;
+    }
+    l[r] = grp16_sum(ls);
+  }
+  short* slab = Ps[wave];
+#pragma unroll
+  for (int t = 0; t < TK; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + (lane >> 4) * 4 + r;
+      const int key = t * 16 + (lane & 15);
+      const float mul = a.drop.on ? drop_mul(a.drop, bhss + (uint32_t)(q * SQ + key)) : 1.f;
+      slab[((lane >> 4) * 4 + r) * PL + key] = (short)f2bf(s[t][r] * mul);
+    }
+  __builtin_amdgcn_wave_barrier();
+  f4v o[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) o[t] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < SQ / 32; ++kk) {
+    const bf16x8 pf = frag_kc<PL>(slab, 0, kk * 32, lane);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, frag_nc<LDT>(Vs, t * 16, kk * 32, lane), o[t], 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float inv = 1.f / l[r];
+    if ((lane & 15) == 0) a.lse[(long)bh * SQ + q0 + (lane >> 4) * 4 + r] = m[r] + log2f(l[r]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[t][r] *= inv;
+  }
+  __builtin_amdgcn_wave_barrier();
+  stage_store(slab, o, a.ctx + ((long)b * SQ + q0) * C + h * D, C, lane);
+}
+
 bool shape_ok(int S, int H) { return S > 0 && S % 64 == 0 && H > 0; }
+
+// CLOUD_AMD_ATTN_FUSED_BWD=0 keeps the three-kernel backward at S <= 128 (A/B runs)
+bool fused_bwd_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_ATTN_FUSED_BWD");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
+}
 
 }  // namespace
 
@@ -415,6 +688,12 @@ int ca_attn_fwd(const bf16_t* qkv, bf16_t* ctx, float* lse, const int* key_len, 
   AttnArgs a{};
   a.qkv = qkv; a.ctx = ctx; a.lse = lse; a.key_len = key_len;
   a.B = B; a.S = S; a.H = H; a.scale = scale; a.drop = make_drop(p_drop, seed);
+  if ((S == 64 || S == 128) && fused_bwd_enabled()) {
+    if (S == 128) attn_fwd_short_kernel<128><<<B * H, 512, 0, s>>>(a);
+    else attn_fwd_short_kernel<64><<<B * H, 256, 0, s>>>(a);
+    CA_LAUNCH_CHECK();
+    return 0;
+  }
   attn_fwd_kernel<<<dim3(S / QB, H, B), 256, 0, s>>>(a);
   CA_LAUNCH_CHECK();
   return 0;
@@ -428,6 +707,12 @@ int ca_attn_bwd(const bf16_t* qkv, const bf16_t* out, const bf16_t* dout, const 
   AttnArgs a{};
   a.qkv = qkv; a.out = out; a.dout = dout; a.lse = const_cast<float*>(lse); a.dvec = dvec; a.dqkv = dqkv;
   a.key_len = key_len; a.B = B; a.S = S; a.H = H; a.scale = scale; a.drop = make_drop(p_drop, seed);
+  if ((S == 64 || S == 128) && fused_bwd_enabled()) {
+    if (S == 128) attn_bwd_fused_kernel<128><<<B * H, 512, 0, s>>>(a);
+    else attn_bwd_fused_kernel<64><<<B * H, 256, 0, s>>>(a);
+    CA_LAUNCH_CHECK();
+    return 0;
+  }
   const long rows = (long)B * S * H;
   attn_bwd_prep_kernel<<<ca_cdiv(rows, 32), 256, 0, s>>>(a);
   CA_LAUNCH_CHECK();

@@ -10,7 +10,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_all_env_vars_declared():
     used = set()
     for base in ("cloud_amd", "bench", "examples", "csrc", "scripts"):
-        for dp, _, files in os.walk(os.path.join(ROOT, base)):
+        for dp, dirs, files in os.walk(os.path.join(ROOT, base)):
+            dirs[:] = [d for d in dirs if d != "old"]  # scripts/old: archived runs of removed switches
             for f in files:
                 if f.endswith((".py", ".cpp", ".h", ".hip", ".sh")):
                     used |= set(re.findall(r"CLOUD_AMD_[A-Z0-9_]+", open(os.path.join(dp, f), errors="ignore").read()))

@@ -19,7 +19,8 @@ def rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("B,S,H,p", [(2, 64, 2, 0.0), (3, 128, 2, 0.0), (2, 128, 3, 0.2), (1, 192, 1, 0.0)])
+@pytest.mark.parametrize("B,S,H,p", [(2, 64, 2, 0.0), (3, 128, 2, 0.0), (2, 128, 3, 0.2), (1, 192, 1, 0.0),
+                                     (2, 64, 2, 0.1), (4, 128, 12, 0.1), (2, 256, 2, 0.1)])
 def test_attention_fwd_bwd(B, S, H, p):
     from cloud_amd.ops import raw
 
@@ -128,6 +129,48 @@ def test_colsum_and_wgrad_into():
     assert rel(gw, dy.float().t() @ x.float()) < 1e-2
 
 
+_WGRAD_CHECK = """
+import sys, torch
+sys.path.insert(0, {root!r})
+from cloud_amd.ops import raw
+def rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+torch.manual_seed(11)
+for M, n_out, k_in in [(8192, 768, 3072), (8192, 2304, 768), (4000, 200, 136)]:
+    dy = torch.randn(M, n_out, device="cuda").to(torch.bfloat16)
+    x = torch.randn(M, k_in, device="cuda").to(torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    outs = []
+    for _ in range(3):
+        g = torch.zeros(n_out, k_in, device="cuda")
+        raw.wgrad_into(dy, x, g)
+        outs.append(g)
+    assert rel(outs[0], ref) < 1e-4, rel(outs[0], ref)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    raw.wgrad_into(dy, x, outs[0])  # accumulate
+    assert rel(outs[0], 2 * ref) < 1e-4
+print("WGRAD_OK")
+"""
+
+
+@pytest.mark.parametrize("inlaunch", ["0", "1"])
+def test_wgrad_splitk_deterministic(inlaunch):
+    """Split-K weight gradients, with the separate reduce kernel (default) and with the
+    in-launch combine (CLOUD_AMD_SPLITK_INLAUNCH=1: the last-arriving split of a tile sums
+    all slabs in split order): exact vs fp32, bitwise reproducible whichever split arrives
+    last, and accumulating into fp32 (beta = 1).  The switch is read once per process, so
+    each mode runs in its own interpreter."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CLOUD_AMD_SPLITK_INLAUNCH=inlaunch)
+    r = subprocess.run([sys.executable, "-c", _WGRAD_CHECK.format(root=root)], env=env, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0 and "WGRAD_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_embedding_sum_and_scatter():
     from cloud_amd.ops import raw
 
@@ -138,6 +181,8 @@ def test_embedding_sum_and_scatter():
     typ = torch.randn(T, C, device=DEV)
     ids = torch.randint(0, V, (B, S), device=DEV, dtype=torch.int32)
     ids[:, -5:] = 3
+    ids[:, :9] = 7  # repeated ids: one owner row summing many tokens
+    ids[0, 10] = V - 1
     tts = torch.randint(0, T, (B, S), device=DEV, dtype=torch.int32)
     h = raw.embed_sum(ids, tts, word, pos, typ, S)
     ref = word[ids.long()] + pos[:S][None] + typ[tts.long()]
@@ -152,6 +197,32 @@ def test_embedding_sum_and_scatter():
     rp[:S] += g.sum(0)
     rt.index_add_(0, tts.long().flatten(), g.reshape(-1, C))
     assert rel(dw, rw) < 1e-5 and rel(dp, rp) < 1e-5 and rel(dt, rt) < 1e-5
+    # the word rows have one writer each (owner kernel): bitwise reproducible, accumulating
+    dw2 = torch.zeros_like(word)
+    raw.embed_bwd(dh, ids, tts, dw2, None, None, S, T, pad_id=3)
+    assert torch.equal(dw, dw2)
+    raw.embed_bwd(dh, ids, tts, dw2, None, None, S, T, pad_id=3)
+    assert rel(dw2, 2 * rw) < 1e-5
+
+
+def test_dropout_hash_statistics():
+    """The per-element dropout hash (ca_rng.h): keep rate at BERT's p, bit-identical
+    regeneration from (seed, index), no correlation between neighbours or between seeds."""
+    from cloud_amd.ops import raw
+
+    n = 64 * 12 * 128 * 128  # one BERT-base attention-probability tensor
+    for p in (0.1, 0.5):
+        m = raw.dropout_mask(n, p, 99).float()
+        assert abs(m.mean().item() - (1 - p)) < 1e-3, (p, m.mean().item())
+    m1 = raw.dropout_mask(n, 0.1, 1234)
+    assert torch.equal(m1, raw.dropout_mask(n, 0.1, 1234))  # regeneration
+    a = m1.float() - m1.float().mean()
+    for lag in (1, 64, 128, 128 * 128):
+        c = (a[:-lag] * a[lag:]).mean().item() / a.var().item()
+        assert abs(c) < 5e-3, (lag, c)
+    b = raw.dropout_mask(n, 0.1, 1235).float()
+    c = (a * (b - b.mean())).mean().item() / a.var().item()
+    assert abs(c) < 5e-3, c
 
 
 def test_dropout_kernel_statistics_and_backward():
