@@ -55,6 +55,9 @@ _VARS = [
     Var("CLOUD_AMD_DENSE_WGRAD_BLOCKS", int, 1024, "dense-layer weight gradients (BERT): split-K workgroup target "
         "(1024 with the split-major XCD mapping: 6,210 / 6,231 vs 6,153 / 6,131 seq/s at 512)",
         "ops"),
+    Var("CLOUD_AMD_WGRAD_256", bool, False, "dense-layer weight gradients with >= 256 x 256 outputs: 1 = split-K "
+        "sized to one round of 256 x 256 ring-core blocks instead of ~1024 128 x 128 blocks (measured slower: BERT "
+        "wgrads 1.92 -> 2.75 ms/step, the ring core's N-contiguous loaders)", "ops"),
     Var("CLOUD_AMD_TAPMASK", bool, True, "convolutions: tap-mask / incremental buffer-mode gather loaders; 0 keeps "
         "the general per-chunk decode loaders (A/B runs)", "ops"),
     Var("CLOUD_AMD_SPLIT_XCD", bool, True, "split-K GEMM/conv grids: give each XCD contiguous (split, tile) "

@@ -130,10 +130,14 @@ static double tile_balance(long tiles) {
 // at >= 85 % slot use, or exactly whole rounds, and >= 16 K tiles of 32 per block.  (BERT's
 // M = 8192 GEMMs get 96-384 tiles -- 1.1-1.5 rounds -- and stay on the 128 core, whose 4
 // co-resident blocks per CU absorb the quantisation.)
+// Split-K grids (weight gradients) also take it when the caller sized the splits to ONE
+// nearly full round of 256 x 256 blocks (ops/raw.py wgrad_into: BERT's FFN / QKV weight
+// gradients = 36 x 7 / 27 x 9 blocks).
 static bool use_256(const CoreParams& p, int splits) {
   if (core_kind() == 4) return p.M >= 256 && p.N >= 256;
   if (core_kind() != 3 || p.M < 256 || p.N < 256 || p.k_per_split < 512) return false;
   const long t = (long)((p.M + 255) / 256) * ((p.N + 255) / 256) * splits;
+  if (splits > 1 && t >= 224 && t <= 256) return true;
   return t >= 256 && (tile_balance(t) >= 0.999 || (t >= 512 && tile_balance(t) >= 0.85));
 }
 

@@ -124,17 +124,42 @@ __global__ void __launch_bounds__(LN_BLK) ln_bwd_kernel(const bf16_t* __restrict
     }
   }
   const float invC = 1.f / (float)C;
-  for (long row = (long)blockIdx.x * 4 + wave; row < M; row += (long)gridDim.x * 4) {
+  // software-pipelined over this wave's rows: the next row's dy / h / statistics are in
+  // flight while the current row is reduced and stored
+  const long stride = (long)gridDim.x * 4;
+  long row = (long)blockIdx.x * 4 + wave;
+  float nd[NV][4], nx[NV][4], nmu = 0.f, nrs = 0.f;
+  auto fetch = [&](long r) {
+    if (r >= M) return;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < C4) {
+        load4(dy + r * C + 4 * c4, nd[i]);
+        load4(h + r * C + 4 * c4, nx[i]);
+      }
+    }
+    nmu = mean[r];
+    nrs = rstd[r];
+  };
+  fetch(row);
+  for (; row < M; row += stride) {
     const long base = row * C;
-    const float mu = mean[row], rs = rstd[row];
+    const float mu = nmu, rs = nrs;
     float d[NV][4], xh[NV][4];
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        d[i][j] = nd[i][j];
+        xh[i][j] = nx[i][j];
+      }
+    fetch(row + stride);
     float sa = 0.f, sb = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c4 = lane + 64 * i;
       if (c4 < C4) {
-        load4(dy + base + 4 * c4, d[i]);
-        load4(h + base + 4 * c4, xh[i]);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (dout.on) d[i][j] *= drop_mul(dout, base + 4 * c4 + j);
@@ -264,44 +289,75 @@ __global__ void __launch_bounds__(256) embed_sum_kernel(const int32_t* __restric
   }
 }
 
-// scatter-add backward of embed_sum.  Token rows: fp32 atomics, skipping the
-// padding id (its row gets no gradient, as nn.Embedding(padding_idx) / BERT);
-// the segment table (<= 2 rows in BERT) is pre-reduced per wave first.
+// scatter-add backward of embed_sum for the token-type table (and, when the owner kernel
+// below cannot take them, word rows): fp32 atomics, skipping the padding id (its row gets
+// no gradient, as nn.Embedding(padding_idx) / BERT); the segment table (<= 2 rows in BERT)
+// is pre-reduced per wave first.  Each wave takes EB_RW consecutive rows and issues all
+// their loads before adding (one memory round trip per column group, not one per row:
+// 111 -> a few us at 8192 x 768).
+constexpr int EB_RW = 16;
 __global__ void __launch_bounds__(256) embed_bwd_kernel(const bf16_t* __restrict__ dh, const int32_t* __restrict__ ids,
                                                         const int32_t* __restrict__ tts, float* __restrict__ dword,
                                                         float* __restrict__ dtype, long M, int C, int T, int pad_id) {
   const int lane = threadIdx.x & 63;
   const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const long nw = (long)gridDim.x * 4;
-  for (int c4 = lane; c4 < C / 4; c4 += 64) {
+  // uniform trip count for every lane (the block barriers below); lanes past C / 4 idle
+  for (int cb = 0; cb < C / 4; cb += 64) {
+    const int c4 = cb + lane < C / 4 ? cb + lane : C / 4 - 1;
+    const bool cok = cb + lane < C / 4;
     float t0[4] = {0.f, 0.f, 0.f, 0.f}, t1[4] = {0.f, 0.f, 0.f, 0.f};
-    for (long row = wave; row < M; row += nw) {
-      float g[4];
-      load4(dh + row * C + 4 * c4, g);
-      const int id = ids[row];
-      const int tt = tts ? tts[row] : 0;
-      if (dword && id != pad_id) {
-        float* w = dword + (long)id * C + 4 * c4;
+    for (long row0 = wave * EB_RW; row0 < M; row0 += nw * EB_RW) {
+      float g[EB_RW][4];
+      int tt[EB_RW];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) atomicAdd(w + j, g[j]);
+      for (int u = 0; u < EB_RW; ++u) {
+        const long row = row0 + u < M ? row0 + u : M - 1;
+        load4(dh + row * C + 4 * c4, g[u]);
+        tt[u] = (row0 + u < M && cok) ? (tts ? tts[row] : 0) : -1;
       }
-      if (dtype) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (T <= 2) {
-            if (tt == 0) t0[j] += g[j];
-            else t1[j] += g[j];
-          } else {
-            atomicAdd(dtype + (long)tt * C + 4 * c4 + j, g[j]);
+      for (int u = 0; u < EB_RW; ++u) {
+        if (tt[u] < 0) continue;
+        const long row = row0 + u;
+        if (dword) {
+          const int id = ids[row];
+          if (id != pad_id) {
+            float* w = dword + (long)id * C + 4 * c4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) atomicAdd(w + j, g[u][j]);
+          }
+        }
+        if (dtype) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (T <= 2) {
+              if (tt[u] == 0) t0[j] += g[u][j];
+              else t1[j] += g[u][j];
+            } else {
+              atomicAdd(dtype + (long)tt[u] * C + 4 * c4 + j, g[u][j]);
+            }
           }
         }
       }
     }
     if (dtype && T <= 2) {
+      // the block's 4 waves pre-reduce through LDS: one atomic per (block, column) --
+      // per-wave atomics put 512 adds on each of the 2 x C addresses (97 us at 8192 x 768)
+      __shared__ float tred[4][2][256];
+      const int w = threadIdx.x >> 6;
+      __syncthreads();
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        atomicAdd(dtype + 4 * c4 + j, t0[j]);
-        if (T == 2) atomicAdd(dtype + C + 4 * c4 + j, t1[j]);
+        tred[w][0][lane * 4 + j] = t0[j];
+        tred[w][1][lane * 4 + j] = t1[j];
+      }
+      __syncthreads();
+      for (int k = threadIdx.x; k < 2 * 256; k += 256) {
+        const int t = k >> 8, e = k & 255;  // e = lane * 4 + j
+        if (t >= T || cb + (e >> 2) >= C / 4) continue;
+        const float v = tred[0][t][e] + tred[1][t][e] + tred[2][t][e] + tred[3][t][e];
+        atomicAdd(dtype + (long)t * C + 4 * (cb + (e >> 2)) + (e & 3), v);
       }
     }
   }
@@ -328,18 +384,28 @@ __global__ void __launch_bounds__(256) embed_word_bwd_kernel(const bf16_t* __res
   const int C4 = C / 4;
   for (int i = tid; i < EW_R * C; i += 256) acc[i] = 0.f;
   if (tid < EW_R) touched[tid] = 0;
-  for (long base = 0; base < M; base += EW_CHUNK) {
+  constexpr int PF = 8;  // chunks whose ids are loaded in one round trip (8192 tokens)
+  for (long sbase = 0; sbase < M; sbase += PF * EW_CHUNK) {
+   int idr[PF][EW_CHUNK / 256];
+#pragma unroll
+   for (int c = 0; c < PF; ++c)
+#pragma unroll
+     for (int u = 0; u < EW_CHUNK / 256; ++u) {
+       const long tok = sbase + c * EW_CHUNK + u * 256 + tid;
+       idr[c][u] = tok < M ? ids[tok] : -1;
+     }
+#pragma unroll
+   for (int c = 0; c < PF; ++c) {  // unrolled: idr stays in registers
+    const long base = sbase + c * EW_CHUNK;
+    if (base >= M) break;
     if (tid == 0) n_s = 0;
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < EW_CHUNK / 256; ++u) {
-      const long tok = base + u * 256 + tid;
-      if (tok < M) {
-        const int id = ids[tok];
-        if (id >= v0 && id < v0 + EW_R && id < V && id != pad_id) {
-          const int k = atomicAdd(&n_s, 1);
-          list[k] = (int)(tok - base) | ((id - v0) << 16);
-        }
+      const int id = idr[c][u];
+      if (id >= v0 && id < v0 + EW_R && id < V && id != pad_id) {
+        const int k = atomicAdd(&n_s, 1);
+        list[k] = (u * 256 + tid) | ((id - v0) << 16);
       }
     }
     __syncthreads();
@@ -378,6 +444,7 @@ __global__ void __launch_bounds__(256) embed_word_bwd_kernel(const bf16_t* __res
     }
     for (int i = tid; i < n; i += 256) touched[list[i] >> 16] = 1;
     __syncthreads();
+   }
   }
   __syncthreads();
   for (int r = 0; r < EW_R; ++r) {
@@ -399,11 +466,19 @@ __global__ void __launch_bounds__(256) embed_pos_bwd_kernel(const bf16_t* __rest
   if (i >= (long)S * C4) return;
   const int s = (int)(i / C4), c4 = (int)(i - (long)s * C4);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (long row = s; row < M; row += S) {
-    float g[4];
-    load4(dh + row * C + 4 * c4, g);
+  // 8 batch rows' loads in flight per trip (fixed order: deterministic)
+  for (long row0 = s; row0 < M; row0 += 8L * S) {
+    float g[8][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] += g[j];
+    for (int u = 0; u < 8; ++u) {
+      const long row = row0 + (long)u * S;
+      if (row < M) load4(dh + row * C + 4 * c4, g[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (row0 + (long)u * S < M)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += g[u][j];
   }
   f4* o = reinterpret_cast<f4*>(dpos + (long)(s + pos_offset) * C + 4 * c4);
   f4 v = *o;
@@ -536,7 +611,10 @@ int ca_embed_bwd(const bf16_t* dh, const int32_t* ids, const int32_t* tts, float
     CA_LAUNCH_CHECK();
   }
   if ((dword && !owner) || dtype) {
-    int grid = ca_cdiv(M, 4 * 16);  // each wave walks ~16 rows (segment pre-reduction)
+    // each wave takes EB_RW consecutive rows per trip; type-only: at most 64 blocks (fewer
+    // atomics per column, see the kernel)
+    int grid = ca_cdiv(M, 4 * EB_RW);
+    if (!(dword && !owner) && grid > 64) grid = 64;
     if (grid < 1) grid = 1;
     embed_bwd_kernel<<<grid, 256, 0, s>>>(dh, ids, tts, owner ? nullptr : dword, dtype, M, C, T, pad_id);
     CA_LAUNCH_CHECK();

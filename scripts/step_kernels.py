@@ -25,7 +25,7 @@ def main(d, marker, skip=3):
     cnt = Counter()
     for a, b in steps:
         for r in rows[a:b]:
-            n = r["Kernel_Name"].split("(")[0][:100]
+            n = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:100]
             tot[n] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
             cnt[n] += 1
     ns = len(steps)
