@@ -102,6 +102,9 @@ _VARS = [
     Var("CLOUD_AMD_BUCKET_MB", float, 16.0, "gradient bucket size (MB) of the DP engine", "distributed"),
     Var("CLOUD_AMD_STEM_TAIL", bool, True, "ResNet stem: BN + ReLU + max-pool fused (fwd) and max-pool backward "
         "fused with the BN-backward statistics", "ops"),
+    Var("CLOUD_AMD_GRAD_FIN_BATCH", bool, True, "BERT layer backward: the eight fixed-order gradient "
+        "finalisations (split-K slab sums, LayerNorm / bias column partials) run as ONE launch at the end of the "
+        "layer (csrc/kernels/gradfin.hip); 0 = one launch each", "ops"),
     Var("CLOUD_AMD_LN_BIAS_SUM", bool, True, "BERT: the LayerNorm backward also sums the bias gradient of the "
         "projection that fed it (no separate column-sum pass)", "ops"),
     Var("CLOUD_AMD_TAIL_BUCKET_MB", float, 1.0, "cap on the last gradient bucket (the first layers' gradients, "

@@ -38,8 +38,8 @@ import torch.nn.functional as F
 
 from .. import config
 from ..ops import _ext, raw
-from ..ops.dense import dense
 from ..ops.dropout import next_seed
+from ..runtime import side_stream
 from ..runtime.side_stream import SideWork
 
 
@@ -208,93 +208,103 @@ class _LayerFn(torch.autograd.Function):
 
         dy2 = dy2.contiguous()
         # weight / bias gradients (compute-bound GEMMs + column sums) go to the side
-        # stream; the memory-bound LN / attention / dgrad chain stays on the main stream
+        # stream; the memory-bound LN / attention / dgrad chain stays on the main stream.
+        # Their fixed-order finalisations (split-K slab sums, column-partial sums) are
+        # batched into one launch at the end of the layer (raw.deferred_finalize), and
+        # the DDP bucket notifications follow it.
         side = SideWork(dy2.device)
-        deferred = []
+        main_ready, side_ready = [], []
 
         fuse_bias = config.get("CLOUD_AMD_LN_BIAS_SUM")
 
         def param_grads(dy, inp, w, b, bias_done=False):
             bias_done = bias_done and fuse_bias
+
             def fn():
                 if not bias_done:
                     raw.colsum_into(dy, G(b))
                 raw.wgrad_into(dy, inp, G(w))
             side.run(fn, dy, inp)
-            if side.enabled:
-                deferred.extend((w,) if bias_done else (b, w))
-            else:
-                if not bias_done:
-                    _notify(b)
-                _notify(w)
+            (side_ready if side.enabled else main_ready).extend((w,) if bias_done else (b, w))
 
-        # LN2 (+ residual y1, + dropout on the FFN output); the same pass sums the
-        # gradient it hands to the FFN output projection into b2's gradient
-        dh2, do = raw.ln_bwd(dy2, h2, m2, r2, layer.ln2_w, G(layer.ln2_w), G(layer.ln2_b), p_in=p_hidden, seed_in=s2,
-                             want_dx=True, dsum=G(layer.b2) if fuse_bias else None)
-        _notify(layer.ln2_b), _notify(layer.ln2_w)
-        if fuse_bias:
-            _notify(layer.b2)
-        param_grads(do, f, layer.w2, layer.b2, bias_done=True)
-        dpre = raw.gemm(do, layer.w2, layout=raw.NN, act=cfg.hidden_act, dact_src=pre)
-        del do, f
-        param_grads(dpre, y1, layer.w1, layer.b1)
-        raw.gemm(dpre, layer.w1, layout=raw.NN, out=dh2, beta=1.0)  # dy1 = dh2 + dpre W1
-        del dpre
-        dy1 = dh2
-        # LN1 (+ residual x, + dropout on the attention output projection)
-        dh1, da = raw.ln_bwd(dy1, h1, m1, r1, layer.ln1_w, G(layer.ln1_w), G(layer.ln1_b), p_in=p_hidden, seed_in=s1,
-                             want_dx=True, dsum=G(layer.bo) if fuse_bias else None)
-        _notify(layer.ln1_b), _notify(layer.ln1_w)
-        if fuse_bias:
-            _notify(layer.bo)
-        del dy1
-        param_grads(da, ctx_, layer.wo, layer.bo, bias_done=True)
-        dctx = raw.gemm(da, layer.wo, layout=raw.NN)
-        del da
-        dqkv = raw.attn_bwd(qkv, ctx_, dctx, lse, B, S, H, key_len, p_attn, sa,
-                            scale=1.0 / math.sqrt(cfg.hidden_size // H))
-        del dctx
-        param_grads(dqkv, x, layer.wqkv, layer.bqkv)
-        raw.gemm(dqkv, layer.wqkv, layout=raw.NN, out=dh1, beta=1.0)  # dx = dh1 + dqkv Wqkv
-        side.join()
-        for p in deferred:
+        with raw.deferred_finalize(enabled=config.get("CLOUD_AMD_GRAD_FIN_BATCH")):
+            # LN2 (+ residual y1, + dropout on the FFN output); the same pass sums the
+            # gradient it hands to the FFN output projection into b2's gradient
+            dh2, do = raw.ln_bwd(dy2, h2, m2, r2, layer.ln2_w, G(layer.ln2_w), G(layer.ln2_b), p_in=p_hidden,
+                                 seed_in=s2, want_dx=True, dsum=G(layer.b2) if fuse_bias else None)
+            main_ready.extend((layer.ln2_b, layer.ln2_w))
+            if fuse_bias:
+                main_ready.append(layer.b2)
+            param_grads(do, f, layer.w2, layer.b2, bias_done=True)
+            dpre = raw.gemm(do, layer.w2, layout=raw.NN, act=cfg.hidden_act, dact_src=pre)
+            del do, f
+            param_grads(dpre, y1, layer.w1, layer.b1)
+            raw.gemm(dpre, layer.w1, layout=raw.NN, out=dh2, beta=1.0)  # dy1 = dh2 + dpre W1
+            del dpre
+            dy1 = dh2
+            # LN1 (+ residual x, + dropout on the attention output projection)
+            dh1, da = raw.ln_bwd(dy1, h1, m1, r1, layer.ln1_w, G(layer.ln1_w), G(layer.ln1_b), p_in=p_hidden,
+                                 seed_in=s1, want_dx=True, dsum=G(layer.bo) if fuse_bias else None)
+            main_ready.extend((layer.ln1_b, layer.ln1_w))
+            if fuse_bias:
+                main_ready.append(layer.bo)
+            del dy1
+            param_grads(da, ctx_, layer.wo, layer.bo, bias_done=True)
+            dctx = raw.gemm(da, layer.wo, layout=raw.NN)
+            del da
+            dqkv = raw.attn_bwd(qkv, ctx_, dctx, lse, B, S, H, key_len, p_attn, sa,
+                                scale=1.0 / math.sqrt(cfg.hidden_size // H))
+            del dctx
+            param_grads(dqkv, x, layer.wqkv, layer.bqkv)
+            raw.gemm(dqkv, layer.wqkv, layout=raw.NN, out=dh1, beta=1.0)  # dx = dh1 + dqkv Wqkv
+        # (the batch flushed per stream on exit: LN finalisations on the main stream, the
+        # weight-gradient / bias ones on the side stream behind their GEMMs)
+        for p in main_ready:
             _notify(p)
+        # the side stream's tail overlaps the next layer: its join + DDP notifications are
+        # deferred one layer (side_stream.defer / settle; a backward callback settles all)
+        side_stream.defer(side.detach(), side_ready, _notify)
+        side_stream.settle(keep_last=1)
         return (dh1, None, None, None, None, None, None) + tuple(owned)
 
 
-class _PoolerFn(torch.autograd.Function):
-    """pooled = tanh(h[:, 0] Wp^T + bp), reading the [CLS] rows in place (row stride S*C)."""
+class _HeadFn(torch.autograd.Function):
+    """logits = drop(tanh(h[:, 0] Wp^T + bp)) Wc^T + bc: the pooler GEMM reads the [CLS]
+    rows in place (row stride S*C) with the tanh in its epilogue; dropout + the classifier
+    (fp32 weights, fp32 logits) are one kernel forward and one backward (head.hip), the
+    pooler's weight / bias gradient finalisations one batched launch."""
 
     @staticmethod
-    def forward(ctx, h, wp, bp, B, S):
+    def forward(ctx, h, wp, bp, wc, bc, B, S, p):
         C = h.shape[-1]
         cls = h.view(B, S * C)[:, :C]
-        pre = torch.empty((B, C), dtype=torch.bfloat16, device=h.device)
-        pooled = raw.gemm(cls, wp, bias=bp, act="tanh", preact=pre)
-        ctx.save_for_backward(h, pre, pooled)
-        ctx.B, ctx.S = B, S
-        ctx.wp, ctx.bp = wp, bp
-        return pooled
+        pooled = raw.gemm(cls, wp, bias=bp, act="tanh")
+        seed = next_seed() if p > 0 else 0
+        logits = raw.cls_head_fwd(pooled, wc, bc, p, seed)
+        ctx.save_for_backward(h, pooled)
+        ctx.B, ctx.S, ctx.p, ctx.seed = B, S, p, seed
+        ctx.params = (wp, bp, wc, bc)
+        return logits
 
     @staticmethod
-    def backward(ctx, dpooled):
-        h, pre, pooled = ctx.saved_tensors
+    def backward(ctx, dlogits):
+        h, pooled = ctx.saved_tensors
         B, S = ctx.B, ctx.S
         C = h.shape[-1]
-        wp, bp = ctx.wp, ctx.bp
-        y = pooled.float()
-        dpre = (dpooled.float() * (1.0 - y * y)).to(torch.bfloat16).contiguous()
+        wp, bp, wc, bc = ctx.params
+        sinks = [_grad_out(t) for t in (wp, bp, wc, bc)]
+        (gw, _), (gb, _), (gwc, _), (gbc, _) = sinks
+        dpre = raw.cls_head_bwd(dlogits, pooled, wc, gwc, gbc, ctx.p, ctx.seed)
         cls = h.view(B, S * C)[:, :C]
-        gw, own_w = _grad_out(wp)
-        gb, own_b = _grad_out(bp)
-        raw.wgrad_into(dpre, cls, gw)
-        raw.colsum_into(dpre, gb)
-        _notify(bp), _notify(wp)
+        with raw.deferred_finalize(enabled=config.get("CLOUD_AMD_GRAD_FIN_BATCH")):
+            raw.wgrad_into(dpre, cls, gw)
+            raw.colsum_into(dpre, gb)
+        for t in (bc, wc, bp, wp):
+            _notify(t)
         dh = torch.zeros_like(h)
         dcls = dh.view(B, S * C)[:, :C]
         raw.gemm(dpre, wp, layout=raw.NN, out=dcls)
-        return dh, (gw if own_w else None), (gb if own_b else None), None, None
+        return (dh,) + tuple(g if own else None for g, own in sinks) + (None, None, None)
 
 
 class BertForSequenceClassification(nn.Module):
@@ -341,11 +351,10 @@ class BertForSequenceClassification(nn.Module):
         h = _EmbedFn.apply(ids, tts, e, ph, e.word, e.pos, e.token_type, e.ln_w, e.ln_b)
         for layer in self.layers:
             h = _LayerFn.apply(h, key_len, layer, B, S, ph, pa, *layer.param_list())
-        pooled = _PoolerFn.apply(h, self.pool_w, self.pool_b, B, S)
-        pooled = F.dropout(pooled, ph, train)
-        # classifier on the native dense kernel (num_labels padded to the tile width); the
-        # fp32 weight is rounded to bf16 per step and its gradient flows back through the cast
-        return dense(pooled, self.cls_w.to(torch.bfloat16), self.cls_b).float()
+        if self.cls_w.shape[0] <= _ext.load(required=True).cls_head_max_labels():
+            return _HeadFn.apply(h, self.pool_w, self.pool_b, self.cls_w, self.cls_b, B, S, ph)
+        pooled = torch.tanh(F.linear(h.view(B, S, -1)[:, 0].float(), self.pool_w.float(), self.pool_b))
+        return F.linear(F.dropout(pooled, ph, train), self.cls_w, self.cls_b)
 
     def _torch_forward(self, input_ids, token_type_ids=None, attention_mask=None):
         """Plain PyTorch (fp32 math) -- CPU path and numerics reference."""

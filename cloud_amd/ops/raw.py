@@ -289,6 +289,79 @@ def gemm(a, w, bias=None, act=None, preact=None, out=None, beta=0.0, layout=NT, 
     return out
 
 
+class GradFinalizeBatch:
+    """Deferred gradient finalisation (csrc/kernels/gradfin.hip): while active (see
+    ``deferred_finalize``), ``wgrad_into`` / ``colsum_into`` / ``ln_bwd`` launch only their
+    partial-producing kernels and queue the fixed-order reductions here; ``flush`` runs them
+    all in one launch (per 8 jobs) on the current stream.  Results are bitwise those of the
+    immediate path.  Workspaces stay referenced until the flush and are recorded on the
+    flushing stream (side-stream allocations must not be reused before it runs)."""
+
+    def __init__(self):
+        self.groups = {}  # issuing stream -> (stream, jobs, betas, keep)
+
+    def _group(self, t):
+        st = torch.cuda.current_stream(t.device) if t.device.type == "cuda" else None
+        key = None if st is None else st.cuda_stream
+        if key not in self.groups:
+            self.groups[key] = (st, [], [], [])
+        return self.groups[key]
+
+    def add_splitk(self, ws, splits, n, out, beta):
+        _, jobs, betas, keep = self._group(ws)
+        jobs += [0, ws.data_ptr(), splits, n, n, out.data_ptr(), 0, 0, int(out.dtype == torch.bfloat16), 0, 0, 0]
+        betas.append(float(beta))
+        keep.append(ws)
+
+    def add_cols(self, part, nparts, stride, n, out0, out1=None, out2=None, accumulate=True):
+        _, jobs, betas, keep = self._group(part)
+        jobs += [1, part.data_ptr(), nparts, stride, n, _ext.ptr(out0), _ext.ptr(out1), _ext.ptr(out2), 0,
+                 int(accumulate), 0, 0]
+        betas.append(0.0)
+        keep.append(part)
+
+    def flush(self):
+        """One launch per issuing stream, on that stream (a job runs after the kernel that
+        produced its partials, and its workspace was allocated from that stream's pool)."""
+        ext = _ext.load(required=True)
+        for st, jobs, betas, keep in self.groups.values():
+            if not betas:
+                continue
+            if st is None:
+                ext.grad_finalize_multi(jobs, betas, 0)
+            else:
+                with torch.cuda.stream(st):
+                    ext.grad_finalize_multi(jobs, betas, st.cuda_stream)
+        self.groups = {}
+
+
+_FIN_BATCH = None
+
+
+class deferred_finalize:
+    """``with raw.deferred_finalize() as b: ...; b.flush()`` -- batch the gradient
+    finalisations issued inside (nesting keeps the outer batch)."""
+
+    def __init__(self, enabled=True):
+        self.enabled = enabled
+        self.batch = None
+        self.prev = None
+
+    def __enter__(self):
+        global _FIN_BATCH
+        self.prev = _FIN_BATCH
+        if self.enabled:
+            self.batch = _FIN_BATCH = GradFinalizeBatch() if self.prev is None else self.prev
+        return self.batch
+
+    def __exit__(self, *exc):
+        global _FIN_BATCH
+        if self.enabled and self.prev is None and self.batch is not None:
+            self.batch.flush()
+        _FIN_BATCH = self.prev
+        return False
+
+
 def wgrad_into(dy, x, out, beta=1.0):
     """out[N_out, K_in] (+)= dy[M, N_out]^T @ x[M, K_in] (split-K over M), bf16 or fp32 out."""
     global _DENSE_WGRAD_BLOCKS, _WGRAD_256
@@ -312,9 +385,12 @@ def wgrad_into(dy, x, out, beta=1.0):
         splits = ext.gemm_splitk_effective(M, wgrad_splits(n_out, k_in, M, target_blocks=_DENSE_WGRAD_BLOCKS,
                                                            min_k=1024))
     ws = torch.empty(splits * n_out * k_in, dtype=torch.float32, device=dy.device)
+    fb = _FIN_BATCH
     ext.gemm_splitk(TN, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
-                    int(out.dtype == torch.bfloat16), float(beta), n_out, k_in, M, splits, ws.data_ptr(),
-                    _st(dy.device))
+                    -1 if fb is not None else int(out.dtype == torch.bfloat16), float(beta), n_out, k_in, M, splits,
+                    ws.data_ptr(), _st(dy.device))
+    if fb is not None:
+        fb.add_splitk(ws, splits, n_out * k_in, out, beta)
     _log("dense_wgrad", n_out, k_in, M, _nb(dy, x, out) + (2 * _nb(ws) if splits > 1 else 0), splits=splits)
     return out
 
@@ -324,7 +400,12 @@ def colsum_into(x, out, accumulate=True):
     ext = _ext.load(required=True)
     M, N = x.shape
     ws = torch.empty(ext.colsum_workspace_floats(M, N), dtype=torch.float32, device=x.device)
-    ext.colsum(x.data_ptr(), M, N, x.stride(0), out.data_ptr(), int(accumulate), ws.data_ptr(), _st(x.device))
+    fb = _FIN_BATCH
+    ext.colsum(x.data_ptr(), M, N, x.stride(0), out.data_ptr(), -1 if fb is not None else int(accumulate),
+               ws.data_ptr(), _st(x.device))
+    if fb is not None:
+        ry = min(max((M + 63) // 64, 1), 256)  # = ca_colsum's partial rows
+        fb.add_cols(ws, ry, N, N, out, accumulate=accumulate)
     return out
 
 
@@ -356,11 +437,40 @@ def ln_bwd(dy, h, mean, rstd, gamma, dgamma=None, dbeta=None, p_in=0.0, seed_in=
     M = dy.numel() // C
     dh = torch.empty_like(dy)
     dx = torch.empty_like(dy) if want_dx else None
-    ws = torch.empty(ext.ln_workspace_floats(M, C), dtype=torch.float32, device=dy.device)
+    nws = ext.ln_workspace_floats(M, C)
+    ws = torch.empty(nws, dtype=torch.float32, device=dy.device)
+    fb = _FIN_BATCH if (dgamma is not None or dbeta is not None or dsum is not None) else None
     ext.ln_bwd(dy.data_ptr(), h.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(), dh.data_ptr(),
-               _ext.ptr(dx), _ext.ptr(dgamma), _ext.ptr(dbeta), int(accumulate), ws.data_ptr(), M, C, float(p_in),
-               int(seed_in), float(p_out), int(seed_out), _st(dy.device), _ext.ptr(dsum))
+               _ext.ptr(dx), _ext.ptr(dgamma), _ext.ptr(dbeta), -1 if fb is not None else int(accumulate),
+               ws.data_ptr(), M, C, float(p_in), int(seed_in), float(p_out), int(seed_out), _st(dy.device),
+               _ext.ptr(dsum))
+    if fb is not None:
+        fb.add_cols(ws, nws // (3 * C), 3 * C, C, dgamma, dbeta, dsum, accumulate=accumulate)
     return dh, dx
+
+
+def cls_head_fwd(pooled, wc, bc, p_drop=0.0, seed=0):
+    """logits[B, L] (fp32) = drop(pooled) @ wc^T + bc  (csrc/kernels/head.hip)."""
+    ext = _ext.load(required=True)
+    B, C = pooled.shape
+    L = wc.shape[0]
+    logits = torch.empty((B, L), dtype=torch.float32, device=pooled.device)
+    ext.cls_head_fwd(pooled.data_ptr(), pooled.stride(0), wc.data_ptr(), bc.data_ptr(), logits.data_ptr(), B, C, L,
+                     float(p_drop), int(seed), _st(pooled.device))
+    return logits
+
+
+def cls_head_bwd(dlogits, pooled, wc, gwc=None, gbc=None, p_drop=0.0, seed=0):
+    """dpre[B, C] (bf16) = (dlogits @ wc) * drop' * (1 - pooled^2); gwc / gbc (+)= the
+    classifier's weight / bias gradients."""
+    ext = _ext.load(required=True)
+    B, C = pooled.shape
+    L = wc.shape[0]
+    dl = dlogits.float().contiguous()
+    dpre = torch.empty((B, C), dtype=torch.bfloat16, device=pooled.device)
+    ext.cls_head_bwd(dl.data_ptr(), pooled.data_ptr(), pooled.stride(0), wc.data_ptr(), dpre.data_ptr(),
+                     _ext.ptr(gwc), _ext.ptr(gbc), B, C, L, float(p_drop), int(seed), _st(pooled.device))
+    return dpre
 
 
 def embed_sum(ids, tts, word, pos, type_, seq_len, pos_offset=0):

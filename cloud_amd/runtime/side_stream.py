@@ -62,3 +62,49 @@ class SideWork:
         if self.used:
             self.main.wait_stream(self.side)
             self.used = False
+
+    def detach(self):
+        """Instead of ``join``: an event marking the side work queued so far (None when
+        nothing ran on the side stream) -- the caller makes the main stream wait for it
+        later (``settle``), so the side stream's tail overlaps the next layer's work."""
+        if not self.used:
+            return None
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        self.used = False
+        return ev
+
+
+# Side-stream gradients whose join (and DDP notification) is deferred across layers:
+# [(event, params)], oldest first.  A backward-pass callback settles all of them, so the
+# optimizer / DDP never read a gradient before the side stream has written it.
+_PENDING = []
+_CALLBACK = [False]
+
+
+def defer(event, params, notify):
+    """Queue params whose gradients the side stream finishes at ``event``; ``notify(p)``
+    runs for each once the main stream has been ordered after it."""
+    if event is None:
+        for p in params:
+            notify(p)
+        return
+    _PENDING.append((event, list(params), notify))
+    if not _CALLBACK[0]:
+        _CALLBACK[0] = True
+        torch.autograd.Variable._execution_engine.queue_callback(settle_all)
+
+
+def settle(keep_last=0):
+    """Order the main stream after all but the newest ``keep_last`` deferred side-stream
+    gradient sets and notify their params."""
+    while len(_PENDING) > keep_last:
+        ev, params, notify = _PENDING.pop(0)
+        torch.cuda.current_stream().wait_event(ev)
+        for p in params:
+            notify(p)
+
+
+def settle_all():
+    _CALLBACK[0] = False
+    settle(0)

@@ -64,6 +64,12 @@ int ca_conv_dgrad(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int
 int ca_conv_wgrad(const bf16_t*, const bf16_t*, void*, int, float, int, int, int, int, int, int, int, int, int, int,
                   int, int, float*, hipStream_t);
 int ca_splitk_reduce(const float*, int, long, void*, int, float, hipStream_t);
+int ca_grad_finalize_multi(const uint64_t*, const float*, int, hipStream_t);
+int ca_cls_head_max_labels();
+int ca_cls_head_fwd(const bf16_t*, long, const float*, const float*, float*, int, int, int, float, uint64_t,
+                    hipStream_t);
+int ca_cls_head_bwd(const float*, const bf16_t*, long, const float*, bf16_t*, float*, float*, int, int, int, float,
+                    uint64_t, hipStream_t);
 int ca_gemm_splitk(int, const bf16_t*, long, const bf16_t*, long, void*, int, float, int, int, int, int, float*,
                    hipStream_t);
 int ca_gemm_splitk_effective(int, int);
@@ -257,6 +263,23 @@ PYBIND11_MODULE(_C, m) {
                          int KH, int KW, int sh, int sw, int ph, int pw, int splits, u64 ws, u64 s) {
     check(ca_conv_wgrad(P(const bf16_t*, dy), P(const bf16_t*, x), P(void*, dw), dw_bf16, beta, Nb, H, W, Cin, Cout,
                         KH, KW, sh, sw, ph, pw, splits, P(float*, ws), S(s)), "conv_wgrad");
+  });
+  // jobs: rows of 12 u64 {kind, src, nparts, stride, n, out0, out1, out2, out_bf16, accumulate, 0, 0}
+  m.def("grad_finalize_multi", [](const std::vector<uint64_t>& jobs, const std::vector<float>& betas, u64 s) {
+    const int n = (int)betas.size();
+    if ((long)jobs.size() != 12L * n) throw std::runtime_error("grad_finalize_multi: 12 fields per job");
+    check(ca_grad_finalize_multi(jobs.data(), betas.data(), n, S(s)), "grad_finalize_multi");
+  });
+  m.def("cls_head_max_labels", []() { return ca_cls_head_max_labels(); });
+  m.def("cls_head_fwd", [](u64 pooled, long ldp, u64 wc, u64 bc, u64 logits, int B, int C, int L, float p, u64 seed,
+                           u64 s) {
+    check(ca_cls_head_fwd(P(const bf16_t*, pooled), ldp, P(const float*, wc), P(const float*, bc), P(float*, logits),
+                          B, C, L, p, seed, S(s)), "cls_head_fwd");
+  });
+  m.def("cls_head_bwd", [](u64 dl, u64 pooled, long ldp, u64 wc, u64 dpre, u64 gwc, u64 gbc, int B, int C, int L,
+                           float p, u64 seed, u64 s) {
+    check(ca_cls_head_bwd(P(const float*, dl), P(const bf16_t*, pooled), ldp, P(const float*, wc), P(bf16_t*, dpre),
+                          P(float*, gwc), P(float*, gbc), B, C, L, p, seed, S(s)), "cls_head_bwd");
   });
   m.def("splitk_reduce", [](u64 ws, int splits, long MN, u64 out, int out_bf16, float beta, u64 s) {
     check(ca_splitk_reduce(P(const float*, ws), splits, MN, P(void*, out), out_bf16, beta, S(s)), "splitk_reduce");

@@ -391,7 +391,7 @@ int ca_gemm_splitk_effective(int K, int splits) {
 }
 
 // Split-K GEMM into fp32 slabs ws[splits][M][N] + deterministic reduction into
-// `out` (bf16 if out_bf16 else fp32): out = sum + beta*out.
+// `out` (bf16 if out_bf16 else fp32): out = sum + beta*out.  out_bf16 < 0: slabs only.
 int ca_gemm_splitk(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, void* out, int out_bf16,
                    float beta, int M, int N, int K, int splits, float* ws, hipStream_t s) {
   if (M <= 0 || N < 8 || N % 8 != 0 || (layout == 2 && M % 8 != 0)) return -1;
@@ -407,8 +407,9 @@ int ca_gemm_splitk(int layout, const bf16_t* A, long lda, const bf16_t* B, long 
   p.red_ld = N;
   p.red_beta = beta;
   p.red_bf16 = out_bf16;
+  if (out_bf16 < 0) p.tile_cnt = nullptr;  // slabs only: the caller reduces them (gradfin.hip)
   int rc = dispatch<EPI_F32_PARTIAL>(layout, p, splits, s);
-  if (rc || p.tile_cnt) return rc;
+  if (rc || p.tile_cnt || out_bf16 < 0) return rc;
   return ca_splitk_reduce(ws, splits, (long)M * N, out, out_bf16, beta, s);
 }
 

@@ -568,7 +568,9 @@ int ca_ln_bwd(const bf16_t* dy, const bf16_t* h, const float* mean, const float*
     default: ln_bwd_launch<8>(dy, h, mean, rstd, gamma, dh, dx, ws, nblk, M, C, din, dout, s); break;
   }
   CA_LAUNCH_CHECK();
-  if (dgamma || dbeta || dsum) {
+  // accumulate < 0: the caller finalises the [nblk][3][C] partials in ws itself (batched
+  // finalisation, gradfin.hip)
+  if (accumulate >= 0 && (dgamma || dbeta || dsum)) {
     col_finalize_kernel<<<ca_cdiv((dsum ? 3 : 2) * C, 16), 256, 0, s>>>(ws, nblk, 3L * C, C, dgamma, dbeta,
                                                                         accumulate, dsum);
     CA_LAUNCH_CHECK();
@@ -587,6 +589,7 @@ int ca_colsum(const bf16_t* x, long M, int N, long ld, float* out, int accumulat
   dim3 grid(ca_cdiv(N, 256), ry);
   colsum_part_kernel<<<grid, 256, 0, s>>>(x, M, N, ld, ws);
   CA_LAUNCH_CHECK();
+  if (accumulate < 0) return 0;  // partials [ry][N] left in ws for a batched finalisation
   col_finalize_kernel<<<ca_cdiv(N, 16), 256, 0, s>>>(ws, ry, N, N, out, nullptr, accumulate);
   CA_LAUNCH_CHECK();
   return 0;

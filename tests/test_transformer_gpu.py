@@ -274,3 +274,31 @@ def test_bert_tiny_native_matches_torch(arena):
     for n in g_ref:
         assert g_nat[n] is not None, n
         assert rel(g_nat[n], g_ref[n]) < 8e-2, (n, rel(g_nat[n], g_ref[n]))
+
+
+def test_grad_finalize_batch_bitwise(monkeypatch):
+    """The BERT layer backward's batched gradient finalisation (one gradfin.hip launch per
+    layer) gives bitwise the gradients of the one-launch-per-reduction path."""
+    from cloud_amd.models.bert import BertConfig, BertForSequenceClassification
+
+    torch.manual_seed(8)
+    cfg = BertConfig.tiny(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0, num_labels=3)
+    m = BertForSequenceClassification(cfg, device=DEV)
+    B, S = 4, 128
+    ids = torch.randint(0, cfg.vocab_size, (B, S), device=DEV)
+    tts = torch.randint(0, 2, (B, S), device=DEV)
+    am = torch.ones(B, S, device=DEV, dtype=torch.long)
+    am[2, 70:] = 0
+    labels = torch.randint(0, 3, (B,), device=DEV)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CLOUD_AMD_GRAD_FIN_BATCH", flag)
+        m.zero_grad(set_to_none=True)
+        F.cross_entropy(m(ids, tts, am), labels).backward()
+        out[flag] = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    assert out["1"].keys() == out["0"].keys() and len(out["1"]) > 0
+    for n in out["1"]:
+        if "token_type" in n:  # block partials added with float atomics: order varies run to run
+            torch.testing.assert_close(out["1"][n], out["0"][n], rtol=1e-5, atol=1e-6)
+        else:
+            assert torch.equal(out["1"][n], out["0"][n]), n
