@@ -413,7 +413,8 @@ __global__ void __launch_bounds__(256) attn_bwd_dq_kernel(AttnArgs a) {
 //          dV = P^T dO, dK = dS^T Q    (P^T / dS^T as transposed reads of the [q][key] arrays)
 //   B      (wave w = queries 16w..16w+15)  dQ = dS K   (dS rows straight from LDS)
 // Every P / dS element is computed (and its dropout bit hashed) once instead of twice.
-// LDS: 3 x [S][72] + 2 x [S][S + 8] bf16 = 124 KB at S = 128 (one 8-wave block per CU).
+// LDS: 2 x [S][72] + [S][S + 8] bf16 = 72 KB at S = 128 (two 8-wave blocks per CU; the
+// first version kept K, P and dS in separate arrays, 124 KB, one block per CU: 37-38 us).
 template <int LD>
 __device__ __forceinline__ bf16x8 frag_kc(const short* lds, int r0, int k0, int lane) {
   s8v v = *reinterpret_cast<const s8v*>(lds + (r0 + (lane & 15)) * LD + k0 + 8 * (lane >> 4));
@@ -447,13 +448,13 @@ __device__ __forceinline__ void stage_store(short* slab, const f4v (&v)[4], bf16
 }
 
 template <int SQ>
-__global__ void __launch_bounds__(SQ * 4) attn_bwd_fused_kernel(AttnArgs a) {
-  constexpr int NW = SQ / 16, NT = NW * 64, TQ = SQ / 16, PL = SQ + 8;
+__global__ void __launch_bounds__(SQ * 4) __attribute__((amdgpu_waves_per_eu(4))) attn_bwd_fused_kernel(AttnArgs a) {
+  constexpr int NW = SQ / 16, NT = NW * 64, TQ = SQ / 16, PL = SQ + 8, LCH = SQ * 8 / NT;
+  // Qs: Q; Gs: dO (phase A), then K (phase B); Xs [q][key]: each wave's P columns, then
+  // its dS columns (P is dead once dV is accumulated).  72 KB at S = 128: two blocks per CU.
   __shared__ __attribute__((aligned(16))) short Qs[SQ * LDT];
-  __shared__ __attribute__((aligned(16))) short Gs[SQ * LDT];  // dO
-  __shared__ __attribute__((aligned(16))) short Ks[SQ * LDT];
-  __shared__ __attribute__((aligned(16))) short Ps[SQ * PL];   // P  [q][key]
-  __shared__ __attribute__((aligned(16))) short Ds[SQ * PL];   // dS [q][key]
+  __shared__ __attribute__((aligned(16))) short Gs[SQ * LDT];
+  __shared__ __attribute__((aligned(16))) short Xs[SQ * PL];
   __shared__ float lse_s[SQ], dv_s[SQ];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bh = blockIdx.x;
@@ -467,17 +468,15 @@ __global__ void __launch_bounds__(SQ * 4) attn_bwd_fused_kernel(AttnArgs a) {
   const bf16_t* gbase = a.dout + (long)b * SQ * C + h * D;
   const bf16_t* obase = a.out + (long)b * SQ * C + h * D;
 
-  // ---- loads: Q / dO / K tiles, Dv = rowsum(dO * O) from the same dO chunks
+  // ---- loads: Q / dO tiles, Dv = rowsum(dO * O)
 #pragma unroll
-  for (int i = 0; i < SQ * 8 / NT; ++i) {
+  for (int i = 0; i < LCH; ++i) {
     const int c = tid + i * NT;
     const int r = c >> 3, col = (c & 7) * 8;
     const s8v qv = *reinterpret_cast<const s8v*>(base + (long)r * ldq + h * D + col);
-    const s8v kv = *reinterpret_cast<const s8v*>(base + (long)r * ldq + C + h * D + col);
     const us8 gv = *reinterpret_cast<const us8*>(gbase + (long)r * C + col);
     const us8 ov = *reinterpret_cast<const us8*>(obase + (long)r * C + col);
     *reinterpret_cast<s8v*>(Qs + r * LDT + col) = qv;
-    *reinterpret_cast<s8v*>(Ks + r * LDT + col) = kv;
     *reinterpret_cast<us8*>(Gs + r * LDT + col) = gv;
     float s = 0.f;
 #pragma unroll
@@ -497,6 +496,7 @@ __global__ void __launch_bounds__(SQ * 4) attn_bwd_fused_kernel(AttnArgs a) {
   __syncthreads();
 
   // ---- phase A: this wave's 16 keys against all queries
+  s4v dsr[TQ];  // this wave's dS^T values, held until P's columns are consumed
   {
     f4v p[TQ], dp[TQ];
 #pragma unroll
@@ -514,43 +514,61 @@ __global__ void __launch_bounds__(SQ * 4) attn_bwd_fused_kernel(AttnArgs a) {
     for (int t = 0; t < TQ; ++t) {
       const int qi = t * 16 + (lane & 15);
       const float ls = lse_s[qi], dvq = dv_s[qi];
-      s4v pk, dk4;
+      s4v pk;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kr + r;
         const float pr = key < klen ? exp2f(p[t][r] * c2 - ls) : 0.f;
         const float mul = a.drop.on ? drop_mul(a.drop, bhss + (uint32_t)(qi * SQ + key)) : 1.f;
         pk[r] = (short)f2bf(pr * mul);
-        dk4[r] = (short)f2bf(pr * (dp[t][r] * mul - dvq));
+        dsr[t][r] = (short)f2bf(pr * (dp[t][r] * mul - dvq));
       }
-      *reinterpret_cast<s4v*>(Ps + qi * PL + kr) = pk;
-      *reinterpret_cast<s4v*>(Ds + qi * PL + kr) = dk4;
+      *reinterpret_cast<s4v*>(Xs + qi * PL + kr) = pk;
     }
   }
-  __builtin_amdgcn_wave_barrier();
   f4v dk[4], dv[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) dk[t] = dv[t] = f4v{0.f, 0.f, 0.f, 0.f};
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
   for (int kk = 0; kk < SQ / 32; ++kk) {
-    const bf16x8 pa = frag_nc<PL>(Ps, k0, kk * 32, lane);  // P^T: row = key, k = query
-    const bf16x8 da = frag_nc<PL>(Ds, k0, kk * 32, lane);
+    const bf16x8 pa = frag_nc<PL>(Xs, k0, kk * 32, lane);  // P^T: row = key, k = query
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < 4; ++t)
       dv[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, frag_nc<LDT>(Gs, t * 16, kk * 32, lane), dv[t], 0, 0, 0);
+  }
+  // P's columns of this wave are read: overwrite them with dS
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  {
+    const int kr = k0 + (lane >> 4) * 4;
+#pragma unroll
+    for (int t = 0; t < TQ; ++t) *reinterpret_cast<s4v*>(Xs + (t * 16 + (lane & 15)) * PL + kr) = dsr[t];
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int kk = 0; kk < SQ / 32; ++kk) {
+    const bf16x8 da = frag_nc<PL>(Xs, k0, kk * 32, lane);  // dS^T
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
       dk[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, frag_nc<LDT>(Qs, t * 16, kk * 32, lane), dk[t], 0, 0, 0);
-    }
   }
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) dk[t][r] *= a.scale;
-  __syncthreads();  // every wave's dS columns written; P / dO no longer read
+  __syncthreads();  // every wave's dS columns written; dO no longer read
 
-  // dK, dV out through this wave's slabs in the (now free) P and dO regions
-  bf16_t* drow = a.dqkv + ((long)b * SQ + k0) * ldq + h * D;
-  stage_store(Ps + wave * 16 * LDT, dk, drow + C, ldq, lane);
-  stage_store(Gs + wave * 16 * LDT, dv, drow + 2 * C, ldq, lane);
+  // K into the dO region (its load latency is covered by the CU's other block)
+#pragma unroll
+  for (int i = 0; i < LCH; ++i) {
+    const int c = tid + i * NT;
+    const int r = c >> 3, col = (c & 7) * 8;
+    *reinterpret_cast<s8v*>(Gs + r * LDT + col) = *reinterpret_cast<const s8v*>(base + (long)r * ldq + C + h * D + col);
+  }
+  __syncthreads();
 
   // ---- phase B: dQ for this wave's 16 queries
   const int q0 = wave * 16;
@@ -559,16 +577,21 @@ __global__ void __launch_bounds__(SQ * 4) attn_bwd_fused_kernel(AttnArgs a) {
   for (int t = 0; t < 4; ++t) dq[t] = f4v{0.f, 0.f, 0.f, 0.f};
   const int nkk = (klen + 31) / 32;
   for (int kk = 0; kk < nkk; ++kk) {
-    const bf16x8 da = frag_kc<PL>(Ds, q0, kk * 32, lane);  // dS: row = query, k = key
+    const bf16x8 da = frag_kc<PL>(Xs, q0, kk * 32, lane);  // dS: row = query, k = key
 #pragma unroll
     for (int t = 0; t < 4; ++t)
-      dq[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, frag_nc<LDT>(Ks, t * 16, kk * 32, lane), dq[t], 0, 0, 0);
+      dq[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, frag_nc<LDT>(Gs, t * 16, kk * 32, lane), dq[t], 0, 0, 0);
   }
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) dq[t][r] *= a.scale;
-  stage_store(Qs + wave * 16 * LDT, dq, a.dqkv + ((long)b * SQ + q0) * ldq + h * D, ldq, lane);
+  __syncthreads();  // dS and K no longer read: every region is staging space now
+
+  bf16_t* drow = a.dqkv + ((long)b * SQ + k0) * ldq + h * D;
+  stage_store(Qs + wave * 16 * LDT, dk, drow + C, ldq, lane);
+  stage_store(Gs + wave * 16 * LDT, dv, drow + 2 * C, ldq, lane);
+  stage_store(Xs + wave * 16 * LDT, dq, a.dqkv + ((long)b * SQ + q0) * ldq + h * D, ldq, lane);
 }
 
 // Forward for S = 64 / 128: one workgroup per (batch, head), all S keys' K and V issued
