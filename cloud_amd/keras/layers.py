@@ -16,6 +16,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..ops.dense import conv2d as conv_act_op
 from ..ops.dense import dense as dense_op
+from ..ops.dropout import dropout as dropout_op
 from . import activations, initializers, regularizers
 from .engine import Input, InputLayer, Layer, global_policy  # noqa: F401
 
@@ -187,7 +188,7 @@ class GlobalAveragePooling2D(Layer):
 
 class GlobalMaxPooling2D(Layer):
     def call(self, x, training=None):
-        return x.amax(dim=(1, 2))
+        return ops.global_max_pool_nhwc(x.contiguous())
 
 
 class Flatten(Layer):
@@ -215,7 +216,7 @@ class Dropout(Layer):
         self.rate = float(rate)
 
     def call(self, x, training=None):
-        return F.dropout(x, self.rate, training=bool(training))
+        return dropout_op(x, self.rate, training=bool(training))
 
     def get_config(self):
         c = super().get_config()

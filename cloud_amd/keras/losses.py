@@ -70,9 +70,11 @@ class SparseCategoricalCrossentropy(Loss):
         p = y_pred.float().clamp_min(1e-7)
         return F.nll_loss(torch.log(p / p.sum(-1, keepdim=True)), y, reduction="none")
 
-    def fused_logits_loss(self, logits, y_true):
-        """(mean loss, correct flags) via the fused softmax-xent kernel."""
-        return ops.softmax_cross_entropy(logits, y_true.reshape(-1), label_smoothing=self.label_smoothing)
+    def fused_logits_loss(self, logits, y_true, acc=None, acc_weight=1.0):
+        """(mean loss, correct flags) via the fused softmax-xent kernel; ``acc`` (device fp32
+        [3]) accumulates [loss sum, correct count, rows] for the metrics inside the kernel."""
+        return ops.softmax_cross_entropy(logits, y_true.reshape(-1), label_smoothing=self.label_smoothing, acc=acc,
+                                         acc_weight=acc_weight)
 
 
 class CategoricalCrossentropy(Loss):

@@ -26,7 +26,7 @@ import time
 import numpy as np
 import torch
 
-from .. import monitoring
+from .. import monitoring, ops
 from ..parallel import strategy as strat
 from ..utils import trace
 from . import callbacks as cbks
@@ -48,6 +48,64 @@ def _to_torch(x, device, dtype=None):
     if dtype is not None and t.is_floating_point():
         t = t.to(dtype)
     return t.to(device, non_blocking=True)
+
+
+def _plain_array(a):
+    return a is not None and not isinstance(a, (dict, list, tuple, Dataset))
+
+
+def _device_arrays(x, y, dev, dtype):
+    """Array inputs go to the device ONCE per fit (x in the compute dtype, integer labels as
+    int64): every step then trains on views of them -- no per-step host slicing, cast or
+    host-to-device copy."""
+    xt = _to_torch(x, dev, dtype)
+    yt = None
+    if y is not None:
+        yt = _to_torch(y, dev)
+        if not yt.is_floating_point():
+            yt = yt.long()
+    return xt, yt
+
+
+def _grouped_to_device(items, dev, dtype, group=16):
+    """Dataset batches -> device in groups: ``group`` consecutive host batches of one shape
+    are concatenated into one pinned buffer and uploaded with ONE asynchronous copy; the
+    steps get views.  Pipeline order is unchanged (the group is filled in order)."""
+    def key(it):
+        xb, yb = np.asarray(it[0]), None if it[1] is None else np.asarray(it[1])
+        return (xb.shape[1:], xb.dtype.str, None if yb is None else (yb.shape[1:], yb.dtype.str))
+
+    def emit(buf):
+        X = torch.as_tensor(np.concatenate([np.asarray(b[0]) for b in buf]))
+        if X.is_floating_point() and dtype is not None:
+            X = X.to(dtype)
+        X = X.pin_memory().to(dev, non_blocking=True)
+        Y = None
+        if buf[0][1] is not None:
+            Y = torch.as_tensor(np.concatenate([np.asarray(b[1]) for b in buf]))
+            if not Y.is_floating_point():
+                Y = Y.long()
+            Y = Y.pin_memory().to(dev, non_blocking=True)
+        off = 0
+        for b in buf:
+            n = len(np.asarray(b[0]))
+            yield X[off:off + n], (None if Y is None else Y[off:off + n]), b[2], b[3]
+            off += n
+
+    buf = []
+    for it in items:
+        if not (_plain_array(it[0]) and (it[1] is None or _plain_array(it[1]))) or \
+                isinstance(it[0], torch.Tensor) and it[0].is_cuda:
+            yield from emit(buf) if buf else ()
+            buf = []
+            yield it
+            continue
+        if buf and (len(buf) == group or key(it) != key(buf[0])):
+            yield from emit(buf)
+            buf = []
+        buf.append(it)
+    if buf:
+        yield from emit(buf)
 
 
 def _first(x):
@@ -87,6 +145,7 @@ class Model(Layer):
         self.compiled_metrics = []
         self.history = None
         self._strategy = None
+        self._dev_acc = None
         self._reducer = None
         self._fused_xent = False
         self._graph = None
@@ -177,7 +236,8 @@ class Model(Layer):
 
     def __call__(self, inputs, *args, **kwargs):
         out = super().__call__(inputs, *args, **kwargs)
-        if isinstance(out, torch.Tensor) and global_policy().name != "float32" and out.is_floating_point():
+        if isinstance(out, torch.Tensor) and global_policy().name != "float32" and out.is_floating_point() \
+                and not getattr(self, "_raw_logits", False):
             out = out.float()
         return out
 
@@ -257,14 +317,24 @@ class Model(Layer):
                 b.data.copy_(t)
 
     def _forward_train(self, x):
+        """Logits for the fused loss, in the compute dtype (the kernel reads bf16 directly:
+        no fp32 cast of the model output)."""
         sm = self._final_softmax_layer() if (self._fused_xent and not self.loss.from_logits) else None
         if sm is not None:
             sm._emit_logits = True
+        self._raw_logits = True
         try:
             return self(x, training=True)
         finally:
+            self._raw_logits = False
             if sm is not None:
                 sm._emit_logits = False
+
+    def _metrics_fusable(self):
+        """Loss and accuracy state kept by the fused loss kernel itself (device accumulator,
+        read once per log): fused sparse-xent with only sparse-categorical-accuracy metrics."""
+        return self._fused_xent and all(type(m) is metrics_mod.SparseCategoricalAccuracy
+                                        for m in self.compiled_metrics)
 
     def train_step(self, xb, yb, sample_weight=None, loss_weight=1.0, n_real=None):
         """One replica step.  ``loss_weight`` rescales this replica's mean loss so that the
@@ -278,10 +348,16 @@ class Model(Layer):
         y = _to_torch(yb, dev) if yb is not None else None
         impl = self.optimizer.impl
         impl.zero_grad()
+        n = _length(x) if n_real is None else n_real
+        fused_metrics = False
         with trace.range("forward"):
             if self._fused_xent:
                 logits = self._forward_train(x)
-                loss, _ = self.loss.fused_logits_loss(logits, y)
+                fused_metrics = self._metrics_fusable()
+                if fused_metrics and self._dev_acc is None:
+                    self._dev_acc = torch.zeros(3, dtype=torch.float32, device=logits.device)
+                loss, _ = self.loss.fused_logits_loss(logits, y, acc=self._dev_acc if fused_metrics else None,
+                                                      acc_weight=1.0 if n else 0.0)
                 pred = logits
             else:
                 pred = self(x, training=True)
@@ -290,14 +366,17 @@ class Model(Layer):
             scaled = loss * loss_weight if loss_weight != 1.0 else loss
             total = scaled + reg if reg is not None else scaled
         with trace.range("backward"):
-            total.backward()
+            if total is loss and self._fused_xent:
+                # the fused loss hands its stored gradient on as-is for the unit seed
+                torch.autograd.backward(total, grad_tensors=ops.unit_seed(total.device))
+            else:
+                total.backward()
         if self._reducer is not None:
             with trace.range("allreduce_join"):
                 self._reducer.finish()
         with trace.range("optimizer"):
             impl.step()
-        n = _length(x) if n_real is None else n_real
-        if n:
+        if n and not fused_metrics:
             self._loss_tracker.update_state(loss.detach().float().reshape(1), sample_weight=[n])
             with torch.no_grad():
                 for m in self.compiled_metrics:
@@ -312,6 +391,12 @@ class Model(Layer):
         return global_policy().compute_dtype
 
     def _logs(self, prefix="", reduce=True):
+        if getattr(self, "_dev_acc", None) is not None:
+            # loss / accuracy state accumulated by the fused loss kernel (one sync per log)
+            tl, tc, rows = self._dev_acc.tolist()
+            self._loss_tracker.set_state([tl, rows])
+            for m in self.compiled_metrics:
+                m.set_state([tc, rows])
         trackers = [self._loss_tracker] + list(self.compiled_metrics)
         if reduce and self._strategy is not None and self._strategy.num_replicas_in_sync > 1:
             state = torch.tensor([v for m in trackers for v in m.state()], dtype=torch.float64)
@@ -324,6 +409,7 @@ class Model(Layer):
         return logs
 
     def _reset_metrics(self):
+        self._dev_acc = None
         self._loss_tracker = metrics_mod.Mean(name="loss")
         for m in self.compiled_metrics:
             m.reset_state()
@@ -359,6 +445,22 @@ class Model(Layer):
         n = _length(x)
         bs = batch_size or 32
         idx = np.random.default_rng(seed + epoch).permutation(n) if shuffle else np.arange(n)
+        if isinstance(x, torch.Tensor) and x.is_cuda and (y is None or isinstance(y, torch.Tensor)):
+            # device-resident arrays: ONE gather per epoch, then every batch is a view
+            if shuffle:
+                perm = torch.from_numpy(idx).to(x.device)
+                x = x.index_select(0, perm)
+                y = y.index_select(0, perm) if y is not None else None
+            for start in range(0, n, bs):
+                stop = min(start + bs, n)
+                gn = stop - start
+                if world == 1:
+                    yield x[start:stop], (y[start:stop] if y is not None else None), gn, gn
+                    continue
+                lo, hi = _replica_range(gn, world, rank)
+                a, b, real = (start + lo, start + hi, hi - lo) if hi > lo else (start, start + 1, 0)
+                yield x[a:b], (y[a:b] if y is not None else None), real, gn
+            return
         for start in range(0, n, bs):
             gb = idx[start:start + bs]
             if world == 1:
@@ -378,6 +480,9 @@ class Model(Layer):
             x, y = _slice(x, slice(0, cut)), _slice(y, slice(0, cut))
         sample = x if not isinstance(x, Dataset) else next(iter(x))[0]
         s = self._setup(sample)
+        on_gpu = s.device.type == "cuda"
+        if on_gpu and _plain_array(x) and (y is None or _plain_array(y)):
+            x, y = _device_arrays(x, y, s.device, self._input_dtype())
         verbose = 1 if verbose == "auto" else verbose
         history = cbks.History()
         cb_list = list(callbacks or []) + ([cbks.ProgbarLogger()] if verbose else []) + [history]
@@ -390,15 +495,22 @@ class Model(Layer):
         self.train()
         callbacks_.on_train_begin({})
         persistent = None
+
+        def batches(epoch):
+            it = self._batches(x, y, batch_size, shuffle, epoch)
+            if on_gpu and isinstance(x, Dataset):
+                it = _grouped_to_device(it, s.device, self._input_dtype())
+            return it
+
         if steps_per_epoch is not None:
-            persistent = iter(self._batches(x, y, batch_size, shuffle, 0))
+            persistent = iter(batches(0))
         from ..utils import faults
 
         global_step = 0
         for epoch in range(initial_epoch, epochs):
             self._reset_metrics()
             callbacks_.on_epoch_begin(epoch, {})
-            it = persistent if persistent is not None else self._batches(x, y, batch_size, shuffle, epoch)
+            it = persistent if persistent is not None else batches(epoch)
             step = 0
             t0 = time.time()
             mon = monitoring.enabled()

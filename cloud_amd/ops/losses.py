@@ -15,41 +15,77 @@ import torch.nn.functional as F
 from . import _ext
 
 
+# batches up to this many logits take the one-block kernel that also reduces the mean
+# loss and the metric sums in place (xent.hip xent_batch_kernel)
+_BATCH_KERNEL_MAX = 1 << 21
+_UNIT = {}
+
+
+def unit_seed(device):
+    """A persistent 1.0 to pass as ``torch.autograd.backward(loss, grad_tensors=...)``: the
+    fused loss recognises it and hands its stored gradient on unscaled (no fill kernel for
+    autograd's implicit ones, no multiply)."""
+    key = str(device)
+    t = _UNIT.get(key)
+    if t is None:
+        t = _UNIT[key] = torch.ones((), dtype=torch.float32, device=device)
+    return t
+
+
 class _XentFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, labels, denom, label_smoothing):
+    def forward(ctx, logits, labels, denom, label_smoothing, acc, acc_w):
         ext = _ext.load(required=True)
         z = logits.contiguous()
         B, C = z.shape
         dev = z.device
-        loss = torch.empty(B, dtype=torch.float32, device=dev)
         correct = torch.empty(B, dtype=torch.float32, device=dev)
         dz = torch.empty_like(z)
-        ext.softmax_xent(z.data_ptr(), int(z.dtype == torch.bfloat16), labels.contiguous().data_ptr(), B, C,
-                         1.0 / float(denom), float(label_smoothing), loss.data_ptr(), correct.data_ptr(),
-                         dz.data_ptr(), _ext.stream_handle(dev))
+        lab = labels.contiguous()
+        if B * C <= _BATCH_KERNEL_MAX:
+            mean = torch.empty(1, dtype=torch.float32, device=dev)
+            ext.softmax_xent_batch(z.data_ptr(), int(z.dtype == torch.bfloat16), lab.data_ptr(), B, C,
+                                   1.0 / float(denom), float(label_smoothing), mean.data_ptr(), correct.data_ptr(),
+                                   dz.data_ptr(), _ext.ptr(acc), float(acc_w), _ext.stream_handle(dev))
+            out = mean.view(())
+        else:
+            loss = torch.empty(B, dtype=torch.float32, device=dev)
+            ext.softmax_xent(z.data_ptr(), int(z.dtype == torch.bfloat16), lab.data_ptr(), B, C,
+                             1.0 / float(denom), float(label_smoothing), loss.data_ptr(), correct.data_ptr(),
+                             dz.data_ptr(), _ext.stream_handle(dev))
+            if acc is not None:
+                acc += torch.stack([loss.sum(), correct.sum(), loss.new_tensor(float(B))]) * float(acc_w)
+            out = loss.sum() / float(denom)
         ctx.save_for_backward(dz)
         ctx.mark_non_differentiable(correct)
-        return loss.sum() / float(denom), correct
+        return out, correct
 
     @staticmethod
     def backward(ctx, gloss, _gcorrect):
         (dz,) = ctx.saved_tensors
-        return dz * gloss.to(dz.dtype), None, None, None
+        u = _UNIT.get(str(gloss.device))
+        if u is not None and gloss.data_ptr() == u.data_ptr():
+            return dz, None, None, None, None, None
+        return dz * gloss.to(dz.dtype), None, None, None, None, None
 
 
-def softmax_cross_entropy(logits, labels, *, denom=None, label_smoothing=0.0):
+def softmax_cross_entropy(logits, labels, *, denom=None, label_smoothing=0.0, acc=None, acc_weight=1.0):
     """Return ``(mean_loss, correct_flags)``.
 
     ``denom`` defaults to the local batch size; pass the GLOBAL batch size to get
-    the MultiWorkerMirrored ``compute_average_loss`` convention.
+    the MultiWorkerMirrored ``compute_average_loss`` convention.  ``acc`` (fp32 [3] on the
+    device): ``acc += [sum of row losses, sum of correct flags, rows] * acc_weight``
+    inside the loss kernel (Keras loss / accuracy metric state without per-step syncs).
     """
     B = logits.shape[0]
     denom = B if denom is None else denom
     labels = labels.long()
     if logits.dtype in (torch.bfloat16, torch.float32) and _ext.use_native(logits, labels):
-        return _XentFn.apply(logits, labels, denom, label_smoothing)
+        return _XentFn.apply(logits, labels, denom, label_smoothing, acc, acc_weight)
     lf = logits.float()
     per = F.cross_entropy(lf, labels, reduction="none", label_smoothing=label_smoothing)
     correct = (lf.argmax(-1) == labels).float()
+    if acc is not None:
+        with torch.no_grad():
+            acc += torch.stack([per.sum(), correct.sum(), per.new_tensor(float(B))]).to(acc.device) * float(acc_weight)
     return per.sum() / float(denom), correct

@@ -80,6 +80,39 @@ def global_avg_pool_nhwc(x):
     return x.mean(dim=(1, 2))
 
 
+class _GmpFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ext = _ext.load(required=True)
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        y = torch.empty((N, C), dtype=x.dtype, device=x.device)
+        cnt = torch.empty((N, C), dtype=torch.float32, device=x.device)
+        ext.gmp_fwd(x.data_ptr(), y.data_ptr(), cnt.data_ptr(), N, H * W, C, _ext.stream_handle(x.device))
+        ctx.save_for_backward(x, y, cnt)
+        ctx.mark_non_differentiable(cnt)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ext = _ext.load(required=True)
+        x, y, cnt = ctx.saved_tensors
+        N, H, W, C = x.shape
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        ext.gmp_bwd(dy.data_ptr(), int(dy.dtype == torch.bfloat16), x.data_ptr(), y.data_ptr(), cnt.data_ptr(),
+                    dx.data_ptr(), N, H * W, C, _ext.stream_handle(dy.device))
+        return dx
+
+
+def global_max_pool_nhwc(x):
+    """[N, H, W, C] -> [N, C] max over H, W (Keras GlobalMaxPooling2D); ties share the
+    gradient evenly, as reduce_max / amax."""
+    if x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0 and _ext.use_native(x):
+        return _GmpFn.apply(x)
+    return x.amax(dim=(1, 2))
+
+
 class _StemTailFn(torch.autograd.Function):
     """maxpool3x3/2/1(relu(BN(z))) for the ResNet stem in one pass each way.
 

@@ -2,8 +2,12 @@
 
 One HIP launch per arena segment (decayed / non-decayed) updates the fp32
 master weights, the optimizer state and the bf16 model copy in a single pass.
-Hyper-parameters live in a tiny device array refreshed before each step, so
-the update kernels themselves are hipGraph-capturable (:meth:`step_kernels`).
+``step()`` passes the hyper-parameters by value in the kernel arguments (no
+host-to-device copy, no stream synchronisation per step); the hipGraph-capturable
+path (:meth:`prepare_step` + :meth:`step_kernels`) reads them from a tiny device
+array refreshed before each replay.  With ``fuse_zero_grad`` (default) the update
+kernel also zeroes the gradient elements it consumed, and the next ``zero_grad()``
+skips its fill pass (the arena is known clean).
 On CPU the same math runs as PyTorch ops on the flat buffers (reference path
 for the numerics tests).
 
@@ -41,6 +45,8 @@ class FusedOptimizer:
         self.iterations = 0
         self.state = [self._init_state(a) for a in self.arenas]
         self._hp = {}
+        self.fuse_zero_grad = True
+        self._grads_clean = True  # arenas are allocated zeroed
 
     # -- hyper-parameters ---------------------------------------------------
     @property
@@ -78,6 +84,11 @@ class FusedOptimizer:
 
     # -- public API -----------------------------------------------------------
     def zero_grad(self, set_to_none=False):
+        if self._grads_clean:
+            # the last native step zeroed every gradient it consumed; skip the fill once
+            # (a second zero_grad before the next step fills as usual)
+            self._grads_clean = False
+            return
         zero_grads(self.arenas)
 
     def parameters(self):
@@ -98,16 +109,25 @@ class FusedOptimizer:
                 hp = self._hp.get((ai, seg))
                 if hp is None:
                     hp = self._hp_tensor(ai, seg, wd)
-                self._update(ai, a, lo, hi, hp)
+                self._update(ai, a, lo, hi, hp, None)
+        self._after_update()
 
     def step(self, closure=None):
         loss = closure() if closure is not None else None
         if self.clipnorm is not None:
             self._clip()
         self.iterations += 1
-        self.prepare_step()
-        self.step_kernels()
+        for ai, a in enumerate(self.arenas):
+            for lo, hi, wd in self._segments(a):
+                self._update(ai, a, lo, hi, None, [float(v) for v in self._hp_values(wd)])
+        self._after_update()
         return loss
+
+    def _zero_in_kernel(self, a):
+        return self.fuse_zero_grad and self._use_native(a)
+
+    def _after_update(self):
+        self._grads_clean = bool(self.arenas) and all(self._zero_in_kernel(a) for a in self.arenas)
 
     def _clip(self):
         tot = 0.0
@@ -157,7 +177,7 @@ class SGD(FusedOptimizer):
     def _hp_values(self, wd):
         return [self.lr, self.momentum, self.dampening, wd, self.grad_scale, 1.0 if self.iterations <= 1 else 0.0]
 
-    def _update(self, ai, a, lo, hi, hp):
+    def _update(self, ai, a, lo, hi, hp, hv):
         st = self.state[ai]
         m = st.get("momentum")
         if self._use_native(a):
@@ -166,9 +186,10 @@ class SGD(FusedOptimizer):
             ext.sgd_step(a.master.data_ptr() + 4 * lo, a.grad.data_ptr() + es * lo, int(a.grad.dtype == torch.bfloat16),
                          0 if m is None else m.data_ptr() + 4 * lo,
                          0 if a.model is None else a.model.data_ptr() + a.model.element_size() * lo,
-                         hp.data_ptr(), hi - lo, int(self.nesterov), _ext.stream_handle(a.device))
+                         0 if hp is None else hp.data_ptr(), hv or [], hi - lo, int(self.nesterov),
+                         int(self._zero_in_kernel(a)), _ext.stream_handle(a.device))
             return
-        lr, mom, damp, wdv, gs, first = hp.tolist()
+        lr, mom, damp, wdv, gs, first = hp.tolist() if hp is not None else hv
         p = a.master[lo:hi]
         g = a.grad[lo:hi].float() * gs + wdv * p
         if mom:
@@ -199,7 +220,7 @@ class Adam(FusedOptimizer):
         return [self.lr, self.beta_1, self.beta_2, self.epsilon, wd, self.grad_scale,
                 1.0 - self.beta_1 ** t, 1.0 - self.beta_2 ** t]
 
-    def _update(self, ai, a, lo, hi, hp):
+    def _update(self, ai, a, lo, hi, hp, hv):
         st = self.state[ai]
         if self._use_native(a):
             ext = _ext.load(required=True)
@@ -207,9 +228,10 @@ class Adam(FusedOptimizer):
             ext.adam_step(a.master.data_ptr() + 4 * lo, a.grad.data_ptr() + es * lo, int(a.grad.dtype == torch.bfloat16),
                           st["m"].data_ptr() + 4 * lo, st["v"].data_ptr() + 4 * lo,
                           0 if a.model is None else a.model.data_ptr() + a.model.element_size() * lo,
-                          hp.data_ptr(), hi - lo, int(self.decoupled), _ext.stream_handle(a.device))
+                          0 if hp is None else hp.data_ptr(), hv or [], hi - lo, int(self.decoupled),
+                          int(self._zero_in_kernel(a)), _ext.stream_handle(a.device))
             return
-        lr, b1, b2, eps, wdv, gs, bc1, bc2 = hp.tolist()
+        lr, b1, b2, eps, wdv, gs, bc1, bc2 = hp.tolist() if hp is not None else hv
         p = a.master[lo:hi]
         g = a.grad[lo:hi].float() * gs
         if not self.decoupled:
@@ -248,7 +270,7 @@ class RMSprop(FusedOptimizer):
     def _hp_values(self, wd):
         return [self.lr, self.rho, self.epsilon, wd, self.grad_scale, self.momentum]
 
-    def _update(self, ai, a, lo, hi, hp):
+    def _update(self, ai, a, lo, hi, hp, hv):
         st = self.state[ai]
         buf = st.get("mom")
         if self._use_native(a):
@@ -258,9 +280,10 @@ class RMSprop(FusedOptimizer):
                              int(a.grad.dtype == torch.bfloat16), st["ms"].data_ptr() + 4 * lo,
                              0 if buf is None else buf.data_ptr() + 4 * lo,
                              0 if a.model is None else a.model.data_ptr() + a.model.element_size() * lo,
-                             hp.data_ptr(), hi - lo, _ext.stream_handle(a.device))
+                             0 if hp is None else hp.data_ptr(), hv or [], hi - lo, int(self._zero_in_kernel(a)),
+                             _ext.stream_handle(a.device))
             return
-        lr, rho, eps, wdv, gs, mom = hp.tolist()
+        lr, rho, eps, wdv, gs, mom = hp.tolist() if hp is not None else hv
         p = a.master[lo:hi]
         g = a.grad[lo:hi].float() * gs + wdv * p
         ms = st["ms"][lo:hi]

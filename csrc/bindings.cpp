@@ -15,9 +15,9 @@ namespace py = pybind11;
 typedef uint16_t bf16_t;
 
 extern "C" {
-int ca_sgd_step(float*, const void*, int, float*, bf16_t*, const float*, long, int, hipStream_t);
-int ca_adam_step(float*, const void*, int, float*, float*, bf16_t*, const float*, long, int, hipStream_t);
-int ca_rmsprop_step(float*, const void*, int, float*, float*, bf16_t*, const float*, long, hipStream_t);
+int ca_sgd_step(float*, void*, int, float*, bf16_t*, const float*, const float*, long, int, int, hipStream_t);
+int ca_adam_step(float*, void*, int, float*, float*, bf16_t*, const float*, const float*, long, int, int, hipStream_t);
+int ca_rmsprop_step(float*, void*, int, float*, float*, bf16_t*, const float*, const float*, long, int, hipStream_t);
 int ca_sumsq(const void*, int, long, float*, hipStream_t);
 int ca_scale(void*, int, long, const float*, hipStream_t);
 long ca_bn_workspace_floats(long, int);
@@ -44,10 +44,14 @@ int ca_conv_dgrad_bnstats(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, 
 int ca_u8_normalize(const uint8_t*, bf16_t*, long, int, const float*, const float*, hipStream_t);
 int ca_stem_s2d(const bf16_t*, bf16_t*, int, int, int, int, int, int, int, hipStream_t);
 int ca_softmax_xent(const void*, int, const int64_t*, int, int, float, float, float*, float*, void*, hipStream_t);
+int ca_softmax_xent_batch(const void*, int, const int64_t*, int, int, float, float, float*, float*, void*, float*, float,
+                          hipStream_t);
 int ca_maxpool_fwd(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ca_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ca_gap_fwd(const bf16_t*, void*, int, int, int, int, hipStream_t);
 int ca_gap_bwd(const void*, int, bf16_t*, int, int, int, hipStream_t);
+int ca_gmp_fwd(const bf16_t*, bf16_t*, float*, int, int, int, hipStream_t);
+int ca_gmp_bwd(const void*, int, const bf16_t*, const bf16_t*, const float*, bf16_t*, int, int, int, hipStream_t);
 int ca_gemm_bf16(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float*, float,
                  hipStream_t);
 int ca_gemm_set_core(int);
@@ -113,17 +117,21 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "cloud_amd gfx950 HIP kernels";
   m.attr("ARCH") = "gfx950";
 
-  m.def("sgd_step", [](u64 p, u64 g, int gbf, u64 mom, u64 p16, u64 hp, long n, int nesterov, u64 s) {
-    check(ca_sgd_step(P(float*, p), P(const void*, g), gbf, P(float*, mom), P(bf16_t*, p16), P(const float*, hp), n,
-                      nesterov, S(s)), "sgd_step");
+  // hp: device hyper-parameter array (0 = use hv, passed by value); zero_g: fused zero_grad
+  m.def("sgd_step", [](u64 p, u64 g, int gbf, u64 mom, u64 p16, u64 hp, const std::vector<float>& hv, long n,
+                       int nesterov, int zero_g, u64 s) {
+    check(ca_sgd_step(P(float*, p), P(void*, g), gbf, P(float*, mom), P(bf16_t*, p16), P(const float*, hp),
+                      hv.empty() ? nullptr : hv.data(), n, nesterov, zero_g, S(s)), "sgd_step");
   });
-  m.def("adam_step", [](u64 p, u64 g, int gbf, u64 mm, u64 vv, u64 p16, u64 hp, long n, int decoupled, u64 s) {
-    check(ca_adam_step(P(float*, p), P(const void*, g), gbf, P(float*, mm), P(float*, vv), P(bf16_t*, p16),
-                       P(const float*, hp), n, decoupled, S(s)), "adam_step");
+  m.def("adam_step", [](u64 p, u64 g, int gbf, u64 mm, u64 vv, u64 p16, u64 hp, const std::vector<float>& hv, long n,
+                        int decoupled, int zero_g, u64 s) {
+    check(ca_adam_step(P(float*, p), P(void*, g), gbf, P(float*, mm), P(float*, vv), P(bf16_t*, p16),
+                       P(const float*, hp), hv.empty() ? nullptr : hv.data(), n, decoupled, zero_g, S(s)), "adam_step");
   });
-  m.def("rmsprop_step", [](u64 p, u64 g, int gbf, u64 ms, u64 buf, u64 p16, u64 hp, long n, u64 s) {
-    check(ca_rmsprop_step(P(float*, p), P(const void*, g), gbf, P(float*, ms), P(float*, buf), P(bf16_t*, p16),
-                          P(const float*, hp), n, S(s)), "rmsprop_step");
+  m.def("rmsprop_step", [](u64 p, u64 g, int gbf, u64 ms, u64 buf, u64 p16, u64 hp, const std::vector<float>& hv,
+                           long n, int zero_g, u64 s) {
+    check(ca_rmsprop_step(P(float*, p), P(void*, g), gbf, P(float*, ms), P(float*, buf), P(bf16_t*, p16),
+                          P(const float*, hp), hv.empty() ? nullptr : hv.data(), n, zero_g, S(s)), "rmsprop_step");
   });
   m.def("sumsq", [](u64 g, int gbf, long n, u64 out, u64 s) {
     check(ca_sumsq(P(const void*, g), gbf, n, P(float*, out), S(s)), "sumsq");
@@ -213,6 +221,11 @@ PYBIND11_MODULE(_C, m) {
     check(ca_softmax_xent(P(const void*, z), zbf, P(const int64_t*, labels), B, C, gscale, ls, P(float*, loss),
                           P(float*, correct), P(void*, dz), S(s)), "softmax_xent");
   });
+  m.def("softmax_xent_batch", [](u64 z, int bf, u64 labels, int B, int C, float gs, float ls, u64 mean, u64 correct,
+                                 u64 dz, u64 acc, float acc_w, u64 s) {
+    check(ca_softmax_xent_batch(P(const void*, z), bf, P(const int64_t*, labels), B, C, gs, ls, P(float*, mean),
+                                P(float*, correct), P(void*, dz), P(float*, acc), acc_w, S(s)), "softmax_xent_batch");
+  });
   m.def("maxpool_fwd", [](u64 x, u64 y, u64 idx, int N, int H, int W, int C, int OH, int OW, int k, int st, int p,
                           u64 s) {
     check(ca_maxpool_fwd(P(const bf16_t*, x), P(bf16_t*, y), P(uint8_t*, idx), N, H, W, C, OH, OW, k, st, p, S(s)),
@@ -292,6 +305,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_splitk_effective", [](int K, int splits) { return ca_gemm_splitk_effective(K, splits); });
   m.def("gap_bwd", [](u64 dy, int dybf, u64 dx, int N, int HW, int C, u64 s) {
     check(ca_gap_bwd(P(const void*, dy), dybf, P(bf16_t*, dx), N, HW, C, S(s)), "gap_bwd");
+  });
+  m.def("gmp_fwd", [](u64 x, u64 y, u64 cnt, int N, int HW, int C, u64 s) {
+    check(ca_gmp_fwd(P(const bf16_t*, x), P(bf16_t*, y), P(float*, cnt), N, HW, C, S(s)), "gmp_fwd");
+  });
+  m.def("gmp_bwd", [](u64 dy, int dy_bf16, u64 x, u64 y, u64 cnt, u64 dx, int N, int HW, int C, u64 s) {
+    check(ca_gmp_bwd(P(const void*, dy), dy_bf16, P(const bf16_t*, x), P(const bf16_t*, y), P(const float*, cnt),
+                     P(bf16_t*, dx), N, HW, C, S(s)), "gmp_bwd");
   });
   m.def("gemm_ex", [](int layout, u64 A, long lda, u64 B, long ldb, u64 C, long ldc, int M, int N, int K, u64 stats,
                       float beta, u64 bias, int act, u64 preact, u64 dact_src, long ld_aux, u64 s) {

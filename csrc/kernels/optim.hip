@@ -55,6 +55,25 @@ __device__ __forceinline__ void st8bf(bf16_t* p, long i, const float (&o)[8]) {
   *reinterpret_cast<us8*>(p + i) = v;
 }
 
+// zero the 8 gradient elements just consumed (fused zero_grad for the next step)
+template <typename G>
+__device__ __forceinline__ void zero8(G* g, long i) {
+  if constexpr (sizeof(G) == 2) {
+    *reinterpret_cast<us8*>(g + i) = us8{0, 0, 0, 0, 0, 0, 0, 0};
+  } else {
+    *reinterpret_cast<f4*>(g + i) = f4{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f4*>(g + i + 4) = f4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+// Hyper-parameters by value (the per-step path: no host -> device copy, no stream sync)
+// or from device memory (hp != null: the hipGraph-capturable path, values refreshed by
+// the host before each replay).
+struct HpVals {
+  float v[8];
+};
+__device__ __forceinline__ float hpv(const float* hp, const HpVals& hv, int k) { return hp ? hp[k] : hv.v[k]; }
+
 template <typename G> __device__ __forceinline__ float gload(const G* g, long i);
 template <> __device__ __forceinline__ float gload<bf16_t>(const bf16_t* g, long i) { return bf2f(g[i]); }
 template <> __device__ __forceinline__ float gload<float>(const float* g, long i) { return g[i]; }
@@ -74,10 +93,12 @@ struct SgdOp {
 };
 
 template <typename G>
-__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const G* __restrict__ g,
+__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, G* __restrict__ g,
                                                   float* __restrict__ m, bf16_t* __restrict__ p16,
-                                                  const float* __restrict__ hp, long n, int nesterov) {
-  SgdOp op{hp[0], hp[1], hp[2], hp[3], hp[4], hp[5] != 0.f, nesterov != 0};
+                                                  const float* __restrict__ hp, HpVals hv, long n, int nesterov,
+                                                  int zero_g) {
+  SgdOp op{hpv(hp, hv, 0), hpv(hp, hv, 1), hpv(hp, hv, 2), hpv(hp, hv, 3), hpv(hp, hv, 4), hpv(hp, hv, 5) != 0.f,
+           nesterov != 0};
   const long nv = n / 8;
   const long stride = (long)gridDim.x * blockDim.x;
   for (long v = (long)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
@@ -85,6 +106,7 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const G
     float pv[8], gv[8], mv[8];
     ld8f(p, i, pv);
     load8<G>(g, i, gv);
+    if (zero_g) zero8<G>(g, i);
     if (op.mom != 0.f) ld8f(m, i, mv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) op(pv[j], mv[j], gv[j]);
@@ -95,6 +117,7 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const G
   for (long i = nv * 8 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float pp = p[i], mm = op.mom != 0.f ? m[i] : 0.f;
     op(pp, mm, gload<G>(g, i));
+    if (zero_g) g[i] = (G)0;
     p[i] = pp;
     if (op.mom != 0.f) m[i] = mm;
     if (p16) p16[i] = f2bf(pp);
@@ -120,11 +143,12 @@ struct AdamOp {
 };
 
 template <typename G>
-__global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const G* __restrict__ g,
+__global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, G* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16_t* __restrict__ p16, const float* __restrict__ hp,
-                                                   long n, int decoupled) {
-  AdamOp op{hp[0], hp[1], hp[2], hp[3], hp[4], hp[5], hp[6], hp[7], decoupled != 0};
+                                                   HpVals hv, long n, int decoupled, int zero_g) {
+  AdamOp op{hpv(hp, hv, 0), hpv(hp, hv, 1), hpv(hp, hv, 2), hpv(hp, hv, 3),
+            hpv(hp, hv, 4), hpv(hp, hv, 5), hpv(hp, hv, 6), hpv(hp, hv, 7), decoupled != 0};
   const long nv = n / 8;
   const long stride = (long)gridDim.x * blockDim.x;
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < nv; t += stride) {
@@ -132,6 +156,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const 
     float pv[8], gv[8], mv[8], vv[8];
     ld8f(p, i, pv);
     load8<G>(g, i, gv);
+    if (zero_g) zero8<G>(g, i);
     ld8f(m, i, mv);
     ld8f(v, i, vv);
 #pragma unroll
@@ -144,6 +169,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, const 
   for (long i = nv * 8 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float pp = p[i], mm = m[i], vv = v[i];
     op(pp, mm, vv, gload<G>(g, i));
+    if (zero_g) g[i] = (G)0;
     p[i] = pp; m[i] = mm; v[i] = vv;
     if (p16) p16[i] = f2bf(pp);
   }
@@ -168,15 +194,16 @@ struct RmsOp {
 };
 
 template <typename G>
-__global__ void __launch_bounds__(256) rmsprop_kernel(float* __restrict__ p, const G* __restrict__ g,
+__global__ void __launch_bounds__(256) rmsprop_kernel(float* __restrict__ p, G* __restrict__ g,
                                                       float* __restrict__ ms, float* __restrict__ buf,
                                                       bf16_t* __restrict__ p16, const float* __restrict__ hp,
-                                                      long n) {
-  RmsOp op{hp[0], hp[1], hp[2], hp[3], hp[4], hp[5]};
+                                                      HpVals hv, long n, int zero_g) {
+  RmsOp op{hpv(hp, hv, 0), hpv(hp, hv, 1), hpv(hp, hv, 2), hpv(hp, hv, 3), hpv(hp, hv, 4), hpv(hp, hv, 5)};
   const long stride = (long)gridDim.x * blockDim.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float pp = p[i], s = ms[i], b = buf ? buf[i] : 0.f;
     op(pp, s, b, gload<G>(g, i));
+    if (zero_g) g[i] = (G)0;
     p[i] = pp; ms[i] = s;
     if (buf) buf[i] = b;
     if (p16) p16[i] = f2bf(pp);
@@ -223,35 +250,46 @@ __global__ void __launch_bounds__(256) scale_kernel<bf16_t>(bf16_t* __restrict__
 // ------------------------------------------------------------ launchers --
 extern "C" {
 
-int ca_sgd_step(float* p, const void* g, int g_is_bf16, float* m, bf16_t* p16, const float* hp,
-                long n, int nesterov, hipStream_t s) {
+static HpVals hp_vals(const float* hv, int k) {
+  HpVals h{};
+  for (int i = 0; i < k && i < 8 && hv; ++i) h.v[i] = hv[i];
+  return h;
+}
+
+// hp: device hyper-parameters (graph-capturable path) or null, then hv (host array) is
+// passed by value; zero_g: also zero the gradient elements consumed (fused zero_grad).
+int ca_sgd_step(float* p, void* g, int g_is_bf16, float* m, bf16_t* p16, const float* hp, const float* hv, long n,
+                int nesterov, int zero_g, hipStream_t s) {
   const int B = 256, G = ca_stream_grid(n / 8 + 1, B);
+  const HpVals h = hp_vals(hv, 6);
   if (g_is_bf16)
-    sgd_kernel<bf16_t><<<G, B, 0, s>>>(p, (const bf16_t*)g, m, p16, hp, n, nesterov);
+    sgd_kernel<bf16_t><<<G, B, 0, s>>>(p, (bf16_t*)g, m, p16, hp, h, n, nesterov, zero_g);
   else
-    sgd_kernel<float><<<G, B, 0, s>>>(p, (const float*)g, m, p16, hp, n, nesterov);
+    sgd_kernel<float><<<G, B, 0, s>>>(p, (float*)g, m, p16, hp, h, n, nesterov, zero_g);
   CA_LAUNCH_CHECK();
   return 0;
 }
 
-int ca_adam_step(float* p, const void* g, int g_is_bf16, float* m, float* v, bf16_t* p16,
-                 const float* hp, long n, int decoupled, hipStream_t s) {
+int ca_adam_step(float* p, void* g, int g_is_bf16, float* m, float* v, bf16_t* p16, const float* hp, const float* hv,
+                 long n, int decoupled, int zero_g, hipStream_t s) {
   const int B = 256, G = ca_stream_grid(n / 8 + 1, B);
+  const HpVals h = hp_vals(hv, 8);
   if (g_is_bf16)
-    adam_kernel<bf16_t><<<G, B, 0, s>>>(p, (const bf16_t*)g, m, v, p16, hp, n, decoupled);
+    adam_kernel<bf16_t><<<G, B, 0, s>>>(p, (bf16_t*)g, m, v, p16, hp, h, n, decoupled, zero_g);
   else
-    adam_kernel<float><<<G, B, 0, s>>>(p, (const float*)g, m, v, p16, hp, n, decoupled);
+    adam_kernel<float><<<G, B, 0, s>>>(p, (float*)g, m, v, p16, hp, h, n, decoupled, zero_g);
   CA_LAUNCH_CHECK();
   return 0;
 }
 
-int ca_rmsprop_step(float* p, const void* g, int g_is_bf16, float* ms, float* buf, bf16_t* p16,
-                    const float* hp, long n, hipStream_t s) {
+int ca_rmsprop_step(float* p, void* g, int g_is_bf16, float* ms, float* buf, bf16_t* p16, const float* hp,
+                    const float* hv, long n, int zero_g, hipStream_t s) {
   const int B = 256, G = ca_stream_grid(n, B);
+  const HpVals h = hp_vals(hv, 6);
   if (g_is_bf16)
-    rmsprop_kernel<bf16_t><<<G, B, 0, s>>>(p, (const bf16_t*)g, ms, buf, p16, hp, n);
+    rmsprop_kernel<bf16_t><<<G, B, 0, s>>>(p, (bf16_t*)g, ms, buf, p16, hp, h, n, zero_g);
   else
-    rmsprop_kernel<float><<<G, B, 0, s>>>(p, (const float*)g, ms, buf, p16, hp, n);
+    rmsprop_kernel<float><<<G, B, 0, s>>>(p, (float*)g, ms, buf, p16, hp, h, n, zero_g);
   CA_LAUNCH_CHECK();
   return 0;
 }

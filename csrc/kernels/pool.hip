@@ -136,6 +136,73 @@ __global__ void __launch_bounds__(256) gap_bwd_kernel(const TI* __restrict__ dy,
   }
 }
 
+// Global max pool (Keras GlobalMaxPooling2D = reduce_max over H, W): y[n][c] = max_hw x, and
+// cnt[n][c] = how many positions attain it, so the backward splits the gradient evenly
+// over ties exactly as reduce_max's gradient (TF) / amax's (torch) does -- an all-zero
+// post-ReLU channel is an HW-way tie.  One thread per (n, 8-channel vector).
+__global__ void __launch_bounds__(256) gmp_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                      float* __restrict__ cnt, int N, int HW, int C) {
+  const int CT = C / 8;
+  const long total = (long)N * CT;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int vc = (int)(t % CT);
+    const int n = (int)(t / CT);
+    float m[8], k[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      m[j] = -INFINITY;
+      k[j] = 0.f;
+    }
+    const bf16_t* base = x + (long)n * HW * C + vc * 8;
+    for (int i = 0; i < HW; ++i) {
+      const us8 v = *reinterpret_cast<const us8*>(base + (long)i * C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = bf2f(v[j]);
+        if (f > m[j]) {
+          m[j] = f;
+          k[j] = 1.f;
+        } else if (f == m[j]) {
+          k[j] += 1.f;
+        }
+      }
+    }
+    us8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = f2bf(m[j]);
+      cnt[(long)n * C + vc * 8 + j] = k[j];
+    }
+    *reinterpret_cast<us8*>(y + (long)n * C + vc * 8) = o;
+  }
+}
+
+// dx = (x == y) * dy / cnt, written for every input element (no separate zero fill)
+template <typename TI>
+__global__ void __launch_bounds__(256) gmp_bwd_kernel(const TI* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                      const bf16_t* __restrict__ y, const float* __restrict__ cnt,
+                                                      bf16_t* __restrict__ dx, int N, int HW, int C) {
+  const int CT = C / 8;
+  const long total = (long)N * HW * CT;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int vc = (int)(t % CT);
+    const long r = t / CT;
+    const int n = (int)(r / HW);
+    const us8 xv = *reinterpret_cast<const us8*>(x + r * C + vc * 8);
+    const us8 yv = *reinterpret_cast<const us8*>(y + (long)n * C + vc * 8);
+    us8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long i = (long)n * C + vc * 8 + j;
+      float g;
+      if constexpr (sizeof(TI) == 2) g = bf2f(dy[i]);
+      else g = dy[i];
+      o[j] = xv[j] == yv[j] ? f2bf(g / cnt[i]) : (bf16_t)0;
+    }
+    *reinterpret_cast<us8*>(dx + r * C + vc * 8) = o;
+  }
+}
+
 }  // namespace
 
 // Space-to-depth of the network input for the 7x7/2 stem (pad 3):
@@ -455,6 +522,26 @@ int ca_gap_fwd(const bf16_t* x, void* y, int y_is_bf16, int N, int HW, int C, hi
   const long total = (long)N * (C / 8);
   if (y_is_bf16) gap_fwd_kernel<bf16_t><<<ca_stream_grid(total, 256), 256, 0, st>>>(x, (bf16_t*)y, N, HW, C);
   else gap_fwd_kernel<float><<<ca_stream_grid(total, 256), 256, 0, st>>>(x, (float*)y, N, HW, C);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+int ca_gmp_fwd(const bf16_t* x, bf16_t* y, float* cnt, int N, int HW, int C, hipStream_t st) {
+  if (C % 8) return -1;
+  const long total = (long)N * (C / 8);
+  gmp_fwd_kernel<<<ca_stream_grid(total, 256), 256, 0, st>>>(x, y, cnt, N, HW, C);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+int ca_gmp_bwd(const void* dy, int dy_is_bf16, const bf16_t* x, const bf16_t* y, const float* cnt, bf16_t* dx, int N,
+               int HW, int C, hipStream_t st) {
+  if (C % 8) return -1;
+  const long total = (long)N * HW * (C / 8);
+  if (dy_is_bf16)
+    gmp_bwd_kernel<bf16_t><<<ca_stream_grid(total, 256), 256, 0, st>>>((const bf16_t*)dy, x, y, cnt, dx, N, HW, C);
+  else
+    gmp_bwd_kernel<float><<<ca_stream_grid(total, 256), 256, 0, st>>>((const float*)dy, x, y, cnt, dx, N, HW, C);
   CA_LAUNCH_CHECK();
   return 0;
 }

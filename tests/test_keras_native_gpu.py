@@ -104,3 +104,40 @@ def test_keras_mnist_cnn_trains_on_native_kernels(monkeypatch):
     monkeypatch.undo()
     pred = model.predict(x[:8])
     assert pred.shape == (8, 10) and np.allclose(pred.sum(-1), 1.0, atol=1e-2)
+
+
+@pytest.mark.parametrize("N,H,W,C", [(4, 7, 7, 64), (3, 5, 9, 24)])
+def test_global_max_pool_native_matches_amax(N, H, W, C):
+    """Keras GlobalMaxPooling2D on the native kernel: forward = amax, backward splits the
+    gradient evenly over ties (all-zero post-ReLU channels are HW-way ties) as amax does."""
+    from cloud_amd import ops
+
+    torch.manual_seed(12)
+    x = torch.relu(torch.randn(N, H, W, C, device="cuda")).to(torch.bfloat16)
+    x[0, :, :, :5] = 0  # whole-channel ties
+    x[1, 0, 0, 7] = x[1, 1, 1, 7] = 9.0  # a two-way tie at the max
+    xr = x.float().clone().requires_grad_()
+    xn = x.clone().requires_grad_()
+    y = ops.global_max_pool_nhwc(xn)
+    yr = xr.amax(dim=(1, 2))
+    assert torch.equal(y.float(), yr)
+    g = torch.randn(N, C, device="cuda")
+    y.backward(g.to(torch.bfloat16))
+    yr.backward(g.to(torch.bfloat16).float())
+    torch.testing.assert_close(xn.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
+
+
+def test_keras_dropout_layer_native():
+    """Keras Dropout runs the native stateless-hash kernel on bf16 activations: keep rate,
+    1/(1-p) scaling, identity at inference, and the backward reuses the forward mask."""
+    from cloud_amd import tf
+
+    layer = tf.keras.layers.Dropout(0.25)
+    x = torch.ones(256, 1024, device="cuda", dtype=torch.bfloat16).requires_grad_()
+    y = layer(x, training=True)
+    kept = (y != 0).float().mean().item()
+    assert abs(kept - 0.75) < 5e-3
+    torch.testing.assert_close(y[y != 0].float(), torch.full_like(y[y != 0].float(), 1 / 0.75), rtol=1e-2, atol=0)
+    y.backward(torch.ones_like(y))
+    assert torch.equal(x.grad != 0, y != 0)
+    assert torch.equal(layer(x, training=False), x)
