@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""Memory-bound small-K GEMMs of ResNet-50 stage 1 at batch 512 (1x1 convs, NHWC):
-cloud_amd MFMA kernels vs hipBLASLt (torch.mm) vs a plain copy of the output size.
-Reports us and effective HBM TB/s (A read + C write [+ C read for beta]).  One JSON line per case."""
+"""Memory-bound small-K GEMMs of ResNet-50 stages 1-2 (1x1 convs, NHWC) at batch
+CLOUD_AMD_SMALLK_BATCH (default 1024): cloud_amd MFMA kernels (with and without the
+BN-statistics epilogue -- the ResNet forward form, on the persistent resident-weight core
+where it applies: compare runs with CLOUD_AMD_GEMM_PRW=0/1) vs hipBLASLt (torch.mm) vs a
+plain copy of the output size.  Reports us and effective HBM TB/s (A read + C write).
+One JSON line per case."""
 import json
 import os
 import sys
@@ -17,12 +20,13 @@ def main():
     ext = _ext.load(required=True)
     dev = torch.device("cuda", 0)
     st = _ext.stream_handle(dev)
-    for (M, K, N) in [(512 * 56 * 56, 64, 256), (512 * 56 * 56, 256, 64), (512 * 56 * 56, 64, 64),
-                      (512 * 28 * 28, 128, 512), (512 * 28 * 28, 512, 128)]:
+    B = int(os.environ.get("CLOUD_AMD_SMALLK_BATCH", "1024"))
+    for (M, K, N) in [(B * 56 * 56, 64, 256), (B * 56 * 56, 256, 64), (B * 56 * 56, 64, 64),
+                      (B * 56 * 56, 256, 128), (B * 28 * 28, 128, 512), (B * 28 * 28, 512, 128)]:
         a = torch.randn(M, K, device=dev).to(torch.bfloat16)
         w = torch.randn(N, K, device=dev).to(torch.bfloat16)
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        stats = torch.empty(((M + 127) // 128, 2, N), device=dev)
+        stats = raw.gemm_stats_buffer(M, N, K, dev)
         byts = (M * K + M * N) * 2
 
         def ours():
@@ -45,7 +49,7 @@ def main():
         def readsum():
             torch.sum(src, dtype=torch.float32)
 
-        r = {"M": M, "K": K, "N": N}
+        r = {"M": M, "K": K, "N": N, "stat_rows": stats.shape[0], "prw": os.environ.get("CLOUD_AMD_GEMM_PRW", "1")}
         for name, fn, b in [("ours", ours, byts), ("ours_stats", ours_st, byts), ("hipblaslt", blas, byts),
                             ("copy_C", copy, 2 * M * N * 2),
                             ("fill_C", fill, M * N * 2), ("read_C", readsum, M * N * 2)]:

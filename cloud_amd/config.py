@@ -70,6 +70,9 @@ _VARS = [
         "with 4 x 1 waves; 0 = 128 x 64 with 2 x 2 waves", "ops"),
     Var("CLOUD_AMD_BN_GROUPS_MAX", int, 512, "BatchNorm statistics: most groups of the first-level reduction of the "
         "per-tile partial rows (1..512; ~64 rows per group)", "ops"),
+    Var("CLOUD_AMD_GEMM_PRW", bool, True, "forward 1x1 convolutions with the BN-statistics epilogue and a "
+        "weight of <= 32K elements (N x K in {64,256} x 64, {64,128} x 256): persistent resident-weight core "
+        "(csrc/include/ca_gemm_prw.h); 0 = the tiled 128 core", "ops"),
     Var("CLOUD_AMD_EPI_PF", bool, True, "GEMM epilogues that read memory or run an activation (BN-statistics "
         "forward 1x1 convs, BERT bias/GELU/GELU'/beta dense layers): 4 staged output rows in flight per trip", "ops"),
     Var("CLOUD_AMD_SPLITK_INLAUNCH", bool, False, "split-K weight gradients (dense and conv): 1 = the last-arriving "

@@ -102,10 +102,7 @@ def can_fuse(blk, x):
 
 
 def _conv_bn(conv, bn, x, residual=None):
-    N, H, W, _ = x.shape
-    OH = raw.out_hw(H, conv.k, conv.stride, conv.padding)
-    OW = raw.out_hw(W, conv.k, conv.stride, conv.padding)
-    part = raw.stats_buffer(N * OH * OW, conv.cout, x.device)
+    part = raw.conv_stats_buffer(x.shape, conv.weight, conv.stride, conv.padding, x.device)
     z = raw.conv_fwd(x, conv.weight, conv.stride, conv.padding, stats=part)
     y, st, mask = raw.bn_fwd(z, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, bn.momentum,
                              bn.relu, residual=residual, partials=part, keep_mask=True)
@@ -125,15 +122,13 @@ class _BottleneckFn(torch.autograd.Function):
             # projection shortcut: its BN is folded into bn3's apply (statistics only here;
             # the shortcut BN output is never written)
             c, bnd = ds["conv"], ds["bn"]
-            N, H, W, _ = x.shape
-            OH, OW = raw.out_hw(H, c.k, c.stride, c.padding), raw.out_hw(W, c.k, c.stride, c.padding)
-            part_d = raw.stats_buffer(N * OH * OW, c.cout, x.device)
+            part_d = raw.conv_stats_buffer(x.shape, c.weight, c.stride, c.padding, x.device)
             zd = raw.conv_fwd(x, c.weight, c.stride, c.padding, stats=part_d)
             st_d = raw.bn_fwd_stats(zd, bnd.weight, bnd.bias, bnd.running_mean, bnd.running_var, bnd.eps,
                                     bnd.momentum, part_d)
             sd = (st_d, None)
             c3, bn3 = blk.conv3, blk.bn3
-            part3 = raw.stats_buffer(y2.numel() // y2.shape[-1], c3.cout, x.device)
+            part3 = raw.conv_stats_buffer(y2.shape, c3.weight, c3.stride, c3.padding, x.device)
             z3 = raw.conv_fwd(y2, c3.weight, c3.stride, c3.padding, stats=part3)
             C3 = c3.cout
             out, st3, mask3 = raw.bn_fwd(z3, bn3.weight, bn3.bias, bn3.running_mean, bn3.running_var, bn3.eps,

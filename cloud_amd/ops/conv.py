@@ -23,7 +23,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import config
-from . import _ext, gemm
+from . import _ext, gemm, raw
 
 
 def _out(n, k, s, p):
@@ -207,7 +207,7 @@ def conv2d_nhwc(x, w, bias=None, stride=1, padding=0, stats=False):
     if KH == 1 and KW == 1 and padding == 0 and stride == 1:
         x2 = x.reshape(N * H * W, Cin)
         if native and stats and gemm._native_ok(N * H * W, Cout, Cin):
-            part = stats_buffer(N * H * W, Cout, x.device)
+            part = raw.gemm_stats_buffer(N * H * W, Cout, Cin, x.device)
         y = gemm.linear(x2, w.reshape(Cout, Cin), bias, param=w, stats=part).view(N, H, W, Cout)
         return (y, part) if stats else y
     if native:

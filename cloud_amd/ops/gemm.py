@@ -151,10 +151,17 @@ def linear(x, w, bias=None, param=None, stats=None):
 
 
 def fill_stats_torch(y2d, stats):
-    """Reference/fallback for the fused BN-statistics epilogue ([tiles][2][C], 128-row tiles)."""
+    """Reference/fallback for the fused BN-statistics epilogue ([tiles][2][C], 128-row tiles;
+    a buffer with fewer rows -- the persistent core's one per workgroup -- gets the column
+    sums in row 0 and zeros elsewhere: consumers only ever sum the rows)."""
     M, C = y2d.shape
     tiles = stats.shape[0]
     yf = y2d.float()
+    if tiles * 128 < M:
+        stats.zero_()
+        stats[0, 0].copy_(yf.sum(0))
+        stats[0, 1].copy_((yf * yf).sum(0))
+        return
     pad = tiles * 128 - M
     if pad:
         yf = torch.cat([yf, yf.new_zeros(pad, C)])

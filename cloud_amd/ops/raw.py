@@ -51,6 +51,24 @@ def stats_buffer(rows, channels, device):
     return torch.empty(((rows + 127) // 128, 2, channels), dtype=torch.float32, device=device)
 
 
+def gemm_stats_buffer(M, N, K, device, lda=None, ldb=None, ldc=None):
+    """Partials buffer for a forward (NT) GEMM with the BN-statistics epilogue: the
+    persistent resident-weight core writes one row per workgroup, the tiled cores one per
+    128 rows (``ext.gemm_stat_rows`` says which)."""
+    ext = _ext.load(required=True)
+    rows = ext.gemm_stat_rows(int(M), int(N), int(K), int(lda or K), int(ldb or K), int(ldc or N))
+    return torch.empty((rows, 2, N), dtype=torch.float32, device=device)
+
+
+def conv_stats_buffer(x_shape, w, stride, padding, device):
+    """Partials buffer for :func:`conv_fwd` ``stats=`` of x [N, H, W, Cin] * w [Cout, KH, KW, Cin]."""
+    N, H, W, Cin = x_shape
+    Cout, KH, KW, _ = w.shape
+    if is_gemm_conv(w, stride, padding):
+        return gemm_stats_buffer(N * H * W, Cout, Cin, device)
+    return stats_buffer(N * out_hw(H, KH, stride, padding) * out_hw(W, KW, stride, padding), Cout, device)
+
+
 _WGRAD_BLOCKS = None
 _GWS_ROWS = 512  # BN statistics group workspace rows (bn.hip group_count)
 _WGRAD_BLOCKS_SMALLM = None

@@ -55,6 +55,7 @@ int ca_gmp_bwd(const void*, int, const bf16_t*, const bf16_t*, const float*, bf1
 int ca_gemm_bf16(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float*, float,
                  hipStream_t);
 int ca_gemm_set_core(int);
+int ca_gemm_stat_rows(int, int, int, long, long, long);
 int ca_bn_relu_maxpool_s2k3(const bf16_t*, const float*, bf16_t*, uint8_t*, int, int, int, int, int, int, hipStream_t);
 int ca_maxpool_bnstats_parts(int, int, int, int);
 int ca_maxpool_bwd_s2k3_bnstats(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, bf16_t*, float*, int, int,
@@ -301,6 +302,9 @@ PYBIND11_MODULE(_C, m) {
                           int N, int K, int splits, u64 ws, u64 s) {
     check(ca_gemm_splitk(layout, P(const bf16_t*, A), lda, P(const bf16_t*, B), ldb, P(void*, out), out_bf16, beta,
                          M, N, K, splits, P(float*, ws), S(s)), "gemm_splitk");
+  });
+  m.def("gemm_stat_rows", [](int M, int N, int K, long lda, long ldb, long ldc) {
+    return ca_gemm_stat_rows(M, N, K, lda, ldb, ldc);
   });
   m.def("gemm_splitk_effective", [](int K, int splits) { return ca_gemm_splitk_effective(K, splits); });
   m.def("gap_bwd", [](u64 dy, int dybf, u64 dx, int N, int HW, int C, u64 s) {

@@ -11,7 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "ca_gemm256.h"
+#include "ca_gemm_prw.h"
 
 namespace {
 using namespace ca;
@@ -78,6 +78,88 @@ int core_kind() {
   return g_core_kind;
 }
 bool use_glds() { return core_kind() != 0; }
+
+// Persistent resident-weight core (csrc/include/ca_gemm_prw.h) for the small-K forward 1x1
+// convolutions with the BN-statistics epilogue.
+template <int BN, int KT, int NS, bool STATS>
+__global__ void __launch_bounds__(512) prw_gemm_kernel(CoreParams P) {
+  prw_gemm_body<BN, KT, NS, STATS>(P);
+}
+
+// CLOUD_AMD_GEMM_PRW=0 keeps these GEMMs on the data-parallel 128 core (A/B runs)
+bool prw_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_GEMM_PRW");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
+}
+
+int cu_count() {
+  static int n = -1;
+  if (n < 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+         prop.multiProcessorCount > 0)
+            ? prop.multiProcessorCount
+            : 256;
+  }
+  return n;
+}
+
+// (N, K) -> instantiation id; 0 = not covered.  The whole [N][K] weight stays in LDS.
+int prw_kind(int M, int N, int K, long lda, long ldb, long ldc) {
+  if (!prw_enabled() || lda != K || ldb != K || ldc != N || M < 128) return 0;
+  if ((long)M * K * 2 >= (long)BUF_CAP || (long)M * N * 2 >= (long)BUF_CAP) return 0;
+  if (N == 64 && K == 64) return 1;
+  if (N == 256 && K == 64) return 2;
+  if (N == 64 && K == 256) return 3;
+  if (N == 128 && K == 256) return 4;
+  return 0;
+}
+
+template <int BN, int KT, int NS>
+int prw_grid_for(int M) {
+  constexpr int bytes = PrwGeom<BN, KT, NS>::BYTES;
+  static_assert(bytes <= 160 * 1024, "LDS");
+  int per_cu = (160 * 1024) / bytes;
+  if (per_cu > 4) per_cu = 4;
+  const int tiles = (M + 127) / 128;
+  const int g = cu_count() * per_cu;
+  return g < tiles ? g : tiles;
+}
+
+int prw_grid(int kind, int M) {
+  switch (kind) {
+    case 1: return prw_grid_for<64, 64, 8>(M);
+    case 2: return prw_grid_for<256, 64, 3>(M);
+    case 3: return prw_grid_for<64, 256, 6>(M);
+    case 4: return prw_grid_for<128, 256, 3>(M);
+  }
+  return 0;
+}
+
+int prw_launch(int kind, const CoreParams& p, hipStream_t s) {
+  const int g = prw_grid(kind, p.M);
+  const bool st = p.stats != nullptr;
+#define CA_PRW(BN_, KT_, NS_)                                                             \
+  do {                                                                                    \
+    if (st) prw_gemm_kernel<BN_, KT_, NS_, true><<<g, 512, 0, s>>>(p);                    \
+    else prw_gemm_kernel<BN_, KT_, NS_, false><<<g, 512, 0, s>>>(p);                      \
+  } while (0)
+  switch (kind) {
+    case 1: CA_PRW(64, 64, 8); break;
+    case 2: CA_PRW(256, 64, 3); break;
+    case 3: CA_PRW(64, 256, 6); break;
+    case 4: CA_PRW(128, 256, 3); break;
+    default: return -2;
+  }
+#undef CA_PRW
+  CA_LAUNCH_CHECK();
+  return 0;
+}
 
 template <bool OUT_BF16>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, int S, long MN,
@@ -317,10 +399,21 @@ int ca_gemm_bf16(int layout, const bf16_t* A, long lda, const bf16_t* B, long ld
   CoreParams p = base_params(A, lda, B, ldb, C, ldc, M, N, K);
   p.stats = stats;
   p.beta = beta;
-  if (stats && layout == 0)  // forward 1x1 conv feeding a BatchNorm: register-accumulated statistics
+  if (!stats && layout == 0 && prw_kind(M, N, K, lda, ldb, ldc) == 2) return prw_launch(2, p, s);
+  if (stats && layout == 0) {  // forward 1x1 conv feeding a BatchNorm: register-accumulated statistics
+    const int kind = prw_kind(M, N, K, lda, ldb, ldc);
+    if (kind) return prw_launch(kind, p, s);  // one partial row per workgroup (ca_gemm_stat_rows)
     return want_small_n(p, 1) ? launch<128, 64, DenseKC, DenseKC, GDenseKC, GDenseKC, EPI_BF16_ST>(p, 1, s)
                               : launch<128, 128, DenseKC, DenseKC, GDenseKC, GDenseKC, EPI_BF16_ST>(p, 1, s);
+  }
   return dispatch<EPI_BF16>(layout, p, 1, s);
+}
+
+// Rows of the [rows][2][N] statistics partials ca_gemm_bf16(layout 0, stats != null) writes:
+// one per workgroup on the persistent core, one per 128 GEMM rows otherwise.
+int ca_gemm_stat_rows(int M, int N, int K, long lda, long ldb, long ldc) {
+  const int kind = prw_kind(M, N, K, lda, ldb, ldc);
+  return kind ? prw_grid(kind, M) : (M + 127) / 128;
 }
 
 // Input-gradient GEMM (NN: dX = dY W) whose output feeds a BatchNorm(+ReLU) backward:

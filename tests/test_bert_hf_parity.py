@@ -121,13 +121,20 @@ def test_native_bf16_path_matches_hf_fp32_gpu(dims):
     loss.backward()
     torch.testing.assert_close(logits.float(), ref_logits, atol=3e-2, rtol=3e-2)
     torch.testing.assert_close(loss, ref_loss, atol=2e-2, rtol=2e-2)
-    worst = []
-    for get, hp in pairs:
+    key_bias = {id(H.attention.self.key.bias) for H in hf.bert.encoder.layer}
+    q_scale = max(float(H.attention.self.query.bias.grad.norm()) for H in hf.bert.encoder.layer)
+    worst, bad = [], []
+    for idx, (get, hp) in enumerate(pairs):
         g = _our_grad(ours, get).float()
-        # the key-projection bias has an exactly-zero true gradient (softmax is invariant to
-        # a per-query constant): |HF| ~ 1e-11, ours ~ 1e-7 of bf16 noise -- hence the floor
-        rel = float((g - hp.grad).norm() / hp.grad.norm().clamp_min(1e-5))
+        if id(hp) in key_bias:
+            # the key-projection bias has an exactly-zero true gradient (softmax is invariant
+            # to a per-query constant): HF's is fp32 round-off, ours bf16 round-off -- both must
+            # be negligible next to the query-bias gradient, which flows through the same scores
+            rel = float(g.norm()) / max(q_scale, 1e-12)
+        else:
+            rel = float((g - hp.grad).norm() / hp.grad.norm().clamp_min(1e-6))
         worst.append(rel)
-        assert rel < 3e-2, (dims, tuple(hp.shape), rel)
+        if rel >= 3e-2:
+            bad.append((idx, tuple(hp.shape), rel))
     print("worst relative gradient error (%s): %.3e" % (dims, max(worst)))
-    assert max(worst) < 3e-2
+    assert not bad, (dims, bad)
