@@ -54,10 +54,11 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one per MI355X)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("CLOUD_AMD_BENCH_BATCH", 1024)),
-                    help="per-GPU batch (default 1024: 41 GB of the 288 GB HBM3E; 8 GPUs -> the 8,192-image "
-                         "global batch of large-batch ImageNet training)")
-    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="per-GPU batch (ResNet-50 default 1024 or CLOUD_AMD_BENCH_BATCH: 41 GB of the 288 GB "
+                         "HBM3E; 8 GPUs -> the 8,192-image global batch of large-batch ImageNet training; "
+                         "--model tiny default 8)")
+    ap.add_argument("--image-size", type=int, default=None, help="default 224 (ResNet-50), 32 (--model tiny)")
     ap.add_argument("--classes", type=int, default=1000)
     ap.add_argument("--model", choices=("resnet50", "tiny"), default="resnet50")
     ap.add_argument("--device", choices=("auto", "cpu"), default="auto")
@@ -126,6 +127,10 @@ def main():
         sys.exit(3)
     dtype = torch.bfloat16 if on_gpu else torch.float32
     torch.manual_seed(1234)  # identical init on every rank (also broadcast below)
+    if args.batch is None:
+        args.batch = int(os.environ.get("CLOUD_AMD_BENCH_BATCH", 1024)) if args.model == "resnet50" else 8
+    if args.image_size is None:
+        args.image_size = 224 if args.model == "resnet50" else 32
     B, S = args.batch, args.image_size
     build = resnet50 if args.model == "resnet50" else resnet18_like_small
     model = build(num_classes=args.classes, dtype=dtype, device=device)

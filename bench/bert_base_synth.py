@@ -72,6 +72,21 @@ def _finite(o):
     return o
 
 
+def _plain_gemm_summary():
+    """Per plain-GEMM shape: which engine the measured policy kept (ops/raw.py PlainGemmPolicy)."""
+    try:
+        from cloud_amd.ops import raw
+    except Exception:  # pragma: no cover
+        return None
+    out = {}
+    for (layout, M, N, K, bias, beta), d in raw.PLAIN_GEMM.decisions.items():
+        name = "%s %dx%dx%d%s%s" % ("NT" if layout == 0 else "NN", M, N, K, "+bias" if bias else "",
+                                    "+C" if beta else "")
+        out[name] = "%s (ours %.1f us, hipBLASLt %.1f us)" % ("hipBLASLt" if d["library"] else "ours", d["ours_us"],
+                                                             d["lib_us"])
+    return out or None
+
+
 def main():
     args = parse()
     from cloud_amd.utils import benchlaunch
@@ -192,7 +207,8 @@ def main():
             "shared_gpu": bool(config.get("CLOUD_AMD_SHARED_GPU")),
             "tokens_per_sec": round(sps * S, 1), "final_loss": round(float(loss.detach().float()), 4),
             "strategy": strategy.name, "replicas_consistent": replicas_consistent,
-            "rank_ms_per_step": {"min": round(min(per_rank), 3), "max": round(max(per_rank), 3)}}),
+            "rank_ms_per_step": {"min": round(min(per_rank), 3), "max": round(max(per_rank), 3)},
+            "plain_gemm_engine": _plain_gemm_summary()}),
             allow_nan=False), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -70,6 +70,11 @@ _VARS = [
         "with 4 x 1 waves; 0 = 128 x 64 with 2 x 2 waves", "ops"),
     Var("CLOUD_AMD_BN_GROUPS_MAX", int, 512, "BatchNorm statistics: most groups of the first-level reduction of the "
         "per-tile partial rows (1..512; ~64 rows per group)", "ops"),
+    Var("CLOUD_AMD_GEMM_LIB", str, "auto", "plain bf16 GEMMs (bias / accumulate only, no fused epilogue): 'auto' "
+        "times the in-tree kernel against hipBLASLt once per shape and keeps the faster, 'never', 'always' "
+        "(ops/raw.py PlainGemmPolicy)", "ops"),
+    Var("CLOUD_AMD_WGRAD64_WIDE", bool, False, "weight gradients of <= 64-output-channel convolutions with > 128 "
+        "columns (ResNet layer-1 3x3): 64 x 256 tiles of 1 x 4 waves instead of 64 x 128 / 2 x 2", "ops"),
     Var("CLOUD_AMD_GEMM_PRW", bool, True, "forward 1x1 convolutions with the BN-statistics epilogue and a "
         "weight of <= 32K elements (N x K in {64,256} x 64, {64,128} x 256): persistent resident-weight core "
         "(csrc/include/ca_gemm_prw.h); 0 = the tiled 128 core", "ops"),
@@ -120,9 +125,13 @@ _VARS = [
         "distributed"),
     Var("CLOUD_AMD_KFD_ROOT", str, "/sys/class/kfd/kfd/topology/nodes", "KFD topology root read by the "
         "node probe (tests point it at a fake tree)", "launcher"),
+    Var("CLOUD_AMD_TUNER_STANDBY", bool, True, "trial scheduler: start the packing wave's workers with the probe "
+        "wave, gated (imports done, no GPU touched) until the measured footprint says how many may run", "tuner"),
     Var("CLOUD_AMD_FOOTPRINT_FILE", str, None, "where a tuner worker reports its first trial's peak HBM "
         "(set by TrialScheduler for the probe wave)", "tuner"),
     Var("CLOUD_AMD_BENCH_VIA_RUN", bool, True, "bench scripts launch their ranks through cloud_amd.run()",
+        "bench"),
+    Var("CLOUD_AMD_SMALLK_BATCH", int, 1024, "bench/smallk_gemm.py: ResNet batch the GEMM shapes are taken at",
         "bench"),
     Var("CLOUD_AMD_BENCH_ALLOW_CPU", bool, False, "let bench.py run ResNet-50 on CPU (debug only)", "bench"),
     Var("CLOUD_AMD_DDP_ORDER", str, "event", "bucket ordering: 'event' (comm stream waits on a compute event), "

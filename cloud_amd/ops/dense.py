@@ -62,6 +62,43 @@ def _act_grad(g, y, pre, act):
     return out.to(torch.bfloat16).contiguous()
 
 
+def _act_grad_dev(dy, src, N, Np, act):
+    """Native form of :func:`_act_grad` (rowops.hip act_grad): ``dy`` [M, N] (any row
+    stride) zero-padded to Np columns and multiplied by act'(src) in one pass; ``src`` is
+    the saved output (relu / elu / tanh) or pre-activation (gelu), [M, Np] contiguous."""
+    ext = _ext.load(required=True)
+    if dy.stride(-1) != 1:
+        dy = dy.contiguous()
+    M = dy.shape[0]
+    out = torch.empty((M, Np), dtype=torch.bfloat16, device=dy.device)
+    code = ACT[act] if act in ACT else 0
+    if src is None:
+        src, code = out, 0  # padding only: src is never read with act code 0 ... but must be a valid pointer
+    ext.act_grad(dy.data_ptr(), dy.stride(0), N, src.data_ptr(), out.data_ptr(), M, Np, code,
+                 _ext.stream_handle(dy.device))
+    return out
+
+
+def _bias_grad(ext, g, M, Np, N, bparam, st):
+    """Column sums of g [M, Np] as the bias gradient: accumulated straight into the arena
+    slot (and the DP engine notified) when there is one of the right width; otherwise
+    returned as (autograd grad, db) like :func:`_deliver`."""
+    ws = torch.empty(ext.colsum_workspace_floats(M, Np), dtype=torch.float32, device=g.device)
+    sink = _arena_grad(bparam)
+    if sink is not None and sink.dtype == torch.float32 and N == Np:
+        ext.colsum(g.data_ptr(), M, Np, Np, sink.data_ptr(), 1, ws.data_ptr(), st)
+        from ..parallel import ddp
+
+        ddp.notify_grad_ready(bparam)
+        return None, None
+    acc = torch.empty(Np, dtype=torch.float32, device=g.device)
+    ext.colsum(g.data_ptr(), M, Np, Np, acc.data_ptr(), 0, ws.data_ptr(), st)
+    sl = acc[:N]
+    if bparam is not None:
+        return _deliver(bparam, acc, sl), None
+    return None, sl
+
+
 def fusable(act):
     return act in ACT
 
@@ -126,8 +163,11 @@ class _DenseFn(torch.autograd.Function):
         ext = _ext.load(required=True)
         xp, wp, y, pre = ctx.saved_tensors
         M, K, N, Kp, Np = ctx.dims
-        dyp = dy if Np == N else F.pad(dy, (0, Np - N))
-        g = _act_grad(dyp, y, pre, ctx.act)
+        if ctx.act in (None, "linear") and Np == N:
+            g = dy.contiguous()
+        else:
+            g = _act_grad_dev(dy, pre if ctx.act == "gelu" else (y if ctx.act not in (None, "linear") else None), N,
+                              Np, ctx.act)
         dx = dw = db = dwp = dbp = None
         if ctx.needs_input_grad[0]:
             dxp = _gemm.mm_nn(g, wp)
@@ -148,14 +188,7 @@ class _DenseFn(torch.autograd.Function):
                 else:
                     dw = sl.to(wp.dtype)
         if ctx.has_b and (ctx.needs_input_grad[2] or ctx.bparam is not None):
-            acc = torch.zeros(Np, dtype=torch.float32, device=g.device)
-            ws = torch.empty(ext.colsum_workspace_floats(M, Np), dtype=torch.float32, device=g.device)
-            ext.colsum(g.data_ptr(), M, Np, Np, acc.data_ptr(), 0, ws.data_ptr(), _ext.stream_handle(g.device))
-            sl = acc[:N]
-            if ctx.bparam is not None:
-                dbp = _deliver(ctx.bparam, acc, sl)
-            else:
-                db = sl
+            dbp, db = _bias_grad(ext, g, M, Np, N, ctx.bparam, _ext.stream_handle(g.device))
         return dx, dw, db, None, dwp, dbp
 
 
@@ -222,7 +255,11 @@ class _ConvActFn(torch.autograd.Function):
         Cout, KH, KW, _ = wp.shape
         OH, OW = y.shape[1], y.shape[2]
         st = _ext.stream_handle(dy.device)
-        g = _act_grad(dy, y, None, act)
+        Mo = N * OH * OW
+        if act in (None, "linear"):
+            g = dy.contiguous()
+        else:
+            g = _act_grad_dev(dy.reshape(Mo, Cout), y.reshape(Mo, Cout), Cout, Cout, act).view_as(y)
         dx = dw = db = dwp = dbp = None
         if ctx.needs_input_grad[0]:
             dxp = torch.empty_like(xp)
@@ -250,14 +287,7 @@ class _ConvActFn(torch.autograd.Function):
                 else:
                     dw = sl.to(wp.dtype)
         if ctx.has_b and (ctx.needs_input_grad[2] or ctx.bparam is not None):
-            acc = torch.zeros(Cout, dtype=torch.float32, device=dy.device)
-            M = N * OH * OW
-            wsb = torch.empty(ext.colsum_workspace_floats(M, Cout), dtype=torch.float32, device=dy.device)
-            ext.colsum(g.data_ptr(), M, Cout, Cout, acc.data_ptr(), 0, wsb.data_ptr(), st)
-            if ctx.bparam is not None:
-                dbp = _deliver(ctx.bparam, acc, acc)
-            else:
-                db = acc
+            dbp, db = _bias_grad(ext, g, Mo, Cout, Cout, ctx.bparam, st)
         return dx, dw, db, None, None, None, dwp, dbp
 
 

@@ -70,6 +70,7 @@ def conv_stats_buffer(x_shape, w, stride, padding, device):
 
 
 _WGRAD_BLOCKS = None
+_WGRAD64_WIDE = os.environ.get("CLOUD_AMD_WGRAD64_WIDE", "0") == "1"
 _GWS_ROWS = 512  # BN statistics group workspace rows (bn.hip group_count)
 _WGRAD_BLOCKS_SMALLM = None
 _DENSE_WGRAD_BLOCKS = None
@@ -188,7 +189,11 @@ def conv_wgrad(dy, x, w_shape, stride, padding, out, beta=1.0, blocks=None):
     # <= 128 output channels: one row of tiles, so the grid is mostly K splits; the fp32
     # slabs stay small next to the pixel operands, and more splits fill the CUs
     target = blocks or (_WGRAD_BLOCKS_SMALLM if Cout <= 128 else _WGRAD_BLOCKS)
-    splits = ext.gemm_splitk_effective(kred, wgrad_splits(Cout, ncols, kred, target_blocks=target))
+    if Cout <= 64 and ncols > 128 and _WGRAD64_WIDE:  # 64 x 256 tiles (conv.hip wgrad64_wide)
+        tiles = (ncols + 255) // 256
+        splits = ext.gemm_splitk_effective(kred, max(1, min(max(kred // 512, 1), (target + tiles - 1) // tiles)))
+    else:
+        splits = ext.gemm_splitk_effective(kred, wgrad_splits(Cout, ncols, kred, target_blocks=target))
     ws = torch.empty(splits * Cout * ncols, dtype=torch.float32, device=x.device)
     obf = int(out.dtype == torch.bfloat16)
     if KH == 1 and KW == 1 and stride == 1 and padding == 0:
@@ -288,15 +293,103 @@ def bn_bwd(dy, y, x, gamma, stats, relu, dgamma=None, dbeta=None, want_dres=Fals
 ACT = {None: 0, "none": 0, "linear": 0, "gelu": 1, "relu": 2, "tanh": 3, "gelu_tanh": 4}
 
 
+class PlainGemmPolicy:
+    """Which engine runs a PLAIN bf16 GEMM -- no activation, no pre-activation store, no
+    act' multiply, no statistics; optional bias and C accumulate (beta = 1): the in-tree
+    MFMA kernels or the vendor library (hipBLASLt through torch), the one the task's
+    rules reserve for "plain library GEMMs".  Every fused GEMM (bias + GELU + pre-activation,
+    GELU' backward, BN statistics, split-K weight gradients into the fp32 arena) stays on
+    the in-tree kernels.
+
+    ``CLOUD_AMD_GEMM_LIB``: ``auto`` (default) times both engines once per (layout, M, N, K,
+    bias, beta) key on the first call -- on scratch outputs, outside any stream capture --
+    and keeps the faster (like a cuDNN benchmark cache; ``decisions`` records the timings);
+    ``never`` = in-tree only; ``always`` = library for every plain GEMM."""
+
+    def __init__(self):
+        self.mode = None
+        self.decisions = {}
+
+    def _mode(self):
+        if self.mode is None:
+            from .. import config
+
+            self.mode = config.get("CLOUD_AMD_GEMM_LIB")
+        return self.mode
+
+    @staticmethod
+    def _time(fn, reps=5):
+        for _ in range(2):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1000.0 / reps
+
+    def use_library(self, key, ours, lib):
+        mode = self._mode()
+        if mode == "never":
+            return False
+        if mode == "always":
+            return True
+        d = self.decisions.get(key)
+        if d is None:
+            if torch.cuda.is_current_stream_capturing():
+                return False
+            t_ours, t_lib = self._time(ours), self._time(lib)
+            d = self.decisions[key] = {"library": t_lib < 0.97 * t_ours, "ours_us": round(t_ours, 1),
+                                       "lib_us": round(t_lib, 1)}
+        return d["library"]
+
+
+PLAIN_GEMM = PlainGemmPolicy()
+
+
+def _plain_lib(a, w, bias, out, beta, layout):
+    """The library form of a plain GEMM into ``out`` (bias added in bf16, as autocast does)."""
+    wm = w.t() if layout == NT else w
+    if beta:
+        out.addmm_(a, wm)
+        if bias is not None:
+            out.add_(bias.to(out.dtype))
+    elif bias is not None:
+        torch.addmm(bias.to(out.dtype), a, wm, out=out)
+    else:
+        torch.mm(a, wm, out=out)
+    return out
+
+
 def gemm(a, w, bias=None, act=None, preact=None, out=None, beta=0.0, layout=NT, dact_src=None, stats=None):
     """Fused dense GEMM.  NT: out[M,N] = act(a[M,K] @ w[N,K]^T + bias); NN: a[M,K] @ w[K,N].
     ``preact`` receives the pre-activation; ``dact_src`` switches to the backward
-    form out = (a @ w) * act'(dact_src).  Row strides of ``a`` are honoured."""
+    form out = (a @ w) * act'(dact_src).  Row strides of ``a`` are honoured.  Plain GEMMs
+    (see :class:`PlainGemmPolicy`) may run on the vendor library when it measures faster."""
     ext = _ext.load(required=True)
     M, K = a.shape
     N = w.shape[0] if layout == NT else w.shape[1]
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if (act in (None, "none", "linear") and preact is None and dact_src is None and stats is None
+            and beta in (0.0, 1.0) and layout in (NT, NN) and a.is_cuda and a.stride(1) == 1 and w.is_contiguous()
+            and out.is_contiguous() and (bias is None or layout == NT) and PLAIN_GEMM._mode() != "never"):
+        key = (layout, M, N, K, bias is not None, float(beta))
+        if key not in PLAIN_GEMM.decisions and PLAIN_GEMM._mode() == "auto":
+            scratch = torch.zeros_like(out)
+
+            def ours_fn():
+                ext.gemm_ex(layout, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), scratch.data_ptr(), N, M,
+                            N, K, 0, float(beta), _ext.ptr(bias), 0, 0, 0, 0, _st(a.device))
+
+            use = PLAIN_GEMM.use_library(key, ours_fn, lambda: _plain_lib(a, w, bias, scratch, beta, layout))
+            del scratch
+        else:
+            use = PLAIN_GEMM.use_library(key, None, None)
+        if use:
+            _log("lib_nt" if layout == NT else "lib_nn", M, N, K, _nb(a, w, out, bias) + (_nb(out) if beta else 0))
+            return _plain_lib(a, w, bias, out, beta, layout)
     aux = preact if preact is not None else dact_src
     ld_aux = aux.stride(0) if aux is not None else 0
     ext.gemm_ex(layout, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0), M, N, K,

@@ -26,7 +26,28 @@ import time
 from ..utils import hbm
 
 
-def _worker(target, tuner_id, device, env):
+def _await_gate(gate_file, poll_s=0.01):
+    """Standby worker: wait for the scheduler's verdict (True = run, False = exit)."""
+    while True:
+        if os.path.exists(gate_file):
+            try:
+                with open(gate_file) as fh:
+                    return bool(json.load(fh)["go"])
+            except (OSError, ValueError, KeyError):
+                pass  # written non-atomically by an older scheduler: retry
+        time.sleep(poll_s)
+
+
+def _worker(target, tuner_id, device, env, gate_file=None):
+    if gate_file:
+        # warm standby: pay interpreter start, `import torch` and the target module import
+        # while the probe wave runs, touching no GPU (HIP is initialised only after the go)
+        import torch  # noqa: F401
+
+        mod_name = target.split(":")[0]
+        importlib.import_module(mod_name)
+        if not _await_gate(gate_file):
+            return
     os.environ.update(env)
     os.environ["CLOUD_AMD_TUNER_ID"] = tuner_id
     os.environ["KERASTUNER_TUNER_ID"] = tuner_id
@@ -97,13 +118,21 @@ class TrialScheduler:
         n = self.workers or self._slots()
         return [self._device(i) for i in range(n)]
 
-    def _spawn(self, ctx, i, footprint_file=None):
+    def _spawn(self, ctx, i, footprint_file=None, gate_file=None):
         env = dict(self.env)
         if footprint_file:
             env["CLOUD_AMD_FOOTPRINT_FILE"] = footprint_file
-        p = ctx.Process(target=_worker, args=(self.target, f"tuner{i}", self._device(i), env), daemon=False)
+        p = ctx.Process(target=_worker, args=(self.target, f"tuner{i}", self._device(i), env, gate_file),
+                        daemon=False)
         p.start()
         return p
+
+    @staticmethod
+    def _open_gate(path, go):
+        tmp = path + ".tmp"
+        with open(tmp, "w") as fh:
+            json.dump({"go": bool(go)}, fh)
+        os.replace(tmp, path)
 
     def packing_from_footprint(self, peak_gb):
         """Workers per GPU for a measured per-trial peak (GiB)."""
@@ -123,6 +152,14 @@ class TrialScheduler:
             os.makedirs(state, exist_ok=True)
             files = [os.path.join(state, f"footprint_tuner{i}.json") for i in range(self._slots())]
             procs = [self._spawn(ctx, i, files[i]) for i in range(self._slots())]
+            # warm standbys for the packing wave: started now, gated until the footprint is
+            # known, so their interpreter start and imports overlap the probe trial
+            # (CLOUD_AMD_TUNER_STANDBY=0: spawn the packing wave only after the probe)
+            from .. import config
+
+            n_standby = max(0, self.max_workers - self._slots()) if config.get("CLOUD_AMD_TUNER_STANDBY") else 0
+            gates = [os.path.join(state, f"gate_tuner{i}.json") for i in range(self._slots(), self._slots() + n_standby)]
+            standby = [self._spawn(ctx, self._slots() + k, gate_file=g) for k, g in enumerate(gates)]
             limit = self.probe_timeout_s if self.probe_timeout_s is not None else timeout
             while self.footprint_gb is None:
                 for f in files:
@@ -137,8 +174,15 @@ class TrialScheduler:
                 time.sleep(0.05)
             self.per_gpu = self.packing_from_footprint(self.footprint_gb) if self.footprint_gb else 1
             want = min(self.max_workers, self._slots() * self.per_gpu)
-            if any(p.is_alive() for p in procs):  # nothing left to pack into if the probe wave is done
-                procs += [self._spawn(ctx, i) for i in range(len(procs), want)]
+            if not any(p.is_alive() for p in procs):  # nothing left to pack into if the probe wave is done
+                want = len(procs)
+            extra = max(0, want - len(procs))
+            for k, (g, sp) in enumerate(zip(gates, standby)):
+                self._open_gate(g, k < extra)
+            procs += standby[:extra]
+            for sp in standby[extra:]:
+                sp.join(30)
+            procs += [self._spawn(ctx, i) for i in range(len(procs), want)]
             self.workers = len(procs)
         for p in procs:
             p.join(None if timeout is None else max(0.0, timeout - (time.time() - t0)))

@@ -87,6 +87,7 @@ int ca_ln_bwd(const bf16_t*, const bf16_t*, const float*, const float*, const fl
               int, float*, long, int, float, uint64_t, float, uint64_t, hipStream_t, float*);
 long ca_colsum_workspace_floats(long, int);
 int ca_colsum(const bf16_t*, long, int, long, float*, int, float*, hipStream_t);
+int ca_act_grad(const bf16_t*, long, int, const bf16_t*, bf16_t*, long, int, int, hipStream_t);
 int ca_embed_sum(const int32_t*, const int32_t*, const float*, const float*, const float*, bf16_t*, long, int, int, int,
                  hipStream_t);
 int ca_embed_bwd(const bf16_t*, const int32_t*, const int32_t*, float*, float*, float*, long, int, int, int, int, int,
@@ -338,6 +339,10 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("dy"), py::arg("h"), py::arg("mu"), py::arg("rs"), py::arg("g"), py::arg("dh"), py::arg("dx"),
         py::arg("dg"), py::arg("db"), py::arg("acc"), py::arg("ws"), py::arg("M"), py::arg("C"), py::arg("p_in"),
         py::arg("seed_in"), py::arg("p_out"), py::arg("seed_out"), py::arg("s"), py::arg("dsum") = 0);
+  m.def("act_grad", [](u64 dy, long ld_dy, int N, u64 src, u64 out, long M, int Np, int act, u64 s) {
+    check(ca_act_grad(P(const bf16_t*, dy), ld_dy, N, P(const bf16_t*, src), P(bf16_t*, out), M, Np, act, S(s)),
+          "act_grad");
+  });
   m.def("colsum_workspace_floats", [](long M, int N) { return ca_colsum_workspace_floats(M, N); });
   m.def("colsum", [](u64 x, long M, int N, long ld, u64 out, int acc, u64 ws, u64 s) {
     check(ca_colsum(P(const bf16_t*, x), M, N, ld, P(float*, out), acc, P(float*, ws), S(s)), "colsum");

@@ -12,6 +12,7 @@
 //  * standalone dropout fwd/bwd and a mask materialiser for tests.
 // Dropout masks come from the stateless hash of ca_rng.h (never stored).
 #include "ca_common.h"
+#include "ca_mfma_core.h"
 #include "ca_rng.h"
 
 namespace {
@@ -525,6 +526,48 @@ int ln_nblk(long M) {
   return (int)(b < 512 ? b : 512);
 }
 
+// Keras Dense / Conv2D backward through a fused activation (ops/dense.py): g = dy * act'(.)
+// in one pass, bf16 in / bf16 out, with the zero column padding of dy to the layer's padded
+// width folded in (the 10-way softmax head runs its GEMMs 16 wide).  relu / elu / tanh take
+// act' from the saved OUTPUT y; gelu from the saved pre-activation (erf form, as the
+// forward epilogue).  src and out are [M][Np]; dy is [M][ld_dy] with N <= Np real columns.
+__global__ void __launch_bounds__(256) act_grad_kernel(const bf16_t* __restrict__ dy, long ld_dy, int N,
+                                                       const bf16_t* __restrict__ src, bf16_t* __restrict__ out,
+                                                       long M, int Np, int act) {
+  const int cpr = Np / 8;
+  const long total = M * cpr;
+  const bool fast = (N == Np) && (ld_dy % 8 == 0);
+  for (long c = (long)blockIdx.x * blockDim.x + threadIdx.x; c < total; c += (long)gridDim.x * blockDim.x) {
+    const long m = c / cpr;
+    const int n0 = (int)(c - m * cpr) * 8;
+    float g[8];
+    if (fast) {
+      const us8 d = *reinterpret_cast<const us8*>(dy + m * ld_dy + n0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = bf2f(d[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = (n0 + j < N) ? bf2f(dy[m * ld_dy + n0 + j]) : 0.f;
+    }
+    const us8 sv = *reinterpret_cast<const us8*>(src + m * Np + n0);
+    us8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = bf2f(sv[j]);
+      float d;
+      switch (act) {
+        case ca::ACT_RELU: d = v > 0.f ? 1.f : 0.f; break;
+        case ca::ACT_ELU: d = v > 0.f ? 1.f : v + 1.f; break;
+        case ca::ACT_TANH: d = 1.f - v * v; break;
+        case ca::ACT_GELU: d = ca::act_grad(ca::ACT_GELU, v); break;
+        default: d = 1.f;
+      }
+      o[j] = f2bf(g[j] * d);
+    }
+    *reinterpret_cast<us8*>(out + m * Np + n0) = o;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -581,6 +624,14 @@ int ca_ln_bwd(const bf16_t* dy, const bf16_t* h, const float* mean, const float*
 long ca_colsum_workspace_floats(long M, int N) { return 256L * N; }
 
 // out[n] (+)= sum_m x[m*ld + n]  (bias gradient), N % 8 == 0; ws >= 64*N floats.
+int ca_act_grad(const bf16_t* dy, long ld_dy, int N, const bf16_t* src, bf16_t* out, long M, int Np, int act,
+                hipStream_t s) {
+  if (Np % 8 != 0 || N > Np || M <= 0) return -1;
+  act_grad_kernel<<<ca_stream_grid(M * (Np / 8), 256), 256, 0, s>>>(dy, ld_dy, N, src, out, M, Np, act);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
 int ca_colsum(const bf16_t* x, long M, int N, long ld, float* out, int accumulate, float* ws, hipStream_t s) {
   if (N % 8 != 0) return -1;
   int ry = (int)((M + 63) / 64);

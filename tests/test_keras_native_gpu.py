@@ -141,3 +141,28 @@ def test_keras_dropout_layer_native():
     y.backward(torch.ones_like(y))
     assert torch.equal(x.grad != 0, y != 0)
     assert torch.equal(layer(x, training=False), x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", ["relu", "elu", "tanh", "gelu", None])
+@pytest.mark.parametrize("N,Np", [(64, 64), (10, 16)])
+def test_act_grad_kernel_matches_torch(act, N, Np):
+    """rowops.hip act_grad (Dense / Conv2D backward through a fused activation) against the
+    fp32 PyTorch form of the same expression, including the zero padding of dy to Np."""
+    from cloud_amd.ops import dense as D
+
+    torch.manual_seed(3)
+    M = 1000
+    dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    src = torch.randn(M, Np, device="cuda").to(torch.bfloat16)
+    y = src if act != "gelu" else None
+    if act in ("relu", "elu"):
+        y = torch.relu(src) if act == "relu" else torch.nn.functional.elu(src.float()).to(torch.bfloat16)
+    if act == "tanh":
+        y = torch.tanh(src.float()).to(torch.bfloat16)
+    s = src if act == "gelu" else y
+    got = D._act_grad_dev(dy, s if act is not None else None, N, Np, act)
+    ref = D._act_grad(torch.nn.functional.pad(dy, (0, Np - N)), src if y is None else y,
+                      src if act == "gelu" else None, act)
+    torch.testing.assert_close(got.float(), ref.float(), atol=2e-2, rtol=2e-2)
+    assert got[:, N:].abs().max().item() == 0.0 if Np > N else True
