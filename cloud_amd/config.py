@@ -73,8 +73,6 @@ _VARS = [
     Var("CLOUD_AMD_GEMM_LIB", str, "auto", "plain bf16 GEMMs (bias / accumulate only, no fused epilogue): 'auto' "
         "times the in-tree kernel against hipBLASLt once per shape and keeps the faster, 'never', 'always' "
         "(ops/raw.py PlainGemmPolicy)", "ops"),
-    Var("CLOUD_AMD_WGRAD64_WIDE", bool, False, "weight gradients of <= 64-output-channel convolutions with > 128 "
-        "columns (ResNet layer-1 3x3): 64 x 256 tiles of 1 x 4 waves instead of 64 x 128 / 2 x 2", "ops"),
     Var("CLOUD_AMD_GEMM_PRW", bool, True, "forward 1x1 convolutions with the BN-statistics epilogue and a "
         "weight of <= 32K elements (N x K in {64,256} x 64, {64,128} x 256): persistent resident-weight core "
         "(csrc/include/ca_gemm_prw.h); 0 = the tiled 128 core", "ops"),

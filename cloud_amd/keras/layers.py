@@ -130,17 +130,15 @@ class Conv2D(_Regularized, Layer):
 
     def call(self, x, training=None):
         x = x.to(self.kernel.dtype)
-        if self.kernel_size[0] != self.kernel_size[1] or self.strides[0] != self.strides[1]:
-            raise NotImplementedError("non-square kernels/strides")
-        pad = 0
+        pad = (0, 0)
         if self.padding == "same":
             (pt, pb), (pl, pr) = self._same_pads(x.shape[1], x.shape[2])
-            if pt == pb and pl == pr and pt == pl:
-                pad = pt
-            else:
+            if pt == pb and pl == pr:
+                pad = (pt, pl)
+            else:  # TF's asymmetric SAME split (extra row/column at the bottom/right)
                 x = F.pad(x, (0, 0, pl, pr, pt, pb))
         act, rest = _fused_act(self.activation)
-        y = conv_act_op(x.contiguous(), self.kernel, self.bias, self.strides[0], pad, act)
+        y = conv_act_op(x.contiguous(), self.kernel, self.bias, tuple(self.strides), pad, act)
         return rest(y) if rest is not None else y
 
     def get_config(self):

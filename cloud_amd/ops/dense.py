@@ -231,16 +231,17 @@ class _ConvActFn(torch.autograd.Function):
         ext = _ext.load(required=True)
         N, H, W, Cin = x.shape
         Cout, KH, KW, _ = w.shape
+        (sh, sw), (ph, pw) = stride, padding
         Cp = _rup8(Cin)
         xp = x if Cp == Cin else F.pad(x, (0, Cp - Cin))
         wp = w if Cp == Cin else F.pad(w, (0, Cp - Cin))
         xp, wp = xp.contiguous(), wp.contiguous()
-        OH, OW = _conv._out(H, KH, stride, padding), _conv._out(W, KW, stride, padding)
+        OH, OW = _conv._out(H, KH, sh, ph), _conv._out(W, KW, sw, pw)
         y = torch.empty((N, OH, OW, Cout), dtype=torch.bfloat16, device=x.device)
         bp = b.float().contiguous() if b is not None else None
         st = _ext.stream_handle(x.device)
-        ext.conv_fwd_ex(xp.data_ptr(), wp.data_ptr(), y.data_ptr(), N, H, W, Cp, Cout, KH, KW, stride, stride,
-                        padding, padding, _ext.ptr(bp), ACT[act], st)
+        ext.conv_fwd_ex(xp.data_ptr(), wp.data_ptr(), y.data_ptr(), N, H, W, Cp, Cout, KH, KW, sh, sw, ph, pw,
+                        _ext.ptr(bp), ACT[act], st)
         ctx.save_for_backward(xp, wp, y)
         ctx.cfg = (stride, padding, act, Cin, Cp)
         ctx.wparam, ctx.bparam, ctx.has_b = wparam, bparam, b is not None
@@ -250,7 +251,7 @@ class _ConvActFn(torch.autograd.Function):
     def backward(ctx, dy):
         ext = _ext.load(required=True)
         xp, wp, y = ctx.saved_tensors
-        stride, padding, act, Cin, Cp = ctx.cfg
+        (sh, sw), (ph, pw), act, Cin, Cp = ctx.cfg
         N, H, W, _ = xp.shape
         Cout, KH, KW, _ = wp.shape
         OH, OW = y.shape[1], y.shape[2]
@@ -263,8 +264,8 @@ class _ConvActFn(torch.autograd.Function):
         dx = dw = db = dwp = dbp = None
         if ctx.needs_input_grad[0]:
             dxp = torch.empty_like(xp)
-            ext.conv_dgrad(g.data_ptr(), wp.data_ptr(), dxp.data_ptr(), N, H, W, Cp, Cout, KH, KW, stride, stride,
-                           padding, padding, 0.0, st)
+            ext.conv_dgrad(g.data_ptr(), wp.data_ptr(), dxp.data_ptr(), N, H, W, Cp, Cout, KH, KW, sh, sw, ph, pw,
+                           0.0, st)
             dx = dxp if Cp == Cin else dxp[..., :Cin]
         if ctx.needs_input_grad[1] or ctx.wparam is not None:
             ncols, kred = KH * KW * Cp, N * OH * OW
@@ -273,14 +274,14 @@ class _ConvActFn(torch.autograd.Function):
             sink = _arena_grad(ctx.wparam)
             if sink is not None and sink.dtype == torch.bfloat16 and Cp == Cin:
                 ext.conv_wgrad(g.data_ptr(), xp.data_ptr(), sink.data_ptr(), 1, 1.0, N, H, W, Cp, Cout, KH, KW,
-                               stride, stride, padding, padding, splits, ws.data_ptr(), st)
+                               sh, sw, ph, pw, splits, ws.data_ptr(), st)
                 from ..parallel import ddp
 
                 ddp.notify_grad_ready(ctx.wparam)
             else:
                 full = torch.empty((Cout, KH, KW, Cp), dtype=torch.float32, device=dy.device)
                 ext.conv_wgrad(g.data_ptr(), xp.data_ptr(), full.data_ptr(), 0, 0.0, N, H, W, Cp, Cout, KH, KW,
-                               stride, stride, padding, padding, splits, ws.data_ptr(), st)
+                               sh, sw, ph, pw, splits, ws.data_ptr(), st)
                 sl = full[..., :Cin]
                 if ctx.wparam is not None:
                     dwp = _deliver(ctx.wparam, full, sl)
@@ -291,9 +292,16 @@ class _ConvActFn(torch.autograd.Function):
         return dx, dw, db, None, None, None, dwp, dbp
 
 
+def _pair2(v):
+    return (int(v), int(v)) if isinstance(v, int) else (int(v[0]), int(v[1]))
+
+
 def conv2d(x, w, b=None, stride=1, padding=0, act=None):
-    """``act(conv2d_nhwc(x, w) + b)``, NHWC x [N,H,W,Cin], w [Cout,KH,KW,Cin]."""
+    """``act(conv2d_nhwc(x, w) + b)``, NHWC x [N,H,W,Cin], w [Cout,KH,KW,Cin]; ``stride`` and
+    ``padding`` are ints or (h, w) pairs -- rectangular kernels, strides and paddings run on
+    the same implicit-GEMM kernels (their geometry carries KH / KW, sh / sw, ph / pw apart)."""
     Cout = w.shape[0]
+    stride, padding = _pair2(stride), _pair2(padding)
     if (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and fusable(act) and Cout % 8 == 0
             and _conv._conv_mode() == "native" and x.shape[0] > 0 and x.numel() < 2 ** 31
             and _ext.use_native(x, w)):
@@ -302,7 +310,11 @@ def conv2d(x, w, b=None, stride=1, padding=0, act=None):
         return _ConvActFn.apply(x.contiguous(), w.detach() if wparam is not None else w,
                                 None if b is None else (b.detach() if bparam is not None else b), stride, padding,
                                 act, wparam, bparam)
-    y = _conv.conv2d_nhwc(x.contiguous(), w.to(x.dtype), None, stride, padding)
+    if stride[0] == stride[1] and padding[0] == padding[1]:
+        y = _conv.conv2d_nhwc(x.contiguous(), w.to(x.dtype), None, stride[0], padding[0])
+    else:  # rectangular geometry off the native path: the same expression in PyTorch
+        y = F.conv2d(x.permute(0, 3, 1, 2), w.to(x.dtype).permute(0, 3, 1, 2), None, stride, padding)
+        y = y.permute(0, 2, 3, 1).contiguous()
     if b is not None:
         y = y + b.to(y.dtype)
     return _torch_act(y, act)

@@ -16,8 +16,11 @@ from . import _ext
 
 
 # batches up to this many logits take the one-block kernel that also reduces the mean
-# loss and the metric sums in place (xent.hip xent_batch_kernel)
-_BATCH_KERNEL_MAX = 1 << 21
+# loss and the metric sums in place (xent.hip xent_batch_kernel): Keras fit batches, the
+# BERT classifier head.  Larger ones (the ResNet-50 head, 1024 x 1000 per GPU) take the
+# row-parallel kernel: one workgroup on 1M logits measured 0.98 ms vs 0.013 ms
+# (profiles/r3_s14/rn_step_kernels.txt).
+_BATCH_KERNEL_MAX = 1 << 17
 _UNIT = {}
 
 

@@ -70,7 +70,6 @@ def conv_stats_buffer(x_shape, w, stride, padding, device):
 
 
 _WGRAD_BLOCKS = None
-_WGRAD64_WIDE = os.environ.get("CLOUD_AMD_WGRAD64_WIDE", "0") == "1"
 _GWS_ROWS = 512  # BN statistics group workspace rows (bn.hip group_count)
 _WGRAD_BLOCKS_SMALLM = None
 _DENSE_WGRAD_BLOCKS = None
@@ -189,11 +188,7 @@ def conv_wgrad(dy, x, w_shape, stride, padding, out, beta=1.0, blocks=None):
     # <= 128 output channels: one row of tiles, so the grid is mostly K splits; the fp32
     # slabs stay small next to the pixel operands, and more splits fill the CUs
     target = blocks or (_WGRAD_BLOCKS_SMALLM if Cout <= 128 else _WGRAD_BLOCKS)
-    if Cout <= 64 and ncols > 128 and _WGRAD64_WIDE:  # 64 x 256 tiles (conv.hip wgrad64_wide)
-        tiles = (ncols + 255) // 256
-        splits = ext.gemm_splitk_effective(kred, max(1, min(max(kred // 512, 1), (target + tiles - 1) // tiles)))
-    else:
-        splits = ext.gemm_splitk_effective(kred, wgrad_splits(Cout, ncols, kred, target_blocks=target))
+    splits = ext.gemm_splitk_effective(kred, wgrad_splits(Cout, ncols, kred, target_blocks=target))
     ws = torch.empty(splits * Cout * ncols, dtype=torch.float32, device=x.device)
     obf = int(out.dtype == torch.bfloat16)
     if KH == 1 and KW == 1 and stride == 1 and padding == 0:

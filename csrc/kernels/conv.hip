@@ -730,15 +730,6 @@ conv_glds_w_kernel(CoreParams P) {
   mfma_gemm_glds<BM, BN, WM, WN, LA, LB, EPI, 1, EPF>(P);
 }
 
-// same, at two waves per SIMD: 256 registers for the 64 x 64 wave tiles of the wide
-// weight-gradient tiles (four waves per SIMD would cap them at 128 and spill the loaders)
-template <int BM, int BN, int WM, int WN, template <int, int, int> class LA, template <int, int, int> class LB,
-          int EPI>
-__global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(2)))
-conv_glds_w2_kernel(CoreParams P) {
-  mfma_gemm_glds<BM, BN, WM, WN, LA, LB, EPI, 1, 1>(P);
-}
-
 // Forward convolutions with the BN-statistics epilogue read 2 staged rows per epilogue trip
 // (fwd3x3 -2..-5 % per call, end-to-end neutral: 14,148 vs 14,137 img/s same box);
 // CLOUD_AMD_CONV_EPI_PF=0 restores one row per trip (A/B runs).
@@ -772,18 +763,6 @@ int core_kind() {
   return v;
 }
 bool use_glds() { return core_kind() != 0; }
-
-// Weight gradients of <= 64-output-channel convolutions with > 128 columns (ResNet layer-1
-// 3x3: 64 x 576): 64 x 256 tiles of 1 x 4 waves (64 x 64 wave tiles: 8 fragment reads per
-// 16 MFMAs instead of 6 per 8 on the 64 x 128 / 2 x 2 tile) -- CLOUD_AMD_WGRAD64_WIDE.
-bool wgrad64_wide() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CLOUD_AMD_WGRAD64_WIDE");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v != 0;
-}
 
 // CLOUD_AMD_TAPMASK=0 keeps the general gather loaders on every convolution (A/B runs).
 bool tapmask_loaders() {
@@ -1031,15 +1010,6 @@ int ca_conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, floa
   p.red_bf16 = dw_bf16;
   int rc;
   if (tapmask_loaders() && (long)p.OH * p.OW >= 2 * BK) {  // incremental pixel walk (GConvWgradBI)
-    if (Cout <= 64 && p.N > 128 && wgrad64_wide() && use_glds()) {
-      CoreParams q = p;
-      q.split_xcd = split_xcd_enabled();
-      conv_glds_w2_kernel<64, 256, 1, 4, GDenseNC, GConvWgradBI, EPI_F32_PARTIAL>
-          <<<dim3((q.N + 255) / 256, 1, splits), 256, 0, s>>>(q);
-      CA_LAUNCH_CHECK();
-      if (p.tile_cnt) return 0;
-      return ca_splitk_reduce(ws, splits, (long)p.M * p.N, dw, dw_bf16, beta, s);
-    }
     if (Cout <= 64)
       rc = (p.N <= 64) ? launch<64, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradBI, EPI_F32_PARTIAL>(p, splits, s)
                        : launch<64, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradBI, EPI_F32_PARTIAL>(p, splits, s);

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-3 session 14: native act-grad / bias-grad Keras backward, persistent small-K GEMM rings,
-# plain-GEMM engine policy (BERT A/B), wide 64-channel conv weight gradients (ResNet A/B),
-# gated standby tuner workers (A/B), MNIST fit and ResNet-50 per-step kernel profiles.
+# plain-GEMM engine policy (BERT A/B),
+# two-row BN apply loops (A/B), gated standby tuner workers (A/B), MNIST fit and ResNet-50 per-step kernel profiles.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -10,16 +10,19 @@ tag=${1:-r3s14}
 chk() { grep -q " passed" gpurun_out/$1 && ! grep -qE " failed| error" gpurun_out/$1 || { echo "tests failed: $1"; tail -60 gpurun_out/$1; exit 1; }; }
 $S 300 ${tag}_t1.log python -u -m pytest tests/test_gemm_prw_gpu.py tests/test_plain_gemm_policy_gpu.py tests/test_keras_native_gpu.py -x -q --timeout 120 --timeout-method thread || exit 1
 chk ${tag}_t1.log
-CLOUD_AMD_WGRAD64_WIDE=1 $S 300 ${tag}_t2.log python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread || exit 1
+$S 300 ${tag}_t2.log python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread || exit 1
 chk ${tag}_t2.log
 CLOUD_AMD_GEMM_PRW=1 $S 300 ${tag}_smallk_prw1.log python bench/smallk_gemm.py || exit 1
+$S 300 ${tag}_bnbw_u21.log python bench/bn_apply_bw.py || exit 1
+CLOUD_AMD_BN_APPLY_U2=0 $S 300 ${tag}_bnbw_u20.log python bench/bn_apply_bw.py || exit 1
+cat gpurun_out/${tag}_bnbw_u21.log gpurun_out/${tag}_bnbw_u20.log
 grep -h '"M"' gpurun_out/${tag}_smallk_prw1.log | python3 -c "
 import json,sys
 for l in sys.stdin:
     r=json.loads(l); print(r['prw'], r['M'], r['K'], r['N'], 'stats', r['ours_stats_us'], 'plain', r['ours_us'])"
 for i in 1 2; do
 $S 240 ${tag}_bench_${i}.log python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1
-CLOUD_AMD_WGRAD64_WIDE=1 $S 240 ${tag}_bench_wide_${i}.log python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1
+CLOUD_AMD_BN_APPLY_U2=0 $S 240 ${tag}_bench_u20_${i}.log python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1
 $S 240 ${tag}_bert_${i}.log python bench/bert_base_synth.py || exit 1
 CLOUD_AMD_GEMM_LIB=never $S 240 ${tag}_bert_never_${i}.log python bench/bert_base_synth.py || exit 1
 done
@@ -34,10 +37,10 @@ python3 scripts/step_kernels.py gpurun_out/${tag}_prof_mnist adam_kernel 8 > gpu
 rm -rf gpurun_out/${tag}_prof_mnist
 head -30 gpurun_out/${tag}_mnist_step_kernels.txt
 rm -rf gpurun_out/${tag}_prof_rn
-CLOUD_AMD_WGRAD_STREAM=0 CLOUD_AMD_WGRAD64_WIDE=1 $S 300 ${tag}_prof_rn.log \
+CLOUD_AMD_WGRAD_STREAM=0 $S 300 ${tag}_prof_rn.log \
   rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof_rn -o run --output-format csv -- python bench.py --via-run 0 --steps 4 --warmup 3 || exit 1
 python3 scripts/step_kernels.py gpurun_out/${tag}_prof_rn sgd_kernel > gpurun_out/${tag}_rn_step_kernels.txt
 rm -rf gpurun_out/${tag}_prof_rn
 head -40 gpurun_out/${tag}_rn_step_kernels.txt
-for f in bench_1 bench_wide_1 bench_2 bench_wide_2 bench_prw0 bert_1 bert_never_1 bert_2 bert_never_2 tuner tuner_nostandby; do echo "$f $(grep -o '"value": [0-9.]*' gpurun_out/${tag}_$f.log)"; done
+for f in bench_1 bench_u20_1 bench_2 bench_u20_2 bench_prw0 bert_1 bert_never_1 bert_2 bert_never_2 tuner tuner_nostandby; do echo "$f $(grep -o '"value": [0-9.]*' gpurun_out/${tag}_$f.log)"; done
 echo SESSION_DONE

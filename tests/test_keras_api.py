@@ -159,3 +159,26 @@ def test_regularizers_and_constant_initializer():
     m.fit(x, np.zeros((4, 2), np.float32), epochs=1, verbose=0)
     assert float((d.kernel.detach().float() ** 2).sum()) < float((k * k).sum())  # data + L2 both shrink it
     assert isinstance(tf.keras.regularizers.get("l1_l2"), tf.keras.regularizers.L1L2)
+
+
+@pytest.mark.parametrize("kernel,strides,padding", [((3, 5), (1, 2), "same"), ((1, 7), (1, 1), "same"),
+                                                    ((5, 3), (2, 1), "valid")])
+def test_conv2d_rectangular_kernels_and_strides(kernel, strides, padding):
+    """Keras Conv2D with rectangular kernels / strides (TF semantics, incl. SAME's asymmetric
+    split) against torch's conv of the same weights."""
+    import torch.nn.functional as F
+
+    torch.manual_seed(0)
+    layer = layers.Conv2D(6, kernel, strides=strides, padding=padding, activation="relu")
+    x = torch.randn(2, 11, 14, 3)
+    y = layer(x)
+    w = layer.kernel.detach().float().permute(0, 3, 1, 2)
+    xin = x.permute(0, 3, 1, 2)
+    if padding == "same":
+        (pt, pb), (pl, pr) = layer._same_pads(11, 14)
+        xin = F.pad(xin, (pl, pr, pt, pb))
+    ref = torch.relu(F.conv2d(xin, w, layer.bias.detach().float(), stride=strides)).permute(0, 2, 3, 1)
+    assert y.shape == ref.shape
+    torch.testing.assert_close(y.float(), ref, atol=1e-4, rtol=1e-4)
+    if padding == "same":
+        assert y.shape[1] == -(-11 // strides[0]) and y.shape[2] == -(-14 // strides[1])

@@ -68,6 +68,35 @@ def test_conv_fused_vs_fp32(N, H, Cin, Cout, k, p, act):
     torch.testing.assert_close(b.grad, br.grad, atol=3e-2 * red ** 0.5, rtol=3e-2)
 
 
+@pytest.mark.parametrize("kh,kw,stride,pad", [((3, 5), None, (1, 2), (1, 2)), ((1, 7), None, (1, 1), (0, 3)),
+                                               ((5, 3), None, (2, 1), (2, 0))])
+def test_conv_rectangular_vs_fp32(kh, kw, stride, pad):
+    """Rectangular kernels / strides / paddings (Keras Conv2D((3, 5), strides=(1, 2)), the
+    7x1 / 1x7 factorised convolutions): the same implicit-GEMM kernels, geometry per axis."""
+    from cloud_amd.ops import _ext
+    from cloud_amd.ops.dense import conv2d
+
+    _ext.load(required=True)
+    KH, KW = kh
+    torch.manual_seed(KH * 10 + KW)
+    N, H, W, Cin, Cout = 3, 17, 22, 16, 32
+    x = torch.randn(N, H, W, Cin, device=DEV).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(Cout, KH, KW, Cin, device=DEV) / (KH * KW * Cin) ** 0.5).to(torch.bfloat16).requires_grad_()
+    b = (0.1 * torch.randn(Cout, device=DEV)).requires_grad_()
+    y = conv2d(x, w, b, stride, pad, "relu")
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = torch.relu(F.conv2d(xr.permute(0, 3, 1, 2), wr.permute(0, 3, 1, 2), br, stride=stride, padding=pad))
+    yr = yr.permute(0, 2, 3, 1)
+    yr.backward(dy.float())
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+    red = y.numel() / Cout
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=5e-2, rtol=3e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=3e-2 * red ** 0.5, rtol=3e-2)
+    torch.testing.assert_close(b.grad, br.grad, atol=3e-2 * red ** 0.5, rtol=3e-2)
+
+
 def test_keras_mnist_cnn_trains_on_native_kernels(monkeypatch):
     """The reference MNIST CNN (mnist_example_using_fit.py:54-68) under the default
     (auto -> mixed_bfloat16) policy: the training step never reaches PyTorch's
