@@ -62,6 +62,23 @@ def _act_grad(g, y, pre, act):
     return out.to(torch.bfloat16).contiguous()
 
 
+def _pad2d(t, cols_out, rows_out=None):
+    """Zero-pad a [rows, cols] tensor (unit column stride, any row stride; bf16 or fp32) to
+    [rows_out, cols_out] in one native launch (rowops.hip pad_cols) -- F.pad is a fill plus
+    a copy.  Returns ``t`` itself when there is nothing to pad."""
+    rows, cols = t.shape
+    rows_out = rows if rows_out is None else rows_out
+    if cols == cols_out and rows == rows_out:
+        return t
+    if t.stride(-1) != 1:
+        t = t.contiguous()
+    ext = _ext.load(required=True)
+    out = torch.empty((rows_out, cols_out), dtype=t.dtype, device=t.device)
+    ext.pad_cols(t.data_ptr(), t.stride(0), cols, out.data_ptr(), cols_out, rows, rows_out, t.element_size(),
+                 _ext.stream_handle(t.device))
+    return out
+
+
 def _act_grad_dev(dy, src, N, Np, act):
     """Native form of :func:`_act_grad` (rowops.hip act_grad): ``dy`` [M, N] (any row
     stride) zero-padded to Np columns and multiplied by act'(src) in one pass; ``src`` is
@@ -123,14 +140,11 @@ class _DenseFn(torch.autograd.Function):
         M, K = x.shape
         N = w.shape[0]
         Kp, Np = _rup8(K), _rup8(N)
-        xp = x if Kp == K else F.pad(x, (0, Kp - K))
-        wp = w if (Kp == K and Np == N) else F.pad(w, (0, Kp - K, 0, Np - N))
+        xp = _pad2d(x, Kp)
+        wp = _pad2d(w, Kp, Np)
         bp = None
         if b is not None:
-            bp = b.float()
-            if Np != N:
-                bp = F.pad(bp, (0, Np - N))
-            bp = bp.contiguous()
+            bp = _pad2d(b.float().reshape(1, N), Np).reshape(Np)
         xp, wp = xp.contiguous(), wp.contiguous()
         st = _ext.stream_handle(x.device)
         tiles = -(-M // 128) * -(-Np // 128)
@@ -139,14 +153,22 @@ class _DenseFn(torch.autograd.Function):
             # one tile would walk all of K alone -- split K over blocks into fp32 slabs,
             # reduce, then bias + activation in one elementwise pass
             splits = ext.gemm_splitk_effective(Kp, max(1, min(Kp // 512, 256 // tiles)))
-            y32 = torch.empty((M, Np), dtype=torch.float32, device=x.device)
             ws = torch.empty(splits * M * Np, dtype=torch.float32, device=x.device)
-            ext.gemm_splitk(_gemm.NT, xp.data_ptr(), Kp, wp.data_ptr(), Kp, y32.data_ptr(), 0, 0.0, M, Np, Kp,
-                            splits, ws.data_ptr(), st)
-            if bp is not None:
-                y32 += bp
-            pre = y32.to(torch.bfloat16) if act == "gelu" else None
-            y = _torch_act(y32, act).to(torch.bfloat16)
+            if act != "gelu":
+                # slabs only, then one pass: sum + bias + activation -> bf16 (gemm.hip splitk_bias_act)
+                y = torch.empty((M, Np), dtype=torch.bfloat16, device=x.device)
+                ext.gemm_splitk(_gemm.NT, xp.data_ptr(), Kp, wp.data_ptr(), Kp, y.data_ptr(), -1, 0.0, M, Np, Kp,
+                                splits, ws.data_ptr(), st)
+                ext.splitk_bias_act(ws.data_ptr(), splits, M, Np, _ext.ptr(bp), ACT[act], y.data_ptr(), st)
+                pre = None
+            else:
+                y32 = torch.empty((M, Np), dtype=torch.float32, device=x.device)
+                ext.gemm_splitk(_gemm.NT, xp.data_ptr(), Kp, wp.data_ptr(), Kp, y32.data_ptr(), 0, 0.0, M, Np, Kp,
+                                splits, ws.data_ptr(), st)
+                if bp is not None:
+                    y32 += bp
+                pre = y32.to(torch.bfloat16)
+                y = _torch_act(y32, act).to(torch.bfloat16)
         else:
             y = torch.empty((M, Np), dtype=torch.bfloat16, device=x.device)
             pre = torch.empty((M, Np), dtype=torch.bfloat16, device=x.device) if act == "gelu" else None
@@ -233,8 +255,8 @@ class _ConvActFn(torch.autograd.Function):
         Cout, KH, KW, _ = w.shape
         (sh, sw), (ph, pw) = stride, padding
         Cp = _rup8(Cin)
-        xp = x if Cp == Cin else F.pad(x, (0, Cp - Cin))
-        wp = w if Cp == Cin else F.pad(w, (0, Cp - Cin))
+        xp = x if Cp == Cin else _pad2d(x.reshape(-1, Cin), Cp).view(N, H, W, Cp)
+        wp = w if Cp == Cin else _pad2d(w.reshape(-1, Cin), Cp).view(Cout, KH, KW, Cp)
         xp, wp = xp.contiguous(), wp.contiguous()
         OH, OW = _conv._out(H, KH, sh, ph), _conv._out(W, KW, sw, pw)
         y = torch.empty((N, OH, OW, Cout), dtype=torch.bfloat16, device=x.device)

@@ -88,6 +88,8 @@ int ca_ln_bwd(const bf16_t*, const bf16_t*, const float*, const float*, const fl
 long ca_colsum_workspace_floats(long, int);
 int ca_colsum(const bf16_t*, long, int, long, float*, int, float*, hipStream_t);
 int ca_act_grad(const bf16_t*, long, int, const bf16_t*, bf16_t*, long, int, int, hipStream_t);
+int ca_pad_cols(const void*, long, int, void*, int, long, long, int, hipStream_t);
+int ca_splitk_bias_act(const float*, int, long, int, const float*, int, bf16_t*, hipStream_t);
 int ca_embed_sum(const int32_t*, const int32_t*, const float*, const float*, const float*, bf16_t*, long, int, int, int,
                  hipStream_t);
 int ca_embed_bwd(const bf16_t*, const int32_t*, const int32_t*, float*, float*, float*, long, int, int, int, int, int,
@@ -339,6 +341,13 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("dy"), py::arg("h"), py::arg("mu"), py::arg("rs"), py::arg("g"), py::arg("dh"), py::arg("dx"),
         py::arg("dg"), py::arg("db"), py::arg("acc"), py::arg("ws"), py::arg("M"), py::arg("C"), py::arg("p_in"),
         py::arg("seed_in"), py::arg("p_out"), py::arg("seed_out"), py::arg("s"), py::arg("dsum") = 0);
+  m.def("pad_cols", [](u64 in, long ld, int cols, u64 out, int cols_out, long rows, long rows_out, int eb, u64 s) {
+    check(ca_pad_cols(P(const void*, in), ld, cols, P(void*, out), cols_out, rows, rows_out, eb, S(s)), "pad_cols");
+  });
+  m.def("splitk_bias_act", [](u64 ws, int splits, long M, int N, u64 bias, int act, u64 out, u64 s) {
+    check(ca_splitk_bias_act(P(const float*, ws), splits, M, N, P(const float*, bias), act, P(bf16_t*, out), S(s)),
+          "splitk_bias_act");
+  });
   m.def("act_grad", [](u64 dy, long ld_dy, int N, u64 src, u64 out, long M, int Np, int act, u64 s) {
     check(ca_act_grad(P(const bf16_t*, dy), ld_dy, N, P(const bf16_t*, src), P(bf16_t*, out), M, Np, act, S(s)),
           "act_grad");

@@ -199,6 +199,24 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
+// Split-K reduce for a skinny dense layer (Keras Flatten -> Dense: small batch, long K):
+// out[m][n] = act(sum_s ws[s][m][n] + bias[n]) in bf16 -- the fp32 sum, bias add, activation
+// and cast of the layer in one pass (no fp32 output tensor, no elementwise kernels).
+__global__ void __launch_bounds__(256) splitk_bias_act_kernel(const float* __restrict__ ws, int S, long M, int N,
+                                                              const float* __restrict__ bias, int act,
+                                                              bf16_t* __restrict__ out) {
+  const long n4 = M * N / 4;
+  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < n4; v += (long)gridDim.x * 256) {
+    f4v acc = {0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < S; ++sp) acc += *reinterpret_cast<const f4v*>(ws + (long)sp * M * N + v * 4);
+    const int c = (int)((v * 4) % N);
+    us4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = f2bf(act_fwd(act, acc[j] + (bias ? bias[c + j] : 0.f)));
+    *reinterpret_cast<us4*>(out + v * 4) = r;
+  }
+}
+
 // Fraction of CU-slots doing work when `tiles` equal blocks are spread over the
 // 256 CUs in rounds (wave quantisation).
 static double tile_balance(long tiles) {
@@ -377,6 +395,14 @@ int* ca_splitk_ring(long n, hipStream_t s) {
   int* out = ring[dev] + pos[dev];
   pos[dev] += n;
   return out;
+}
+
+int ca_splitk_bias_act(const float* ws, int splits, long M, int N, const float* bias, int act, bf16_t* out,
+                       hipStream_t s) {
+  if (N % 4 || M <= 0) return -1;
+  splitk_bias_act_kernel<<<ca_stream_grid(M * N / 4, 256), 256, 0, s>>>(ws, splits, M, N, bias, act, out);
+  CA_LAUNCH_CHECK();
+  return 0;
 }
 
 int ca_splitk_reduce(const float* ws, int splits, long MN, void* out, int out_bf16, float beta, hipStream_t s) {

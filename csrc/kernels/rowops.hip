@@ -568,6 +568,20 @@ __global__ void __launch_bounds__(256) act_grad_kernel(const bf16_t* __restrict_
   }
 }
 
+// Zero-pad the columns of a row-major matrix to a multiple the MFMA tiles take (Keras
+// layers with Cin = 1 / 3 or a 10-way head): out[r][c] = c < cols ? in[r * ld + c] : 0,
+// out row stride cols_out; 2- or 4-byte elements.  One launch instead of F.pad's fill + copy.
+template <typename T>
+__global__ void __launch_bounds__(256) pad_cols_kernel(const T* __restrict__ in, long ld, int cols,
+                                                       T* __restrict__ out, int cols_out, long rows, long rows_out) {
+  const long n = rows_out * cols_out;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const long r = i / cols_out;
+    const int c = (int)(i - r * cols_out);
+    out[i] = (c < cols && r < rows) ? in[r * ld + c] : (T)0;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -624,6 +638,22 @@ int ca_ln_bwd(const bf16_t* dy, const bf16_t* h, const float* mean, const float*
 long ca_colsum_workspace_floats(long M, int N) { return 256L * N; }
 
 // out[n] (+)= sum_m x[m*ld + n]  (bias gradient), N % 8 == 0; ws >= 64*N floats.
+int ca_pad_cols(const void* in, long ld, int cols, void* out, int cols_out, long rows, long rows_out, int elem_bytes,
+                hipStream_t s) {
+  if (cols > cols_out || rows <= 0 || rows > rows_out) return -1;
+  const int g = ca_stream_grid(rows_out * cols_out, 256);
+  if (elem_bytes == 2)
+    pad_cols_kernel<uint16_t><<<g, 256, 0, s>>>((const uint16_t*)in, ld, cols, (uint16_t*)out, cols_out, rows,
+                                                 rows_out);
+  else if (elem_bytes == 4)
+    pad_cols_kernel<uint32_t><<<g, 256, 0, s>>>((const uint32_t*)in, ld, cols, (uint32_t*)out, cols_out, rows,
+                                                 rows_out);
+  else
+    return -1;
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
 int ca_act_grad(const bf16_t* dy, long ld_dy, int N, const bf16_t* src, bf16_t* out, long M, int Np, int act,
                 hipStream_t s) {
   if (Np % 8 != 0 || N > Np || M <= 0) return -1;
