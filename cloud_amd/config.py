@@ -73,9 +73,9 @@ _VARS = [
     Var("CLOUD_AMD_GEMM_LIB", str, "auto", "plain bf16 GEMMs (bias / accumulate only, no fused epilogue): 'auto' "
         "times the in-tree kernel against hipBLASLt once per shape and keeps the faster, 'never', 'always' "
         "(ops/raw.py PlainGemmPolicy)", "ops"),
-    Var("CLOUD_AMD_GEMM_PRW", bool, True, "forward 1x1 convolutions with the BN-statistics epilogue and a "
-        "weight of <= 32K elements (N x K in {64,256} x 64, {64,128} x 256): persistent resident-weight core "
-        "(csrc/include/ca_gemm_prw.h); 0 = the tiled 128 core", "ops"),
+    Var("CLOUD_AMD_GEMM_PRW", bool, True, "forward 1x1 convolutions with N = 256, K = 64 (ResNet layer-1 conv3 "
+        "and shortcut): persistent resident-weight core (csrc/include/ca_gemm_prw.h); 0 = the tiled 128 core",
+        "ops"),
     Var("CLOUD_AMD_EPI_PF", bool, True, "GEMM epilogues that read memory or run an activation (BN-statistics "
         "forward 1x1 convs, BERT bias/GELU/GELU'/beta dense layers): 4 staged output rows in flight per trip", "ops"),
     Var("CLOUD_AMD_SPLITK_INLAUNCH", bool, False, "split-K weight gradients (dense and conv): 1 = the last-arriving "

@@ -39,15 +39,17 @@ class _XentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, denom, label_smoothing, acc, acc_w):
         ext = _ext.load(required=True)
-        z = logits.contiguous()
-        B, C = z.shape
+        B, C = logits.shape
+        small = B * C <= _BATCH_KERNEL_MAX
+        # the one-block kernel takes strided rows (a padded head's [:, :C] view: no copy)
+        z = logits if (small and logits.stride(1) == 1) else logits.contiguous()
         dev = z.device
         correct = torch.empty(B, dtype=torch.float32, device=dev)
-        dz = torch.empty_like(z)
+        dz = torch.empty((B, C), dtype=z.dtype, device=dev)
         lab = labels.contiguous()
-        if B * C <= _BATCH_KERNEL_MAX:
+        if small:
             mean = torch.empty(1, dtype=torch.float32, device=dev)
-            ext.softmax_xent_batch(z.data_ptr(), int(z.dtype == torch.bfloat16), lab.data_ptr(), B, C,
+            ext.softmax_xent_batch(z.data_ptr(), z.stride(0), int(z.dtype == torch.bfloat16), lab.data_ptr(), B, C,
                                    1.0 / float(denom), float(label_smoothing), mean.data_ptr(), correct.data_ptr(),
                                    dz.data_ptr(), _ext.ptr(acc), float(acc_w), _ext.stream_handle(dev))
             out = mean.view(())

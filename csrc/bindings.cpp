@@ -44,7 +44,8 @@ int ca_conv_dgrad_bnstats(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, 
 int ca_u8_normalize(const uint8_t*, bf16_t*, long, int, const float*, const float*, hipStream_t);
 int ca_stem_s2d(const bf16_t*, bf16_t*, int, int, int, int, int, int, int, hipStream_t);
 int ca_softmax_xent(const void*, int, const int64_t*, int, int, float, float, float*, float*, void*, hipStream_t);
-int ca_softmax_xent_batch(const void*, int, const int64_t*, int, int, float, float, float*, float*, void*, float*, float,
+int ca_softmax_xent_batch(const void*, long, int, const int64_t*, int, int, float, float, float*, float*, void*, float*,
+                          float,
                           hipStream_t);
 int ca_maxpool_fwd(const bf16_t*, bf16_t*, uint8_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int ca_maxpool_bwd(const bf16_t*, const uint8_t*, bf16_t*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -225,9 +226,9 @@ PYBIND11_MODULE(_C, m) {
     check(ca_softmax_xent(P(const void*, z), zbf, P(const int64_t*, labels), B, C, gscale, ls, P(float*, loss),
                           P(float*, correct), P(void*, dz), S(s)), "softmax_xent");
   });
-  m.def("softmax_xent_batch", [](u64 z, int bf, u64 labels, int B, int C, float gs, float ls, u64 mean, u64 correct,
+  m.def("softmax_xent_batch", [](u64 z, long ldz, int bf, u64 labels, int B, int C, float gs, float ls, u64 mean, u64 correct,
                                  u64 dz, u64 acc, float acc_w, u64 s) {
-    check(ca_softmax_xent_batch(P(const void*, z), bf, P(const int64_t*, labels), B, C, gs, ls, P(float*, mean),
+    check(ca_softmax_xent_batch(P(const void*, z), ldz, bf, P(const int64_t*, labels), B, C, gs, ls, P(float*, mean),
                                 P(float*, correct), P(void*, dz), P(float*, acc), acc_w, S(s)), "softmax_xent_batch");
   });
   m.def("maxpool_fwd", [](u64 x, u64 y, u64 idx, int N, int H, int W, int C, int OH, int OW, int k, int st, int p,

@@ -110,13 +110,20 @@ int cu_count() {
 }
 
 // (N, K) -> instantiation id; 0 = not covered.  The whole [N][K] weight stays in LDS.
+// Only N = 256, K = 64 (ResNet layer-1 conv3 and projection shortcut) is taken: measured on
+// MI355X at M = 3.2M (bench/smallk_gemm.py, profiles/r3_s12, r3_s14), with statistics,
+// persistent vs tiled 128 core:
+//   N 256, K  64: 413-420 vs 492 us   (the tile's 128 x 256 output per 16 KB of A is where
+//                                     overlapping the next tile's loads with the stores pays)
+//   N  64, K 256: 403-418 vs 377 us   (ring depth 4 and 6)
+//   N  64, K  64: 168 vs 155 us       (ring depth 3 and 8)
+//   N 128, K 256: 468-492 vs 468 us
+// so the other shapes stay on the tiled core, whose 4 co-resident blocks per CU already keep
+// enough loads in flight for their read-heavy tiles.
 int prw_kind(int M, int N, int K, long lda, long ldb, long ldc) {
   if (!prw_enabled() || lda != K || ldb != K || ldc != N || M < 128) return 0;
   if ((long)M * K * 2 >= (long)BUF_CAP || (long)M * N * 2 >= (long)BUF_CAP) return 0;
-  if (N == 64 && K == 64) return 1;
   if (N == 256 && K == 64) return 2;
-  if (N == 64 && K == 256) return 3;
-  if (N == 128 && K == 256) return 4;
   return 0;
 }
 
@@ -131,15 +138,7 @@ int prw_grid_for(int M) {
   return g < tiles ? g : tiles;
 }
 
-int prw_grid(int kind, int M) {
-  switch (kind) {
-    case 1: return prw_grid_for<64, 64, 8>(M);
-    case 2: return prw_grid_for<256, 64, 3>(M);
-    case 3: return prw_grid_for<64, 256, 6>(M);
-    case 4: return prw_grid_for<128, 256, 3>(M);
-  }
-  return 0;
-}
+int prw_grid(int kind, int M) { return kind == 2 ? prw_grid_for<256, 64, 3>(M) : 0; }
 
 int prw_launch(int kind, const CoreParams& p, hipStream_t s) {
   const int g = prw_grid(kind, p.M);
@@ -149,13 +148,8 @@ int prw_launch(int kind, const CoreParams& p, hipStream_t s) {
     if (st) prw_gemm_kernel<BN_, KT_, NS_, true><<<g, 512, 0, s>>>(p);                    \
     else prw_gemm_kernel<BN_, KT_, NS_, false><<<g, 512, 0, s>>>(p);                      \
   } while (0)
-  switch (kind) {
-    case 1: CA_PRW(64, 64, 8); break;
-    case 2: CA_PRW(256, 64, 3); break;
-    case 3: CA_PRW(64, 256, 6); break;
-    case 4: CA_PRW(128, 256, 3); break;
-    default: return -2;
-  }
+  if (kind != 2) return -2;
+  CA_PRW(256, 64, 3);
 #undef CA_PRW
   CA_LAUNCH_CHECK();
   return 0;

@@ -76,7 +76,8 @@ __global__ void __launch_bounds__(256) xent_kernel(const T* __restrict__ z, cons
 // accumulator -- the loss's sum / divide kernels and the metrics' argmax / compare /
 // reduce kernels (and their host syncs) are gone from the step.  Deterministic.
 template <typename T>
-__global__ void __launch_bounds__(1024) xent_batch_kernel(const T* __restrict__ z, const int64_t* __restrict__ labels,
+__global__ void __launch_bounds__(1024) xent_batch_kernel(const T* __restrict__ z, long ldz,
+                                                         const int64_t* __restrict__ labels,
                                                          int B, int C, float grad_scale, float label_smoothing,
                                                          float* __restrict__ mean_out, float* __restrict__ correct,
                                                          T* __restrict__ dz, float* __restrict__ acc, float acc_w) {
@@ -84,7 +85,7 @@ __global__ void __launch_bounds__(1024) xent_batch_kernel(const T* __restrict__ 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float wl = 0.f, wc = 0.f;
   for (int row = wave; row < B; row += 16) {
-    const T* zr = z + (long)row * C;
+    const T* zr = z + (long)row * ldz;  // logits rows may be strided (a padded head's [:, :C] view)
     float m = -INFINITY;
     int am = 0;
     for (int c = lane; c < C; c += 64) {
@@ -147,16 +148,16 @@ __global__ void __launch_bounds__(1024) xent_batch_kernel(const T* __restrict__ 
 
 }  // namespace
 
-extern "C" int ca_softmax_xent_batch(const void* logits, int is_bf16, const int64_t* labels, int B, int C,
+extern "C" int ca_softmax_xent_batch(const void* logits, long ldz, int is_bf16, const int64_t* labels, int B, int C,
                                      float grad_scale, float label_smoothing, float* mean_out, float* correct,
                                      void* dlogits, float* acc, float acc_w, hipStream_t s) {
-  if (B <= 0 || C <= 0) return -1;
+  if (B <= 0 || C <= 0 || ldz < C) return -1;
   if (is_bf16)
-    xent_batch_kernel<bf16_t><<<1, 1024, 0, s>>>((const bf16_t*)logits, labels, B, C, grad_scale, label_smoothing,
-                                                mean_out, correct, (bf16_t*)dlogits, acc, acc_w);
+    xent_batch_kernel<bf16_t><<<1, 1024, 0, s>>>((const bf16_t*)logits, ldz, labels, B, C, grad_scale,
+                                                label_smoothing, mean_out, correct, (bf16_t*)dlogits, acc, acc_w);
   else
-    xent_batch_kernel<float><<<1, 1024, 0, s>>>((const float*)logits, labels, B, C, grad_scale, label_smoothing,
-                                               mean_out, correct, (float*)dlogits, acc, acc_w);
+    xent_batch_kernel<float><<<1, 1024, 0, s>>>((const float*)logits, ldz, labels, B, C, grad_scale,
+                                               label_smoothing, mean_out, correct, (float*)dlogits, acc, acc_w);
   CA_LAUNCH_CHECK();
   return 0;
 }
