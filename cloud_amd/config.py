@@ -55,9 +55,6 @@ _VARS = [
     Var("CLOUD_AMD_DENSE_WGRAD_BLOCKS", int, 1024, "dense-layer weight gradients (BERT): split-K workgroup target "
         "(1024 with the split-major XCD mapping: 6,210 / 6,231 vs 6,153 / 6,131 seq/s at 512)",
         "ops"),
-    Var("CLOUD_AMD_WGRAD_256", bool, False, "dense-layer weight gradients with >= 256 x 256 outputs: 1 = split-K "
-        "sized to one round of 256 x 256 ring-core blocks instead of ~1024 128 x 128 blocks (measured slower: BERT "
-        "wgrads 1.92 -> 2.75 ms/step, the ring core's N-contiguous loaders)", "ops"),
     Var("CLOUD_AMD_TAPMASK", bool, True, "convolutions: tap-mask / incremental buffer-mode gather loaders; 0 keeps "
         "the general per-chunk decode loaders (A/B runs)", "ops"),
     Var("CLOUD_AMD_SPLIT_XCD", bool, True, "split-K GEMM/conv grids: give each XCD contiguous (split, tile) "
@@ -78,9 +75,6 @@ _VARS = [
         "ops"),
     Var("CLOUD_AMD_EPI_PF", bool, True, "GEMM epilogues that read memory or run an activation (BN-statistics "
         "forward 1x1 convs, BERT bias/GELU/GELU'/beta dense layers): 4 staged output rows in flight per trip", "ops"),
-    Var("CLOUD_AMD_SPLITK_INLAUNCH", bool, False, "split-K weight gradients (dense and conv): 1 = the last-arriving "
-        "split of each tile sums the fp32 slabs inside the GEMM launch (measured slower on BERT/ResNet: "
-        "4,791 vs 6,414 seq/s); default keeps the separate reduce kernel", "ops"),
     Var("CLOUD_AMD_ATTN_FUSED_BWD", bool, True, "attention at S = 64 / 128: one workgroup per (batch, head) for "
         "the forward and a single fused backward kernel; 0 keeps the 64-query-block kernels", "ops"),
     Var("CLOUD_AMD_CONV_EPI_PF", bool, True, "implicit-GEMM forward convolutions with the BN-statistics epilogue: "

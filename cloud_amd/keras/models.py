@@ -384,7 +384,11 @@ class Model(Layer):
         return loss
 
     def _regularization(self):
-        regs = [m.regularization_loss() for m in self.modules() if hasattr(m, "regularization_loss")]
+        # layers without regularizers report a plain 0.0: leave them out, so an unregularized
+        # model's loss stays the fused loss tensor itself (no add kernel, and the unit-seed
+        # backward path of train_step applies)
+        regs = [r for r in (m.regularization_loss() for m in self.modules() if hasattr(m, "regularization_loss"))
+                if torch.is_tensor(r) or r != 0]
         return sum(regs) if regs else None
 
     def _input_dtype(self):

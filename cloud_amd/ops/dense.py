@@ -125,6 +125,21 @@ def _deliver(param, full_grad, sliced):
     and notify the DP engine; returns the autograd gradient when there is no arena."""
     sink = _arena_grad(param)
     if sink is not None:
+        if (sliced.is_cuda and full_grad.dtype == torch.float32 and full_grad.is_contiguous()
+                and sink.dtype in (torch.bfloat16, torch.float32) and sliced.data_ptr() == full_grad.data_ptr()):
+            # the parameter-shaped block is the top-left corner of the padded gradient:
+            # rows = leading dims, cols = last dim (rowops.hip slice_acc, one launch)
+            cols = sliced.shape[-1]
+            rows = sliced.numel() // cols
+            ld = full_grad.shape[-1]
+            if sliced.dim() == 1 or sliced.stride(-2) == ld:
+                _ext.load(required=True).slice_acc(full_grad.data_ptr(), ld, sink.data_ptr(),
+                                                    int(sink.dtype == torch.bfloat16), rows, cols,
+                                                    _ext.stream_handle(sink.device))
+                from ..parallel import ddp
+
+                ddp.notify_grad_ready(param)
+                return None
         sink.view_as(sliced).add_(sliced.to(sink.dtype))
         from ..parallel import ddp
 

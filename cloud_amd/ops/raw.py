@@ -73,7 +73,6 @@ _WGRAD_BLOCKS = None
 _GWS_ROWS = 512  # BN statistics group workspace rows (bn.hip group_count)
 _WGRAD_BLOCKS_SMALLM = None
 _DENSE_WGRAD_BLOCKS = None
-_WGRAD_256 = None
 
 
 def wgrad_splits(m, n, kred, target_blocks=1024, min_k=512):
@@ -470,7 +469,7 @@ class deferred_finalize:
 
 def wgrad_into(dy, x, out, beta=1.0):
     """out[N_out, K_in] (+)= dy[M, N_out]^T @ x[M, K_in] (split-K over M), bf16 or fp32 out."""
-    global _DENSE_WGRAD_BLOCKS, _WGRAD_256
+    global _DENSE_WGRAD_BLOCKS
     ext = _ext.load(required=True)
     if _DENSE_WGRAD_BLOCKS is None:
         from .. import config
@@ -478,18 +477,9 @@ def wgrad_into(dy, x, out, beta=1.0):
         _DENSE_WGRAD_BLOCKS = config.get("CLOUD_AMD_DENSE_WGRAD_BLOCKS")
     M, n_out = dy.shape
     k_in = x.shape[1]
-    t256 = ((n_out + 255) // 256) * ((k_in + 255) // 256)
-    if _WGRAD_256 is None:
-        from .. import config
-
-        _WGRAD_256 = config.get("CLOUD_AMD_WGRAD_256")
-    if _WGRAD_256 and n_out >= 256 and k_in >= 256 and t256 <= 128 and M // (256 // t256) >= 512:
-        # one nearly full round of 256 x 256 split-K blocks on the ring core (gemm.hip use_256)
-        splits = ext.gemm_splitk_effective(M, 256 // t256)
-    else:
-        # dense layers: K = tokens is moderate, so fewer/larger K slices (less slab traffic)
-        splits = ext.gemm_splitk_effective(M, wgrad_splits(n_out, k_in, M, target_blocks=_DENSE_WGRAD_BLOCKS,
-                                                           min_k=1024))
+    # dense layers: K = tokens is moderate, so fewer/larger K slices (less slab traffic).
+    # (A one-round 256 x 256 ring-core variant measured slower on BERT and was removed.)
+    splits = ext.gemm_splitk_effective(M, wgrad_splits(n_out, k_in, M, target_blocks=_DENSE_WGRAD_BLOCKS, min_k=1024))
     ws = torch.empty(splits * n_out * k_in, dtype=torch.float32, device=dy.device)
     fb = _FIN_BATCH
     ext.gemm_splitk(TN, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),

@@ -108,13 +108,6 @@ struct CoreParams {
   FastDiv div_wq, div_hq, div_nw;
   int split_xcd;  // split-K grids: deal (split, tile) ranges to XCDs split-major (blk_pos)
   unsigned long long* stamps;  // diagnostic builds only (in-kernel s_memtime stamps)
-  // EPI_F32_PARTIAL with tile_cnt set: the last-arriving split of each tile sums the slabs
-  // into red_out[M][red_ld] (fp32, or bf16 with red_bf16) = sum + red_beta * red_out
-  int* tile_cnt;
-  void* red_out;
-  long red_ld;
-  float red_beta;
-  int red_bf16;
 };
 
 // output row of GEMM row gm (identity unless the parity-class row map is on)
@@ -369,92 +362,15 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
     // N % 8 == 0 and ldc % 4 == 0 (slabs are [M][N]): a column group is whole or absent
     const BlkPos bp = blk_pos(P);
     float* Cp = reinterpret_cast<float*>(P.C) + (long)bp.split * P.split_stride;
-    if (!P.tile_cnt) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int gm = m0 + rbase + i * 16, gn = n0 + cbase + j * 16;
-          if (gm < P.M && gn < P.N) *reinterpret_cast<f4v*>(Cp + (long)gm * P.ldc + gn) = acc[i][j];
-        }
-      return;
-    }
-    // In-launch split-K combine (cdna_hip_programming.md, "In-launch split-K reduction", sc1
-    // form): slabs stored write-through (sc1: no L2 write-back fence), every wave drained,
-    // then one relaxed agent-scope ticket; the block drawing the last ticket acquires and
-    // sums ALL slabs of the tile in split order (its own included, bitwise equal to acc:
-    // deterministic whoever arrives last) into the output.
-    {
-      const auto rs = __builtin_amdgcn_make_buffer_rsrc(Cp, (short)0, (int)buf_span(P.split_stride * 4), 0x00020000);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int gm = m0 + rbase + i * 16, gn = n0 + cbase + j * 16;
-          if (gm < P.M && gn < P.N)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
-                                                   (int)(((long)gm * P.ldc + gn) * 4), 0, 16);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(smem);
-    const int S = gridDim.z;
-    if (tid == 0) {
-      const int t = __hip_atomic_fetch_add(P.tile_cnt + bp.tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = t == S - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // ready for the next launch that draws this slot (the kernel boundary publishes it)
-        __hip_atomic_store(P.tile_cnt + bp.tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      flag[0] = last;
-    }
-    __syncthreads();
-    if (!flag[0]) return;
-    const float* W0 = reinterpret_cast<const float*>(P.C);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
-    // unconditional loads (clamped into the slab; out-of-range sums are never stored): a
-    // per-element guard would make hipcc wait for every load separately
-    for (int sp = 0; sp < S; ++sp) {
-      const float* Ws = W0 + (long)sp * P.split_stride;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int gm = min(m0 + rbase + i * 16, P.M - 1), gn = min(n0 + cbase + j * 16, P.N - 4);
-          acc[i][j] += *reinterpret_cast<const f4v*>(Ws + (long)gm * P.ldc + gn);
-        }
-    }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int gm = m0 + rbase + i * 16, gn = n0 + cbase + j * 16;
-        if (gm >= P.M || gn >= P.N) continue;
-        const long o = (long)gm * P.red_ld + gn;
-        f4v v = acc[i][j];
-        if (P.red_bf16) {
-          us4* dst = reinterpret_cast<us4*>(reinterpret_cast<bf16_t*>(P.red_out) + o);
-          if (P.red_beta != 0.f) {
-            const us4 old = *dst;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += P.red_beta * bf2f(old[r]);
-          }
-          us4 w;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) w[r] = f2bf(v[r]);
-          *dst = w;
-        } else {
-          f4v* dst = reinterpret_cast<f4v*>(reinterpret_cast<float*>(P.red_out) + o);
-          if (P.red_beta != 0.f) v += P.red_beta * *dst;
-          *dst = v;
-        }
+        if (gm < P.M && gn < P.N) *reinterpret_cast<f4v*>(Cp + (long)gm * P.ldc + gn) = acc[i][j];
       }
+    // (an in-launch combine -- the last-arriving split summing all slabs behind an agent-scope
+    // ticket -- measured 3-4x slower than the separate streaming reduce and was removed)
     return;
   } else {
     short* Cs = smem;

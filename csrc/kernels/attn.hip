@@ -597,13 +597,17 @@ __global__ void __launch_bounds__(SQ * 4) __attribute__((amdgpu_waves_per_eu(4))
 // Forward for S = 64 / 128: one workgroup per (batch, head), all S keys' K and V issued
 // to LDS up front (one memory round trip instead of one per 64-key block), then each
 // wave's 16 query rows take an exact (not online) softmax over the whole key row.
-// LDS: 2 x [S][72] + per-wave P slabs [16][S + 8] = 72 KB at S = 128 (two blocks per CU).
+// LDS: 2 x [S][72] = 36 KB at S = 128.  Once every wave holds its scores in registers the
+// K image is dead, and each wave stages its P (64 keys at a time, [16][72]) and finally its
+// output tile in its own 16 rows of it -- three 8-wave blocks per CU (72 VGPRs), so the
+// B x H = 768 blocks of BERT-base b64 run in one round instead of 1.5 (per-wave P slabs
+// beside K / V took 72 KB: two blocks per CU).
 template <int SQ>
 __global__ void __launch_bounds__(SQ * 4) attn_fwd_short_kernel(AttnArgs a) {
-  constexpr int NW = SQ / 16, NT = NW * 64, TK = SQ / 16, PL = SQ + 8;
+  constexpr int NW = SQ / 16, NT = NW * 64, TK = SQ / 16;
+  static_assert(NW * 16 == SQ, "one 16-row slab of the K image per wave");
   __shared__ __attribute__((aligned(16))) short Ks[SQ * LDT];
   __shared__ __attribute__((aligned(16))) short Vs[SQ * LDT];
-  __shared__ __attribute__((aligned(16))) short Ps[NW][16 * PL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bh = blockIdx.x;
   const int b = bh / a.H, h = bh - b * a.H;
@@ -656,26 +660,34 @@ __global__ void __launch_bounds__(SQ * 4) attn_fwd_short_kernel(AttnArgs a) {
     }
     l[r] = grp16_sum(ls);
   }
-  short* slab = Ps[wave];
-#pragma unroll
-  for (int t = 0; t < TK; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = q0 + (lane >> 4) * 4 + r;
-      const int key = t * 16 + (lane & 15);
-      const float mul = a.drop.on ? drop_mul(a.drop, bhss + (uint32_t)(q * SQ + key)) : 1.f;
-      slab[((lane >> 4) * 4 + r) * PL + key] = (short)f2bf(s[t][r] * mul);
-    }
-  __builtin_amdgcn_wave_barrier();
+  // every wave's QK^T reads of Ks are done past this barrier: its rows become P slabs
+  __syncthreads();
+  short* slab = Ks + wave * 16 * LDT;
   f4v o[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) o[t] = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int kk = 0; kk < SQ / 32; ++kk) {
-    const bf16x8 pf = frag_kc<PL>(slab, 0, kk * 32, lane);
+  for (int half = 0; half < SQ / 64; ++half) {
+    if (half) __builtin_amdgcn_wave_barrier();  // the previous half's P reads precede these writes
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, frag_nc<LDT>(Vs, t * 16, kk * 32, lane), o[t], 0, 0, 0);
+    for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = half * 4 + tt;
+        const int q = q0 + (lane >> 4) * 4 + r;
+        const int key = t * 16 + (lane & 15);
+        const float mul = a.drop.on ? drop_mul(a.drop, bhss + (uint32_t)(q * SQ + key)) : 1.f;
+        slab[((lane >> 4) * 4 + r) * LDT + tt * 16 + (lane & 15)] = (short)f2bf(s[t][r] * mul);
+      }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      const bf16x8 pf = frag_kc<LDT>(slab, 0, k2 * 32, lane);
+      const int kk = half * 2 + k2;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, frag_nc<LDT>(Vs, t * 16, kk * 32, lane), o[t], 0, 0, 0);
+    }
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {

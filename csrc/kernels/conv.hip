@@ -848,7 +848,6 @@ bool geom_ok(int Cin, int Cout, long pixels) {
 }  // namespace
 
 extern "C" int ca_splitk_reduce(const float*, int, long, void*, int, float, hipStream_t);
-extern "C" int* ca_splitk_ring(long n, hipStream_t s);
 
 extern "C" {
 
@@ -1003,11 +1002,6 @@ int ca_conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, floa
   splits = (p.K + kps - 1) / kps;
   p.k_per_split = kps;
   p.C = ws; p.ldc = p.N; p.split_stride = (long)p.M * p.N;
-  p.tile_cnt = ca_splitk_ring((long)((p.M + 63) / 64) * ((p.N + 63) / 64), s);
-  p.red_out = dw;
-  p.red_ld = p.N;
-  p.red_beta = beta;
-  p.red_bf16 = dw_bf16;
   int rc;
   if (tapmask_loaders() && (long)p.OH * p.OW >= 2 * BK) {  // incremental pixel walk (GConvWgradBI)
     if (Cout <= 64)
@@ -1016,7 +1010,7 @@ int ca_conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, floa
     else
       rc = (p.N <= 64) ? launch<128, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradBI, EPI_F32_PARTIAL>(p, splits, s)
                        : launch<128, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradBI, EPI_F32_PARTIAL>(p, splits, s);
-    if (rc || p.tile_cnt) return rc;
+    if (rc) return rc;
     return ca_splitk_reduce(ws, splits, (long)p.M * p.N, dw, dw_bf16, beta, s);
   }
   if (tapmask_loaders()) {
@@ -1026,7 +1020,7 @@ int ca_conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, floa
     else
       rc = (p.N <= 64) ? launch<128, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradBT, EPI_F32_PARTIAL>(p, splits, s)
                        : launch<128, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradBT, EPI_F32_PARTIAL>(p, splits, s);
-    if (rc || p.tile_cnt) return rc;
+    if (rc) return rc;
     return ca_splitk_reduce(ws, splits, (long)p.M * p.N, dw, dw_bf16, beta, s);
   }
   if (Cout <= 64)  // 64 output channels: 64-row tiles (no MFMA rows past Cout)
@@ -1035,7 +1029,7 @@ int ca_conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, floa
   else
     rc = (p.N <= 64) ? launch<128, 64, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s)
                      : launch<128, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s);
-  if (rc || p.tile_cnt) return rc;
+  if (rc) return rc;
   return ca_splitk_reduce(ws, splits, (long)p.M * p.N, dw, dw_bf16, beta, s);
 }
 

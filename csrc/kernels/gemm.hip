@@ -349,48 +349,6 @@ int ca_gemm_set_core(int kind) {
   return prev;
 }
 
-// Tile tickets of the in-launch split-K combine (ca_mfma_core.h, EPI_F32_PARTIAL with
-// tile_cnt): a per-device ring of counters zeroed once; every launch takes the next n slots
-// and each tile's reducer puts its slot back to 0.  Consecutive launches on one stream reuse
-// slots only after a wrap (1M slots, thousands of launches later); concurrent launches on
-// different streams get disjoint slots.  nullptr = use the separate reduce kernel (the
-// default: CLOUD_AMD_SPLITK_INLAUNCH=1 opts in; first use inside a stream capture, where
-// the ring cannot be allocated, also falls back).
-// Measured (MI355X, sc1 slab stores + relaxed ticket + acquiring reducer): BERT-base FFN
-// weight gradients (144 tiles x 8 splits) 56 + 16 us (GEMM + reduce kernel) -> 178-245 us in
-// one launch; BERT 6,414 -> 4,791 seq/s, ResNet-50 13,790 -> 11,895 img/s.  The last
-// arriver of a tile reads 8 x 64 KB of slabs serially; the separate reduce streams them at
-// ~6 TB/s.  Kept as an opt-in for grids with few, small slabs.
-int* ca_splitk_ring(long n, hipStream_t s) {
-  static int enabled = -1;
-  if (enabled < 0) {
-    const char* e = getenv("CLOUD_AMD_SPLITK_INLAUNCH");
-    enabled = (e && e[0] == '1') ? 1 : 0;
-  }
-  constexpr long CAP = 1L << 20;
-  if (!enabled || n > CAP) return nullptr;
-  static int* ring[64] = {};
-  static long pos[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!ring[dev]) {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return nullptr;
-    int* r = nullptr;
-    if (hipMalloc(&r, CAP * sizeof(int)) != hipSuccess) return nullptr;
-    if (hipMemset(r, 0, CAP * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-      (void)hipFree(r);
-      return nullptr;
-    }
-    ring[dev] = r;
-  }
-  n = (n + 63) / 64 * 64;
-  if (pos[dev] + n > CAP) pos[dev] = 0;
-  int* out = ring[dev] + pos[dev];
-  pos[dev] += n;
-  return out;
-}
-
 int ca_splitk_bias_act(const float* ws, int splits, long M, int N, const float* bias, int act, bf16_t* out,
                        hipStream_t s) {
   if (N % 4 || M <= 0) return -1;
@@ -514,15 +472,8 @@ int ca_gemm_splitk(int layout, const bf16_t* A, long lda, const bf16_t* B, long 
   CoreParams p = base_params(A, lda, B, ldb, ws, N, M, N, K);
   p.k_per_split = kps;
   p.split_stride = (long)M * N;
-  // tile count bound: the smallest tiles any core uses are 64 x 64
-  p.tile_cnt = ca_splitk_ring((long)((M + 63) / 64) * ((N + 63) / 64), s);
-  p.red_out = out;
-  p.red_ld = N;
-  p.red_beta = beta;
-  p.red_bf16 = out_bf16;
-  if (out_bf16 < 0) p.tile_cnt = nullptr;  // slabs only: the caller reduces them (gradfin.hip)
   int rc = dispatch<EPI_F32_PARTIAL>(layout, p, splits, s);
-  if (rc || p.tile_cnt || out_bf16 < 0) return rc;
+  if (rc || out_bf16 < 0) return rc;  // out_bf16 < 0: slabs only, the caller reduces them (gradfin.hip)
   return ca_splitk_reduce(ws, splits, (long)M * N, out, out_bf16, beta, s);
 }
 

@@ -582,6 +582,25 @@ __global__ void __launch_bounds__(256) pad_cols_kernel(const T* __restrict__ in,
   }
 }
 
+// Accumulate the [rows][cols] top-left block of an fp32 [rows_in][ld_in] gradient into a
+// parameter-shaped arena slot (bf16 or fp32): the padded Keras layers (Cin 1 / 3, 10-way
+// heads) compute their weight gradients on the padded shape -- one launch instead of a
+// slice copy, a cast and an add.
+template <typename T>
+__global__ void __launch_bounds__(256) slice_acc_kernel(const float* __restrict__ in, long ld_in,
+                                                        T* __restrict__ out, long rows, int cols) {
+  const long n = rows * cols;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const long r = i / cols;
+    const int c = (int)(i - r * cols);
+    if constexpr (sizeof(T) == 2) {
+      out[i] = f2bf(bf2f(out[i]) + in[r * ld_in + c]);
+    } else {
+      out[i] += in[r * ld_in + c];
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -650,6 +669,15 @@ int ca_pad_cols(const void* in, long ld, int cols, void* out, int cols_out, long
                                                  rows_out);
   else
     return -1;
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+int ca_slice_acc(const float* in, long ld_in, void* out, int out_bf16, long rows, int cols, hipStream_t s) {
+  if (rows <= 0 || cols <= 0 || ld_in < cols) return -1;
+  const int g = ca_stream_grid(rows * cols, 256);
+  if (out_bf16) slice_acc_kernel<bf16_t><<<g, 256, 0, s>>>(in, ld_in, (bf16_t*)out, rows, cols);
+  else slice_acc_kernel<float><<<g, 256, 0, s>>>(in, ld_in, (float*)out, rows, cols);
   CA_LAUNCH_CHECK();
   return 0;
 }

@@ -101,7 +101,13 @@ def _worker(rank, port, mode, n, out_dir):
 
 @pytest.mark.parametrize("mode,n", [("fit_array", 70), ("fit_array", 65), ("fit_dataset", 65),
                                     ("ctl", 70), ("ctl", 65)])
-def test_two_replicas_match_single_process(tmp_path, mode, n):
+def test_two_replicas_match_single_process(tmp_path, mode, n, monkeypatch):
+    # the replicas train on the CPU (gloo); the single-process reference must too, also when
+    # this file runs on a GPU box (where the default strategy would pick the GPU and bf16)
+    from cloud_amd.keras import engine
+
+    monkeypatch.setenv("CLOUD_AMD_DEVICE", "cpu")
+    monkeypatch.setattr(engine, "_POLICY", None)  # re-resolved for the CPU (float32)
     port = _free_port()
     mp.spawn(_worker, args=(port, mode, n, str(tmp_path)), nprocs=WORLD, join=True)
     sys.path.insert(0, ROOT)
