@@ -79,6 +79,27 @@ def _pad2d(t, cols_out, rows_out=None):
     return out
 
 
+def _pad2d_many(specs):
+    """Several :func:`_pad2d` jobs [(t, cols_out, rows_out or None), ...] in ONE launch
+    (rowops.hip pad_cols_multi); entries that need no padding are returned as-is."""
+    outs, jobs = [], []
+    for t, cols_out, rows_out in specs:
+        rows, cols = t.shape
+        rows_out = rows if rows_out is None else rows_out
+        if cols == cols_out and rows == rows_out:
+            outs.append(t)
+            continue
+        if t.stride(-1) != 1:
+            t = t.contiguous()
+        o = torch.empty((rows_out, cols_out), dtype=t.dtype, device=t.device)
+        jobs += [t.data_ptr(), t.stride(0), cols, o.data_ptr(), cols_out, rows, rows_out, t.element_size()]
+        outs.append(o)
+    if jobs:
+        dev = next(t for t, _, _ in specs).device
+        _ext.load(required=True).pad_cols_multi(jobs, _ext.stream_handle(dev))
+    return outs
+
+
 def _act_grad_dev(dy, src, N, Np, act):
     """Native form of :func:`_act_grad` (rowops.hip act_grad): ``dy`` [M, N] (any row
     stride) zero-padded to Np columns and multiplied by act'(src) in one pass; ``src`` is
@@ -155,11 +176,10 @@ class _DenseFn(torch.autograd.Function):
         M, K = x.shape
         N = w.shape[0]
         Kp, Np = _rup8(K), _rup8(N)
-        xp = _pad2d(x, Kp)
-        wp = _pad2d(w, Kp, Np)
-        bp = None
-        if b is not None:
-            bp = _pad2d(b.float().reshape(1, N), Np).reshape(Np)
+        specs = [(x, Kp, None), (w, Kp, Np)] + ([(b.float().reshape(1, N), Np, None)] if b is not None else [])
+        padded = _pad2d_many(specs)  # input, weight and bias padding in one launch
+        xp, wp = padded[0], padded[1]
+        bp = padded[2].reshape(Np) if b is not None else None
         xp, wp = xp.contiguous(), wp.contiguous()
         st = _ext.stream_handle(x.device)
         tiles = -(-M // 128) * -(-Np // 128)
@@ -270,8 +290,11 @@ class _ConvActFn(torch.autograd.Function):
         Cout, KH, KW, _ = w.shape
         (sh, sw), (ph, pw) = stride, padding
         Cp = _rup8(Cin)
-        xp = x if Cp == Cin else _pad2d(x.reshape(-1, Cin), Cp).view(N, H, W, Cp)
-        wp = w if Cp == Cin else _pad2d(w.reshape(-1, Cin), Cp).view(Cout, KH, KW, Cp)
+        if Cp == Cin:
+            xp, wp = x, w
+        else:  # input and weight channel padding in one launch
+            xp, wp = _pad2d_many([(x.reshape(-1, Cin), Cp, None), (w.reshape(-1, Cin), Cp, None)])
+            xp, wp = xp.view(N, H, W, Cp), wp.view(Cout, KH, KW, Cp)
         xp, wp = xp.contiguous(), wp.contiguous()
         OH, OW = _conv._out(H, KH, sh, ph), _conv._out(W, KW, sw, pw)
         y = torch.empty((N, OH, OW, Cout), dtype=torch.bfloat16, device=x.device)

@@ -38,6 +38,8 @@ def unit_seed(device):
 class _XentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, denom, label_smoothing, acc, acc_w):
+        # the `correct` output never receives a gradient: no zero tensor materialised for it
+        ctx.set_materialize_grads(False)
         ext = _ext.load(required=True)
         B, C = logits.shape
         small = B * C <= _BATCH_KERNEL_MAX
@@ -68,6 +70,8 @@ class _XentFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gloss, _gcorrect):
         (dz,) = ctx.saved_tensors
+        if gloss is None:  # (grads are not materialised)
+            return None, None, None, None, None, None
         u = _UNIT.get(str(gloss.device))
         if u is not None and gloss.data_ptr() == u.data_ptr():
             return dz, None, None, None, None, None

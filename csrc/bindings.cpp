@@ -91,6 +91,7 @@ int ca_colsum(const bf16_t*, long, int, long, float*, int, float*, hipStream_t);
 int ca_act_grad(const bf16_t*, long, int, const bf16_t*, bf16_t*, long, int, int, hipStream_t);
 int ca_pad_cols(const void*, long, int, void*, int, long, long, int, hipStream_t);
 int ca_slice_acc(const float*, long, void*, int, long, int, hipStream_t);
+int ca_pad_cols_multi(const long*, int, hipStream_t);
 int ca_splitk_bias_act(const float*, int, long, int, const float*, int, bf16_t*, hipStream_t);
 int ca_embed_sum(const int32_t*, const int32_t*, const float*, const float*, const float*, bf16_t*, long, int, int, int,
                  hipStream_t);
@@ -349,6 +350,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("splitk_bias_act", [](u64 ws, int splits, long M, int N, u64 bias, int act, u64 out, u64 s) {
     check(ca_splitk_bias_act(P(const float*, ws), splits, M, N, P(const float*, bias), act, P(bf16_t*, out), S(s)),
           "splitk_bias_act");
+  });
+  m.def("pad_cols_multi", [](std::vector<long> jobs, u64 s) {
+    check(ca_pad_cols_multi(jobs.data(), (int)(jobs.size() / 8), S(s)), "pad_cols_multi");
   });
   m.def("slice_acc", [](u64 in, long ld_in, u64 out, int out_bf16, long rows, int cols, u64 s) {
     check(ca_slice_acc(P(const float*, in), ld_in, P(void*, out), out_bf16, rows, cols, S(s)), "slice_acc");

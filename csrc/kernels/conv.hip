@@ -389,6 +389,43 @@ struct GConvFwdAT {
   }
 };
 
+// forward A of a stride-1, unpadded convolution whose kernel row spans exactly one K tile
+// (KW * Cin == BK): the space-to-depth ResNet stem, 4x4 over 16 channels.  K tile kh of
+// output pixel (n, oy, ox) is the CONTIGUOUS 128-B run X[n, oy + kh, ox .. ox + KW - 1, :],
+// so a chunk's address is its row base plus kh whole input rows -- no per-tile tap decode
+// (the general GConvFwdA loader re-derives tap and channel for every chunk and K tile).
+template <int R, int CPT, int NT>
+struct GConvRowA {
+  static constexpr bool KC = true, BUF = true;
+  const CoreParams& P;
+  const bf16_t* sbase;  // &X[n0]
+  uint32_t nrec;
+  uint32_t rofs[CPT];   // byte offset of X[n, oy, ox, col] from sbase; nrec for rows past M
+  uint32_t rowb;        // bytes of one input row (W * Cin * 2)
+  __device__ GConvRowA(const CoreParams& p, bool, int r0, int tid) : P(p) {
+    const int row_t = tid >> 3;
+    const int col = ((tid & 7) ^ (row_t & 7)) << 3;
+    const long img = (long)P.H * P.W * P.Cin;
+    const int n0 = (int)fdiv(fdiv((uint32_t)r0, P.div_ow), P.div_oh);
+    sbase = P.A + n0 * img;
+    nrec = buf_span((P.Nb - n0) * img * 2);
+    rowb = (uint32_t)(P.W * P.Cin * 2);
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int m = r0 + row_t + i * (NT / 8);
+      uint32_t o = nrec;
+      if (m < P.M) {
+        const Pix q = decode((uint32_t)m, P.div_ow, P.div_oh);
+        o = (uint32_t)(((((long)(q.n - n0) * P.H + q.y) * P.W + q.x) * P.Cin + col) * 2);
+      }
+      rofs[i] = o;
+    }
+  }
+  __device__ __forceinline__ uint32_t off(int i, int k0) const {
+    return rofs[i] >= nrec ? nrec : rofs[i] + (uint32_t)(k0 / BK) * rowb;
+  }
+};
+
 // stride-1 dgrad A: dY[n, iy + p - kh, ix + p - kw, co]; Cout % BK == 0.
 template <int R, int CPT, int NT>
 struct GConvDgradAT {
@@ -859,6 +896,15 @@ int ca_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   p.A = x; p.B = w; p.lda = Cin; p.ldb = (long)KH * KW * Cin; p.C = y; p.ldc = Cout;
   p.M = Nb * p.OH * p.OW; p.N = Cout; p.K = KH * KW * Cin; p.k_per_split = p.K;
   p.stats = stats;
+  if (sh == 1 && sw == 1 && ph == 0 && pw == 0 && KW * Cin == BK && tapmask_loaders() && use_glds() &&
+      (long)Nb * H * W * Cin * 2 < (long)BUF_CAP) {
+    // one K tile per kernel row (the space-to-depth stem): row-segment loader
+    if (Cout <= 64)
+      return stats ? launch<128, 64, ConvFwdA, DenseKC, GConvRowA, GDenseKC, EPI_BF16_ST>(p, 1, s)
+                   : launch<128, 64, ConvFwdA, DenseKC, GConvRowA, GDenseKC, EPI_BF16>(p, 1, s);
+    return stats ? launch<128, 128, ConvFwdA, DenseKC, GConvRowA, GDenseKC, EPI_BF16_ST>(p, 1, s)
+                 : launch<128, 128, ConvFwdA, DenseKC, GConvRowA, GDenseKC, EPI_BF16>(p, 1, s);
+  }
   if (p.cin_tile && KH * KW <= 32 && tapmask_loaders()) {
     if (stats) {
       if (Cout <= 64) return launch_n64<ConvFwdA, DenseKC, GConvFwdAT, GDenseKC, EPI_BF16_ST>(p, s);

@@ -246,7 +246,8 @@ __global__ void __launch_bounds__(256) col_finalize_kernel(const float* __restri
 
 // per-block column partial sums of bf16 X[M][N] (N % 8 == 0): block = 32 col-groups(8 cols) x 8 row lanes
 __global__ void __launch_bounds__(256) colsum_part_kernel(const bf16_t* __restrict__ x, long M, int N, long ld,
-                                                          float* __restrict__ part) {
+                                                          float* __restrict__ part, float* __restrict__ fin = nullptr,
+                                                          int fin_acc = 0) {
   __shared__ float red[8][256];
   const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int c0 = (blockIdx.x * 32 + cg) * 8;
@@ -267,7 +268,11 @@ __global__ void __launch_bounds__(256) colsum_part_kernel(const bf16_t* __restri
     float t = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) t += red[k][c];
-    part[(long)blockIdx.y * N + gc] = t;
+    if (fin) {  // one row-part (gridDim.y == 1): this is the column sum itself
+      fin[gc] = fin_acc ? fin[gc] + t : t;
+    } else {
+      part[(long)blockIdx.y * N + gc] = t;
+    }
   }
 }
 
@@ -571,6 +576,32 @@ __global__ void __launch_bounds__(256) act_grad_kernel(const bf16_t* __restrict_
 // Zero-pad the columns of a row-major matrix to a multiple the MFMA tiles take (Keras
 // layers with Cin = 1 / 3 or a 10-way head): out[r][c] = c < cols ? in[r * ld + c] : 0,
 // out row stride cols_out; 2- or 4-byte elements.  One launch instead of F.pad's fill + copy.
+struct PadJob {
+  const void* in;
+  void* out;
+  long ld, rows, rows_out;
+  int cols, cols_out, eb;
+};
+struct PadJobs {
+  PadJob j[4];
+};
+
+// several pad_cols jobs in one launch (blockIdx.y = job): a layer's padded input, weight
+// and bias cost one dispatch
+__global__ void __launch_bounds__(256) pad_cols_multi_kernel(PadJobs jobs) {
+  const PadJob& J = jobs.j[blockIdx.y];
+  const long n = J.rows_out * J.cols_out;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const long r = i / J.cols_out;
+    const int c = (int)(i - r * J.cols_out);
+    const bool ok = c < J.cols && r < J.rows;
+    if (J.eb == 2)
+      reinterpret_cast<uint16_t*>(J.out)[i] = ok ? reinterpret_cast<const uint16_t*>(J.in)[r * J.ld + c] : 0;
+    else
+      reinterpret_cast<uint32_t*>(J.out)[i] = ok ? reinterpret_cast<const uint32_t*>(J.in)[r * J.ld + c] : 0u;
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) pad_cols_kernel(const T* __restrict__ in, long ld, int cols,
                                                        T* __restrict__ out, int cols_out, long rows, long rows_out) {
@@ -673,6 +704,30 @@ int ca_pad_cols(const void* in, long ld, int cols, void* out, int cols_out, long
   return 0;
 }
 
+// jobs: n x [in, ld, cols, out, cols_out, rows, rows_out, elem_bytes] (n <= 4)
+int ca_pad_cols_multi(const long* jobs, int n, hipStream_t s) {
+  if (n < 1 || n > 4) return -1;
+  PadJobs P{};
+  long most = 1;
+  for (int k = 0; k < n; ++k) {
+    const long* q = jobs + 8 * k;
+    PadJob& J = P.j[k];
+    J.in = reinterpret_cast<const void*>(q[0]);
+    J.ld = q[1];
+    J.cols = (int)q[2];
+    J.out = reinterpret_cast<void*>(q[3]);
+    J.cols_out = (int)q[4];
+    J.rows = q[5];
+    J.rows_out = q[6];
+    J.eb = (int)q[7];
+    if (J.cols > J.cols_out || J.rows > J.rows_out || (J.eb != 2 && J.eb != 4)) return -1;
+    if (J.rows_out * J.cols_out > most) most = J.rows_out * J.cols_out;
+  }
+  pad_cols_multi_kernel<<<dim3(ca_stream_grid(most, 256), n), 256, 0, s>>>(P);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
 int ca_slice_acc(const float* in, long ld_in, void* out, int out_bf16, long rows, int cols, hipStream_t s) {
   if (rows <= 0 || cols <= 0 || ld_in < cols) return -1;
   const int g = ca_stream_grid(rows * cols, 256);
@@ -696,6 +751,11 @@ int ca_colsum(const bf16_t* x, long M, int N, long ld, float* out, int accumulat
   if (ry > 256) ry = 256;
   if (ry < 1) ry = 1;
   dim3 grid(ca_cdiv(N, 256), ry);
+  if (ry == 1 && accumulate >= 0) {  // <= 64 rows (a Keras Dense bias): one launch, no finalize
+    colsum_part_kernel<<<grid, 256, 0, s>>>(x, M, N, ld, ws, out, accumulate);
+    CA_LAUNCH_CHECK();
+    return 0;
+  }
   colsum_part_kernel<<<grid, 256, 0, s>>>(x, M, N, ld, ws);
   CA_LAUNCH_CHECK();
   if (accumulate < 0) return 0;  // partials [ry][N] left in ws for a batched finalisation

@@ -238,7 +238,9 @@ def test_linear_autograd_writes_arena_grad():
     (2, 14, 128, 256, 1, 2, 0), (1, 9, 24, 40, 3, 1, 1), (2, 8, 256, 64, 1, 1, 0),
     # tap-mask loaders: two 64-channel slices per tap, 7x7 maps (every row touches a border),
     # even-sized strided input, 3 images (pixel decode across image boundaries)
-    (3, 7, 128, 64, 3, 1, 1), (2, 10, 64, 128, 3, 2, 1), (3, 5, 64, 192, 3, 1, 1)])
+    (3, 7, 128, 64, 3, 1, 1), (2, 10, 64, 128, 3, 2, 1), (3, 5, 64, 192, 3, 1, 1),
+    # one K tile per kernel row (KW * Cin = 64, stride 1, no padding): the row-segment loader
+    (2, 9, 16, 64, 4, 1, 0), (3, 11, 16, 128, 4, 1, 0)])
 def test_conv_fwd_dgrad_wgrad_vs_fp32(N, H, Cin, Cout, k, s, p):
     from cloud_amd.ops import conv2d_nhwc
 
