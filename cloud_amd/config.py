@@ -119,6 +119,8 @@ _VARS = [
         "node probe (tests point it at a fake tree)", "launcher"),
     Var("CLOUD_AMD_TUNER_STANDBY", bool, True, "trial scheduler: start the packing wave's workers with the probe "
         "wave, gated (imports done, no GPU touched) until the measured footprint says how many may run", "tuner"),
+    Var("CLOUD_AMD_TUNER_EARLY_FOOTPRINT", bool, True, "tuner probe worker: report the trial HBM footprint after "
+        "the first training step of its first trial (0 = after the whole trial)", "tuner"),
     Var("CLOUD_AMD_FOOTPRINT_FILE", str, None, "where a tuner worker reports its first trial's peak HBM "
         "(set by TrialScheduler for the probe wave)", "tuner"),
     Var("CLOUD_AMD_BENCH_VIA_RUN", bool, True, "bench scripts launch their ranks through cloud_amd.run()",

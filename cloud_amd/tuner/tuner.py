@@ -200,6 +200,18 @@ class _TunerCallback:
         from ..keras.callbacks import Callback
 
         class CB(Callback):
+            def on_train_batch_end(cb, batch, logs=None):
+                # the scheduler's probe worker: report the measured footprint after the
+                # first optimizer step of the first trial (the training step is the trial's
+                # memory peak; the scheduler adds its headroom), so the packing wave starts
+                # a whole trial earlier than after the trial ends
+                if tuner._early_report_pending and batch == 0:
+                    from ..utils import hbm
+
+                    tuner._early_report_pending = False
+                    if hbm.report_footprint() is not None:
+                        tuner._reported = True
+
             def on_epoch_end(cb, epoch, logs=None):
                 status = tuner.oracle.update_trial(trial.trial_id, dict(logs or {}), step=epoch + 1)
                 if status == TrialStatus.STOPPED:
@@ -289,7 +301,12 @@ class Tuner:
         from ..utils import faults  # noqa: F401  (fault injection reaches trials through fit)
         from ..utils import hbm
 
-        reported = False
+        from .. import config
+
+        self._reported = False
+        # CLOUD_AMD_TUNER_EARLY_FOOTPRINT: report after the first step (default) or the first trial
+        self._early_report_pending = bool(os.environ.get("CLOUD_AMD_FOOTPRINT_FILE")) and bool(
+            config.get("CLOUD_AMD_TUNER_EARLY_FOOTPRINT"))
         while True:
             trial = self.oracle.create_trial(self.tuner_id)
             if trial.status == TrialStatus.STOPPED:
@@ -302,9 +319,10 @@ class Tuner:
                 self.oracle.end_trial(trial.trial_id, TrialStatus.INVALID)
                 continue
             self.oracle.end_trial(trial.trial_id, TrialStatus.COMPLETED)
-            if not reported:  # the scheduler packs more workers per GPU from this measurement
+            if not self._reported:  # the scheduler packs more workers per GPU from this measurement
                 hbm.report_footprint()
-                reported = True
+                self._reported = True
+                self._early_report_pending = False
 
     def get_best_hyperparameters(self, num_trials=1):
         return [t.hyperparameters for t in self.oracle.get_best_trials(num_trials)]
