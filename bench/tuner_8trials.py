@@ -71,6 +71,7 @@ def main():
     ap.add_argument("--trials", type=int, default=8)
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--train", type=int, default=8192)
+    ap.add_argument("--timeline", type=int, default=1, help="per-worker phase marks + per-trial spans in the JSON")
     args = ap.parse_args()
     from cloud_amd.core.topology import visible_gpu_count
     from cloud_amd.tuner.scheduler import TrialScheduler, study_report
@@ -85,7 +86,7 @@ def main():
     # workers=None: probe one worker per GPU, then pack more per GPU from the first trial's
     # measured peak HBM (no more workers than trials)
     sched = TrialScheduler("bench.tuner_8trials:worker", n_gpus=n_gpus, workers=workers, env=env,
-                           max_workers=args.trials)
+                           max_workers=args.trials, timeline=bool(args.timeline))
     res = sched.run(timeout=3000)
     wall = time.time() - t0
     sid = next(d for d in os.listdir(study_dir) if d.endswith("mnist_cnn_8"))  # CloudTuner prefixes the id
@@ -110,6 +111,13 @@ def main():
         "exit_codes": res["exit_codes"], "data": "synthetic MNIST", "config": {"epochs": args.epochs,
                                                                              "train_examples": args.train},
     }
+    if args.timeline:
+        # where the wall time goes: worker phases (s after start) and each trial's span
+        out["timeline"] = {
+            "workers": res.get("timeline"),
+            "trials": [{"client": t.get("clientId"), "start": round(t["startTs"] - t0, 2),
+                        "end": round(t["endTs"] - t0, 2)} for t in trials if "startTs" in t and "endTs" in t],
+        }
     print(json.dumps(out), flush=True)
 
 

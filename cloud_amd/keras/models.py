@@ -316,7 +316,7 @@ class Model(Layer):
             if t is not b.data:
                 b.data.copy_(t)
 
-    def _forward_train(self, x):
+    def _forward_train(self, x, training=True):
         """Logits for the fused loss, in the compute dtype (the kernel reads bf16 directly:
         no fp32 cast of the model output)."""
         sm = self._final_softmax_layer() if (self._fused_xent and not self.loss.from_logits) else None
@@ -324,7 +324,7 @@ class Model(Layer):
             sm._emit_logits = True
         self._raw_logits = True
         try:
-            return self(x, training=True)
+            return self(x, training=training)
         finally:
             self._raw_logits = False
             if sm is not None:
@@ -368,7 +368,7 @@ class Model(Layer):
         with trace.range("backward"):
             if total is loss and self._fused_xent:
                 # the fused loss hands its stored gradient on as-is for the unit seed
-                torch.autograd.backward(total, grad_tensors=ops.unit_seed(total.device))
+                ops.backward_with_seed(total, ops.unit_seed(total.device))
             else:
                 total.backward()
         if self._reducer is not None:
@@ -564,10 +564,15 @@ class Model(Layer):
         if not _internal:
             self._setup(sample)
         dev = self._strategy.device
-        saved = (self._loss_tracker, [m.state() for m in self.compiled_metrics]) if hasattr(self, "_loss_tracker") \
-            else None
+        saved = (self._loss_tracker, [m.state() for m in self.compiled_metrics], self._dev_acc) \
+            if hasattr(self, "_loss_tracker") else None
         self._reset_metrics()
         self.eval()
+        if dev.type == "cuda" and _plain_array(x) and (y is None or _plain_array(y)):
+            x, y = _device_arrays(x, y, dev, self._input_dtype())  # one upload, not one per batch
+        # the training step's fused softmax-xent kernel scores the batch too (loss + accuracy
+        # into the device accumulator): no separate softmax / log / nll / argmax kernels
+        fused = self._metrics_fusable() and self.loss is not None and sample_weight is None
         with torch.no_grad():
             for i, (xb, yb, n_local, _) in enumerate(self._batches(x, y, batch_size, False, 0)):
                 if steps is not None and i >= steps:
@@ -576,6 +581,12 @@ class Model(Layer):
                     continue  # stand-in row of an empty replica slice: nothing to score
                 xt = _to_torch(xb, dev, self._input_dtype())
                 yt = _to_torch(yb, dev) if yb is not None else None
+                if fused and yt is not None:
+                    logits = self._forward_train(xt, training=False)
+                    if self._dev_acc is None:
+                        self._dev_acc = torch.zeros(3, dtype=torch.float32, device=logits.device)
+                    self.loss.fused_logits_loss(logits, yt, acc=self._dev_acc)
+                    continue
                 pred = self(xt, training=False)
                 if self.loss is not None and yt is not None:
                     loss = self.loss(yt, pred)
@@ -587,6 +598,7 @@ class Model(Layer):
             self._loss_tracker = saved[0]
             for m, st in zip(self.compiled_metrics, saved[1]):
                 m.set_state(st)
+            self._dev_acc = saved[2]
         if return_dict:
             return logs
         vals = list(logs.values())

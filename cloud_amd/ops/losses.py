@@ -35,6 +35,20 @@ def unit_seed(device):
     return t
 
 
+def backward_with_seed(loss, seed):
+    """``torch.autograd.backward(loss, grad_tensors=seed)`` without its Python-side shape
+    check: in this torch that check imports ``torch.fx.experimental.symbolic_shapes`` -- and
+    with it sympy, 0.86 s cold on the GPU box -- on the first seeded backward of every process
+    (every tuner worker's first trial; scripts/debug/cold_trial.py)."""
+    if loss.shape != seed.shape:
+        raise ValueError(f"seed shape {tuple(seed.shape)} != loss shape {tuple(loss.shape)}")
+    try:
+        from torch.autograd.graph import _engine_run_backward
+    except ImportError:  # pragma: no cover - other torch versions
+        return torch.autograd.backward(loss, grad_tensors=seed)
+    _engine_run_backward((loss,), (seed,), False, False, (), allow_unreachable=True, accumulate_grad=True)
+
+
 class _XentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, denom, label_smoothing, acc, acc_w):

@@ -38,7 +38,25 @@ def _await_gate(gate_file, poll_s=0.01):
         time.sleep(poll_s)
 
 
-def _worker(target, tuner_id, device, env, gate_file=None):
+def _mark(timeline, key):
+    if timeline is not None:
+        timeline[key] = time.time()
+
+
+def _worker(target, tuner_id, device, env, gate_file=None, timeline_file=None):
+    tl = {"entered": time.time()} if timeline_file else None
+    try:
+        _worker_body(target, tuner_id, device, env, gate_file, tl)
+    finally:
+        if tl is not None:
+            _mark(tl, "exited")
+            tmp = timeline_file + ".tmp"
+            with open(tmp, "w") as fh:
+                json.dump(tl, fh)
+            os.replace(tmp, timeline_file)
+
+
+def _worker_body(target, tuner_id, device, env, gate_file, tl):
     if gate_file:
         # warm standby: pay interpreter start, `import torch` and the target module import
         # while the probe wave runs, touching no GPU (HIP is initialised only after the go)
@@ -46,7 +64,10 @@ def _worker(target, tuner_id, device, env, gate_file=None):
 
         mod_name = target.split(":")[0]
         importlib.import_module(mod_name)
-        if not _await_gate(gate_file):
+        _mark(tl, "imported")
+        go = _await_gate(gate_file)
+        _mark(tl, "released" if go else "dismissed")
+        if not go:
             return
     os.environ.update(env)
     os.environ["CLOUD_AMD_TUNER_ID"] = tuner_id
@@ -56,6 +77,7 @@ def _worker(target, tuner_id, device, env, gate_file=None):
 
         torch.cuda.set_device(int(device.split(":")[1]))
         os.environ["LOCAL_RANK"] = device.split(":")[1]
+        _mark(tl, "device_ready")
     else:
         os.environ["CLOUD_AMD_DEVICE"] = "cpu"
     mod, fn = target.split(":")
@@ -78,7 +100,7 @@ class TrialScheduler:
     every worker also needs a core for its input pipeline and launches)."""
 
     def __init__(self, target, n_gpus=None, trial_gb=None, workers=None, max_workers=None, env=None,
-                 hbm_gb=None, headroom=1.25, state_dir=None, probe_timeout_s=None):
+                 hbm_gb=None, headroom=1.25, state_dir=None, probe_timeout_s=None, timeline=False):
         self.target = target
         if n_gpus is None:
             from ..core.topology import hbm_gb_per_gpu, visible_gpu_count
@@ -98,6 +120,8 @@ class TrialScheduler:
         self.env = dict(env or {})
         self.state_dir = state_dir
         self.probe_timeout_s = probe_timeout_s
+        self.timeline = timeline
+        self._state = None
         self.footprint_gb = None
         self.per_gpu = None
         if workers:
@@ -122,7 +146,8 @@ class TrialScheduler:
         env = dict(self.env)
         if footprint_file:
             env["CLOUD_AMD_FOOTPRINT_FILE"] = footprint_file
-        p = ctx.Process(target=_worker, args=(self.target, f"tuner{i}", self._device(i), env, gate_file),
+        tl_file = os.path.join(self._state, f"timeline_tuner{i}.json") if self.timeline else None
+        p = ctx.Process(target=_worker, args=(self.target, f"tuner{i}", self._device(i), env, gate_file, tl_file),
                         daemon=False)
         p.start()
         return p
@@ -145,11 +170,11 @@ class TrialScheduler:
         ctx = mp.get_context("spawn")
         t0 = time.time()
         procs = []
+        state = self._state = self.state_dir or tempfile.mkdtemp(prefix="cloud_amd_sched_")
+        os.makedirs(state, exist_ok=True)
         if self.workers is not None:
             procs = [self._spawn(ctx, i) for i in range(self.workers)]
         else:
-            state = self.state_dir or tempfile.mkdtemp(prefix="cloud_amd_sched_")
-            os.makedirs(state, exist_ok=True)
             files = [os.path.join(state, f"footprint_tuner{i}.json") for i in range(self._slots())]
             procs = [self._spawn(ctx, i, files[i]) for i in range(self._slots())]
             # warm standbys for the packing wave: started now, gated until the footprint is
@@ -192,8 +217,23 @@ class TrialScheduler:
                 p.terminate()
                 p.join(5)
             codes.append(p.exitcode)
-        return {"workers": len(procs), "exit_codes": codes, "wall_s": time.time() - t0,
-                "trials_per_gpu": self.per_gpu, "footprint_gb": self.footprint_gb}
+        out = {"workers": len(procs), "exit_codes": codes, "wall_s": time.time() - t0,
+               "trials_per_gpu": self.per_gpu, "footprint_gb": self.footprint_gb}
+        if self.timeline:
+            out["timeline"] = self.read_timeline(t0)
+        return out
+
+    def read_timeline(self, t0):
+        """Per-worker phase marks (seconds after the scheduler started): ``entered`` (the
+        spawned interpreter runs), ``imported`` / ``released`` / ``dismissed`` (standbys),
+        ``device_ready`` (HIP initialised), ``exited``."""
+        rows = {}
+        for name in sorted(os.listdir(self._state)):
+            if name.startswith("timeline_") and name.endswith(".json"):
+                with open(os.path.join(self._state, name)) as fh:
+                    marks = json.load(fh)
+                rows[name[len("timeline_"):-len(".json")]] = {k: round(v - t0, 3) for k, v in marks.items()}
+        return rows
 
 
 def study_report(study_dir, study_id):

@@ -254,7 +254,8 @@ class StudyService:
                 tid = data["next_id"]
                 data["next_id"] += 1
                 trial = {"name": f"{study['name']}/trials/{tid}", "state": "ACTIVE", "parameters": params,
-                         "clientId": client_id, "measurements": [], "startTime": _ts()}
+                         "clientId": client_id, "measurements": [], "startTime": _ts(),
+                         "startTs": time.time()}
                 data["trials"].append(trial)
                 out.append(trial)
             self._write(sid, data)

@@ -182,3 +182,38 @@ def test_conv2d_rectangular_kernels_and_strides(kernel, strides, padding):
     torch.testing.assert_close(y.float(), ref, atol=1e-4, rtol=1e-4)
     if padding == "same":
         assert y.shape[1] == -(-11 // strides[0]) and y.shape[2] == -(-14 // strides[1])
+
+
+def test_evaluate_on_fused_loss_matches_reference_and_keeps_train_logs():
+    """evaluate() scores with the training step's fused softmax-xent (loss + accuracy into
+    the device accumulator); the numbers equal the plain formulas on predict()'s
+    probabilities, and fit's validation pass leaves the epoch's TRAIN logs intact."""
+    from cloud_amd import keras
+
+    rng = np.random.default_rng(5)
+    x = rng.normal(size=(200, 12)).astype("float32")
+    y = (x[:, 0] + 0.5 * x[:, 1] > 0).astype("int64") + (x[:, 2] > 1).astype("int64")
+    model = keras.Sequential([keras.layers.Dense(16, activation="relu", input_shape=(12,)),
+                              keras.layers.Dense(3, activation="softmax")])
+    model.compile(loss="sparse_categorical_crossentropy", optimizer=keras.optimizers.Adam(1e-2),
+                  metrics=["accuracy"])
+    from cloud_amd.keras import losses as L
+
+    def banned(*a, **k):
+        raise AssertionError("unfused loss path reached")
+
+    orig = L.SparseCategoricalCrossentropy.per_example
+    L.SparseCategoricalCrossentropy.per_example = banned
+    try:
+        hist = model.fit(x, y, batch_size=32, epochs=2, validation_data=(x[:96], y[:96]), verbose=0)
+    finally:
+        L.SparseCategoricalCrossentropy.per_example = orig
+    h = hist.history
+    assert h["loss"][-1] != h["val_loss"][-1]  # train logs not overwritten by the eval accumulator
+    loss, acc = model.evaluate(x[:96], y[:96], batch_size=40, verbose=0)
+    p = model.predict(x[:96], batch_size=96).astype("float64")
+    ref_loss = float(np.mean(-np.log(np.clip(p[np.arange(96), y[:96]], 1e-7, None))))
+    ref_acc = float(np.mean(p.argmax(-1) == y[:96]))
+    assert abs(loss - ref_loss) < 2e-2 * max(1.0, ref_loss), (loss, ref_loss)
+    assert abs(acc - ref_acc) <= 1.0 / 96 + 1e-9, (acc, ref_acc)
+    assert abs(h["val_loss"][-1] - loss) < 1e-5 and abs(h["val_accuracy"][-1] - acc) < 1e-6

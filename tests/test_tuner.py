@@ -302,7 +302,7 @@ def test_scheduler_packs_from_measured_footprint(tmp_path):
     env = {"STUDY_ID": "packed", "STUDY_DIR": str(tmp_path), "PYTHONPATH": os.path.join(HERE, "data"),
            "FAKE_FOOTPRINT_GB": "1.0"}
     sched = TrialScheduler("tuner_worker:run", n_gpus=0, env=env, hbm_gb=4.0, max_workers=8,
-                           state_dir=str(tmp_path / "sched"))
+                           state_dir=str(tmp_path / "sched"), timeline=True)
     assert sched.packing_from_footprint(1.0) == 2          # 4 GB * 0.9 // (1.0 * 1.25)
     assert sched.packing_from_footprint(0.05) == 57
     res = sched.run(timeout=600)
@@ -311,6 +311,13 @@ def test_scheduler_packs_from_measured_footprint(tmp_path):
     with open(tmp_path / "CloudTuner_study_packed" / "study.json") as f:
         trials = json.load(f)["trials"]
     assert len(trials) == 6 and all(t["state"] == "COMPLETED" for t in trials)
+    assert all(t["startTs"] <= t["endTs"] for t in trials)
+    # per-worker phase marks: the probe, then 7 gated standbys (1 released, 6 dismissed)
+    tl = res["timeline"]
+    assert tl["tuner0"]["entered"] <= tl["tuner0"]["exited"] and "imported" not in tl["tuner0"]
+    standby = [tl[f"tuner{i}"] for i in range(1, 8)]
+    assert sum("released" in m for m in standby) == 1 and sum("dismissed" in m for m in standby) == 6
+    assert all(m["imported"] <= m.get("released", m.get("dismissed")) for m in standby)
 
 
 def test_tuner_reports_footprint_after_first_trial(tmp_path, monkeypatch):
