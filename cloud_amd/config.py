@@ -105,6 +105,8 @@ _VARS = [
     Var("CLOUD_AMD_GRAD_FIN_BATCH", bool, True, "BERT layer backward: the eight fixed-order gradient "
         "finalisations (split-K slab sums, LayerNorm / bias column partials) run as ONE launch at the end of the "
         "layer (csrc/kernels/gradfin.hip); 0 = one launch each", "ops"),
+    Var("CLOUD_AMD_LN_BIAS_FWD", bool, True, "BERT: the LayerNorm forward adds the bias of the output projection "
+        "that feeds it (attention output, FFN2), so those GEMMs run without a bias epilogue", "ops"),
     Var("CLOUD_AMD_LN_BIAS_SUM", bool, True, "BERT: the LayerNorm backward also sums the bias gradient of the "
         "projection that fed it (no separate column-sum pass)", "ops"),
     Var("CLOUD_AMD_TAIL_BUCKET_MB", float, 1.0, "cap on the last gradient bucket (the first layers' gradients, "
@@ -119,6 +121,8 @@ _VARS = [
         "node probe (tests point it at a fake tree)", "launcher"),
     Var("CLOUD_AMD_TUNER_STANDBY", bool, True, "trial scheduler: start the packing wave's workers with the probe "
         "wave, gated (imports done, no GPU touched) until the measured footprint says how many may run", "tuner"),
+    Var("CLOUD_AMD_TUNER_FAST_EXIT", bool, True, "tuner workers end with os._exit after their last trial is in the "
+        "study (no interpreter / HIP teardown on the study's critical path)", "tuner"),
     Var("CLOUD_AMD_TUNER_EARLY_FOOTPRINT", bool, True, "tuner probe worker: report the trial HBM footprint after "
         "the first training step of its first trial (0 = after the whole trial)", "tuner"),
     Var("CLOUD_AMD_FOOTPRINT_FILE", str, None, "where a tuner worker reports its first trial's peak HBM "

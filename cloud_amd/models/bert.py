@@ -175,13 +175,18 @@ class _LayerFn(torch.autograd.Function):
         s2 = next_seed() if p_hidden > 0 else 0
         qkv = raw.gemm(x, layer.wqkv, bias=layer.bqkv)
         ctx_, lse = raw.attn_fwd(qkv, B, S, H, key_len, p_attn, sa, scale=1.0 / math.sqrt(cfg.hidden_size // H))
-        a = raw.gemm(ctx_, layer.wo, bias=layer.bo)
-        y1, h1, m1, r1 = raw.ln_fwd(a, layer.ln1_w, layer.ln1_b, eps, residual=x, p_in=p_hidden, seed_in=s1)
+        # the output projections' biases (bo, b2) are added by the LayerNorm pass that reads
+        # their outputs (their gradients already come from its backward): the GEMMs are plain
+        lnb = config.get("CLOUD_AMD_LN_BIAS_FWD")
+        a = raw.gemm(ctx_, layer.wo, bias=None if lnb else layer.bo)
+        y1, h1, m1, r1 = raw.ln_fwd(a, layer.ln1_w, layer.ln1_b, eps, residual=x, p_in=p_hidden, seed_in=s1,
+                                    x_bias=layer.bo if lnb else None)
         del a
         pre = torch.empty((x.shape[0], cfg.intermediate_size), dtype=torch.bfloat16, device=x.device)
         f = raw.gemm(y1, layer.w1, bias=layer.b1, act=cfg.hidden_act, preact=pre)
-        o = raw.gemm(f, layer.w2, bias=layer.b2)
-        y2, h2, m2, r2 = raw.ln_fwd(o, layer.ln2_w, layer.ln2_b, eps, residual=y1, p_in=p_hidden, seed_in=s2)
+        o = raw.gemm(f, layer.w2, bias=None if lnb else layer.b2)
+        y2, h2, m2, r2 = raw.ln_fwd(o, layer.ln2_w, layer.ln2_b, eps, residual=y1, p_in=p_hidden, seed_in=s2,
+                                    x_bias=layer.b2 if lnb else None)
         del o
         ctx.layer, ctx.B, ctx.S = layer, B, S
         ctx.cfgs = (p_hidden, p_attn, sa, s1, s2)

@@ -505,20 +505,26 @@ def colsum_into(x, out, accumulate=True):
     return out
 
 
-def ln_fwd(x, gamma, beta, eps, residual=None, p_in=0.0, seed_in=0, p_out=0.0, seed_out=0, keep_h=True):
-    """y = drop_out(LN(residual + drop_in(x))).  Returns (y, h, mean, rstd); h is the
-    pre-norm sum (None when it equals x: no residual, no input dropout, or keep_h=False)."""
+def ln_fwd(x, gamma, beta, eps, residual=None, p_in=0.0, seed_in=0, p_out=0.0, seed_out=0, keep_h=True,
+           x_bias=None):
+    """y = drop_out(LN(residual + drop_in(x + x_bias))).  Returns (y, h, mean, rstd); h is
+    the pre-norm sum (None when it equals x: no residual, no input dropout, no bias, or
+    keep_h=False).  ``x_bias`` (fp32 [C]): the bias of the GEMM that produced x, added here
+    so that GEMM runs without a bias epilogue."""
     ext = _ext.load(required=True)
     C = x.shape[-1]
     M = x.numel() // C
     y = torch.empty_like(x)
-    need_h = keep_h and (residual is not None or p_in > 0)
+    if x_bias is not None and (x_bias.dtype != torch.float32 or x_bias.numel() != C or not x_bias.is_contiguous()
+                               or x_bias.data_ptr() % 16):
+        raise ValueError("ln_fwd x_bias: contiguous 16-byte-aligned fp32 [C] expected")
+    need_h = keep_h and (residual is not None or p_in > 0 or x_bias is not None)
     h = torch.empty_like(x) if need_h else None
     mean = torch.empty(M, dtype=torch.float32, device=x.device)
     rstd = torch.empty(M, dtype=torch.float32, device=x.device)
     ext.ln_fwd(x.data_ptr(), _ext.ptr(residual), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), _ext.ptr(h),
                mean.data_ptr(), rstd.data_ptr(), M, C, float(eps), float(p_in), int(seed_in), float(p_out),
-               int(seed_out), _st(x.device))
+               int(seed_out), _st(x.device), _ext.ptr(x_bias))
     return y, h, mean, rstd
 
 

@@ -83,7 +83,7 @@ int ca_gemm_ex(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int
                int, bf16_t*, const bf16_t*, long, hipStream_t);
 long ca_ln_workspace_floats(long, int);
 int ca_ln_fwd(const bf16_t*, const bf16_t*, const float*, const float*, bf16_t*, bf16_t*, float*, float*, long, int,
-              float, float, uint64_t, float, uint64_t, hipStream_t);
+              float, float, uint64_t, float, uint64_t, const float*, hipStream_t);
 int ca_ln_bwd(const bf16_t*, const bf16_t*, const float*, const float*, const float*, bf16_t*, bf16_t*, float*, float*,
               int, float*, long, int, float, uint64_t, float, uint64_t, hipStream_t, float*);
 long ca_colsum_workspace_floats(long, int);
@@ -331,9 +331,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("ln_workspace_floats", [](long M, int C) { return ca_ln_workspace_floats(M, C); });
   m.def("ln_fwd", [](u64 x, u64 res, u64 g, u64 b, u64 y, u64 h, u64 mu, u64 rs, long M, int C, float eps, float p_in,
-                     u64 seed_in, float p_out, u64 seed_out, u64 s) {
+                     u64 seed_in, float p_out, u64 seed_out, u64 s, u64 xb) {
     check(ca_ln_fwd(P(const bf16_t*, x), P(const bf16_t*, res), P(const float*, g), P(const float*, b), P(bf16_t*, y),
-                    P(bf16_t*, h), P(float*, mu), P(float*, rs), M, C, eps, p_in, seed_in, p_out, seed_out, S(s)),
+                    P(bf16_t*, h), P(float*, mu), P(float*, rs), M, C, eps, p_in, seed_in, p_out, seed_out,
+                    P(const float*, xb), S(s)),
           "ln_fwd");
   });
   m.def("ln_bwd", [](u64 dy, u64 h, u64 mu, u64 rs, u64 g, u64 dh, u64 dx, u64 dg, u64 db, int acc, u64 ws, long M,

@@ -38,7 +38,8 @@ __global__ void __launch_bounds__(LN_BLK) ln_fwd_kernel(const bf16_t* __restrict
                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
                                                         bf16_t* __restrict__ y, bf16_t* __restrict__ h_out,
                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                        long M, int C, float eps, DropCfg din, DropCfg dout) {
+                                                        long M, int C, float eps, DropCfg din, DropCfg dout,
+                                                        const float* __restrict__ xbias) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * (LN_BLK / 64) + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -51,6 +52,11 @@ __global__ void __launch_bounds__(LN_BLK) ln_fwd_kernel(const bf16_t* __restrict
     const int c4 = lane + 64 * i;
     if (c4 < C4) {
       load4(x + base + 4 * c4, v[i]);
+      if (xbias) {  // the producing GEMM's bias, applied here instead of in its epilogue
+        const f4 xb = *reinterpret_cast<const f4*>(xbias + 4 * c4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[i][j] += xb[j];
+      }
       if (din.on) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[i][j] *= drop_mul(din, base + 4 * c4 + j);
@@ -512,8 +518,8 @@ __global__ void dropout_mask_kernel(uint8_t* __restrict__ m, long n, long base, 
 
 template <int NV>
 int ln_fwd_launch(const bf16_t* x, const bf16_t* res, const float* g, const float* b, bf16_t* y, bf16_t* h, float* mu,
-                  float* rs, long M, int C, float eps, DropCfg din, DropCfg dout, hipStream_t s) {
-  ln_fwd_kernel<NV><<<ca_cdiv(M, 4), LN_BLK, 0, s>>>(x, res, g, b, y, h, mu, rs, M, C, eps, din, dout);
+                  float* rs, long M, int C, float eps, DropCfg din, DropCfg dout, const float* xb, hipStream_t s) {
+  ln_fwd_kernel<NV><<<ca_cdiv(M, 4), LN_BLK, 0, s>>>(x, res, g, b, y, h, mu, rs, M, C, eps, din, dout, xb);
   return 0;
 }
 
@@ -638,20 +644,21 @@ extern "C" {
 
 long ca_ln_workspace_floats(long M, int C) { return (long)ln_nblk(M) * 3 * C; }
 
-// y = drop_out(LN(res + drop_in(x))); h_out (optional) keeps the pre-norm sum for the backward.
+// y = drop_out(LN(res + drop_in(x + xbias))); h_out (optional) keeps the pre-norm sum for the
+// backward; xbias (optional, fp32 [C]) is the bias of the GEMM that produced x.
 int ca_ln_fwd(const bf16_t* x, const bf16_t* res, const float* gamma, const float* beta, bf16_t* y, bf16_t* h_out,
               float* mean, float* rstd, long M, int C, float eps, float p_in, uint64_t seed_in, float p_out,
-              uint64_t seed_out, hipStream_t s) {
+              uint64_t seed_out, const float* xbias, hipStream_t s) {
   if (C % 4 != 0 || C > 2048) return -1;
   const DropCfg din = make_drop(p_in, seed_in), dout = make_drop(p_out, seed_out);
   const int nv = (C / 4 + 63) / 64;
   int rc;
   switch (nv) {
-    case 1: rc = ln_fwd_launch<1>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, s); break;
-    case 2: rc = ln_fwd_launch<2>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, s); break;
-    case 3: rc = ln_fwd_launch<3>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, s); break;
-    case 4: rc = ln_fwd_launch<4>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, s); break;
-    default: rc = ln_fwd_launch<8>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, s); break;
+    case 1: rc = ln_fwd_launch<1>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, xbias, s); break;
+    case 2: rc = ln_fwd_launch<2>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, xbias, s); break;
+    case 3: rc = ln_fwd_launch<3>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, xbias, s); break;
+    case 4: rc = ln_fwd_launch<4>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, xbias, s); break;
+    default: rc = ln_fwd_launch<8>(x, res, gamma, beta, y, h_out, mean, rstd, M, C, eps, din, dout, xbias, s); break;
   }
   if (rc) return rc;
   CA_LAUNCH_CHECK();

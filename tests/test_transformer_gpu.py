@@ -48,10 +48,13 @@ def test_attention_fwd_bwd(B, S, H, p):
     assert rel(dqkv, ref) < 2e-2, rel(dqkv, ref)
 
 
-@pytest.mark.parametrize("M,C,res,p_in,p_out", [(64, 768, True, 0.0, 0.0), (100, 768, True, 0.1, 0.0),
-                                                 (37, 128, False, 0.0, 0.1), (16, 1024, True, 0.0, 0.0),
-                                                 (8, 96, False, 0.0, 0.0)])
-def test_layernorm_fwd_bwd(M, C, res, p_in, p_out):
+@pytest.mark.parametrize("M,C,res,p_in,p_out,xb", [(64, 768, True, 0.0, 0.0, False), (100, 768, True, 0.1, 0.0, False),
+                                                    (37, 128, False, 0.0, 0.1, False), (16, 1024, True, 0.0, 0.0, False),
+                                                    (8, 96, False, 0.0, 0.0, False), (100, 768, True, 0.1, 0.0, True),
+                                                    (64, 768, True, 0.0, 0.0, True), (37, 128, False, 0.0, 0.1, True)])
+def test_layernorm_fwd_bwd(M, C, res, p_in, p_out, xb):
+    """LN forward/backward (+ residual, input / output dropout, and the producing GEMM's
+    bias added in the forward pass: BERT's attention-output / FFN2 bias)."""
     from cloud_amd.ops import raw
 
     torch.manual_seed(2)
@@ -59,8 +62,10 @@ def test_layernorm_fwd_bwd(M, C, res, p_in, p_out):
     r = torch.randn(M, C, device=DEV).to(torch.bfloat16) if res else None
     g = torch.randn(C, device=DEV) * 0.5 + 1
     b = torch.randn(C, device=DEV) * 0.1
+    xbias = torch.randn(C, device=DEV) * 0.3 if xb else None
     s_in, s_out = 77, 78
-    y, h, mu, rs = raw.ln_fwd(x, g, b, 1e-12, residual=r, p_in=p_in, seed_in=s_in, p_out=p_out, seed_out=s_out)
+    y, h, mu, rs = raw.ln_fwd(x, g, b, 1e-12, residual=r, p_in=p_in, seed_in=s_in, p_out=p_out, seed_out=s_out,
+                              x_bias=xbias)
     dy = torch.randn_like(y)
     dg = torch.zeros(C, device=DEV)
     db = torch.ones(C, device=DEV)  # accumulate semantics
@@ -71,7 +76,7 @@ def test_layernorm_fwd_bwd(M, C, res, p_in, p_out):
 
     xr = x.float().requires_grad_()
     gr, br = g.clone().requires_grad_(), b.clone().requires_grad_()
-    t = xr
+    t = xr if xbias is None else xr + xbias
     if p_in > 0:
         t = t * raw.dropout_mask(M * C, p_in, s_in).view(M, C).float() / (1 - p_in)
     if r is not None:
