@@ -121,6 +121,9 @@ _VARS = [
         "node probe (tests point it at a fake tree)", "launcher"),
     Var("CLOUD_AMD_TUNER_STANDBY", bool, True, "trial scheduler: start the packing wave's workers with the probe "
         "wave, gated (imports done, no GPU touched) until the measured footprint says how many may run", "tuner"),
+    Var("CLOUD_AMD_TUNER_STANDBY_HIP", bool, False, "gated standby tuner workers also create their HIP context and "
+        "load the kernel library before the gate opens (measured neutral on the 8-trial bench, "
+        "profiles/r3_s28/: off by default, so a dismissed standby never touches the GPU)", "tuner"),
     Var("CLOUD_AMD_TUNER_FAST_EXIT", bool, True, "tuner workers end with os._exit after their last trial is in the "
         "study (no interpreter / HIP teardown on the study's critical path)", "tuner"),
     Var("CLOUD_AMD_TUNER_EARLY_FOOTPRINT", bool, True, "tuner probe worker: report the trial HBM footprint after "

@@ -70,13 +70,24 @@ def _worker(target, tuner_id, device, env, gate_file=None, timeline_file=None):
 
 def _worker_body(target, tuner_id, device, env, gate_file, tl):
     if gate_file:
-        # warm standby: pay interpreter start, `import torch` and the target module import
-        # while the probe wave runs, touching no GPU (HIP is initialised only after the go)
-        import torch  # noqa: F401
+        # warm standby: pay interpreter start, `import torch`, the target module import and
+        # (CLOUD_AMD_TUNER_STANDBY_HIP) the device's HIP context + the kernel library while
+        # the probe wave runs; a dismissed standby gives its context back when it exits
+        os.environ.update(env)
+        import torch
+
+        from .. import config
 
         mod_name = target.split(":")[0]
         importlib.import_module(mod_name)
         _mark(tl, "imported")
+        if device.startswith("cuda") and config.get("CLOUD_AMD_TUNER_STANDBY_HIP"):
+            torch.cuda.set_device(int(device.split(":")[1]))
+            torch.empty(1, device=device)
+            from ..ops import _ext
+
+            _ext.load(required=False)
+            _mark(tl, "device_ready")
         go = _await_gate(gate_file)
         _mark(tl, "released" if go else "dismissed")
         if not go:
@@ -89,10 +100,10 @@ def _worker_body(target, tuner_id, device, env, gate_file, tl):
 
         torch.cuda.set_device(int(device.split(":")[1]))
         os.environ["LOCAL_RANK"] = device.split(":")[1]
-        _mark(tl, "device_ready")
     else:
         os.environ["CLOUD_AMD_DEVICE"] = "cpu"
     mod, fn = target.split(":")
+    _mark(tl, "running")
     getattr(importlib.import_module(mod), fn)(tuner_id, device)
 
 
@@ -237,8 +248,8 @@ class TrialScheduler:
 
     def read_timeline(self, t0):
         """Per-worker phase marks (seconds after the scheduler started): ``entered`` (the
-        spawned interpreter runs), ``imported`` / ``released`` / ``dismissed`` (standbys),
-        ``device_ready`` (HIP initialised), ``exited``."""
+        spawned interpreter runs), ``imported`` / ``device_ready`` / ``released`` / ``dismissed`` (standbys),
+        ``running`` (the target called), ``exited``."""
         rows = {}
         for name in sorted(os.listdir(self._state)):
             if name.startswith("timeline_") and name.endswith(".json"):
