@@ -169,7 +169,9 @@ def main():
     # first step = end-to-end "first-step latency" (process start -> step done)
     loss = train_step()
     sync()
-    first_step_latency = time.time() - T_START
+    t_first_done = time.time()
+    first_step_latency = t_first_done - T_START
+    phases = benchlaunch.startup_phases(T_START, t_first_done)
     run_t0 = os.environ.get("CLOUD_AMD_RUN_T0")
     run_to_first = (time.time() - float(run_t0)) if run_t0 else None
 
@@ -251,6 +253,7 @@ def main():
             "rank_ms_per_step": {"min": round(min(per_rank_ms), 3), "max": round(max(per_rank_ms), 3)},
             "first_step_latency_s": round(first_lat, 3),
             "run_to_first_step_s": round(run_to_first, 3) if run_to_first is not None else None,
+            "startup_phases_rank0": phases,
             "launched_via": launched,
             "final_loss": round(final_loss, 4),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2) if on_gpu else None,

@@ -155,7 +155,9 @@ def main():
 
     loss = train_step()
     torch.cuda.synchronize()
-    first = time.time() - T_START
+    t_first_done = time.time()
+    first = t_first_done - T_START
+    phases = benchlaunch.startup_phases(T_START, t_first_done)
     run_t0 = os.environ.get("CLOUD_AMD_RUN_T0")
     run_to_first = (time.time() - float(run_t0)) if run_t0 else None
     for _ in range(max(args.warmup - 1, 0)):
@@ -202,6 +204,7 @@ def main():
                        "optimizer": "adamw"},
             "impl": impl, "first_step_latency_s": round(first, 3),
             "run_to_first_step_s": round(run_to_first, 3) if run_to_first is not None else None,
+            "startup_phases_rank0": phases,
             "launched_via": benchlaunch.launched_via(), "comm": comm,
             "backend": dist.get_backend() if world > 1 else None,
             "shared_gpu": bool(config.get("CLOUD_AMD_SHARED_GPU")),

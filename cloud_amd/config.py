@@ -31,6 +31,8 @@ _VARS = [
     Var("CLOUD_AMD_JOB_ID", str, "", "job id (set in every rank)", "launcher"),
     Var("CLOUD_AMD_JOB_DIR", str, "", "job directory (set in every rank)", "launcher"),
     Var("CLOUD_AMD_LAUNCH_TIME", float, None, "launcher spawn time, epoch seconds (set in every rank)", "launcher"),
+    Var("CLOUD_AMD_RANK_T0", float, None, "wall time at which a launched rank's wrapper started (set by the "
+        "generated entry-point wrapper; the benches split run()->first step into phases with it)", "launcher"),
     Var("CLOUD_AMD_RUN_T0", float, None, "run() entry time, for run()->first-step latency (set in ranks)",
         "launcher"),
     Var("CLOUD_AMD_PIP_INSTALL", bool, False, "pip install --user the job's requirements (needs an index)",

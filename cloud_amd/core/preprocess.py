@@ -25,6 +25,8 @@ from . import machine_config
 
 HEADER = [
     "import os\n",
+    "import time as _ca_time\n",
+    'os.environ.setdefault("CLOUD_AMD_RANK_T0", repr(_ca_time.time()))\n',  # rank start, for the bench phases
     'os.environ["TF_KERAS_RUNNING_REMOTELY"]="1"\n',
     'os.environ["CLOUD_AMD_RUNNING_REMOTELY"]="1"\n',
     "import cloud_amd.parallel.strategy as _ca_strategy\n",

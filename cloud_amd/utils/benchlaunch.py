@@ -74,6 +74,19 @@ def check_world(gpus, world, tag="bench"):
         sys.exit(3)
 
 
+def startup_phases(t_start, t_first_done):
+    """run() -> first step split into: ``launch_s`` (run() call -> the rank's wrapper runs:
+    staging, launcher, interpreter start), ``rank_setup_s`` (wrapper -> the bench script
+    body: strategy + torch imports), ``first_step_s`` (script body -> first step done:
+    model build, HIP init, first-launch kernel loads).  None outside run()."""
+    run_t0, rank_t0 = os.environ.get("CLOUD_AMD_RUN_T0"), os.environ.get("CLOUD_AMD_RANK_T0")
+    if not run_t0 or not rank_t0:
+        return None
+    run_t0, rank_t0 = float(run_t0), float(rank_t0)
+    return {"launch_s": round(rank_t0 - run_t0, 3), "rank_setup_s": round(t_start - rank_t0, 3),
+            "first_step_s": round(t_first_done - t_start, 3)}
+
+
 def launched_via():
     if os.environ.get("CLOUD_AMD_RUN_T0"):
         return "cloud_amd.run()"

@@ -34,6 +34,9 @@ def test_bench_two_ranks_via_run_cpu(tmp_path):
     assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2"
     assert j["launched_via"] == "cloud_amd.run()"
     assert j["run_to_first_step_s"] is not None and j["run_to_first_step_s"] > 0
+    ph = j["startup_phases_rank0"]  # run() -> first step split at the wrapper and the script body
+    assert set(ph) == {"launch_s", "rank_setup_s", "first_step_s"} and all(v >= 0 for v in ph.values())
+    assert abs(sum(ph.values()) - j["run_to_first_step_s"]) < 0.5
     assert j["comm"]["buckets"] >= 1 and j["comm"]["allreduce_ms"] > 0
     assert j["backend"] == "gloo" and j["config"]["global_batch"] == 8
     job = os.listdir(tmp_path / "jobs")

@@ -35,7 +35,7 @@ def test_wrapper_golden(tmp_path, chief, workers, expect):
 
 def test_wrapper_no_strategy(tmp_path):
     p = preprocess.get_preprocessed_entry_point("train.py", CPU, CPU, 0, None, output_dir=str(tmp_path))
-    assert not any("strategy" in ln and "=" in ln for ln in _lines(p)[4:])
+    assert not any("strategy" in ln and "=" in ln for ln in _lines(p)[len(preprocess.HEADER):])
 
 
 def test_wrapper_notebook(tmp_path):
@@ -46,7 +46,7 @@ def test_wrapper_notebook(tmp_path):
     f = tmp_path / "nb.ipynb"
     f.write_text(json.dumps(nb))
     p = preprocess.get_preprocessed_entry_point(str(f), CPU, CPU, 0, "auto", output_dir=str(tmp_path))
-    body = _lines(p)[6:]
+    body = _lines(p)[len(preprocess.HEADER) + 2:]
     assert body[:2] == ["import os\n", "print('hi')\n"]
     assert not any(ln.startswith(("!", "%", "#")) for ln in body)
 

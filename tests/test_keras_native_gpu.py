@@ -195,3 +195,42 @@ def test_act_grad_kernel_matches_torch(act, N, Np):
                       src if act == "gelu" else None, act)
     torch.testing.assert_close(got.float(), ref.float(), atol=2e-2, rtol=2e-2)
     assert got[:, N:].abs().max().item() == 0.0 if Np > N else True
+
+
+def test_keras_evaluate_fused_loss_matches_predict():
+    """evaluate() on the GPU scores with the fused softmax-xent kernel (bf16 logits, device
+    accumulator); its loss / accuracy equal the plain formulas on predict()'s
+    probabilities, and fit's validation numbers equal a standalone evaluate."""
+    import numpy as np
+
+    from cloud_amd import keras
+    from cloud_amd.keras import losses as L
+
+    rng = np.random.default_rng(4)
+    x = rng.random((384, 28, 28, 1), dtype=np.float32)
+    y = (x[:, :14].mean(axis=(1, 2, 3)) > x[:, 14:].mean(axis=(1, 2, 3))).astype("int64")
+    model = keras.Sequential([
+        keras.layers.Conv2D(16, 3, activation="relu", input_shape=(28, 28, 1)),
+        keras.layers.MaxPooling2D(),
+        keras.layers.Flatten(),
+        keras.layers.Dense(10, activation="softmax"),
+    ])
+    model.compile(loss="sparse_categorical_crossentropy", optimizer=keras.optimizers.Adam(), metrics=["accuracy"])
+    orig = L.SparseCategoricalCrossentropy.per_example
+
+    def banned(*a, **k):
+        raise AssertionError("unfused loss path reached")
+
+    L.SparseCategoricalCrossentropy.per_example = banned
+    try:
+        hist = model.fit(x[:256], y[:256], batch_size=64, epochs=2, validation_data=(x[256:], y[256:]), verbose=0)
+        loss, acc = model.evaluate(x[256:], y[256:], batch_size=64, verbose=0)
+    finally:
+        L.SparseCategoricalCrossentropy.per_example = orig
+    p = model.predict(x[256:], batch_size=128).astype("float64")
+    n = len(p)
+    ref_loss = float(np.mean(-np.log(np.clip(p[np.arange(n), y[256:]], 1e-7, None))))
+    ref_acc = float(np.mean(p.argmax(-1) == y[256:]))
+    assert abs(loss - ref_loss) < 3e-2 * max(1.0, ref_loss), (loss, ref_loss)
+    assert abs(acc - ref_acc) <= 2.0 / n + 1e-9, (acc, ref_acc)
+    assert abs(hist.history["val_loss"][-1] - loss) < 1e-4 and abs(hist.history["val_accuracy"][-1] - acc) < 1e-6
