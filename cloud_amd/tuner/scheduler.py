@@ -244,6 +244,10 @@ class TrialScheduler:
                "trials_per_gpu": self.per_gpu, "footprint_gb": self.footprint_gb}
         if self.timeline:
             out["timeline"] = self.read_timeline(t0)
+        if self.state_dir is None:  # our own scratch directory (footprints, gates, timelines)
+            import shutil
+
+            shutil.rmtree(state, ignore_errors=True)
         return out
 
     def read_timeline(self, t0):
