@@ -217,3 +217,29 @@ def test_evaluate_on_fused_loss_matches_reference_and_keeps_train_logs():
     assert abs(loss - ref_loss) < 2e-2 * max(1.0, ref_loss), (loss, ref_loss)
     assert abs(acc - ref_acc) <= 1.0 / 96 + 1e-9, (acc, ref_acc)
     assert abs(h["val_loss"][-1] - loss) < 1e-5 and abs(h["val_accuracy"][-1] - acc) < 1e-6
+
+
+def test_backward_with_seed_matches_autograd_and_skips_sympy():
+    """ops.backward_with_seed == torch.autograd.backward(loss, grad_tensors=seed), without the
+    Python shape check that imports sympy on a process's first seeded backward."""
+    import subprocess
+    import sys
+
+    import torch
+
+    from cloud_amd import ops
+
+    w = torch.randn(5, 3, requires_grad=True)
+    x = torch.randn(4, 5)
+    ops.backward_with_seed((x @ w).square().mean(), torch.tensor(2.0))
+    g1 = w.grad.clone()
+    w.grad = None
+    torch.autograd.backward((x @ w).square().mean(), grad_tensors=torch.tensor(2.0))
+    torch.testing.assert_close(g1, w.grad)
+    with pytest.raises(ValueError):
+        ops.backward_with_seed((x @ w).sum(), torch.ones(2))
+    code = ("import sys, torch; from cloud_amd import ops; w = torch.ones(3, requires_grad=True); "
+            "ops.backward_with_seed((w * 2).sum(), torch.tensor(1.0)); print('sympy' in sys.modules)")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.stdout.strip().splitlines()[-1] == "False", out.stdout + out.stderr
