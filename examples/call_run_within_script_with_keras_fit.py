@@ -37,7 +37,11 @@ outputs = tf.keras.layers.Dense(NUM_CLASSES)(h)
 model = tf.keras.Model(inputs, outputs)
 base_model.trainable = False
 
-ckpt_dir = os.environ.get("CLOUD_AMD_EXAMPLE_OUT", tempfile.mkdtemp())
+# one directory for every rank of the job (the reference writes to a GCS bucket): the job
+# directory run() created, else a fresh local one
+ckpt_dir = os.environ.get("CLOUD_AMD_EXAMPLE_OUT") or (
+    os.path.join(os.environ["CLOUD_AMD_JOB_DIR"], "model_out") if os.environ.get("CLOUD_AMD_JOB_DIR")
+    else tempfile.mkdtemp())
 callbacks = [
     tf.keras.callbacks.ModelCheckpoint(os.path.join(ckpt_dir, "save_at_{epoch}")),
     tf.keras.callbacks.TensorBoard(log_dir=os.path.join(ckpt_dir, "logs")),
