@@ -51,3 +51,24 @@ def test_keras_tuner_workload_gpu(tmp_path):
 
 def test_mlp_no_reqs_workload_gpu(tmp_path):
     _result(_run([os.path.join(WL, "mnist_example_using_fit_no_reqs.py")], tmp_path), "mlp")
+
+
+@pytest.mark.timeout(300)
+def test_ctl_workload_two_ranks_share_the_gpu(tmp_path):
+    """call_run_on_script_with_keras_ctl through run(): chief + worker (MultiWorkerMirrored),
+    both ranks on this box's one GPU over gloo (CLOUD_AMD_SHARED_GPU) -- the DP data plane on
+    device tensors; strategy.reduce gives both replicas the same loss."""
+    import glob
+
+    env = dict(os.environ)
+    env.pop("CLOUD_AMD_DEVICE", None)
+    env.update({"CLOUD_AMD_EXAMPLE_SMALL": "1", "CLOUD_AMD_JOBS_DIR": str(tmp_path / "jobs"), "PYTHONPATH": ROOT,
+                "CLOUD_AMD_SHARED_GPU": "1", "CLOUD_AMD_DIST_BACKEND": "gloo", "CLOUD_AMD_NUM_GPUS": "2"})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "call_run_on_script_with_keras_ctl.py")],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    res = []
+    for log in sorted(glob.glob(str(tmp_path / "jobs" / "*" / "logs" / "*.log"))):
+        res += [ln.strip() for ln in open(log) if ln.startswith("RESULT")]
+    assert len(res) == 2 and all("replicas=2" in r for r in res), res
+    assert len({r.split("loss=")[1] for r in res}) == 1, res
