@@ -65,8 +65,8 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--bucket-mb", type=float, default=None,
                     help="gradient all-reduce bucket size (default CLOUD_AMD_BUCKET_MB or 16)")
-    ap.add_argument("--grad-reduce-dtype", choices=("bf16", "fp32"), default=None,
-                    help="wire dtype of the gradient reduction of bf16 layers")
+    ap.add_argument("--grad-reduce-dtype", choices=("auto", "bf16", "fp32", "native"), default=None,
+                    help="wire dtype of the gradient all-reduce (default auto: bf16 for every bucket of a bf16 model)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--via-run", type=int, default=int(os.environ.get("CLOUD_AMD_BENCH_VIA_RUN", "1")),
                     help="1 (default): launch the ranks through cloud_amd.run(); 0: train in this process")
@@ -192,17 +192,33 @@ def main():
     dist_env.barrier()
     sync()
     reducer.timing_start()
+    host0 = benchlaunch.host_state()
+    # per-step device time from events on the compute stream and per-step host launch time
+    # (no added synchronisation: events are read after the closing sync)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if on_gpu else None
+    host_ms = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    if evs:
+        evs[0].record()
+    for i in range(args.steps):
+        th = time.perf_counter()
         loss = step_fn()
+        host_ms.append((time.perf_counter() - th) * 1e3)
+        if evs:
+            evs[i + 1].record()
     sync()
     dist_env.barrier()
     t1 = time.perf_counter()
+    step_stats = benchlaunch.step_stats(
+        [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)] if evs else None, host_ms,
+        host0, benchlaunch.host_state())
     comm = reducer.timing_summary()
     per_rank_ms = [v / args.steps * 1000.0 for v in dist_env.all_gather_floats(t1 - t0, device)]
     elapsed = dist_env.all_reduce_max(t1 - t0, device)
     ms = elapsed / args.steps * 1000.0
     busbw = dist_env.allreduce_busbw(device) if world > 1 else None  # after the timed steps
+    # both transports on the same buffers: decides the default data plane (CLOUD_AMD_COMM)
+    probe = dist_env.comm_probe(device) if world > 1 else None
     ips = global_batch * args.steps / elapsed
     first_lat = dist_env.all_reduce_max(first_step_latency, device)
     if run_to_first is not None:
@@ -248,8 +264,10 @@ def main():
             "strategy": strategy.name,
             "comm": dict(reducer.describe(), allreduce_ms=comm["allreduce_ms"],
                          exposed_comm_ms=comm["exposed_comm_ms"], timing=comm.get("timing"),
-                         busbw_gbs=busbw),
+                         busbw_gbs=busbw, comm_probe=probe),
             "replicas_consistent": replicas_consistent,
+            "step_stats_rank0": step_stats,
+            "warnings": step_stats.pop("warnings"),
             "rank_ms_per_step": {"min": round(min(per_rank_ms), 3), "max": round(max(per_rank_ms), 3)},
             "first_step_latency_s": round(first_lat, 3),
             "run_to_first_step_s": round(run_to_first, 3) if run_to_first is not None else None,

@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--stock", type=int, default=0)
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--bucket-mb", type=float, default=None)
-    ap.add_argument("--grad-reduce-dtype", choices=("bf16", "fp32"), default=None)
+    ap.add_argument("--grad-reduce-dtype", choices=("auto", "bf16", "fp32", "native"), default=None)
     ap.add_argument("--via-run", type=int, default=int(os.environ.get("CLOUD_AMD_BENCH_VIA_RUN", "1")))
     return ap.parse_args()
 
@@ -182,6 +182,7 @@ def main():
     per_rank = [v / args.steps * 1000.0 for v in dist_env.all_gather_floats(dt, device)]
     elapsed = dist_env.all_reduce_max(dt, device)
     busbw = dist_env.allreduce_busbw(device) if world > 1 else None
+    probe = dist_env.comm_probe(device) if world > 1 else None  # torch.distributed vs native RcclComm
     sps = B * world * args.steps / elapsed
     first = dist_env.all_reduce_max(first, device)
     if run_to_first is not None:
@@ -191,7 +192,7 @@ def main():
         t = reducer.timing_summary()
         comm = dict(reducer.describe(), allreduce_ms=dist_env.all_reduce_max(t["allreduce_ms"], device),
                     exposed_comm_ms=dist_env.all_reduce_max(t["exposed_comm_ms"], device), timing=t.get("timing"),
-                    busbw_gbs=busbw)
+                    busbw_gbs=busbw, comm_probe=probe)
     if rank == 0:
         print(json.dumps(_finite({
             "metric": "sequences/sec BERT-base fine-tune synthetic GLUE (seq %d)" % S,

@@ -24,8 +24,15 @@ class Var:
 _VARS = [
     # launcher / run()
     Var("CLOUD_AMD_JOBS_DIR", str, "./jobs", "where run() stages job directories", "launcher"),
-    Var("CLOUD_AMD_STAGE_COPY", bool, False, "stage the entry directory by copying instead of hard-linking "
-        "(a running job then never sees in-place edits of its sources)", "launcher"),
+    Var("CLOUD_AMD_STAGE_COPY", bool, False, "stage code files by copying too (default: code "
+        "hard-linked, every other file copied; a running job then never sees in-place edits of its sources)", "launcher"),
+    Var("CLOUD_AMD_CPU_AFFINITY", bool, True, "launcher pins each GPU rank to the cores of its GPU's NUMA node "
+        "(KFD io_links + sysfs cpulist), split between the ranks on that node; 0 = leave placement to the OS",
+        "launcher"),
+    Var("CLOUD_AMD_NUMA_ROOT", str, "/sys/devices/system/node", "sysfs NUMA-node tree read for rank CPU placement "
+        "(tests point it at a fake tree)", "launcher"),
+    Var("CLOUD_AMD_CPU_ROOT", str, "/sys/devices/system/cpu", "sysfs CPU tree (SMT siblings) read for rank CPU "
+        "placement (tests point it at a fake tree)", "launcher"),
     Var("CLOUD_AMD_NUM_GPUS", int, None, "override the visible-GPU count (0 = CPU node)", "launcher"),
     Var("CLOUD_AMD_RUNNING_REMOTELY", str, "", "set by the launcher inside job ranks (remote() is True)", "launcher"),
     Var("CLOUD_AMD_JOB_ID", str, "", "job id (set in every rank)", "launcher"),
@@ -113,8 +120,10 @@ _VARS = [
         "projection that fed it (no separate column-sum pass)", "ops"),
     Var("CLOUD_AMD_TAIL_BUCKET_MB", float, 1.0, "cap on the last gradient bucket (the first layers' gradients, "
         "ready only when backward ends: its all-reduce is exposed)", "distributed"),
-    Var("CLOUD_AMD_GRAD_REDUCE_DTYPE", str, "bf16", "wire dtype of the gradient all-reduce of bf16 layers: "
-        "'bf16' (native, half the bytes) or 'fp32' (reduce an fp32 copy)", "distributed"),
+    Var("CLOUD_AMD_GRAD_REDUCE_DTYPE", str, "auto", "wire dtype of the gradient all-reduce: 'bf16' (every "
+        "bucket, fp32 arenas through a bf16 copy: half the bytes), 'fp32' (every bucket through fp32), 'native' "
+        "(each arena in its own dtype), 'auto' (bf16 for mixed-precision models, native for all-fp32 ones)",
+        "distributed"),
     Var("CLOUD_AMD_RCCL_ENV", bool, True, "launcher sets the xGMI RCCL defaults (NCCL_MIN_NCHANNELS, "
         "HSA_NO_SCRATCH_RECLAIM) for multi-GPU jobs", "distributed"),
     Var("CLOUD_AMD_RCCL_CHANNELS", int, 0, "NCCL_MIN_NCHANNELS the launcher sets (0 = one per xGMI link)",
@@ -123,6 +132,10 @@ _VARS = [
         "node probe (tests point it at a fake tree)", "launcher"),
     Var("CLOUD_AMD_TUNER_STANDBY", bool, True, "trial scheduler: start the packing wave's workers with the probe "
         "wave, gated (imports done, no GPU touched) until the measured footprint says how many may run", "tuner"),
+    Var("CLOUD_AMD_TUNER_STANDBY_PER_GPU", int, 8, "trial scheduler: at most this many gated standbys per GPU "
+        "(and never more than max_workers - GPUs)", "tuner"),
+    Var("CLOUD_AMD_TUNER_GATE_TIMEOUT_S", float, 600.0, "a gated standby tuner worker exits after waiting this long "
+        "for the scheduler's verdict (it also exits when the scheduler is gone)", "tuner"),
     Var("CLOUD_AMD_TUNER_STANDBY_HIP", bool, False, "gated standby tuner workers also create their HIP context and "
         "load the kernel library before the gate opens (measured neutral on the 8-trial bench, "
         "profiles/r3_s28/: off by default, so a dismissed standby never touches the GPU)", "tuner"),
@@ -130,6 +143,10 @@ _VARS = [
         "study (no interpreter / HIP teardown on the study's critical path)", "tuner"),
     Var("CLOUD_AMD_TUNER_EARLY_FOOTPRINT", bool, True, "tuner probe worker: report the trial HBM footprint after "
         "the first training step of its first trial (0 = after the whole trial)", "tuner"),
+    Var("CLOUD_AMD_TRIAL_DEVICE", str, None, "device of a tuner worker (set by TrialScheduler); recorded on every "
+        "trial it runs in the study", "tuner"),
+    Var("CLOUD_AMD_SCHED_FAKE_DEVICES", bool, False, "TrialScheduler placement rehearsal on a CPU host: workers keep "
+        "their assigned cuda:<i> name for the study record but compute on CPU (tests)", "tuner"),
     Var("CLOUD_AMD_FOOTPRINT_FILE", str, None, "where a tuner worker reports its first trial's peak HBM "
         "(set by TrialScheduler for the probe wave)", "tuner"),
     Var("CLOUD_AMD_BENCH_VIA_RUN", bool, True, "bench scripts launch their ranks through cloud_amd.run()",

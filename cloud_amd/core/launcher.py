@@ -39,6 +39,7 @@ import threading
 import time
 import uuid
 
+from .. import config
 from . import topology
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -271,8 +272,18 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
         "backend": "nccl(rccl)" if any_gpu else "gloo", "master_port": port, "cpu_rehearsal": rehearsal,
         "ranks": ranks, "node": node, "comm_env": {k: os.environ.get(k, v) for k, v in comm_env.items()},
     }
+    # each GPU rank pinned to the cores of its GPU's NUMA node (KFD io_links + sysfs
+    # cpulist; CLOUD_AMD_CPU_AFFINITY=0 leaves placement to the OS scheduler)
+    cpu_sets = [None] * len(ranks)
+    if any_gpu and config.get("CLOUD_AMD_CPU_AFFINITY"):
+        try:
+            cpu_sets = topology.rank_cpu_sets([r["gpu"] for r in ranks])
+        except Exception:  # noqa: BLE001 - placement is an optimisation, never a launch failure
+            cpu_sets = [None] * len(ranks)
+    for info, cpus in zip(ranks, cpu_sets):
+        info["cpus"] = topology.format_cpulist(cpus) if cpus else None
     procs = []
-    for info in ranks:
+    for info, cpus in zip(ranks, cpu_sets):
         env = dict(os.environ)
         for k, v in comm_env.items():
             env.setdefault(k, v)
@@ -302,7 +313,7 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
                    "--output-format", "csv", "--"] + cmd
         logf = open(os.path.join(job_dir, "logs", log_name(info)), "w")
         p = subprocess.Popen(cmd, cwd=app_dir, env=env, stdout=logf, stderr=subprocess.STDOUT,
-                             start_new_session=True)
+                             start_new_session=True, preexec_fn=_pin(cpus))
         logf.close()
         procs.append(p)
     job = Job(job_id, job_dir, procs, ranks, meta)
@@ -314,6 +325,22 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
     except Exception:  # metrics are best-effort in the launcher
         pass
     return job
+
+
+def _pin(cpus):
+    """preexec_fn of a rank: set its CPU affinity in the child, before exec (the launcher
+    never initialises HIP, so nothing GPU-side is forked)."""
+    if not cpus:
+        return None
+    cpus = list(cpus)
+
+    def fn():
+        try:
+            os.sched_setaffinity(0, cpus)
+        except OSError:
+            pass
+
+    return fn
 
 
 def deploy_job(job_id, job_dir, target, chief_config, worker_count, worker_config, entry_point_args,

@@ -17,12 +17,18 @@ Requirements are installed best-effort with ``pip install --user`` only when
 
 Staging is part of ``run()`` -> first-step latency, so it stays cheap:
 
-* the entry directory is *hard-linked* file by file into ``app/`` (a copy only across
-  filesystems, or with ``CLOUD_AMD_STAGE_COPY=1``).  A hard link shares the bytes: an
-  in-place edit of a source file while its job runs is visible to that job (editors that
-  save by rename are not), which ``CLOUD_AMD_STAGE_COPY=1`` avoids;
-* build trees and results that no rank reads are skipped (``build/``, ``profiles/``,
-  ``gpurun_out/``, ``jobs/``, ``*.o``, VCS and cache directories);
+* **code** files of the entry directory (``.py``, ``.ipynb``, built extensions ``.so`` and
+  native sources) are *hard-linked* into ``app/``; **every other file is copied**.  Ranks
+  run with ``cwd=app``, so a job that rewrites a file it finds there (``model.h5``, a
+  checkpoint, a CSV log, opened ``"w"`` or ``"a"``) writes its own copy and never the
+  user's tree, and two jobs staged from one directory never share a writable file -- the
+  isolation of the reference's tarball (``containerize.py:124-132``) at the cost of
+  copying data files only.  ``CLOUD_AMD_STAGE_COPY=1`` copies code too (a source edited
+  in place while its job runs is then invisible to the job);
+* VCS / cache directories and ``jobs/`` are skipped; project-specific excludes come from
+  a ``.cloudamdignore`` file at the top of the entry directory (one ``fnmatch`` pattern
+  per line, ``#`` comments), so a user package named ``build/`` or ``profiles/`` ships
+  unless the project says otherwise;
 * the framework stamp reads package metadata and never imports torch (a cold
   ``import torch`` costs ~2 s in the launching process, which never needs it).
 """
@@ -37,15 +43,29 @@ import time
 
 from ..version import ARCH, __version__
 
-IGNORE = shutil.ignore_patterns("__pycache__", "*.pyc", ".git", "jobs", ".ipynb_checkpoints", "gpurun_out",
-                                "build", "profiles", "*.o", ".pytest_cache", ".hypothesis")
+IGNORE = shutil.ignore_patterns("__pycache__", "*.pyc", ".git", "jobs", ".ipynb_checkpoints", ".pytest_cache",
+                                ".hypothesis")
+IGNORE_FILE = ".cloudamdignore"
+# hard-linked (read by the job, never written by it); everything else is copied
+LINK_SUFFIXES = (".py", ".pyi", ".ipynb", ".so", ".hip", ".h", ".hpp", ".cpp", ".cc", ".c")
 
 
-def _ignore(root):
+def _user_ignores(src_dir):
+    path = os.path.join(src_dir, IGNORE_FILE)
+    if not os.path.isfile(path):
+        return ()
+    with open(path) as f:
+        return tuple(ln.strip().rstrip("/") for ln in f if ln.strip() and not ln.lstrip().startswith("#"))
+
+
+def _ignore(root, src_dir=None):
     root = os.path.abspath(root)
+    extra = shutil.ignore_patterns(*_user_ignores(src_dir)) if src_dir else None
 
     def ign(d, names):
         out = set(IGNORE(d, names))
+        if extra is not None:
+            out.update(extra(d, names))
         out.update(n for n in names if os.path.abspath(os.path.join(d, n)) == root)
         return out
 
@@ -103,6 +123,13 @@ def _link_or_copy(src, dst):
     return dst
 
 
+def _stage_file(src, dst):
+    """Code is hard-linked, data copied (``CLOUD_AMD_STAGE_COPY=1``: everything copied)."""
+    if os.environ.get("CLOUD_AMD_STAGE_COPY") != "1" and src.endswith(LINK_SUFFIXES):
+        return _link_or_copy(src, dst)
+    return shutil.copy2(src, dst)
+
+
 def stage_job(job_id, entry_point, preprocessed_entry_point, requirements_txt=None, entry_point_args=None,
               env=None, root=None):
     """Create the job directory; return (job_dir, run_target) where run_target is the script to exec."""
@@ -116,16 +143,15 @@ def stage_job(job_id, entry_point, preprocessed_entry_point, requirements_txt=No
         if os.path.isdir(src):
             if os.path.abspath(src).startswith(os.path.abspath(job_dir)):
                 raise ValueError("entry-point directory is inside the job directory")
-            copy = shutil.copy2 if os.environ.get("CLOUD_AMD_STAGE_COPY") == "1" else _link_or_copy
-            shutil.copytree(src, dst, ignore=_ignore(root), dirs_exist_ok=True, symlinks=False,
-                            copy_function=copy)
+            shutil.copytree(src, dst, ignore=_ignore(root, src), dirs_exist_ok=True, symlinks=False,
+                            copy_function=_stage_file)
         else:
             os.makedirs(os.path.dirname(dst), exist_ok=True)
             if os.path.exists(dst):
                 if os.path.samefile(src, dst):  # already linked in with the entry directory
                     continue
                 os.remove(dst)
-            _link_or_copy(src, dst)
+            _stage_file(src, dst)
     if preprocessed_entry_point is not None:
         target = os.path.join(app, os.path.basename(preprocessed_entry_point))
     else:

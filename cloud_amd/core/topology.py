@@ -170,6 +170,150 @@ def xgmi_links_per_gpu(n_gpus: int, root=None) -> int:
     return max(0, min(n_gpus, 8) - 1)
 
 
+NUMA_ROOT = "/sys/devices/system/node"
+CPU_ROOT = "/sys/devices/system/cpu"
+
+
+def parse_cpulist(text):
+    """Kernel cpulist syntax -> sorted ints: ``"0-3,8,10-11"`` -> [0, 1, 2, 3, 8, 10, 11]."""
+    out = set()
+    for part in (text or "").strip().split(","):
+        part = part.strip()
+        if not part:
+            continue
+        if "-" in part:
+            lo, hi = part.split("-", 1)
+            out.update(range(int(lo), int(hi) + 1))
+        else:
+            out.add(int(part))
+    return sorted(out)
+
+
+def format_cpulist(cpus):
+    """Sorted ints -> kernel cpulist syntax: [0, 1, 2, 5] -> ``"0-2,5"``."""
+    cpus, out, i = sorted(cpus), [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else "%d-%d" % (cpus[i], cpus[j]))
+        i = j + 1
+    return ",".join(out)
+
+
+def _cpu_agents(root):
+    """KFD CPU agents in enumeration order: [(kfd node id, props)].  KFD creates one CPU
+    agent per NUMA node, in NUMA order, so the k-th agent is NUMA node k."""
+    out = []
+    for nid in _subdirs(root):
+        props = _read_props(os.path.join(root, nid, "properties"))
+        if props and int(props.get("simd_count", 0)) == 0 and int(props.get("cpu_cores_count", 0)) > 0:
+            out.append((int(nid), props))
+    return out
+
+
+def _links(root, nid):
+    out = []
+    for l in _subdirs(os.path.join(root, str(nid), "io_links")):
+        lp = _read_props(os.path.join(root, str(nid), "io_links", l, "properties")) or {}
+        if "node_to" in lp:
+            out.append(lp)
+    return out
+
+
+def gpu_numa_nodes(root=None):
+    """NUMA node of every visible GPU (None when unknown), from the KFD link table: the
+    GPU's own PCIe link to a CPU agent, or else a CPU agent's link to the GPU (a job that
+    sees one GPU of eight can read every CPU agent's links but only its own GPU's)."""
+    root = root or kfd_root()
+    cpus = _cpu_agents(root)
+    numa_of_agent = {nid: k for k, (nid, _) in enumerate(cpus)}
+    out = []
+    for g in visible_gpus(root):
+        numa = None
+        for l in _links(root, g["node"]):
+            if l.get("node_to") in numa_of_agent:
+                numa = numa_of_agent[l["node_to"]]
+                break
+        if numa is None:
+            for nid, _ in cpus:
+                if any(l.get("node_to") == g["node"] for l in _links(root, nid)):
+                    numa = numa_of_agent[nid]
+                    break
+        out.append(numa)
+    return out
+
+
+def numa_cpus(numa, root=None, kfd=None):
+    """Logical CPUs of NUMA node ``numa``: sysfs ``node<k>/cpulist``, else the KFD CPU
+    agent's ``cpu_core_id_base`` + ``cpu_cores_count``."""
+    root = root or os.environ.get("CLOUD_AMD_NUMA_ROOT", NUMA_ROOT)
+    try:
+        with open(os.path.join(root, "node%d" % numa, "cpulist")) as f:
+            cpus = parse_cpulist(f.read())
+        if cpus:
+            return cpus
+    except OSError:
+        pass
+    agents = _cpu_agents(kfd or kfd_root())
+    if numa < len(agents):
+        p = agents[numa][1]
+        base = int(p.get("cpu_core_id_base", 0))
+        return list(range(base, base + int(p.get("cpu_cores_count", 0))))
+    return []
+
+
+def _cores(cpus, cpu_root=None):
+    """Group logical CPUs into physical cores (SMT siblings together), ordered by first id."""
+    cpu_root = cpu_root or os.environ.get("CLOUD_AMD_CPU_ROOT", CPU_ROOT)
+    allowed, seen, cores = set(cpus), set(), []
+    for c in sorted(cpus):
+        if c in seen:
+            continue
+        sib = None
+        try:
+            with open(os.path.join(cpu_root, "cpu%d" % c, "topology", "thread_siblings_list")) as f:
+                sib = [x for x in parse_cpulist(f.read()) if x in allowed]
+        except OSError:
+            pass
+        core = sorted(set(sib or []) | {c})
+        seen.update(core)
+        cores.append(core)
+    return cores
+
+
+def rank_cpu_sets(gpus, root=None, numa_root=None, cpu_root=None, allowed=None):
+    """CPU set for each rank of a job whose ranks drive visible GPUs ``gpus`` (list of
+    visible-GPU indices, one per rank; None for a CPU rank): the cores of the GPU's NUMA
+    node, split into disjoint contiguous groups of whole physical cores among the ranks on
+    that node (4 ranks per socket on an 8x MI355X node), intersected with the CPUs this
+    process may use.  None for a rank whose placement is unknown (no KFD / NUMA data)."""
+    if allowed is None:
+        try:
+            allowed = set(os.sched_getaffinity(0))
+        except AttributeError:  # pragma: no cover
+            allowed = None
+    numa = gpu_numa_nodes(root)
+    per_node = {}
+    for r, g in enumerate(gpus):
+        n = numa[g] if g is not None and g < len(numa) else None
+        if n is not None:
+            per_node.setdefault(n, []).append(r)
+    out = [None] * len(gpus)
+    for n, ranks in per_node.items():
+        cpus = numa_cpus(n, numa_root, kfd=root)
+        if allowed is not None:
+            cpus = [c for c in cpus if c in allowed]
+        cores = _cores(cpus, cpu_root)
+        if len(cores) < len(ranks):
+            continue  # fewer cores than ranks: leave placement to the scheduler
+        k = len(ranks)
+        for i, r in enumerate(ranks):
+            lo, hi = i * len(cores) // k, (i + 1) * len(cores) // k
+            out[r] = sorted(c for core in cores[lo:hi] for c in core)
+    return out
+
+
 def describe_node(root=None):
     gpus = visible_gpus(root)
     n = visible_gpu_count(root)

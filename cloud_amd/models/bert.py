@@ -353,6 +353,8 @@ class BertForSequenceClassification(nn.Module):
         tts = token_type_ids.to(torch.int32).contiguous() if token_type_ids is not None else torch.zeros_like(ids)
         key_len = (attention_mask.sum(1).to(torch.int32).contiguous() if attention_mask is not None else None)
         e = self.embeddings
+        if torch.is_grad_enabled():
+            side_stream.begin_pass()  # drop deferred state of a backward that raised
         h = _EmbedFn.apply(ids, tts, e, ph, e.word, e.pos, e.token_type, e.ln_w, e.ln_b)
         for layer in self.layers:
             h = _LayerFn.apply(h, key_len, layer, B, S, ph, pa, *layer.param_list())

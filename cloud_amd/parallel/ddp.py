@@ -95,14 +95,16 @@ class _TorchTransport:
 
 
 class Bucket:
-    __slots__ = ("arena", "lo", "hi", "slots", "pending", "work", "launched", "index", "wire", "ev", "span")
+    __slots__ = ("arena", "lo", "hi", "slots", "pending", "work", "launched", "index", "wire", "wire_buf", "ev",
+                 "span")
 
     def __init__(self, arena, lo, hi, slots, index):
         self.arena, self.lo, self.hi, self.slots, self.index = arena, lo, hi, slots, index
         self.pending = len(slots)
         self.work = None
         self.launched = False
-        self.wire = None   # reduce-dtype copy on the wire (fp32 reduction of bf16 grads)
+        self.wire = None   # this step's reduce-dtype copy on the wire (None: reduced in place)
+        self.wire_buf = None  # persistent storage of that copy (allocated on first use)
         self.ev = None     # (start, end) timing events of this step's collective (GPU)
         self.span = None   # [start_s, end_s] host clock of this step's collective (gloo / CPU)
 
@@ -123,12 +125,23 @@ class GradAllReducer:
         self.bucket_mb = mb
         self.bucket_bytes = int(mb * (1 << 20))
         self.overlap = overlap
-        # Wire dtype of the reduction.  None = the gradient's own dtype (bf16 sums for bf16
-        # layers: half the bytes on xGMI); torch.float32 = reduce an fp32 copy (exact-er
-        # sums at 2x the bytes; the copy and the cast back run on the comm stream).
-        rd = reduce_dtype if reduce_dtype is not None else os.environ.get("CLOUD_AMD_GRAD_REDUCE_DTYPE")
+        # Wire dtype of the reduction (CLOUD_AMD_GRAD_REDUCE_DTYPE, default "auto"):
+        #   bf16   -- every bucket reduced in bf16: bf16 arenas in place, fp32 arenas (BERT's
+        #             word-embedding table, BatchNorm / LayerNorm parameters) through a bf16
+        #             copy cast back into the fp32 gradient -- half the xGMI bytes of fp32;
+        #   fp32   -- every bucket reduced in fp32 (bf16 arenas through an fp32 copy);
+        #   native -- each arena in its own dtype;
+        #   auto   -- bf16 for a mixed-precision model (it has a bf16 arena), native for an
+        #             all-fp32 one (a user who trains in fp32 keeps fp32 gradient sums).
+        # The casts run on the comm stream, next to the collective, into a wire buffer kept
+        # per bucket (allocated once).  RCCL adds bf16 operands in fp32 and rounds each hop's
+        # partial sum to bf16 (error: tests/test_grad_reduce_precision.py).
+        rd = reduce_dtype if reduce_dtype is not None else os.environ.get("CLOUD_AMD_GRAD_REDUCE_DTYPE", "auto")
+        if rd == "auto":
+            rd = "bf16" if any(a.grad.dtype == torch.bfloat16 for a in arenas) else "native"
         if isinstance(rd, str):
-            rd = {"fp32": torch.float32, "float32": torch.float32, "bf16": None, "native": None}[rd]
+            rd = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
+                  "bfloat16": torch.bfloat16, "native": None}[rd]
         self.reduce_dtype = rd
         # Per-step communication timing (bench / monitoring): see timing_start/timing_summary.
         # With the metrics exporter on, every step is timed and completed steps are drained
@@ -223,9 +236,13 @@ class GradAllReducer:
             self._launch_ready()
 
     def _wire(self, b):
+        """The tensor this bucket's collective reduces; runs on the comm stream."""
         if self.reduce_dtype is None or self.reduce_dtype == b.tensor.dtype:
             return b.tensor
-        b.wire = b.tensor.to(self.reduce_dtype)
+        if b.wire_buf is None:
+            b.wire_buf = torch.empty(b.hi - b.lo, dtype=self.reduce_dtype, device=b.tensor.device)
+        b.wire_buf.copy_(b.tensor)
+        b.wire = b.wire_buf
         return b.wire
 
     def _launch(self, b):
@@ -445,10 +462,15 @@ class GradAllReducer:
         """Bucket layout for reports: count, target size, wire dtype, transport."""
         transport = ("native RcclComm" if self.comm is not None else
                      "torch.distributed(%s)" % (dist.get_backend(self.pg) if dist.is_initialized() else "none"))
+        def name(dt):
+            return str(dt).replace("torch.", "")
+
+        wire = sorted({name(self.reduce_dtype or a.grad.dtype) for a in self.arenas})
+        wire_mb = sum((b.hi - b.lo) * (self.reduce_dtype or b.tensor.dtype).itemsize for b in self.buckets) / 2 ** 20
         return {"buckets": len(self.buckets), "bucket_mb": self.bucket_mb,
-                "reduce_dtype": str(self.reduce_dtype or (self.arenas[0].grad.dtype if self.arenas else None)
-                                    ).replace("torch.", ""),
-                "transport": transport, "world": self.world}
+                "reduce_dtype": wire[0] if len(wire) == 1 else "mixed(%s)" % ",".join(wire),
+                "grad_dtypes": sorted({name(a.grad.dtype) for a in self.arenas}),
+                "wire_mb_per_step": round(wire_mb, 2), "transport": transport, "world": self.world}
 
     def broadcast_parameters(self, src=0):
         """C2: make every rank start from rank ``src``'s weights (one call per arena)."""

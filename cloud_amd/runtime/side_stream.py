@@ -78,8 +78,24 @@ class SideWork:
 # Side-stream gradients whose join (and DDP notification) is deferred across layers:
 # [(event, params)], oldest first.  A backward-pass callback settles all of them, so the
 # optimizer / DDP never read a gradient before the side stream has written it.
+# A backward that raises (OOM inside a tuner trial, which then moves on in the same
+# process) never runs its queued callback: ``begin_pass`` -- called by every forward that
+# builds a graph using ``defer`` -- drops that stale state, so the next backward queues
+# its own settle callback and no gradient of the failed graph is ever announced to DDP.
 _PENDING = []
 _CALLBACK = [False]
+
+
+def begin_pass():
+    """Start of a new forward/backward: discard deferred work of a backward that never
+    finished.  The main stream still waits for the stale side-stream events (their
+    kernels may be queued and write memory the allocator would otherwise recycle); their
+    params are NOT notified (the failed step's gradients are never reduced)."""
+    if _PENDING:
+        for ev, _params, _notify in _PENDING:
+            torch.cuda.current_stream().wait_event(ev)
+        del _PENDING[:]
+    _CALLBACK[0] = False
 
 
 def defer(event, params, notify):

@@ -25,10 +25,10 @@ class _OptimizerClient:
         self.service = service
         self.project_id, self.region, self.study_id = project_id, region, study_id
 
-    def get_suggestions(self, client_id):
+    def get_suggestions(self, client_id, max_trials=None):
         try:
             resp = self.service.suggest(self._make_study_name(), client_id,
-                                        count=constants.SUGGESTION_COUNT_PER_REQUEST)
+                                        count=constants.SUGGESTION_COUNT_PER_REQUEST, max_trials=max_trials)
         except TooManyTrials:
             return {}
         if "trials" not in resp:

@@ -27,8 +27,19 @@ import time
 from ..utils import hbm
 
 
-def _await_gate(gate_file, poll_s=0.01):
-    """Standby worker: wait for the scheduler's verdict (True = run, False = exit)."""
+def _await_gate(gate_file, poll_s=0.01, parent=None, deadline_s=None):
+    """Standby worker: wait for the scheduler's verdict (True = run, False = exit).
+
+    A standby never outlives its scheduler: it gives up (False) when its parent process
+    is gone (re-parented: ``os.getppid()`` changed), when the gate's directory was removed,
+    or after ``deadline_s`` (``CLOUD_AMD_TUNER_GATE_TIMEOUT_S``)."""
+    from .. import config
+
+    parent = os.getppid() if parent is None else parent
+    if deadline_s is None:
+        deadline_s = config.get("CLOUD_AMD_TUNER_GATE_TIMEOUT_S")
+    t_end = time.time() + deadline_s if deadline_s else None
+    state_dir = os.path.dirname(gate_file)
     while True:
         if os.path.exists(gate_file):
             try:
@@ -36,6 +47,10 @@ def _await_gate(gate_file, poll_s=0.01):
                     return bool(json.load(fh)["go"])
             except (OSError, ValueError, KeyError):
                 pass  # written non-atomically by an older scheduler: retry
+        if os.getppid() != parent or not os.path.isdir(state_dir):
+            return False
+        if t_end is not None and time.time() > t_end:
+            return False
         time.sleep(poll_s)
 
 
@@ -95,12 +110,17 @@ def _worker_body(target, tuner_id, device, env, gate_file, tl):
     os.environ.update(env)
     os.environ["CLOUD_AMD_TUNER_ID"] = tuner_id
     os.environ["KERASTUNER_TUNER_ID"] = tuner_id
-    if device.startswith("cuda"):
+    os.environ["CLOUD_AMD_TRIAL_DEVICE"] = device  # recorded on every trial this worker runs
+    if device.startswith("cuda") and os.environ.get("CLOUD_AMD_SCHED_FAKE_DEVICES") != "1":
         import torch
 
         torch.cuda.set_device(int(device.split(":")[1]))
         os.environ["LOCAL_RANK"] = device.split(":")[1]
     else:
+        # CPU node, or a placement rehearsal on a CPU host (CLOUD_AMD_SCHED_FAKE_DEVICES=1:
+        # the worker keeps its assigned GPU name for the study record but computes on CPU)
+        if device.startswith("cuda"):
+            os.environ["LOCAL_RANK"] = device.split(":")[1]
         os.environ["CLOUD_AMD_DEVICE"] = "cpu"
     mod, fn = target.split(":")
     _mark(tl, "running")
@@ -158,6 +178,15 @@ class TrialScheduler:
     def _slots(self):
         return max(self.n_gpus, 1)
 
+    def standby_count(self):
+        """Gated standbys started with the probe wave: bounded by ``max_workers`` and by an
+        estimate of what packing can use (``CLOUD_AMD_TUNER_STANDBY_PER_GPU`` per GPU), so a
+        many-core node does not start 100+ interpreters that packing then dismisses."""
+        from .. import config
+
+        per = max(0, int(config.get("CLOUD_AMD_TUNER_STANDBY_PER_GPU")))
+        return max(0, min(self.max_workers - self._slots(), self._slots() * per))
+
     def _device(self, i):
         return f"cuda:{i % self.n_gpus}" if self.n_gpus else "cpu"
 
@@ -205,31 +234,39 @@ class TrialScheduler:
             # (CLOUD_AMD_TUNER_STANDBY=0: spawn the packing wave only after the probe)
             from .. import config
 
-            n_standby = max(0, self.max_workers - self._slots()) if config.get("CLOUD_AMD_TUNER_STANDBY") else 0
+            n_standby = self.standby_count() if config.get("CLOUD_AMD_TUNER_STANDBY") else 0
             gates = [os.path.join(state, f"gate_tuner{i}.json") for i in range(self._slots(), self._slots() + n_standby)]
             standby = [self._spawn(ctx, self._slots() + k, gate_file=g) for k, g in enumerate(gates)]
             limit = self.probe_timeout_s if self.probe_timeout_s is not None else timeout
-            while self.footprint_gb is None:
-                for f in files:
-                    if os.path.exists(f):
-                        with open(f) as fh:
-                            self.footprint_gb = float(json.load(fh)["peak_gb"])
+            extra = 0
+            try:
+                while self.footprint_gb is None:
+                    for f in files:
+                        if os.path.exists(f):
+                            with open(f) as fh:
+                                self.footprint_gb = float(json.load(fh)["peak_gb"])
+                            break
+                    if self.footprint_gb is not None or all(not p.is_alive() for p in procs):
                         break
-                if self.footprint_gb is not None or all(not p.is_alive() for p in procs):
-                    break
-                if limit is not None and time.time() - t0 > limit:
-                    break
-                time.sleep(0.05)
-            self.per_gpu = self.packing_from_footprint(self.footprint_gb) if self.footprint_gb else 1
-            want = min(self.max_workers, self._slots() * self.per_gpu)
-            if not any(p.is_alive() for p in procs):  # nothing left to pack into if the probe wave is done
-                want = len(procs)
-            extra = max(0, want - len(procs))
-            for k, (g, sp) in enumerate(zip(gates, standby)):
-                self._open_gate(g, k < extra)
+                    if limit is not None and time.time() - t0 > limit:
+                        break
+                    time.sleep(0.05)
+                self.per_gpu = self.packing_from_footprint(self.footprint_gb) if self.footprint_gb else 1
+                want = min(self.max_workers, self._slots() * self.per_gpu)
+                if not any(p.is_alive() for p in procs):  # nothing left to pack into if the probe wave is done
+                    want = len(procs)
+                extra = max(0, want - len(procs))
+            finally:
+                # every gate gets a verdict, also when the probe loop raised (Ctrl-C): a
+                # standby left waiting would keep multiprocessing's atexit join hanging
+                for k, g in enumerate(gates):
+                    self._open_gate(g, k < extra)
             procs += standby[:extra]
             for sp in standby[extra:]:
                 sp.join(30)
+                if sp.is_alive():
+                    sp.terminate()
+                    sp.join(5)
             procs += [self._spawn(ctx, i) for i in range(len(procs), want)]
             self.workers = len(procs)
         for p in procs:

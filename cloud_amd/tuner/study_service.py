@@ -231,7 +231,10 @@ class StudyService:
                     return dict(t)
         raise KeyError(trial_name)
 
-    def suggest(self, study_name, client_id, count=1):
+    def suggest(self, study_name, client_id, count=1, max_trials=None):
+        """New (or this client's still pending) trials.  ``max_trials`` is checked under
+        the study lock, so N concurrent tuner processes never create more trials than the
+        cap between their own ``list_trials`` check and the suggestion."""
         sid = self.study_id_of(study_name)
         with self._locked(sid):
             data = self._read(sid)
@@ -242,6 +245,8 @@ class StudyService:
                                                                                                   "REQUESTED")]
             if mine:
                 return {"trials": mine[:count], "studyState": "ACTIVE"}
+            if max_trials and len(data["trials"]) >= max_trials:
+                return {"studyState": "ACTIVE"}  # the oracle's cap: no trial, search ends
             if len(data["trials"]) >= MAX_TRIALS:
                 raise TooManyTrials(f"study {sid} reached {MAX_TRIALS} trials")
             out = []
@@ -256,6 +261,9 @@ class StudyService:
                 trial = {"name": f"{study['name']}/trials/{tid}", "state": "ACTIVE", "parameters": params,
                          "clientId": client_id, "measurements": [], "startTime": _ts(),
                          "startTs": time.time()}
+                dev = os.environ.get("CLOUD_AMD_TRIAL_DEVICE")  # set by TrialScheduler per worker
+                if dev:
+                    trial["device"] = dev
                 data["trials"].append(trial)
                 out.append(trial)
             self._write(sid, data)

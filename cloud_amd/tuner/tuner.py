@@ -111,7 +111,7 @@ class CloudOracle(Oracle):
             hps = self.hyperparameters.copy()
             hps.values = None
             return Trial(hyperparameters=hps, trial_id="n", status=TrialStatus.STOPPED)
-        suggestions = self.service.get_suggestions(tuner_id)
+        suggestions = self.service.get_suggestions(tuner_id, max_trials=self.max_trials)
         if "trials" not in suggestions:
             return Trial(hyperparameters={}, status=TrialStatus.STOPPED)
         opt_trial = suggestions["trials"][0]
@@ -209,7 +209,7 @@ class _TunerCallback:
                     from ..utils import hbm
 
                     tuner._early_report_pending = False
-                    if hbm.report_footprint() is not None:
+                    if hbm.report_footprint(extra_gb=tuner._val_gb) is not None:
                         tuner._reported = True
 
             def on_epoch_end(cb, epoch, logs=None):
@@ -304,6 +304,9 @@ class Tuner:
         from .. import config
 
         self._reported = False
+        # measured after batch 0 of the first trial, before evaluate() uploads the
+        # validation set to the device: its bytes are added to the reported peak
+        self._val_gb = hbm.array_gb(fit_kwargs.get("validation_data"))
         # CLOUD_AMD_TUNER_EARLY_FOOTPRINT: report after the first step (default) or the first trial
         self._early_report_pending = bool(os.environ.get("CLOUD_AMD_FOOTPRINT_FILE")) and bool(
             config.get("CLOUD_AMD_TUNER_EARLY_FOOTPRINT"))
@@ -320,7 +323,7 @@ class Tuner:
                 continue
             self.oracle.end_trial(trial.trial_id, TrialStatus.COMPLETED)
             if not self._reported:  # the scheduler packs more workers per GPU from this measurement
-                hbm.report_footprint()
+                hbm.report_footprint(extra_gb=self._val_gb)
                 self._reported = True
                 self._early_report_pending = False
 

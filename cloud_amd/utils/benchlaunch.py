@@ -91,3 +91,69 @@ def launched_via():
     if os.environ.get("CLOUD_AMD_RUN_T0"):
         return "cloud_amd.run()"
     return "torch.distributed.run" if os.environ.get("TORCHELASTIC_RUN_ID") else "direct"
+
+
+def host_state():
+    """What the host looked like: 1/5/15-minute load average, this process's CPU set and
+    the CPU it is on, voluntary / involuntary context switches so far."""
+    st = {}
+    try:
+        with open("/proc/loadavg") as f:
+            st["loadavg"] = [float(x) for x in f.read().split()[:3]]
+    except OSError:
+        st["loadavg"] = None
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+        from ..core.topology import format_cpulist
+
+        st["affinity"] = format_cpulist(cpus)
+        st["n_affinity"] = len(cpus)
+    except AttributeError:  # pragma: no cover
+        st["affinity"], st["n_affinity"] = None, None
+    try:
+        with open("/proc/self/stat") as f:
+            st["cpu"] = int(f.read().rsplit(")", 1)[1].split()[36])
+    except (OSError, IndexError, ValueError):
+        st["cpu"] = None
+    try:
+        import resource
+
+        ru = resource.getrusage(resource.RUSAGE_SELF)
+        st["ctx_voluntary"], st["ctx_involuntary"] = ru.ru_nvcsw, ru.ru_nivcsw
+    except Exception:  # noqa: BLE001 - informational
+        pass
+    return st
+
+
+def _mmm(v):
+    s = sorted(v)
+    n = len(s)
+    med = s[n // 2] if n % 2 else 0.5 * (s[n // 2 - 1] + s[n // 2])
+    return {"min": round(s[0], 3), "median": round(med, 3), "max": round(s[-1], 3)}
+
+
+def step_stats(device_ms, host_ms, host_before, host_after, outlier_ratio=1.5):
+    """Per-step timing of the timed region (device time between step-boundary events on
+    the compute stream, host time to enqueue a step) plus the host state around it.  A
+    step slower than ``outlier_ratio`` x the median adds a warning, with the evidence
+    needed to name the cause: the host launch time (a starved / descheduled host makes
+    host time ~ device time), involuntary context switches (another process on our
+    cores), the CPU the rank ran on before and after (migration), the load average."""
+    out = {"host_launch_ms": _mmm(host_ms) if host_ms else None,
+           "device_ms": _mmm(device_ms) if device_ms else None,
+           "host_before": host_before, "host_after": host_after, "warnings": []}
+    ref = device_ms or host_ms
+    if ref:
+        m = out["device_ms" if device_ms else "host_launch_ms"]
+        if m["median"] > 0 and m["max"] / m["median"] > outlier_ratio:
+            slow = [i for i, v in enumerate(ref) if v > outlier_ratio * m["median"]]
+            inv = None
+            if "ctx_involuntary" in host_before and "ctx_involuntary" in host_after:
+                inv = host_after["ctx_involuntary"] - host_before["ctx_involuntary"]
+            out["warnings"].append(
+                "slow steps %s: max/median step time %.2f > %.1f (host launch ms of those steps %s; "
+                "involuntary context switches during the timed steps %s; cpu %s -> %s; loadavg %s -> %s)"
+                % (slow, m["max"] / m["median"], outlier_ratio, [round(host_ms[i], 2) for i in slow if i < len(host_ms)],
+                   inv, host_before.get("cpu"), host_after.get("cpu"), host_before.get("loadavg"),
+                   host_after.get("loadavg")))
+    return out

@@ -138,3 +138,52 @@ def allreduce_busbw(device, nbytes=64 << 20, iters=5, dtype=torch.float32):
     dt = all_reduce_max((time.perf_counter() - t0) / iters, device)
     size = t.numel() * t.element_size()
     return round(size * 2.0 * (n - 1) / n / dt / 1e9, 2)
+
+
+def comm_probe(device, sizes_mb=(16, 64), iters=5, dtype=torch.bfloat16):
+    """All-reduce bandwidth of BOTH data-plane transports on the same buffers: the
+    ``torch.distributed`` process group (RCCL backend) and the native C++ communicator
+    (``parallel/comm.RcclComm``, its own stream), bf16 at the gradient-bucket size and at
+    64 MB.  One 8-GPU run then says which transport to make the default
+    (``CLOUD_AMD_COMM``).  Per transport and size: ``busbw_gbs`` (nccl-tests convention,
+    slowest rank) and ``algbw_gbs``; a transport that cannot run reports its error.
+    Needs a multi-rank group (None otherwise); every rank must call it."""
+    if not dist.is_initialized() or dist.get_world_size() < 2:
+        return None
+    import time
+
+    n = dist.get_world_size()
+    out = {}
+
+    def timed(fn, t, sync_stream):
+        fn(t)
+        sync_stream()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn(t)
+        sync_stream()
+        dt = all_reduce_max((time.perf_counter() - t0) / iters, device)
+        size = t.numel() * t.element_size()
+        return {"busbw_gbs": round(size * 2.0 * (n - 1) / n / dt / 1e9, 2), "algbw_gbs": round(size / dt / 1e9, 2),
+                "ms": round(dt * 1e3, 3)}
+
+    def dev_sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+
+    bufs = {mb: torch.ones((mb << 20) // torch.tensor([], dtype=dtype).element_size(), dtype=dtype, device=device)
+            for mb in sizes_mb}
+    out["torch"] = {str(mb): timed(lambda t: dist.all_reduce(t), t, dev_sync) for mb, t in bufs.items()}
+    if device.type == "cuda":
+        try:
+            from ..parallel.comm import RcclComm
+
+            c = RcclComm(tag="comm_probe", device=device)
+            try:
+                out["rccl"] = {str(mb): timed(lambda t: c.all_reduce(t), t, c.synchronize) for mb, t in bufs.items()}
+            finally:
+                c.close()
+        except Exception as e:  # noqa: BLE001 - a probe reports, it never fails the bench
+            out["rccl"] = {"error": "%s: %s" % (type(e).__name__, e)}
+    return out

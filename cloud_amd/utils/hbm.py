@@ -48,13 +48,30 @@ def trial_footprint_gb(device=None):
     return None
 
 
-def report_footprint(gb=None, path=None):
+def array_gb(obj):
+    """Bytes (GiB) of the arrays / tensors in ``obj`` (nested tuples, lists, dicts)."""
+    if obj is None:
+        return 0.0
+    if isinstance(obj, (tuple, list)):
+        return sum(array_gb(o) for o in obj)
+    if isinstance(obj, dict):
+        return sum(array_gb(o) for o in obj.values())
+    n = getattr(obj, "nbytes", None)
+    if n is None and hasattr(obj, "element_size") and hasattr(obj, "numel"):
+        n = obj.element_size() * obj.numel()
+    return float(n or 0) / 2 ** 30
+
+
+def report_footprint(gb=None, path=None, extra_gb=0.0):
     """Write this worker's measured trial footprint for the scheduler
-    (``CLOUD_AMD_FOOTPRINT_FILE``); returns the value written (None: nothing to report)."""
+    (``CLOUD_AMD_FOOTPRINT_FILE``); returns the value written (None: nothing to report).
+    ``extra_gb``: device memory the trial will still claim after the measurement (the
+    validation arrays ``evaluate`` uploads at epoch end)."""
     path = path or os.environ.get("CLOUD_AMD_FOOTPRINT_FILE")
     gb = trial_footprint_gb() if gb is None else gb
     if not path or gb is None:
         return None
+    gb = gb + float(extra_gb or 0.0)
     import json
 
     tmp = path + ".tmp"

@@ -26,7 +26,7 @@ def run(tuner_id, device):
     x = rng.normal(size=(256, 20)).astype("float32")
     y = (x[:, 0] > 0).astype("int64")
     tuner = CloudTuner(build_model, project_id="p", region="r", objective="acc", hyperparameters=hps,
-                       max_trials=6, study_id=os.environ["STUDY_ID"], study_dir=os.environ["STUDY_DIR"],
+                       max_trials=int(os.environ.get("MAX_TRIALS", 6)), study_id=os.environ["STUDY_ID"], study_dir=os.environ["STUDY_DIR"],
                        directory=os.path.join(os.environ["STUDY_DIR"], "results", tuner_id))
     if os.environ.get("FAKE_FOOTPRINT_GB"):  # CPU stand-in for the measured HBM peak of a GPU trial
         from cloud_amd.utils import hbm

@@ -39,6 +39,11 @@ def test_bench_two_ranks_via_run_cpu(tmp_path):
     assert abs(sum(ph.values()) - j["run_to_first_step_s"]) < 0.5
     assert j["comm"]["buckets"] >= 1 and j["comm"]["allreduce_ms"] > 0
     assert j["backend"] == "gloo" and j["config"]["global_batch"] == 8
+    probe = j["comm"]["comm_probe"]  # both transports measured on the same buffers
+    assert set(probe) == {"torch"} and probe["torch"]["16"]["busbw_gbs"] > 0  # CPU: no native RCCL
+    ss = j["step_stats_rank0"]
+    assert ss["host_launch_ms"]["min"] <= ss["host_launch_ms"]["median"] <= ss["host_launch_ms"]["max"]
+    assert ss["host_before"]["n_affinity"] >= 1 and isinstance(j["warnings"], list)
     job = os.listdir(tmp_path / "jobs")
     assert len(job) == 1
     meta = json.load(open(tmp_path / "jobs" / job[0] / "job.json"))

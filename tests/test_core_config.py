@@ -193,3 +193,73 @@ def test_topology_real_mi355x_box_dump(monkeypatch):
     assert abs(topology.hbm_gb_per_gpu(root) - 288.0) < 0.5
     assert sum(1 for l in gpus[0]["links"] if l["type"] == topology.IOLINK_XGMI) == 7
     assert topology.xgmi_links_per_gpu(1, root) == 0
+
+
+def _full_node_tree(tmp_path):
+    """The real 1-of-8 KFD dump completed to all eight GPUs (the job that dumped it could
+    read only its own GPU node's properties; the CPU agents' links, which decide NUMA
+    placement, are all real), plus a fake sysfs NUMA / SMT tree: 2 sockets x 8 cores x 2
+    threads (cpus n and n+32 are siblings)."""
+    import shutil
+
+    src = os.path.join(os.path.dirname(__file__), "data", "kfd_mi355x_1of8")
+    kfd = tmp_path / "kfd"
+    shutil.copytree(src, kfd)
+    gpu_props = (kfd / "6" / "properties").read_text()
+    for g in (2, 3, 4, 5, 7, 8, 9):
+        (kfd / str(g) / "properties").write_text(gpu_props)
+    numa = tmp_path / "node"
+    cpu = tmp_path / "cpu"
+    for k in range(2):
+        (numa / ("node%d" % k)).mkdir(parents=True)
+        (numa / ("node%d" % k) / "cpulist").write_text("%d-%d,%d-%d\n" % (16 * k, 16 * k + 15, 32 + 16 * k,
+                                                                           32 + 16 * k + 15))
+    for c in range(64):
+        d = cpu / ("cpu%d" % c) / "topology"
+        d.mkdir(parents=True)
+        base = c % 32
+        d.joinpath("thread_siblings_list").write_text("%d,%d\n" % (base, base + 32))
+    return str(kfd), str(numa), str(cpu)
+
+
+def test_rank_cpu_sets_eight_mi355x_ranks(tmp_path, monkeypatch):
+    """each rank pinned to the cores local to its GPU.  KFD CPU agent 0
+    (NUMA 0) links GPUs 2-5, agent 1 (NUMA 1) GPUs 6-9: ranks 0-3 split socket 0's cores,
+    ranks 4-7 socket 1's, whole physical cores (both SMT threads) per rank, disjoint."""
+    for v in ("CLOUD_AMD_NUM_GPUS", "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    kfd, numa, cpu = _full_node_tree(tmp_path)
+    monkeypatch.setenv("CLOUD_AMD_KFD_ROOT", kfd)
+    monkeypatch.setenv("CLOUD_AMD_NUMA_ROOT", numa)
+    monkeypatch.setenv("CLOUD_AMD_CPU_ROOT", cpu)
+    assert topology.visible_gpu_count() == 8
+    assert topology.gpu_numa_nodes() == [0, 0, 0, 0, 1, 1, 1, 1]
+    sets = topology.rank_cpu_sets(list(range(8)), allowed=set(range(64)))
+    want = []
+    for k in range(2):
+        for i in range(4):
+            cores = list(range(16 * k + 4 * i, 16 * k + 4 * i + 4))
+            want.append(sorted(cores + [c + 32 for c in cores]))
+    assert sets == want
+    assert topology.format_cpulist(sets[5]) == "20-23,52-55"
+    # a restricted launcher (cgroup / taskset) only hands out CPUs it may use
+    allowed = set(range(0, 8)) | set(range(32, 40)) | set(range(16, 32)) | set(range(48, 64))
+    sets = topology.rank_cpu_sets(list(range(8)), allowed=allowed)
+    assert sets[0] == [0, 1, 32, 33] and sets[3] == [6, 7, 38, 39] and sets[4] == want[4]
+    # one GPU visible (the box the dump came from: KFD node 6 = NUMA 1)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "4")
+    assert topology.gpu_numa_nodes() == [1]
+    assert topology.rank_cpu_sets([0], allowed=set(range(64))) == [sorted(list(range(16, 32)) + list(range(48, 64)))]
+
+
+def test_rank_cpu_sets_from_the_real_dump_alone(monkeypatch):
+    """Only the real dump (no sysfs NUMA tree for it): the one visible GPU (KFD node 6)
+    hangs off CPU agent 1, whose KFD cpu_core_id_base / cpu_cores_count give cores 128-255."""
+    for v in ("CLOUD_AMD_NUM_GPUS", "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    root = os.path.join(os.path.dirname(__file__), "data", "kfd_mi355x_1of8")
+    monkeypatch.setenv("CLOUD_AMD_NUMA_ROOT", "/nonexistent")
+    monkeypatch.setenv("CLOUD_AMD_CPU_ROOT", "/nonexistent")
+    assert topology.gpu_numa_nodes(root) == [1]
+    assert topology.rank_cpu_sets([0], root=root, allowed=set(range(512))) == [list(range(128, 256))]
+    assert topology.rank_cpu_sets([None], root=root, allowed=set(range(512))) == [None]

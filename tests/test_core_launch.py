@@ -266,7 +266,7 @@ def test_launcher_process_never_imports_torch(tmp_path):
     assert "TORCH_IMPORTED False" in r.stdout, r.stdout
 
 
-def test_stage_hardlinks_and_skips_build_artifacts(tmp_path):
+def test_stage_links_code_copies_data_and_honours_cloudamdignore(tmp_path):
     proj = tmp_path / "proj"
     (proj / "build").mkdir(parents=True)
     (proj / "profiles").mkdir()
@@ -276,9 +276,16 @@ def test_stage_hardlinks_and_skips_build_artifacts(tmp_path):
     (proj / "pkg" / "obj.o").write_text("object")
     (proj / "build" / "big.o").write_text("object")
     (proj / "profiles" / "p.txt").write_text("x")
+    (proj / "data.csv").write_text("1,2\n")
     cwd = os.getcwd()
     os.chdir(proj)
     try:
+        # no .cloudamdignore: a user package called build/ or profiles/ ships
+        job_dir, _ = stage.stage_job("j0", "train.py", None, root=str(tmp_path / "jobs"))
+        app0 = os.path.join(job_dir, "app")
+        assert os.path.isfile(os.path.join(app0, "build", "big.o"))
+        assert os.path.isfile(os.path.join(app0, "profiles", "p.txt"))
+        (proj / ".cloudamdignore").write_text("# project excludes\nbuild/\nprofiles\n*.o\n")
         job_dir, target = stage.stage_job("j1", "train.py", None, root=str(tmp_path / "jobs"))
     finally:
         os.chdir(cwd)
@@ -287,10 +294,37 @@ def test_stage_hardlinks_and_skips_build_artifacts(tmp_path):
     assert not os.path.exists(os.path.join(app, "build"))
     assert not os.path.exists(os.path.join(app, "profiles"))
     assert not os.path.exists(os.path.join(app, "pkg", "obj.o"))
-    # hard links: same inode as the source
+    # code is hard-linked (same inode), data is copied (its own inode)
     assert os.stat(os.path.join(app, "pkg", "mod.py")).st_ino == os.stat(proj / "pkg" / "mod.py").st_ino
+    assert os.stat(os.path.join(app, "data.csv")).st_ino != os.stat(proj / "data.csv").st_ino
     man = json.load(open(os.path.join(job_dir, "manifest.json")))
     assert man["framework"]["torch"] and "hip" in man["framework"]
+
+
+def test_job_writing_a_staged_file_leaves_the_source_tree_unchanged(tmp_path):
+    """A rank that rewrites / appends to a file it finds in its cwd (a checkpoint, a CSV log)
+    changes the job's copy only -- and two jobs staged from one directory stay apart."""
+    proj = tmp_path / "proj"
+    proj.mkdir()
+    (proj / "train.py").write_text("print('hi')\n")
+    (proj / "model.h5").write_bytes(b"ORIGINAL")
+    (proj / "log.csv").write_text("epoch,loss\n")
+    cwd = os.getcwd()
+    os.chdir(proj)
+    try:
+        jd1, _ = stage.stage_job("w1", "train.py", None, root=str(tmp_path / "jobs"))
+        jd2, _ = stage.stage_job("w2", "train.py", None, root=str(tmp_path / "jobs"))
+    finally:
+        os.chdir(cwd)
+    for jd, tag in ((jd1, b"JOB1"), (jd2, b"JOB2")):
+        with open(os.path.join(jd, "app", "model.h5"), "wb") as f:  # truncating rewrite
+            f.write(tag)
+        with open(os.path.join(jd, "app", "log.csv"), "a") as f:
+            f.write("0,1.0\n")
+    assert (proj / "model.h5").read_bytes() == b"ORIGINAL"
+    assert (proj / "log.csv").read_text() == "epoch,loss\n"
+    assert open(os.path.join(jd1, "app", "model.h5"), "rb").read() == b"JOB1"
+    assert open(os.path.join(jd2, "app", "model.h5"), "rb").read() == b"JOB2"
 
 
 def _write_nb(path):

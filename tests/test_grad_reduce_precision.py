@@ -54,10 +54,40 @@ def _worker(rank, port, out_dir):
         p.grad.copy_(_grads(rank))
         red.finish()
         res[wire] = p.grad.float().tolist()[:N]
+    # BERT's fp32 arena (word-embedding table rows + LayerNorm / bias vectors): the
+    # default bf16 wire reduces a bf16 copy and casts the sum back into the fp32 gradient
+    bert = {}
+    for wire in ("bf16", "fp32"):
+        emb = torch.nn.Parameter(torch.zeros(EMB_ROWS, 768))
+        ln = torch.nn.Parameter(torch.zeros(LN))
+        opt = SGD([emb, ln], learning_rate=0.0)
+        red = GradAllReducer(opt.arenas, bucket_mb=1.0, reduce_dtype=wire)
+        ge, gl = _bert_grads(rank)
+        emb.grad.copy_(ge)
+        ln.grad.copy_(gl)
+        red.finish()
+        bert[wire] = {"emb": emb.grad.flatten().tolist(), "ln": ln.grad.tolist(),
+                      "describe": red.describe()}
     if rank == 0:
         with open(os.path.join(out_dir, "sums.json"), "w") as f:
             json.dump(res, f)
+        with open(os.path.join(out_dir, "bert.json"), "w") as f:
+            json.dump(bert, f)
     dist.destroy_process_group()
+
+
+EMB_ROWS, LN = 512, 9 * 768
+
+
+def _bert_grads(rank):
+    """Per-rank fp32 gradients shaped like BERT-base's fp32 arena: embedding rows that
+    only some ranks touched (sparse token overlap: 1/4 of the rows per rank, scale ~1e-3)
+    and dense LayerNorm gamma/beta gradients (scale ~1e-2)."""
+    g = torch.Generator().manual_seed(500 + rank)
+    emb = torch.randn(EMB_ROWS, 768, generator=g) * 1e-3
+    emb[torch.rand(EMB_ROWS, generator=g) > 0.25] = 0.0
+    ln = torch.randn(LN, generator=g) * 1e-2 + 0.02 * torch.randn(LN, generator=torch.Generator().manual_seed(3))
+    return emb, ln
 
 
 def test_bf16_vs_fp32_wire_error_at_8_ranks(tmp_path):
@@ -76,3 +106,20 @@ def test_bf16_vs_fp32_wire_error_at_8_ranks(tmp_path):
     assert err["bf16"] < 3.0 * ulp, err
     assert err["bf16"] >= err["fp32"]
     print("relative L2 error of the 8-rank gradient sum:", json.dumps(err))
+
+    bert = json.load(open(tmp_path / "bert.json"))
+    emb_exact = sum(_bert_grads(r)[0].double() for r in range(WORLD)).flatten()
+    ln_exact = sum(_bert_grads(r)[1].double() for r in range(WORLD))
+    berr = {}
+    for wire in ("bf16", "fp32"):
+        for k, ex in (("emb", emb_exact), ("ln", ln_exact)):
+            got = torch.tensor(bert[wire][k], dtype=torch.float64)
+            berr[wire + "_" + k] = float((got - ex).norm() / ex.norm())
+    # fp32 on the wire: fp32 sums (~1e-7); bf16 on the wire: a few bf16 roundings
+    assert berr["fp32_emb"] < 1e-6 and berr["fp32_ln"] < 1e-6, berr
+    assert berr["bf16_emb"] < 3.0 * ulp and berr["bf16_ln"] < 3.0 * ulp, berr
+    d_bf, d_fp = bert["bf16"]["describe"], bert["fp32"]["describe"]
+    assert d_bf["reduce_dtype"] == "bfloat16" and d_fp["reduce_dtype"] == "float32"
+    assert d_bf["grad_dtypes"] == ["float32"]
+    assert abs(d_bf["wire_mb_per_step"] * 2 - d_fp["wire_mb_per_step"]) < 0.05  # half the bytes
+    print("BERT fp32-arena 8-rank sums, relative L2 error:", json.dumps(berr))

@@ -304,3 +304,62 @@ def test_grad_finalize_batch_bitwise(monkeypatch):
             torch.testing.assert_close(out["1"][n], out["0"][n], rtol=1e-5, atol=1e-6)
         else:
             assert torch.equal(out["1"][n], out["0"][n]), n
+
+
+def test_backward_raising_midway_does_not_poison_next_step():
+    """A BERT backward that raises after a layer deferred its side-stream gradients (an
+    OOM inside a tuner trial) leaves no stale state: the next forward/backward queues its
+    own settle callback and produces the same gradients as a clean model."""
+    from cloud_amd.models.bert import BertConfig, BertForSequenceClassification
+    from cloud_amd.runtime import side_stream
+
+    torch.manual_seed(9)
+    cfg = BertConfig.tiny(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0, num_labels=2,
+                          num_hidden_layers=3)
+    m = BertForSequenceClassification(cfg, device=DEV)
+    B, S = 2, 128
+    ids = torch.randint(0, cfg.vocab_size, (B, S), device=DEV)
+    labels = torch.randint(0, 2, (B,), device=DEV)
+
+    def step():
+        m.zero_grad(set_to_none=True)
+        F.cross_entropy(m(ids), labels).backward()
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+
+    clean = step()
+    assert side_stream._PENDING == [] and side_stream._CALLBACK[0] is False
+
+    # raise inside the backward of the first layer's output (after layers 3 and 2 deferred)
+    calls = {"n": 0}
+    h_hook = []
+
+    class Boom(RuntimeError):
+        pass
+
+    import cloud_amd.models.bert as bert_mod
+    real_layer = bert_mod._LayerFn.apply
+
+    def hooked(h, *args):
+        y = real_layer(h, *args)
+        calls["n"] += 1
+        if calls["n"] == 1:  # first layer's output: its gradient arrives after layers 3, 2 ran
+            def raise_(_g):
+                raise Boom("injected mid-backward failure")
+            h_hook.append(y.register_hook(raise_))
+        return y
+
+    bert_mod._LayerFn.apply = hooked
+    try:
+        m.zero_grad(set_to_none=True)
+        with pytest.raises(Boom):
+            F.cross_entropy(m(ids), labels).backward()
+    finally:
+        bert_mod._LayerFn.apply = real_layer
+    torch.cuda.synchronize()
+    assert side_stream._CALLBACK[0] is True or side_stream._PENDING  # the failure left state behind
+    again = step()
+    assert side_stream._PENDING == [] and side_stream._CALLBACK[0] is False
+    assert again.keys() == clean.keys()
+    for n in clean:
+        torch.testing.assert_close(again[n].float(), clean[n].float(), rtol=2e-2, atol=1e-5)

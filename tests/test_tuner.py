@@ -2,6 +2,7 @@
 golden values), oracle lifecycle (tuner_test.py), local study service
 semantics (optimizer_client_test.py) and a real multi-process search."""
 import json
+import time
 import os
 import threading
 
@@ -320,6 +321,51 @@ def test_scheduler_packs_from_measured_footprint(tmp_path):
     assert all(m["imported"] <= m.get("released", m.get("dismissed")) for m in standby)
 
 
+def test_scheduler_places_trials_round_robin_over_eight_gpus(tmp_path):
+    """BASELINE config 4 (one trial per MI355X and packing within each GPU's HBM) on an
+    8-GPU placement rehearsed on CPU: one probe worker per GPU, packing from the measured
+    footprint, round-robin device assignment, and each trial's device in the study."""
+    import sys
+
+    sys.path.insert(0, os.path.join(HERE, "data"))
+    env = {"STUDY_ID": "eight", "STUDY_DIR": str(tmp_path), "PYTHONPATH": os.path.join(HERE, "data"),
+           "FAKE_FOOTPRINT_GB": "1.0", "MAX_TRIALS": "16", "CLOUD_AMD_SCHED_FAKE_DEVICES": "1",
+           "OMP_NUM_THREADS": "1"}
+    sched = TrialScheduler("tuner_worker:run", n_gpus=8, env=env, hbm_gb=4.0, max_workers=16,
+                           state_dir=str(tmp_path / "sched"), timeline=True)
+    # probe wave = one worker per GPU; standbys capped by max_workers - GPUs
+    assert sched.devices() == ["cuda:%d" % i for i in range(8)]
+    assert sched.standby_count() == 8
+    res = sched.run(timeout=900)
+    assert res["footprint_gb"] == 1.0 and res["trials_per_gpu"] == 2   # 4 GB * 0.9 // 1.25
+    assert res["workers"] == 16 and res["exit_codes"] == [0] * 16
+    assert sched.devices() == ["cuda:%d" % (i % 8) for i in range(16)]
+    tl = res["timeline"]
+    probes = [tl["tuner%d" % i] for i in range(8)]
+    assert all("imported" not in m for m in probes)          # probes run at once, ungated
+    assert sum("released" in tl["tuner%d" % i] for i in range(8, 16)) == 8
+    with open(tmp_path / "CloudTuner_study_eight" / "study.json") as f:
+        trials = json.load(f)["trials"]
+    assert len(trials) == 16 and all(t["state"] == "COMPLETED" for t in trials)
+    for t in trials:  # trial -> device record follows the worker's round-robin slot
+        i = int(t["clientId"][len("tuner"):])
+        assert t["device"] == "cuda:%d" % (i % 8), t
+    assert len({t["device"] for t in trials}) >= 2
+
+
+def test_standby_gate_gives_up_without_scheduler(tmp_path):
+    from cloud_amd.tuner.scheduler import _await_gate
+
+    gate = str(tmp_path / "gate.json")
+    t0 = time.time()
+    assert _await_gate(gate, parent=-1, deadline_s=30) is False        # parent gone
+    assert _await_gate(gate, deadline_s=0.2) is False                  # deadline
+    assert _await_gate(str(tmp_path / "gone" / "g.json"), deadline_s=30) is False  # state dir removed
+    assert time.time() - t0 < 5
+    TrialScheduler._open_gate(gate, True)
+    assert _await_gate(gate) is True
+
+
 def test_tuner_reports_footprint_after_first_trial(tmp_path, monkeypatch):
     from cloud_amd.utils import hbm
 
@@ -333,3 +379,26 @@ def test_tuner_reports_footprint_after_first_trial(tmp_path, monkeypatch):
                        study_dir=str(tmp_path), directory=str(tmp_path / "res"))
     tuner.search(x, y, epochs=1, batch_size=32)
     assert json.load(open(out))["peak_gb"] == 3.5
+
+
+def test_reported_footprint_includes_validation_arrays(tmp_path, monkeypatch):
+    """The probe reports after batch 0 of its first trial, before evaluate() uploads the
+    validation set at epoch end: the validation bytes are added to the measured peak."""
+    from cloud_amd.utils import hbm
+
+    out = tmp_path / "fp.json"
+    monkeypatch.setenv("CLOUD_AMD_FOOTPRINT_FILE", str(out))
+    monkeypatch.setattr(hbm, "trial_footprint_gb", lambda device=None: 1.0)
+    rng = np.random.default_rng(3)
+    x = rng.normal(size=(64, 20)).astype("float32")
+    y = (x[:, 0] > 0).astype("int64")
+    xv = rng.normal(size=(4096, 1024)).astype("float32")  # 16 MiB
+    yv = np.zeros(4096, dtype="int64")
+    tuner = CloudTuner(_build, objective="acc", hyperparameters=_hps(), max_trials=1, study_id="fpv",
+                       study_dir=str(tmp_path), directory=str(tmp_path / "res"))
+    assert abs(hbm.array_gb((xv, yv)) - (xv.nbytes + yv.nbytes) / 2 ** 30) < 1e-12
+    tuner._val_gb = 0.0
+    monkeypatch.setattr(tuner, "run_trial", lambda trial, *a, **k: None)
+    tuner.search(x, y, epochs=1, batch_size=32, validation_data=(xv, yv))
+    got = json.load(open(out))["peak_gb"]
+    assert abs(got - (1.0 + (xv.nbytes + yv.nbytes) / 2 ** 30)) < 1e-9
