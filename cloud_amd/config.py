@@ -90,6 +90,11 @@ _VARS = [
         "read 2 staged output rows from LDS before storing", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "
         "K, minimum HBM bytes) to this file, for scripts/gemm_roofline.py", "ops"),
+    Var("CLOUD_AMD_BN_FOLD", bool, True, "ResNet block backward: the bn3 / bn1 backward apply runs in the operand "
+        "fetch of the 1x1 input-gradient GEMM that consumes it (ca_gemm_xa.h) instead of a separate pass", "ops"),
+    Var("CLOUD_AMD_BN_FOLD_FWD", bool, True, "ResNet block forward: bn2's apply runs in conv3's operand fetch and "
+        "bn3's (+ residual) in the next block's conv1 (ca_gemm_xa.h); the applied tensors are written once, by "
+        "those GEMMs", "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "
         "second HIP stream, overlapping the memory-bound BN/LN/dgrad chain", "ops"),
     Var("CLOUD_AMD_BN_BWD_EPILOGUE", bool, True, "ResNet block backward: BatchNorm-backward statistics from the "

@@ -109,15 +109,53 @@ def _conv_bn(conv, bn, x, residual=None):
     return z, y, (st, mask)
 
 
+def _bn_stats(bn, z, part, res_ss=None):
+    """BN-forward statistics + finalize only (running stats updated, [mean|rstd|scale|shift])."""
+    return raw.bn_fwd_stats(z, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, bn.momentum, part)
+
+
+def _fold_conv(conv, src, ss, side, mask, res=None, res_ss=None):
+    """1x1 forward conv whose input BN(+residual)+ReLU apply runs in its operand fetch; the
+    applied input is written once to ``side`` (+ ReLU bitmask ``mask``).  Returns (z, partials)."""
+    N, H, W, _ = src.shape
+    part = raw.stats_buffer(N * H * W, conv.cout, src.device)
+    z = raw.conv1x1_fwd_bnapply(src, ss, conv.weight, side, mask, res=res, res_ss=res_ss, stats=part)
+    return z, part
+
+
 class _BottleneckFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, blk, prev_src, *params):
+    def forward(ctx, x, blk, prev_src, pend, defer, *params):
         # prev_src: (z, mask) of the BatchNorm+ReLU that produced x (the previous fused
-        # block's bn3), or None -- this block's backward computes its statistics
+        # block's bn3), or None -- this block's backward computes its statistics.
+        # pend: the previous block's bn3 apply, deferred into this block's conv1 (x is its
+        # still-unwritten output buffer); defer: leave this block's own bn3 apply to the next.
         ctx.prev_src = prev_src
         ds = blk.downsample
-        z1, y1, s1 = _conv_bn(blk.conv1, blk.bn1, x)
-        z2, y2, s2 = _conv_bn(blk.conv2, blk.bn2, y1)
+        fold = config.get("CLOUD_AMD_BN_FOLD_FWD")
+        if pend is not None:
+            z1, part1 = _fold_conv(blk.conv1, pend["z"], pend["ss"], x, pend["mask"], res=pend["res"],
+                                   res_ss=pend["res_ss"])
+            y1, st1, m1 = raw.bn_fwd(z1, blk.bn1.weight, blk.bn1.bias, blk.bn1.running_mean, blk.bn1.running_var,
+                                     blk.bn1.eps, blk.bn1.momentum, blk.bn1.relu, partials=part1, keep_mask=True)
+            s1 = (st1, m1)
+        else:
+            z1, y1, s1 = _conv_bn(blk.conv1, blk.bn1, x)
+        c2, c3 = blk.conv2, blk.conv3
+        N, H2, W2 = x.shape[0], raw.out_hw(x.shape[1], 3, c2.stride, 1), raw.out_hw(x.shape[2], 3, c2.stride, 1)
+        if fold and not raw.uses_prw(N * H2 * W2, c3.cout, c2.cout):
+            # bn2 + ReLU applied in conv3's operand fetch (y2 written once, by that GEMM)
+            part2 = raw.conv_stats_buffer(y1.shape, c2.weight, c2.stride, c2.padding, x.device)
+            z2 = raw.conv_fwd(y1, c2.weight, c2.stride, c2.padding, stats=part2)
+            st2 = _bn_stats(blk.bn2, z2, part2)
+            y2 = torch.empty_like(z2)
+            m2 = torch.empty((z2.numel() // z2.shape[-1], z2.shape[-1] // 8), dtype=torch.uint8, device=x.device)
+            s2 = (st2, m2)
+            C2 = z2.shape[-1]
+            z3_part = _fold_conv(c3, z2, st2[2 * C2:4 * C2], y2, m2)
+        else:
+            z2, y2, s2 = _conv_bn(blk.conv2, blk.bn2, y1)
+            z3_part = None
         if ds is not None:
             # projection shortcut: its BN is folded into bn3's apply (statistics only here;
             # the shortcut BN output is never written)
@@ -127,17 +165,38 @@ class _BottleneckFn(torch.autograd.Function):
             st_d = raw.bn_fwd_stats(zd, bnd.weight, bnd.bias, bnd.running_mean, bnd.running_var, bnd.eps,
                                     bnd.momentum, part_d)
             sd = (st_d, None)
-            c3, bn3 = blk.conv3, blk.bn3
-            part3 = raw.conv_stats_buffer(y2.shape, c3.weight, c3.stride, c3.padding, x.device)
-            z3 = raw.conv_fwd(y2, c3.weight, c3.stride, c3.padding, stats=part3)
+            bn3 = blk.bn3
+            if z3_part is not None:
+                z3, part3 = z3_part
+            else:
+                part3 = raw.conv_stats_buffer(y2.shape, c3.weight, c3.stride, c3.padding, x.device)
+                z3 = raw.conv_fwd(y2, c3.weight, c3.stride, c3.padding, stats=part3)
             C3 = c3.cout
-            out, st3, mask3 = raw.bn_fwd(z3, bn3.weight, bn3.bias, bn3.running_mean, bn3.running_var, bn3.eps,
-                                         bn3.momentum, bn3.relu, residual=zd, partials=part3, keep_mask=True,
-                                         residual_ss=st_d[2 * C3:4 * C3])
-            s3 = (st3, mask3)
+            res, res_ss = zd, st_d[2 * C3:4 * C3]
         else:
             zd, sd = None, None
-            z3, out, s3 = _conv_bn(blk.conv3, blk.bn3, y2, residual=x)
+            bn3 = blk.bn3
+            if z3_part is not None:
+                z3, part3 = z3_part
+            else:
+                part3 = raw.conv_stats_buffer(y2.shape, c3.weight, c3.stride, c3.padding, x.device)
+                z3 = raw.conv_fwd(y2, c3.weight, c3.stride, c3.padding, stats=part3)
+            C3 = c3.cout
+            res, res_ss = x, None
+        if defer:
+            # bn3 (+ residual) + ReLU is applied by the next block's conv1 operand fetch, which
+            # also writes `out` and the ReLU mask: only the statistics here
+            st3 = _bn_stats(bn3, z3, part3)
+            out = torch.empty_like(z3)
+            mask3 = torch.empty((z3.numel() // C3, C3 // 8), dtype=torch.uint8, device=x.device)
+            blk._ca_pending = {"z": z3, "res": res, "ss": st3[2 * C3:4 * C3], "res_ss": res_ss, "mask": mask3}
+        else:
+            out, st3, mask3 = raw.bn_fwd(z3, bn3.weight, bn3.bias, bn3.running_mean, bn3.running_var, bn3.eps,
+                                         bn3.momentum, bn3.relu, residual=res, partials=part3, keep_mask=True,
+                                         residual_ss=res_ss)
+        s3 = (st3, mask3)
+        if ds is None:
+            sd = None
         ctx.blk = blk
         (s1, m1), (s2, m2), (s3, m3) = s1, s2, s3
         ctx.save_for_backward(x, z1, y1, z2, y2, z3, s1, m1, s2, m2, s3, m3,
@@ -201,8 +260,27 @@ class _BottleneckFn(torch.autograd.Function):
         # it in conv1's dgrad epilogue (res=), projection blocks in the shortcut BN backward
         gate_res = m3 is not None
         p3, p_short = _take(dout) if epi else (None, None)
-        dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=not gate_res, partials=p3)
-        dy2, p2, _ = dgrad(blk.conv3, dz3, y2.shape, (z2, m2))
+        fold = epi and config.get("CLOUD_AMD_BN_FOLD")
+
+        def bn_coef(bn, z, st, partials):
+            """BN backward finalize only: dgamma / dbeta into the arena, [A | B | D] for the
+            apply that runs in the consuming dgrad GEMM's operand fetch (ca_gemm_xa.h)."""
+            C = z.shape[-1]
+            coef = raw.bn_bwd_coef(C, z.numel() // C, bn.weight, st, partials, dgamma=bn.weight.grad,
+                                   dbeta=bn.bias.grad, accumulate=1)
+            ddp.notify_grad_ready(bn.weight)
+            ddp.notify_grad_ready(bn.bias)
+            return coef
+
+        if fold and p3 is not None and gate_res:
+            # bn3's backward apply folded into conv3's input-gradient GEMM: dz3 is produced in
+            # its operand fetch (and written once, for the weight gradient), never read back
+            coef3 = bn_coef(blk.bn3, z3, s3, p3)
+            dz3, dres = torch.empty_like(z3), None
+            dy2, p2 = raw.conv1x1_dgrad_bnbwd(dout, z3, m3, coef3, blk.conv3.weight, dz3, bn=(z2, m2))
+        else:
+            dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=not gate_res, partials=p3)
+            dy2, p2, _ = dgrad(blk.conv3, dz3, y2.shape, (z2, m2))
         wgrad(blk.conv3, dz3, y2)
         del dz3
         dz2, _ = bn_back(blk.bn2, dy2, z2, (s2, m2), partials=p2)
@@ -210,8 +288,14 @@ class _BottleneckFn(torch.autograd.Function):
         dy1, p1, _ = dgrad(blk.conv2, dz2, y1.shape, (z1, m1))
         wgrad(blk.conv2, dz2, y1)
         del dz2
-        dz1, _ = bn_back(blk.bn1, dy1, z1, (s1, m1), partials=p1)
-        del dy1, p1
+        coef1 = None
+        if fold and p1 is not None:
+            coef1 = bn_coef(blk.bn1, z1, s1, p1)  # bn1's apply runs in conv1's dgrad below
+            dz1 = torch.empty_like(z1)
+        else:
+            dz1, _ = bn_back(blk.bn1, dy1, z1, (s1, m1), partials=p1)
+            del dy1
+        del p1
         if ds is not None:
             zd, sd = saved[12], saved[13]
             if gate_res:
@@ -228,8 +312,17 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             dx = dres  # identity gradient; conv1's input gradient is summed into it below
         # the last write of dx: its epilogue sees the complete block-input gradient
-        _, p_prev, p_prev2 = dgrad(blk.conv1, dz1, x.shape, ctx.prev_src, out=dx, beta=1.0,
-                                   res=(dout, m3) if (gate_res and ds is None) else None)
+        res1 = (dout, m3) if (gate_res and ds is None) else None
+        if coef1 is not None:
+            bn_src = ctx.prev_src
+            if bn_src is not None and res1 is None:
+                bn_src = bn_src[:2]
+            r = raw.conv1x1_dgrad_bnbwd(dy1, z1, m1, coef1, blk.conv1.weight, dz1, out=dx, beta=1.0, bn=bn_src,
+                                        res=res1)
+            del dy1
+            p_prev, p_prev2 = (None, None) if bn_src is None else (r[1], r[2] if len(r) > 2 else None)
+        else:
+            _, p_prev, p_prev2 = dgrad(blk.conv1, dz1, x.shape, ctx.prev_src, out=dx, beta=1.0, res=res1)
         del dout
         if p_prev is not None:
             _park(dx, p_prev, p_prev2)
@@ -243,10 +336,27 @@ class _BottleneckFn(torch.autograd.Function):
         return (dx, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
 
-def bottleneck_forward(blk, x):
+def bottleneck_forward(blk, x, next_blk=None):
+    """Run ``blk`` as one autograd node.  ``next_blk``: the fused block that will consume this
+    block's output next (ResNet.forward passes it): this block's bn3 apply is then left to that
+    block's conv1 (CLOUD_AMD_BN_FOLD_FWD), which writes the output tensor returned here."""
     prev = getattr(x, "_ca_bn_src", None) if config.get("CLOUD_AMD_BN_BWD_EPILOGUE") else None
-    out = _BottleneckFn.apply(x, blk, prev, *block_params(blk))
+    pend = x.__dict__.pop("_ca_pending", None)
+    defer = (next_blk is not None and config.get("CLOUD_AMD_BN_FOLD_FWD") and not blk._forward_hooks
+             and not next_blk._forward_pre_hooks and getattr(next_blk, "fused_block", False)
+             and can_fuse(next_blk, x) and raw.is_gemm_conv(next_blk.conv1.weight, next_blk.conv1.stride,
+                                                            next_blk.conv1.padding))
+    out = _BottleneckFn.apply(x, blk, prev, pend, defer, *block_params(blk))
     src = blk.__dict__.pop("_ca_out_src", None)
     if src is not None:
         out._ca_bn_src = src  # (z3, mask3): the next fused block computes bn3's backward statistics
+    pending = blk.__dict__.pop("_ca_pending", None)
+    if pending is not None:
+        out._ca_pending = pending  # `out` is written by next_blk's conv1
     return out
+
+
+def check_not_pending(x):
+    """A tensor whose BN apply was deferred to a fused consumer must never reach another op."""
+    if "_ca_pending" in getattr(x, "__dict__", {}):
+        raise RuntimeError("internal error: a deferred BatchNorm output reached a non-fused consumer")

@@ -40,9 +40,10 @@ class Bottleneck(nn.Module):
                 "bn": BatchNormAct(cout, relu=False, device=device),
             })
 
-    def forward(self, x):
+    def forward(self, x, next_block=None):
         if self.fused_block and fused_block.can_fuse(self, x):
-            return fused_block.bottleneck_forward(self, x)
+            return fused_block.bottleneck_forward(self, x, next_block)
+        fused_block.check_not_pending(x)
         identity = x
         fs = self.fused_stats
         if self.downsample is not None:
@@ -85,7 +86,10 @@ class ResNet(nn.Module):
             if self.stem_cin != self.in_channels:
                 x = torch.nn.functional.pad(x, (0, self.stem_cin - self.in_channels))
             x = self._stem_tail(self.conv1(x, stats=True))
-        x = self.layers(x)
+        blocks = list(self.layers)
+        for i, blk in enumerate(blocks):
+            # a fused block hands its bn3 apply to the next fused block's conv1 (fused_block)
+            x = blk(x, blocks[i + 1] if i + 1 < len(blocks) else None)
         return self.fc(self.pool(x))
 
     def _stem_tail(self, out):

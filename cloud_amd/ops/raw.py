@@ -201,6 +201,103 @@ def conv_wgrad(dy, x, w_shape, stride, padding, out, beta=1.0, blocks=None):
     return out
 
 
+# ------------------------------------------- BN folded into the consuming 1x1 GEMM
+XA_BN_RELU, XA_BN_RES_RELU, XA_BN_BWD, XA_BN_RESBN_RELU = 0, 1, 2, 3
+
+
+def conv1x1_dgrad_bnbwd(dy, z, mask, coef, w, side, out=None, beta=0.0, bn=None, res=None):
+    """Input gradient of a 1x1 convolution (``w`` [Cout, 1, 1, Cin]) whose output gradient is
+    a BatchNorm(+ReLU) backward: ``dz = A*(dy * relu'(mask)) + B*z + D`` with ``coef`` = [A | B | D]
+    (:func:`bn_bwd_coef`).  ``dz`` is computed in the GEMM's operand fetch (``ca_gemm_xa.h``),
+    never read back; it is also written to ``side`` (the weight gradient's operand).  Epilogue
+    options and return values are :func:`conv_dgrad`'s (``bn=``, ``res=``, ``out=`` / ``beta``)."""
+    ext = _ext.load(required=True)
+    N, H, W, Cout = z.shape
+    Cin = w.shape[3]
+    M = N * H * W
+    x_shape = (N, H, W, Cin)
+    assert dy.shape == z.shape and side.shape == z.shape and w.shape[1:3] == (1, 1)
+    assert dy.is_contiguous() and z.is_contiguous() and side.is_contiguous() and coef.numel() == 3 * Cout
+    assert mask is None or mask.shape == (M, Cout // 8)
+    dx = out if out is not None else torch.empty(x_shape, dtype=torch.bfloat16, device=dy.device)
+    src, rmask, zp, mp, part, part2, z2p = 0, 0, 0, 0, None, None, 0
+    if res is not None:
+        src_t, rm_t = res
+        assert src_t.shape == dx.shape and src_t.is_contiguous()
+        src, rmask = src_t.data_ptr(), _ext.ptr(rm_t)
+    if bn is not None:
+        zb, mb = bn[0], bn[1]
+        assert zb.shape == dx.shape and zb.is_contiguous() and (mb is None or mb.shape == (M, Cin // 8))
+        part = torch.empty(((M + 127) // 128, 2, Cin), dtype=torch.float32, device=dy.device)
+        zp, mp = zb.data_ptr(), _ext.ptr(mb)
+        if len(bn) > 2 and bn[2] is not None:
+            assert res is not None, "second-BN statistics need the residual-gated (res=) form"
+            part2 = torch.empty_like(part)
+            z2p = bn[2].data_ptr()
+    cp = coef.data_ptr()
+    ext.gemm_xa(NN, XA_BN_BWD, dy.data_ptr(), z.data_ptr(), _ext.ptr(mask), cp, cp + 4 * Cout, cp + 8 * Cout, 0,
+                side.data_ptr(), 0, Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, M, Cin, Cout, float(beta), src, rmask,
+                zp, mp, _ext.ptr(part), z2p, _ext.ptr(part2), _st(dy.device))
+    _log("dgrad1x1_xa", M, Cin, Cout, _nb(dy, z, mask, side, w, dx) + (_nb(dx) if beta else 0))
+    if bn is None:
+        return dx
+    return (dx, part, part2) if (len(bn) > 2 and bn[2] is not None) else (dx, part)
+
+
+def conv1x1_fwd_bnapply(z, ss, w, side, mask_out, res=None, res_ss=None, stats=None):
+    """Forward 1x1 convolution (``w`` [Cout, 1, 1, Cin]) of a BatchNorm(+residual)+ReLU output
+    that is never written by a separate pass: ``y = relu(z*scale + shift [+ r | + bf16(r*rscale +
+    rshift)])`` is computed in the GEMM's operand fetch (``ca_gemm_xa.h``) from ``ss`` = [scale |
+    shift] (and ``res_ss`` for a projection shortcut's BN), and written once to ``side`` with its
+    ReLU bitmask ``mask_out`` ([M, Cin/8]) -- bit for bit what bn_fwd would have stored.
+    ``stats``: the BN-forward statistics partials of the output ([ceil(M/128)][2][Cout])."""
+    ext = _ext.load(required=True)
+    N, H, W, Cin = z.shape
+    Cout = w.shape[0]
+    M = N * H * W
+    assert w.shape[1:] == (1, 1, Cin) and z.is_contiguous() and side.shape == z.shape and side.is_contiguous()
+    assert ss.numel() == 2 * Cin and mask_out.shape == (M, Cin // 8)
+    mode, src1, c2, c3 = XA_BN_RELU, 0, 0, 0
+    if res is not None:
+        assert res.shape == z.shape and res.is_contiguous()
+        src1 = res.data_ptr()
+        mode = XA_BN_RES_RELU
+        if res_ss is not None:
+            assert res_ss.numel() == 2 * Cin
+            mode, c2, c3 = XA_BN_RESBN_RELU, res_ss.data_ptr(), res_ss.data_ptr() + 4 * Cin
+    assert stats is None or stats.shape == ((M + 127) // 128, 2, Cout)
+    y = torch.empty((N, H, W, Cout), dtype=torch.bfloat16, device=z.device)
+    sp = ss.data_ptr()
+    ext.gemm_xa(NT, mode, z.data_ptr(), src1, 0, sp, sp + 4 * Cin, c2, c3, side.data_ptr(), mask_out.data_ptr(), Cin,
+                w.data_ptr(), Cin, y.data_ptr(), Cout, M, Cout, Cin, 0.0, 0, 0, 0, 0, _ext.ptr(stats), 0, 0,
+                _st(z.device))
+    _log("fwd1x1_xa", M, Cout, Cin, _nb(z, res, side, mask_out, w, y))
+    return y
+
+
+def uses_prw(M, N, K):
+    """Whether a forward NT GEMM with statistics runs on the persistent resident-weight core
+    (its statistics partials are then one row per workgroup, not per 128 rows)."""
+    ext = _ext.load(required=True)
+    return ext.gemm_stat_rows(int(M), int(N), int(K), int(K), int(K), int(N)) != (M + 127) // 128
+
+
+def bn_bwd_coef(C, M, gamma, stats, partials, dgamma=None, dbeta=None, accumulate=0):
+    """BN backward statistics finalize only (no apply pass): dgamma / dbeta written (or
+    accumulated) from the dgrad epilogue's ``partials``; returns the [A | B | D] coefficients
+    of ``dz = A*g + B*z + D`` for :func:`conv1x1_dgrad_bnbwd`."""
+    ext = _ext.load(required=True)
+    dev = partials.device
+    assert partials.shape[1:] == (2, C)
+    coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
+    gws = torch.empty(_GWS_ROWS * 2 * C, dtype=torch.float32, device=dev) if partials.shape[0] > 64 else None
+    sp = stats.data_ptr()
+    ext.bn_bwd_partials(0, 0, 0, 0, int(M), int(C), partials.data_ptr(), partials.shape[0], _ext.ptr(gamma), sp,
+                        sp + 4 * C, 0, 0, _ext.ptr(dgamma), _ext.ptr(dbeta), coef.data_ptr(), _ext.ptr(gws),
+                        1 | (2 if accumulate else 0), _st(dev))
+    return coef
+
+
 # ------------------------------------------------------------------ batchnorm
 def bn_fwd_stats(x, gamma, beta, running_mean, running_var, eps, momentum, partials):
     """Training BN statistics only (no apply pass): returns stats[4C] = mean, rstd, scale,

@@ -37,6 +37,9 @@ long ca_conv_dgrad_stat_tiles(int, int, int, int, int);
 int ca_bn_fwd_partials_ex(const bf16_t*, const bf16_t*, const float*, bf16_t*, long, int, const float*, int,
                           const float*, const float*, float, float, float*, float*, float*, float*, float*, int,
                           uint8_t*, float*, hipStream_t);
+int ca_gemm_xa(int, int, const bf16_t*, const bf16_t*, const uint8_t*, const float*, const float*, const float*,
+               const float*, bf16_t*, uint8_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float, const bf16_t*,
+               const uint8_t*, const bf16_t*, const uint8_t*, float*, const bf16_t*, float*, hipStream_t);
 int ca_dgrad_gemm(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float, const bf16_t*,
                   const uint8_t*, const bf16_t*, const uint8_t*, float*, hipStream_t, const bf16_t*, float*);
 int ca_conv_dgrad_bnstats(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
@@ -196,6 +199,17 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("layout"), py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("beta"), py::arg("res"), py::arg("res_mask"), py::arg("z"),
         py::arg("mask"), py::arg("stats"), py::arg("s"), py::arg("z2") = 0, py::arg("stats2") = 0);
+  m.def("gemm_xa", [](int layout, int mode, u64 src0, u64 src1, u64 mask_in, u64 c0, u64 c1, u64 c2, u64 c3, u64 side,
+                      u64 mask_out, long lda, u64 B, long ldb, u64 C, long ldc, int M, int N, int K, float beta,
+                      u64 res, u64 res_mask, u64 z, u64 mask, u64 stats, u64 z2, u64 stats2, u64 s) {
+    check(ca_gemm_xa(layout, mode, P(const bf16_t*, src0), P(const bf16_t*, src1), P(const uint8_t*, mask_in),
+                     P(const float*, c0), P(const float*, c1), P(const float*, c2), P(const float*, c3),
+                     P(bf16_t*, side),
+                     P(uint8_t*, mask_out), lda, P(const bf16_t*, B), ldb, P(bf16_t*, C), ldc, M, N, K, beta,
+                     P(const bf16_t*, res), P(const uint8_t*, res_mask), P(const bf16_t*, z), P(const uint8_t*, mask),
+                     P(float*, stats), P(const bf16_t*, z2), P(float*, stats2), S(s)),
+          "gemm_xa");
+  });
   m.def("bn_fwd_partials_ex", [](u64 x, u64 res, u64 res_ss, u64 y, long M, int C, u64 parts, int nparts, u64 gamma,
                                  u64 beta, float eps, float momentum, u64 rm, u64 rv, u64 sm, u64 sr, u64 ss, int relu,
                                  u64 mask, u64 gws, u64 s) {

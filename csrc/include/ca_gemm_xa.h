@@ -1,0 +1,236 @@
+// GEMM core whose A operand is PRODUCED in the load path by a BatchNorm transform
+// (gfx950 / CDNA4): the ResNet-50 "BN folded into the consuming convolution" kernels.
+//
+//   C[M, N] = X(A-sources)[M, K] * B        X = per-element BN transform, per-K coefficients
+//
+// Why: in a bottleneck block every BatchNorm pass is a full read + write of an activation
+// tensor, and the 1x1 convolution that consumes its output reads it straight back.  Folding
+// the BN pass into the convolution's operand fetch removes that re-read (and a launch):
+//
+//   XA_BN_BWD       dz = A[k] * g + B[k] * z + D[k],  g = dy * relu'(mask)
+//                   the BN(+ReLU) backward apply (bn.hip bn_bwd_apply_kernel) feeding the
+//                   input-gradient GEMM of the 1x1 conv that produced z (conv3 / conv1 dgrad)
+//   XA_BN_RELU      y = relu(z * scale[k] + shift[k])                  (forward, bn -> conv)
+//   XA_BN_RES_RELU  y = relu(z * scale[k] + shift[k] + r)              (bn3 + identity residual)
+//   XA_BN_RESBN_RELU y = relu(z * scale[k] + shift[k] + bf16(r * rscale[k] + rshift[k]))
+//                   (bn3 + a projection shortcut whose own BN is applied on the fly, exactly
+//                   as bn.hip bn_apply_resbn_kernel)
+//
+// The transformed tile is ALSO written to global memory (`side`, plus the forward's ReLU
+// bitmask) by the blocks of the first N tile, so the tensors the rest of the step reads
+// (the weight gradient's operand, the backward's ReLU mask) exist exactly as the unfused
+// passes would have written them -- bit for bit: the arithmetic below is the BN kernels'.
+//
+// Pipeline (4 waves, 128 x BN tile, one LDS stage, several blocks per CU):
+//   * A is register-staged: the next K step's 16-B source chunks (and coefficients, mask
+//     bytes) are loaded into VGPRs while this step's MFMAs run, then transformed and written
+//     to LDS with the swizzle read_frag_sw expects (phys chunk = logical ^ (row & 7));
+//   * B (the weights, L2-resident) is register-staged the same way.  No LDS-DMA here: with
+//     a DMA in flight the compiler's waitcnt pass cannot tell which LDS bytes it writes and
+//     drains the A prefetch before the first LDS read of every step;
+//   * all loads and side stores are buffer operations with a range check (rows past M or K
+//     read zeros / are dropped), so no vector-memory operation sits behind a branch.
+// Epilogues are the shared gemm_epilogue (BN statistics, residual-gated beta, ...).
+#pragma once
+#include "ca_gemm_prw.h"
+
+namespace ca {
+
+enum XaMode { XA_BN_RELU = 0, XA_BN_RES_RELU = 1, XA_BN_BWD = 2, XA_BN_RESBN_RELU = 3 };
+
+struct XaParams {
+  const bf16_t* src0;      // z (forward) / dy (backward)                [M][K], row stride lda
+  const bf16_t* src1;      // residual r (XA_BN_RES_RELU) / z (XA_BN_BWD) [M][K], row stride lda
+  const uint8_t* mask_in;  // XA_BN_BWD: ReLU bitmask [M][K/8] or null (no ReLU)
+  const float* c0;         // scale (forward) / A (backward)  [K]
+  const float* c1;         // shift (forward) / B (backward)  [K]
+  const float* c2;         // D (backward) / rscale (XA_BN_RESBN_RELU) [K]
+  const float* c3;         // rshift (XA_BN_RESBN_RELU)                [K]
+  bf16_t* side;            // transformed A [M][K] (row stride lda), written by N tile 0; may be null
+  uint8_t* mask_out;       // forward: ReLU bitmask of the transformed A [M][K/8]; may be null
+};
+
+template <int XM>
+struct XaTraits {
+  static constexpr bool TWO = XM != XA_BN_RELU;        // second source tensor
+  static constexpr bool MASK_IN = XM == XA_BN_BWD;      // backward ReLU gate
+  static constexpr int NCOEF = XM == XA_BN_BWD ? 3 : (XM == XA_BN_RESBN_RELU ? 4 : 2);
+};
+
+template <int BM, int BN, bool B_KC, int EPI, int XM>
+__device__ __forceinline__ void mfma_gemm_xa(const CoreParams& P, const XaParams& X) {
+  constexpr int WM = 2, WN = 2, NT = 256;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;
+  constexpr int STAGE = A_ELEMS + B_ELEMS;
+  constexpr int EPI_LD = EpiLayout<BN>::LD;
+  constexpr int SMEM = (STAGE > BM * EPI_LD ? STAGE : BM * EPI_LD);
+  constexpr int CPA = A_ELEMS / 8 / NT;  // A chunks (16 B) per thread and K step
+  constexpr int CPB = B_ELEMS / 8 / NT;
+  constexpr int RSTEP = NT / 8;          // tile rows between a thread's A chunks
+  using T = XaTraits<XM>;
+  static_assert(A_ELEMS % (8 * NT) == 0 && B_ELEMS % (8 * NT) == 0, "tile chunks must divide threads");
+  __shared__ __attribute__((aligned(16))) short smem[SMEM];
+  short* const As = smem;
+  short* const Bs = smem + A_ELEMS;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = (P.N + BN - 1) / BN;
+  const BlkPos bp = blk_pos(P);
+  const int tm = bp.tile / tiles_n, tn = bp.tile % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = (P.K + BK - 1) / BK;
+  const int K8 = P.K >> 3;
+
+  // B: the whole weight matrix is one buffer resource (KC: [N][K] rows, NC: [K][N] rows);
+  // rows past its end read zeros.  A chunk's k / column beyond K / N only feeds products with
+  // a zero A element or output columns that are never stored.
+  const auto rbw = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(P.B), (short)0,
+                                                     (int)buf_span((long)(B_KC ? P.N : P.K) * P.ldb * 2), 0x00020000);
+  s8v bw[CPB];
+  auto b_coord = [&](int i, int& lrow, int& lcol) {  // chunk i of this thread in the B tile
+    const int c = tid + i * NT;
+    if constexpr (B_KC) {
+      lrow = c >> 3;                   // n
+      lcol = c & 7;                    // 8-k group
+    } else {
+      lrow = c / (BN / 8);             // k
+      lcol = c % (BN / 8);             // 8-n group
+    }
+  };
+
+  // A geometry: thread tid owns logical 8-channel group c8 = tid & 7 of rows (tid >> 3) + RSTEP i
+  const int arow = tid >> 3, c8 = tid & 7;
+  const long rows_left = (long)P.M - m0;
+  const uint32_t span = buf_span(rows_left * P.lda * 2);
+  const auto r0s = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X.src0 + (long)m0 * P.lda), (short)0,
+                                                     (int)span, 0x00020000);
+  const auto r1s = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>((T::TWO ? X.src1 : X.src0) + (long)m0 * P.lda), (short)0, (int)span, 0x00020000);
+  const uint32_t mspan = buf_span(rows_left * K8);
+  const auto rms = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(X.mask_in ? X.mask_in + (long)m0 * K8 : reinterpret_cast<const uint8_t*>(ca_zero16)),
+      (short)0, X.mask_in ? (int)mspan : 0, 0x00020000);
+  // side outputs: buffer stores through resources that are empty (num_records 0: every store
+  // dropped) unless this block writes them -- every thread issues the same vector-memory
+  // stream whatever its tile, so the compiler's and our counted waits stay exact (a store
+  // behind a branch makes the waitcnt pass drain to vmcnt(0) before the LDS reads)
+  const bool write_side = tn == 0;
+  const auto rside = __builtin_amdgcn_make_buffer_rsrc(
+      write_side && X.side ? X.side + (long)m0 * P.lda : const_cast<bf16_t*>(ca_zero16), (short)0,
+      write_side && X.side ? (int)span : 0, 0x00020000);
+  const auto rmout = __builtin_amdgcn_make_buffer_rsrc(
+      write_side && X.mask_out ? X.mask_out + (long)m0 * K8 : reinterpret_cast<uint8_t*>(ca_zero16), (short)0,
+      write_side && X.mask_out ? (int)mspan : 0, 0x00020000);
+
+  s8v a0[CPA], a1[CPA];
+  uint32_t mb[CPA];
+  f4v cf[T::NCOEF][2];
+
+  auto gload = [&](int t) {
+    const int k = t * BK + 8 * c8;
+    const int kc = k < P.K ? k : P.K - 8;  // K tail: a valid address, zeroed after the transform
+#pragma unroll
+    for (int i = 0; i < CPA; ++i) {
+      const uint32_t off = (uint32_t)(((long)(arow + i * RSTEP) * P.lda + kc) * 2);
+      a0[i] = __builtin_bit_cast(s8v, __builtin_amdgcn_raw_buffer_load_b128(r0s, (int)off, 0, 0));
+      if constexpr (T::TWO) a1[i] = __builtin_bit_cast(s8v, __builtin_amdgcn_raw_buffer_load_b128(r1s, (int)off, 0, 0));
+      if constexpr (T::MASK_IN)
+        mb[i] = __builtin_amdgcn_raw_buffer_load_b8(rms, (int)((arow + i * RSTEP) * K8 + (kc >> 3)), 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < CPB; ++i) {
+      int lr, lc;
+      b_coord(i, lr, lc);
+      const long off = B_KC ? (long)(n0 + lr) * P.ldb + t * BK + 8 * lc
+                            : (long)(t * BK + lr) * P.ldb + (n0 + 8 * lc < P.N ? n0 + 8 * lc : P.N - 8);
+      bw[i] = __builtin_bit_cast(s8v, __builtin_amdgcn_raw_buffer_load_b128(rbw, (int)(off * 2), 0, 0));
+    }
+    const float* cs[4] = {X.c0, X.c1, X.c2, X.c3};
+#pragma unroll
+    for (int q = 0; q < T::NCOEF; ++q) {
+      cf[q][0] = *reinterpret_cast<const f4v*>(cs[q] + kc);
+      cf[q][1] = *reinterpret_cast<const f4v*>(cs[q] + kc + 4);
+    }
+  };
+
+  auto transform_store = [&](int t) {
+    const int k = t * BK + 8 * c8;
+    const bool kok = k < P.K;
+#pragma unroll
+    for (int i = 0; i < CPA; ++i) {
+      const int row = arow + i * RSTEP;
+      s8v o;
+      uint32_t bits = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c0 = cf[0][j >> 2][j & 3], c1 = cf[1][j >> 2][j & 3];
+        float v;
+        if constexpr (XM == XA_BN_BWD) {
+          // bn_bwd_apply_kernel: d gated by the ReLU bit, then A*d + B*x + D
+          float d = bf2f((bf16_t)a0[i][j]);
+          if (X.mask_in) d = ((mb[i] >> j) & 1u) ? d : 0.f;
+          const float c2 = cf[2][j >> 2][j & 3];
+          v = c0 * d + c1 * bf2f((bf16_t)a1[i][j]) + c2;
+        } else {
+          // bn_apply_kernel<true, RES>: z*scale + shift (+ r), ReLU, bit = y > 0
+          float z = bf2f((bf16_t)a0[i][j]) * c0 + c1;
+          if constexpr (XM == XA_BN_RES_RELU) z += bf2f((bf16_t)a1[i][j]);
+          if constexpr (XM == XA_BN_RESBN_RELU) {
+            // the shortcut BN output rounded to bf16 as if stored (bn_apply_resbn_kernel)
+            const float idn = bf2f(f2bf(bf2f((bf16_t)a1[i][j]) * cf[2][j >> 2][j & 3] + cf[3][j >> 2][j & 3]));
+            z = bf2f((bf16_t)a0[i][j]) * c0 + c1 + idn;
+          }
+          z = fmaxf(z, 0.f);
+          bits |= (z > 0.f ? 1u : 0u) << j;
+          v = z;
+        }
+        o[j] = kok ? (short)f2bf(v) : (short)0;
+      }
+      *reinterpret_cast<s8v*>(As + row * BK + ((c8 ^ (row & 7)) << 3)) = o;
+      // rows past M and the K tail land beyond the resource's range: dropped by the hardware
+      const uint32_t soff = kok ? (uint32_t)(((long)row * P.lda + k) * 2) : span;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rside, (int)soff, 0, 0);
+      if constexpr (XM != XA_BN_BWD)
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bits, rmout, kok ? (int)(row * K8 + (k >> 3)) : (int)mspan, 0,
+                                             0);
+    }
+#pragma unroll
+    for (int i = 0; i < CPB; ++i) {  // B chunks at the swizzled slots read_frag_sw reads
+      int lr, lc;
+      b_coord(i, lr, lc);
+      short* dst = B_KC ? Bs + lr * BK + ((lc ^ (lr & 7)) << 3) : Bs + lr * BN + ((lc ^ nc_swz<BN>(lr)) << 3);
+      *reinterpret_cast<s8v*>(dst) = bw[i];
+    }
+  };
+
+  f4v acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) gload(0);
+  for (int t = 0; t < nk; ++t) {
+    transform_store(t);            // the stage is free: every wave passed the closing barrier of t - 1
+    if (t + 1 < nk) gload(t + 1);  // next step's operands in flight during this step's MFMAs
+    lgkm_wait0();
+    bar256();
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = read_frag_sw<BM, true>(As, wm * (BM / WM) + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = read_frag_sw<BN, B_KC>(Bs, wn * (BN / WN) + j * 16, kk, lane);
+      mfma_acc<FM, FN>(acc, af, bfr);
+    }
+    lgkm_wait0();
+    bar256();
+  }
+  vm_wait<0>();
+  gemm_epilogue<BM, BN, WM, WN, EPI, SMEM, 1>(P, acc, smem, m0, n0, tm, tid);
+}
+
+}  // namespace ca

@@ -621,7 +621,8 @@ int ca_bn_bwd(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16
 
 // Backward from the [nparts][2][C] partials [sum dz | sum dz*x] written by a dgrad
 // GEMM's BN-statistics epilogue (ca_gemm_bf16_bnstats / ca_conv_dgrad_bnstats): no
-// reduction pass over dy and x; finalize (+group reduce) then the apply pass.
+// reduction pass over dy and x; finalize (+group reduce) then the apply pass -- or, with
+// dx == null, the finalize only (dgamma / dbeta and the [A | B | D] coefficients).
 int ca_bn_bwd_partials(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16_t* x, long M, int C,
                        const float* partials, int nparts, const float* gamma, const float* save_mean,
                        const float* save_rstd, bf16_t* dx, bf16_t* dres, float* dgamma, float* dbeta,
@@ -645,6 +646,7 @@ int ca_bn_bwd_partials(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, c
   bn_bwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(fin, nfin, 2L * C, (long)C, M, C, gamma, save_mean, save_rstd,
                                                          dgamma, dbeta, coef, accum, 1);
   CA_LAUNCH_CHECK();
+  if (!dx) return 0;  // finalize only: the apply runs in the consuming GEMM's operand fetch (ca_gemm_xa)
   if (relu && dres) bn_bwd_apply_kernel<true, true><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
   else if (relu) bn_bwd_apply_kernel<true, false><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
   else if (dres) bn_bwd_apply_kernel<false, true><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);

@@ -11,7 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "ca_gemm_prw.h"
+#include "ca_gemm_xa.h"
 
 namespace {
 using namespace ca;
@@ -304,6 +304,27 @@ static bool want_small_n(const CoreParams& p, int splits) {
   return p.N <= 64 || (tile_balance(t128) < 0.8 && tile_balance(t64) > tile_balance(t128) + 0.1);
 }
 
+// Transform-A GEMMs (csrc/include/ca_gemm_xa.h): the BN pass that feeds a 1x1 convolution
+// runs in that convolution's operand fetch.
+template <int BM, int BN, bool BKC, int EPI, int XM>
+__global__ void __launch_bounds__(256) xa_gemm_kernel(CoreParams P, XaParams X) {
+  mfma_gemm_xa<BM, BN, BKC, EPI, XM>(P, X);
+}
+
+template <bool LB, int EPI, int XM>
+int xa_launch(const CoreParams& p0, const XaParams& x, hipStream_t s) {
+  CoreParams p = p0;
+  p.split_xcd = 0;
+  const int tm = (p.M + 127) / 128;
+  if (want_small_n(p, 1)) {
+    xa_gemm_kernel<128, 64, LB, EPI, XM><<<tm * ((p.N + 63) / 64), 256, 0, s>>>(p, x);
+  } else {
+    xa_gemm_kernel<128, 128, LB, EPI, XM><<<tm * ((p.N + 127) / 128), 256, 0, s>>>(p, x);
+  }
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
 template <int EPI>
 int dispatch(int layout, const CoreParams& p, int splits, hipStream_t s) {
   const bool small_n = want_small_n(p, splits);
@@ -453,6 +474,55 @@ int ca_gemm_ex(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb,
   p.dact_src = dact_src;
   p.ld_aux = ld_aux;
   return dispatch<EPI_BF16>(layout, p, 1, s);
+}
+
+// Transform-A GEMM (ca_gemm_xa.h).  layout 0 (NT, forward 1x1 conv: B = W [N][K]) with
+// mode XA_BN_RELU / XA_BN_RES_RELU / XA_BN_RESBN_RELU and the BN-forward statistics epilogue
+// when `stats`;
+// layout 1 (NN, input gradient: B = W [K][N]) with mode XA_BN_BWD and the dgrad epilogues of
+// ca_dgrad_gemm (BN-backward statistics bnz/bnmask/stats, residual-gated beta res_src/res_mask,
+// second BN bnz2/stats2).  The A operand is X(src0, src1, mask_in; c0, c1, c2) [M][K] with row
+// stride lda; `side` / `mask_out` receive the transformed A and (forward) its ReLU bitmask.
+int ca_gemm_xa(int layout, int mode, const bf16_t* src0, const bf16_t* src1, const uint8_t* mask_in,
+               const float* c0, const float* c1, const float* c2, const float* c3, bf16_t* side, uint8_t* mask_out,
+               long lda,
+               const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N, int K, float beta,
+               const bf16_t* res_src, const uint8_t* res_mask, const bf16_t* bnz, const uint8_t* bnmask,
+               float* stats, const bf16_t* bnz2, float* stats2, hipStream_t s) {
+  if (M <= 0 || N < 8 || N % 8 != 0 || K < 8 || K % 8 != 0 || lda % 8 != 0 || !src0 || !c0 || !c1) return -1;
+  if ((mode == XA_BN_RES_RELU && !src1) || (mode == XA_BN_BWD && (!src1 || !c2))) return -1;
+  if (mode == XA_BN_RESBN_RELU && (!src1 || !c2 || !c3)) return -1;
+  if ((bnz && !stats) || (bnz2 && (!bnz || !stats2 || !res_src))) return -1;
+  CoreParams p = base_params(src0, lda, B, ldb, C, ldc, M, N, K);
+  p.beta = beta;
+  XaParams x{src0, src1, mask_in, c0, c1, c2, c3, side, mask_out};
+  if (layout == 0) {
+    if (beta != 0.f || res_src || bnz) return -1;
+    p.stats = stats;
+    if (mode == XA_BN_RELU)
+      return stats ? xa_launch<true, EPI_BF16_ST, XA_BN_RELU>(p, x, s) : xa_launch<true, EPI_BF16, XA_BN_RELU>(p, x, s);
+    if (mode == XA_BN_RES_RELU)
+      return stats ? xa_launch<true, EPI_BF16_ST, XA_BN_RES_RELU>(p, x, s)
+                   : xa_launch<true, EPI_BF16, XA_BN_RES_RELU>(p, x, s);
+    if (mode == XA_BN_RESBN_RELU)
+      return stats ? xa_launch<true, EPI_BF16_ST, XA_BN_RESBN_RELU>(p, x, s)
+                   : xa_launch<true, EPI_BF16, XA_BN_RESBN_RELU>(p, x, s);
+    return -2;
+  }
+  if (layout != 1 || mode != XA_BN_BWD) return -2;
+  p.res_src = res_src;
+  p.res_mask = res_mask;
+  if (!bnz) return xa_launch<false, EPI_BF16, XA_BN_BWD>(p, x, s);
+  p.stats = stats;
+  p.bnz = bnz;
+  p.bnmask = bnmask;
+  if (bnz2) {
+    p.bnz2 = bnz2;
+    p.stats2 = stats2;
+    return xa_launch<false, EPI_BF16_BNR2, XA_BN_BWD>(p, x, s);
+  }
+  if (res_src) return xa_launch<false, EPI_BF16_BNR, XA_BN_BWD>(p, x, s);
+  return xa_launch<false, EPI_BF16_BN, XA_BN_BWD>(p, x, s);
 }
 
 int ca_gemm_splitk_effective(int K, int splits) {

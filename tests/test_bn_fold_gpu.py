@@ -1,0 +1,132 @@
+"""BatchNorm folded into the consuming 1x1 convolution (csrc/include/ca_gemm_xa.h).
+
+* Kernel level: ``raw.conv1x1_dgrad_bnbwd`` against a plain PyTorch fp32 reference of the
+  same op -- dz = A*(dy*relu') + B*z + D, dx = dz W -- for the plain, BN-statistics and
+  residual-gated epilogues, including M and channel counts that are not tile multiples.
+* Model level: a ResNet trained a few steps with ``CLOUD_AMD_BN_FOLD=1`` against ``=0``
+  (the separate BN apply pass): the fused kernels use the BN kernels' arithmetic and the
+  GEMM's accumulation order, so the gradients must be BITWISE equal.
+"""
+import os
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _mask_bits(m):
+    """[M, C] bool -> [M, C/8] uint8 bitmask (bit j = channel 8c+j)."""
+    M, C = m.shape
+    w = (1 << torch.arange(8, device=m.device, dtype=torch.int32))
+    return (m.view(M, C // 8, 8).int() * w).sum(-1).to(torch.uint8)
+
+
+@pytest.mark.parametrize("M,Cout,Cin", [(4096, 256, 64), (1000, 128, 64), (777, 64, 256), (2048, 512, 128),
+                                        (300, 72, 40)])
+@pytest.mark.parametrize("epi", ["plain", "bn", "res"])
+def test_dgrad_bnbwd_vs_fp32(M, Cout, Cin, epi):
+    from cloud_amd.ops import raw
+
+    torch.manual_seed(M + Cout)
+    dy = torch.randn(M, Cout, device=DEV).to(torch.bfloat16)
+    z = torch.randn(M, Cout, device=DEV).to(torch.bfloat16)
+    act = torch.rand(M, Cout, device=DEV) > 0.4
+    mask = _mask_bits(act)
+    coef = torch.randn(3 * Cout, device=DEV) * torch.tensor([1.0, 0.1, 0.01], device=DEV).repeat_interleave(Cout)
+    w = (torch.randn(Cout, 1, 1, Cin, device=DEV) * 0.05).to(torch.bfloat16)
+    A, B, D = coef[:Cout], coef[Cout:2 * Cout], coef[2 * Cout:]
+    g = dy.float() * act.float()
+    dz_ref = A * g + B * z.float() + D
+    dx_ref = dz_ref.to(torch.bfloat16).float() @ w.view(Cout, Cin).float()
+    side = torch.empty(1, 1, M, Cout, device=DEV, dtype=torch.bfloat16)
+    shp = lambda t: t.view(1, 1, M, -1)  # noqa: E731  (NHWC view of the row-major matrix)
+    kw = {}
+    zb = torch.randn(M, Cin, device=DEV).to(torch.bfloat16)
+    act_b = torch.rand(M, Cin, device=DEV) > 0.5
+    src = torch.randn(M, Cin, device=DEV).to(torch.bfloat16)
+    act_r = torch.rand(M, Cin, device=DEV) > 0.5
+    if epi == "bn":
+        kw["bn"] = (shp(zb), _mask_bits(act_b))
+    if epi == "res":
+        kw.update(res=(shp(src), _mask_bits(act_r)), beta=1.0, out=torch.empty(1, 1, M, Cin, device=DEV,
+                                                                                dtype=torch.bfloat16))
+    r = raw.conv1x1_dgrad_bnbwd(shp(dy), shp(z), mask, coef, w, side, **kw)
+    dx = r[0] if isinstance(r, tuple) else r
+    assert rel(side.view(M, Cout), dz_ref) < 1e-2
+    want = dx_ref + (src.float() * act_r.float() if epi == "res" else 0.0)
+    assert rel(dx.view(M, Cin), want) < 2e-2, rel(dx.view(M, Cin), want)
+    if epi == "bn":
+        part = r[1]
+        gd = dx.view(M, Cin).float() * act_b.float()
+        s = part[:, 0].sum(0)
+        q = part[:, 1].sum(0)
+        assert rel(s, gd.sum(0)) < 1e-3 and rel(q, (gd * zb.float()).sum(0)) < 1e-3
+
+
+def _train(fold, steps=3):
+    os.environ["CLOUD_AMD_BN_FOLD"] = "1" if fold else "0"
+    os.environ["CLOUD_AMD_BN_FOLD_FWD"] = "1" if fold else "0"
+    from cloud_amd.models.resnet import ResNet
+    from cloud_amd.ops import softmax_cross_entropy
+    from cloud_amd.optim import SGD
+
+    torch.manual_seed(0)
+    m = ResNet((2, 2, 2, 1), num_classes=10, stem_channels_pad=5, device=DEV)
+    opt = SGD(m, learning_rate=0.05, momentum=0.9)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    X = torch.randn(steps, 16, 64, 64, 3, device=DEV, generator=g).to(torch.bfloat16)
+    Y = torch.randint(0, 10, (steps, 16), device=DEV, generator=g)
+    grads = []
+    for i in range(steps):
+        opt.zero_grad()
+        loss, _ = softmax_cross_entropy(m(X[i]), Y[i], denom=16)
+        loss.backward()
+        torch.cuda.synchronize()
+        grads.append([a.grad.detach().clone() for a in opt.arenas])
+        opt.step()
+    torch.cuda.synchronize()
+    return grads, [a.master.detach().clone() for a in opt.arenas]
+
+
+def test_resnet_bn_fold_bitwise(monkeypatch):
+    from cloud_amd.models import fused_block
+    from cloud_amd.ops import raw
+
+    calls = {"bwd": 0, "fwd": 0}
+    real_b, real_f = raw.conv1x1_dgrad_bnbwd, raw.conv1x1_fwd_bnapply
+
+    def counting_b(*a, **k):
+        calls["bwd"] += 1
+        return real_b(*a, **k)
+
+    def counting_f(*a, **k):
+        calls["fwd"] += 1
+        return real_f(*a, **k)
+
+    monkeypatch.setattr(raw, "conv1x1_dgrad_bnbwd", counting_b)
+    monkeypatch.setattr(raw, "conv1x1_fwd_bnapply", counting_f)
+    try:
+        g1, w1 = _train(True)
+        n_fold = dict(calls)
+        g0, w0 = _train(False)
+    finally:
+        os.environ.pop("CLOUD_AMD_BN_FOLD", None)
+        os.environ.pop("CLOUD_AMD_BN_FOLD_FWD", None)
+    # 7 blocks: bwd folds bn3 (6 blocks get their partials from the next block) and bn1 (7);
+    # fwd folds bn3 into the next conv1 (6 hand-offs) and bn2 into conv3 (all but layer 1's prw)
+    assert n_fold["bwd"] > 0 and n_fold["fwd"] > 0, n_fold
+    assert calls == n_fold, "the fused paths must run with the fold on and only then"
+    for step, (a, b) in enumerate(zip(g1, g0)):
+        for ai, (x, y) in enumerate(zip(a, b)):
+            assert torch.equal(x, y), (step, ai, rel(x, y))
+    for x, y in zip(w1, w0):
+        assert torch.equal(x, y)
+    assert fused_block is not None
