@@ -7,7 +7,13 @@ all sharing one study through the local study service).
     python bench/tuner_8trials.py --workers 8     # fixed worker count
 
 Reports trials/hour and time-to-best (seconds from start until the trial that
-ends up best completed).  Synthetic MNIST (no network).  The CNN is the
+ends up best completed).  Synthetic MNIST (no network).
+
+``--pool 1`` (default): the scheduler runs on a warm ``WorkerPool`` -- worker processes
+that imported torch / cloud_amd once and serve study after study.  The pool is started
+first (``pool_warm_s``), then ``--studies`` studies run back to back on it; ``value`` /
+``time_to_best_s`` are the first warm study's, ``cold_*`` include the pool's start-up.
+``--pool 0``: one process per worker per study (spawned, gated standbys).  The CNN is the
 reference's ``mnist_example_using_fit.py`` model with tuned filters / dense
 width / learning rate.
 """
@@ -72,24 +78,56 @@ def main():
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--train", type=int, default=8192)
     ap.add_argument("--timeline", type=int, default=1, help="per-worker phase marks + per-trial spans in the JSON")
+    ap.add_argument("--pool", type=int, default=1, help="1: warm WorkerPool reused across studies")
+    ap.add_argument("--studies", type=int, default=2, help="studies run back to back on the pool")
     args = ap.parse_args()
     from cloud_amd.core.topology import visible_gpu_count
-    from cloud_amd.tuner.scheduler import TrialScheduler, study_report
+    from cloud_amd.tuner.scheduler import TrialScheduler, WorkerPool
 
     n_gpus = visible_gpu_count()
     workers = args.workers if args.workers else (None if n_gpus else 2)
     study_dir = tempfile.mkdtemp(prefix="tuner_bench_")
-    env = {"STUDY_ID": "mnist_cnn_8", "STUDY_DIR": study_dir, "BENCH_TRIALS": str(args.trials),
-           "BENCH_EPOCHS": str(args.epochs), "BENCH_TRAIN": str(args.train), "PYTHONPATH": ROOT}
-    os.environ.update(env)
-    t0 = time.time()
-    # workers=None: probe one worker per GPU, then pack more per GPU from the first trial's
-    # measured peak HBM (no more workers than trials)
-    sched = TrialScheduler("bench.tuner_8trials:worker", n_gpus=n_gpus, workers=workers, env=env,
-                           max_workers=args.trials, timeline=bool(args.timeline))
-    res = sched.run(timeout=3000)
-    wall = time.time() - t0
-    sid = next(d for d in os.listdir(study_dir) if d.endswith("mnist_cnn_8"))  # CloudTuner prefixes the id
+    base = {"STUDY_DIR": study_dir, "BENCH_TRIALS": str(args.trials), "BENCH_EPOCHS": str(args.epochs),
+            "BENCH_TRAIN": str(args.train), "PYTHONPATH": ROOT}
+    os.environ.update(base)
+    t_cold = time.time()
+    pool, pool_warm = None, None
+    if args.pool:
+        pool = WorkerPool(min(args.trials, args.workers or args.trials), preload=["bench.tuner_8trials"], env=base)
+        pool_warm = pool.wait_ready()
+    runs = []
+    try:
+        for k in range(args.studies if args.pool else 1):
+            sid = "mnist_cnn_8" if k == 0 else "mnist_cnn_8_%d" % k
+            env = dict(base, STUDY_ID=sid)
+            os.environ.update(env)
+            t0 = time.time()
+            # workers=None: probe one worker per GPU, then pack more per GPU from the first
+            # trial's measured peak HBM (no more workers than trials)
+            sched = TrialScheduler("bench.tuner_8trials:worker", n_gpus=n_gpus, workers=workers, env=env,
+                                   max_workers=args.trials, timeline=bool(args.timeline), pool=pool)
+            res = sched.run(timeout=3000)
+            runs.append((sid, t0, time.time() - t0, res))
+    finally:
+        if pool is not None:
+            pool.close()
+    outs = [_summary(study_dir, sid, t0, wall, res, n_gpus, args) for sid, t0, wall, res in runs]
+    out = outs[0]
+    out["pool"] = bool(args.pool)
+    if args.pool:
+        out["pool_warm_s"] = round(pool_warm, 2)
+        out["cold_wall_s"] = round(runs[0][1] + runs[0][2] - t_cold, 2)
+        out["cold_time_to_best_s"] = (round(out["time_to_best_s"] + runs[0][1] - t_cold, 2)
+                                      if out["time_to_best_s"] is not None else None)
+        out["studies"] = [{k: o[k] for k in ("value", "wall_s", "time_to_best_s", "trials_completed",
+                                             "best_val_accuracy")} for o in outs]
+    print(json.dumps(out), flush=True)
+
+
+def _summary(study_dir, sid_suffix, t0, wall, res, n_gpus, args):
+    from cloud_amd.tuner.scheduler import study_report
+
+    sid = next(d for d in os.listdir(study_dir) if d.endswith(sid_suffix))  # CloudTuner prefixes the id
     trials = study_report(study_dir, sid)
     done = [t for t in trials if t["state"] == "COMPLETED" and t.get("finalMeasurement")]
 
@@ -118,7 +156,7 @@ def main():
             "trials": [{"client": t.get("clientId"), "start": round(t["startTs"] - t0, 2),
                         "end": round(t["endTs"] - t0, 2)} for t in trials if "startTs" in t and "endTs" in t],
         }
-    print(json.dumps(out), flush=True)
+    return out
 
 
 if __name__ == "__main__":

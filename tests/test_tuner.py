@@ -402,3 +402,39 @@ def test_reported_footprint_includes_validation_arrays(tmp_path, monkeypatch):
     tuner.search(x, y, epochs=1, batch_size=32, validation_data=(xv, yv))
     got = json.load(open(out))["peak_gb"]
     assert abs(got - (1.0 + (xv.nbytes + yv.nbytes) / 2 ** 30)) < 1e-9
+
+
+def test_worker_pool_reused_across_studies(tmp_path):
+    """Warm pool: the workers import once, then run two studies back to back (the second
+    starts its trials with no interpreter start / import on its critical path)."""
+    import sys
+
+    from cloud_amd.tuner.scheduler import WorkerPool
+
+    sys.path.insert(0, os.path.join(HERE, "data"))
+    pool = WorkerPool(3, preload=["tuner_worker"], env={"PYTHONPATH": os.path.join(HERE, "data"),
+                                                        "OMP_NUM_THREADS": "1"})
+    try:
+        warm_s = pool.wait_ready()
+        assert warm_s > 0
+        pids = [p.pid for p in pool._procs]
+        walls = []
+        for sid in ("pool_a", "pool_b"):
+            env = {"STUDY_ID": sid, "STUDY_DIR": str(tmp_path), "MAX_TRIALS": "6"}
+            sched = TrialScheduler("tuner_worker:run", n_gpus=0, workers=3, env=env, pool=pool, timeline=True)
+            res = sched.run(timeout=600)
+            assert res["pool"] and res["exit_codes"] == [0, 0, 0], res
+            walls.append(res["wall_s"])
+            with open(tmp_path / ("CloudTuner_study_" + sid) / "study.json") as f:
+                trials = json.load(f)["trials"]
+            assert len(trials) == 6 and all(t["state"] == "COMPLETED" for t in trials)
+            assert all("imported" not in m for m in res["timeline"].values())  # no per-study import
+        assert [p.pid for p in pool._procs] == pids and all(p.is_alive() for p in pool._procs)
+        # measured packing on a pool: one probe, then the packing wave on idle warm workers
+        env = {"STUDY_ID": "pool_c", "STUDY_DIR": str(tmp_path), "MAX_TRIALS": "6", "FAKE_FOOTPRINT_GB": "1.0"}
+        sched = TrialScheduler("tuner_worker:run", n_gpus=0, env=env, pool=pool, hbm_gb=4.0, max_workers=3)
+        res = sched.run(timeout=600)
+        assert res["footprint_gb"] == 1.0 and res["workers"] == 2 and res["exit_codes"] == [0, 0]
+    finally:
+        pool.close()
+    assert all(not p.is_alive() for p in pool._procs)
