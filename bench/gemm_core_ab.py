@@ -17,7 +17,7 @@ from cloud_amd.ops import raw  # noqa: E402
 SHAPES = [  # (M, N, K, tag)
     (8192, 2304, 768, "bert_qkv"), (8192, 768, 768, "bert_o"), (8192, 3072, 768, "bert_ffn1"),
     (8192, 768, 3072, "bert_ffn2"), (50176, 1024, 256, "rn_l3_c3"), (12544, 2048, 512, "rn_l4_c3"),
-    (200704, 128, 512, "rn_l2_c1"), (4096, 4096, 4096, "square4k"),
+    (200704, 128, 512, "rn_l2_c1"), (4096, 4096, 4096, "square4k"), (8192, 8192, 8192, "square8k"),
 ]
 
 
@@ -35,7 +35,8 @@ def timeit(fn, iters=20, warm=3):
 
 
 def main():
-    core = os.environ.get("CLOUD_AMD_GEMM_CORE", "glds")
+    os.environ.setdefault("CLOUD_AMD_GEMM_LIB", "never")  # the in-tree core, not the plain-GEMM library policy
+    core = os.environ.get("CLOUD_AMD_GEMM_CORE", "default")
     torch.manual_seed(0)
     out = {"core": core, "shapes": []}
     for M, N, K, tag in SHAPES:

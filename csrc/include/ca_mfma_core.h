@@ -348,16 +348,21 @@ __device__ __forceinline__ void mfma_acc(f4v (&acc)[FM][FN], const bf16x8 (&af)[
 // storing any (batched LDS latency; dense GEMMs only -- the conv loaders' registers leave
 // no room, see docs/performance.md)
 template <int BM, int BN, int WM, int WN, int EPI, int SMEM_SHORTS, int EPF = 1, int FM = BM / WM / 16,
-          int FN = BN / WN / 16>
+          int FN = BN / WN / 16, bool QUAD = false>
 __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM][FN], short* smem, int m0, int n0,
                                               int tm, int tid) {
   constexpr int NT = WM * WN * 64;
   using EL = EpiLayout<BN>;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  // accumulator layout (mfma_acc): acc[i][j][r] = C[rbase + 16 i][cbase + 16 j + r]
-  const int rbase = wm * (BM / WM) + (lane & 15);
-  const int cbase = wn * (BN / WN) + 4 * (lane >> 4);
+  // accumulator layout (mfma_acc): acc[i][j][r] = C[frow(i)][fcol(j) + r].  Default: a wave owns
+  // one (BM/WM) x (BN/WN) block, frow(i) = rbase + 16 i.  QUAD (the 8-phase 256 core): the tile
+  // is four quadrants, each split over all waves -- a wave owns one (BM/2/WM) x (BN/2/WN) block
+  // per quadrant, fragments i < FM/2 / j < FN/2 in the top / left quadrants.
+  const int rbase = QUAD ? wm * (BM / 2 / WM) + (lane & 15) : wm * (BM / WM) + (lane & 15);
+  const int cbase = QUAD ? wn * (BN / 2 / WN) + 4 * (lane >> 4) : wn * (BN / WN) + 4 * (lane >> 4);
+  auto frow = [&](int i) { return QUAD ? rbase + (i / (FM / 2)) * (BM / 2) + (i % (FM / 2)) * 16 : rbase + i * 16; };
+  auto fcol = [&](int j) { return QUAD ? cbase + (j / (FN / 2)) * (BN / 2) + (j % (FN / 2)) * 16 : cbase + j * 16; };
   if constexpr (EPI == EPI_F32_PARTIAL) {
     // N % 8 == 0 and ldc % 4 == 0 (slabs are [M][N]): a column group is whole or absent
     const BlkPos bp = blk_pos(P);
@@ -366,7 +371,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int gm = m0 + rbase + i * 16, gn = n0 + cbase + j * 16;
+        const int gm = m0 + frow(i), gn = n0 + fcol(j);
         if (gm < P.M && gn < P.N) *reinterpret_cast<f4v*>(Cp + (long)gm * P.ldc + gn) = acc[i][j];
       }
     // (an in-launch combine -- the last-arriving split summing all slabs behind an agent-scope
@@ -379,7 +384,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
       for (int j = 0; j < FN; ++j) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int gn = n0 + cbase + j * 16 + r;
+          const int gn = n0 + fcol(j) + r;
           const float bv = gn < P.N ? P.bias[gn] : 0.f;
 #pragma unroll
           for (int i = 0; i < FM; ++i) acc[i][j][r] += bv;
@@ -393,7 +398,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
         s4v pk;
 #pragma unroll
         for (int r = 0; r < 4; ++r) pk[r] = (short)f2bf(acc[i][j][r]);
-        *reinterpret_cast<s4v*>(Cs + EL::idx(rbase + i * 16, cbase + j * 16)) = pk;
+        *reinterpret_cast<s4v*>(Cs + EL::idx(frow(i), fcol(j))) = pk;
       }
     __syncthreads();
     const bool fx = P.act != ACT_NONE || P.dact_src != nullptr || P.preact != nullptr;

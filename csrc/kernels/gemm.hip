@@ -11,6 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "ca_gemm256p8.h"
 #include "ca_gemm_xa.h"
 
 namespace {
@@ -61,22 +62,35 @@ __global__ void __launch_bounds__(512) dense_gemm_256_kernel(CoreParams P) {
   mfma_gemm_256<LA, LB, EPI>(P);
 }
 
+// The 256 x 256 x 64 core with the 4-phase-per-K-tile interleave (csrc/include/ca_gemm256p8.h).
+template <template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
+__global__ void __launch_bounds__(512) dense_gemm_256p8_kernel(CoreParams P) {
+  mfma_gemm_256p8<LA, LB, EPI>(P);
+}
+
 // CLOUD_AMD_GEMM_CORE selects the core (A/B comparisons; ca_gemm_set_core overrides it):
 // 0 "reg" = register-staged, 1 "glds" = glds single stage (4 waves) only, 2 "glds8" = glds
 // double-buffered (8 waves), 3 (default) = glds plus the 256 x 256 ring core for large
 // GEMMs (use_256 below; 4096^3: 904 -> 1126-1148 TF/s, 8192^3: 845 -> 1166-1175), 4 "v256"
 // = the 256 core for every GEMM with M, N >= 256 (tests).
+// 5 "p8" = glds plus the 8-phase 256 x 256 x 64 core (ca_gemm256p8.h) for large GEMMs, 6 "vp8"
+// = the 8-phase core for every GEMM with M, N >= 256 (tests).
 int g_core_kind = -1;
 int core_kind() {
   if (g_core_kind < 0) {
     const char* e = getenv("CLOUD_AMD_GEMM_CORE");
     g_core_kind = !e ? 3
                      : (e[0] == 'r' ? 0
-                                    : (strcmp(e, "glds8") == 0 ? 2
-                                                              : (strcmp(e, "glds") == 0 ? 1 : (strcmp(e, "v256") == 0 ? 4 : 3))));
+                        : strcmp(e, "glds8") == 0 ? 2
+                        : strcmp(e, "glds") == 0  ? 1
+                        : strcmp(e, "v256") == 0  ? 4
+                        : strcmp(e, "p8") == 0    ? 5
+                        : strcmp(e, "vp8") == 0   ? 6
+                                                  : 3);
   }
   return g_core_kind;
 }
+bool core_p8() { return core_kind() == 5 || core_kind() == 6; }
 bool use_glds() { return core_kind() != 0; }
 
 // Persistent resident-weight core (csrc/include/ca_gemm_prw.h) for the small-K forward 1x1
@@ -228,8 +242,8 @@ static double tile_balance(long tiles) {
 // nearly full round of 256 x 256 blocks (ops/raw.py wgrad_into: BERT's FFN / QKV weight
 // gradients = 36 x 7 / 27 x 9 blocks).
 static bool use_256(const CoreParams& p, int splits) {
-  if (core_kind() == 4) return p.M >= 256 && p.N >= 256;
-  if (core_kind() != 3 || p.M < 256 || p.N < 256 || p.k_per_split < 512) return false;
+  if (core_kind() == 4 || core_kind() == 6) return p.M >= 256 && p.N >= 256;
+  if ((core_kind() != 3 && core_kind() != 5) || p.M < 256 || p.N < 256 || p.k_per_split < 512) return false;
   const long t = (long)((p.M + 255) / 256) * ((p.N + 255) / 256) * splits;
   if (splits > 1 && t >= 224 && t <= 256) return true;
   return t >= 256 && (tile_balance(t) >= 0.999 || (t >= 512 && tile_balance(t) >= 0.85));
@@ -249,6 +263,18 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
     if (use_256(p, splits)) {
       const int t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
       constexpr bool AK = GA<BM, 1, 256>::KC, BKC = GB<BN, 1, 256>::KC;
+      if (core_p8()) {
+        if constexpr (AK && BKC)
+          dense_gemm_256p8_kernel<GDenseKC, GDenseKC, EPI><<<dim3(t256, 1, splits), 512, 0, s>>>(p);
+        else if constexpr (AK && !BKC)
+          dense_gemm_256p8_kernel<GDenseKC, GDenseNC, EPI><<<dim3(t256, 1, splits), 512, 0, s>>>(p);
+        else if constexpr (!AK && !BKC)
+          dense_gemm_256p8_kernel<GDenseNC, GDenseNC, EPI><<<dim3(t256, 1, splits), 512, 0, s>>>(p);
+        else
+          return -2;
+        CA_LAUNCH_CHECK();
+        return 0;
+      }
       if constexpr (AK && BKC)
         dense_gemm_256_kernel<GDenseKC32, GDenseKC32, EPI><<<dim3(t256, 1, splits), 512, 0, s>>>(p);
       else if constexpr (AK && !BKC)
@@ -366,7 +392,7 @@ int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long l
 // the previous one.
 int ca_gemm_set_core(int kind) {
   const int prev = core_kind();
-  if (kind >= 0 && kind <= 4) g_core_kind = kind;
+  if (kind >= 0 && kind <= 6) g_core_kind = kind;
   return prev;
 }
 

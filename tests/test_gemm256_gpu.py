@@ -1,5 +1,6 @@
-"""The 256 x 256 ring GEMM core (csrc/include/ca_gemm256.h mfma_gemm_256; forced on every
-GEMM with M, N >= 256 by core kind 4 = CLOUD_AMD_GEMM_CORE=v256) against a plain PyTorch fp32
+"""The 256 x 256 GEMM cores -- the ring core (csrc/include/ca_gemm256.h, core kind 4 = v256)
+and the 8-phase core (csrc/include/ca_gemm256p8.h, core kind 6 = vp8), each forced on every
+GEMM with M, N >= 256 -- against a plain PyTorch fp32
 GEMM of the same bf16 operands: forward (NT), input grad (NN), weight grad (TN, split-K fp32
 slabs), the fused bias + activation and BN-statistics epilogues, ragged M / N / K (partial
 tiles, K tails read as zeros through the buffer range check), one to many K tiles -- plus
@@ -10,13 +11,15 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def core256():
+@pytest.fixture(params=[4, 6], ids=["ring256", "p8"])
+def core256(request):
+    """Force a 256 x 256 core on every GEMM with M, N >= 256: 4 = the ring core (v256),
+    6 = the 8-phase core (vp8, csrc/include/ca_gemm256p8.h)."""
     from cloud_amd.ops import _ext
 
     ext = _ext.load(required=True)
-    prev = ext.gemm_set_core(4)  # v256: force the 256 core
-    yield
+    prev = ext.gemm_set_core(request.param)
+    yield request.param
     ext.gemm_set_core(prev)
 
 
