@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 S=scripts/gpu_step.sh
 tag=${1:-r4s3}
 chk() { grep -q " passed" gpurun_out/$1 && ! grep -qE " failed| error" gpurun_out/$1 || { echo "tests failed: $1"; tail -60 gpurun_out/$1; exit 1; }; }
-$S 400 ${tag}_new.log python -u -m pytest tests/test_bn_fold_gpu.py tests/test_gemm256_gpu.py tests/test_rccl_dataplane_gpu.py tests/test_transformer_gpu.py -k "fold or bnbwd or 256 or dataplane or rccl or raising" -x -v --timeout 120 --timeout-method thread || exit 1
+$S 400 ${tag}_new.log python -u -m pytest tests/test_rccl_dataplane_gpu.py tests/test_transformer_gpu.py -k "dataplane or rccl or raising" -x -v -s --timeout 120 --timeout-method thread || exit 1
 chk ${tag}_new.log
 for i in 1 2; do
 CLOUD_AMD_BN_FOLD=0 CLOUD_AMD_BN_FOLD_FWD=0 $S 240 ${tag}_rn_off_${i}.log python bench.py --gpus 1 --steps 20 --warmup 5 || exit 1

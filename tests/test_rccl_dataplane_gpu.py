@@ -154,5 +154,6 @@ def test_rccl_data_plane_world1_forced_multirank(tmp_path, transport, wire):
     assert math.isfinite(s["allreduce_ms"]) and math.isfinite(s["exposed_comm_ms"])
     assert s["allreduce_ms"] > 0.0
     assert 0.0 <= s["exposed_comm_ms"] <= r["ms_per_step"], (s, r["ms_per_step"])
-    # no host synchronisation added by the data plane
-    assert r["syncs_dp"] == r["syncs_ref"], (r["syncs_dp"], r["syncs_ref"])
+    # no host synchronisation added by the data plane (the reference's one-off first-use sync
+    # of a kernel library may show up on its side only)
+    assert r["syncs_dp"] <= r["syncs_ref"], (r["syncs_dp"], r["syncs_ref"])
