@@ -95,6 +95,12 @@ _VARS = [
     Var("CLOUD_AMD_BN_FOLD_FWD", bool, True, "ResNet block forward: bn2's apply runs in conv3's operand fetch and "
         "bn3's (+ residual) in the next block's conv1 (ca_gemm_xa.h); the applied tensors are written once, by "
         "those GEMMs", "ops"),
+    Var("CLOUD_AMD_BN_FOLD_MAX_N", int, 4096, "BN fold sites kept: only GEMMs with K >= 2N and N <= this "
+        "(ResNet-50: bn3 -> conv3 dgrad and bn3 -> next conv1, every stage); the transform-A core re-runs the "
+        "BN transform per N tile and cannot pipeline a one-K-tile GEMM, so the short-K sites (bn2 -> conv3, "
+        "bn1 -> conv1 dgrad) measured slower than the separate pass (docs/performance.md, round 4)", "ops"),
+    Var("CLOUD_AMD_BN_FOLD_ALL", bool, False, "fold every BN site regardless of CLOUD_AMD_BN_FOLD_MAX_N (tests, A/B)",
+        "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "
         "second HIP stream, overlapping the memory-bound BN/LN/dgrad chain", "ops"),
     Var("CLOUD_AMD_BN_BWD_EPILOGUE", bool, True, "ResNet block backward: BatchNorm-backward statistics from the "

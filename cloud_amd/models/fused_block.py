@@ -114,6 +114,16 @@ def _bn_stats(bn, z, part, res_ss=None):
     return raw.bn_fwd_stats(z, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, bn.momentum, part)
 
 
+def _fold_site(K, N):
+    """Whether a BN apply is folded into a 1x1 GEMM of reduction K and N output channels.
+    The transform-A core (ca_gemm_xa.h) repeats the BN transform for every N tile and has no
+    operand pipeline for a single K tile; measured on MI355X (ResNet-50, b1024) only the long-K,
+    narrow-N sites beat the separate BN pass (docs/performance.md, round 4)."""
+    if config.get("CLOUD_AMD_BN_FOLD_ALL"):
+        return True
+    return K >= 2 * N and N <= config.get("CLOUD_AMD_BN_FOLD_MAX_N")
+
+
 def _fold_conv(conv, src, ss, side, mask, res=None, res_ss=None):
     """1x1 forward conv whose input BN(+residual)+ReLU apply runs in its operand fetch; the
     applied input is written once to ``side`` (+ ReLU bitmask ``mask``).  Returns (z, partials)."""
@@ -143,7 +153,7 @@ class _BottleneckFn(torch.autograd.Function):
             z1, y1, s1 = _conv_bn(blk.conv1, blk.bn1, x)
         c2, c3 = blk.conv2, blk.conv3
         N, H2, W2 = x.shape[0], raw.out_hw(x.shape[1], 3, c2.stride, 1), raw.out_hw(x.shape[2], 3, c2.stride, 1)
-        if fold and not raw.uses_prw(N * H2 * W2, c3.cout, c2.cout):
+        if fold and not raw.uses_prw(N * H2 * W2, c3.cout, c2.cout) and _fold_site(c2.cout, c3.cout):
             # bn2 + ReLU applied in conv3's operand fetch (y2 written once, by that GEMM)
             part2 = raw.conv_stats_buffer(y1.shape, c2.weight, c2.stride, c2.padding, x.device)
             z2 = raw.conv_fwd(y1, c2.weight, c2.stride, c2.padding, stats=part2)
@@ -272,7 +282,7 @@ class _BottleneckFn(torch.autograd.Function):
             ddp.notify_grad_ready(bn.bias)
             return coef
 
-        if fold and p3 is not None and gate_res:
+        if fold and p3 is not None and gate_res and _fold_site(blk.conv3.cout, blk.conv3.cin):
             # bn3's backward apply folded into conv3's input-gradient GEMM: dz3 is produced in
             # its operand fetch (and written once, for the weight gradient), never read back
             coef3 = bn_coef(blk.bn3, z3, s3, p3)
@@ -289,7 +299,7 @@ class _BottleneckFn(torch.autograd.Function):
         wgrad(blk.conv2, dz2, y1)
         del dz2
         coef1 = None
-        if fold and p1 is not None:
+        if fold and p1 is not None and _fold_site(blk.conv1.cout, blk.conv1.cin):
             coef1 = bn_coef(blk.bn1, z1, s1, p1)  # bn1's apply runs in conv1's dgrad below
             dz1 = torch.empty_like(z1)
         else:
@@ -344,7 +354,8 @@ def bottleneck_forward(blk, x, next_blk=None):
     pend = x.__dict__.pop("_ca_pending", None)
     defer = (next_blk is not None and config.get("CLOUD_AMD_BN_FOLD_FWD") and not blk._forward_hooks
              and not next_blk._forward_pre_hooks and getattr(next_blk, "fused_block", False)
-             and can_fuse(next_blk, x) and raw.is_gemm_conv(next_blk.conv1.weight, next_blk.conv1.stride,
+             and can_fuse(next_blk, x) and _fold_site(next_blk.conv1.cin, next_blk.conv1.cout)
+             and raw.is_gemm_conv(next_blk.conv1.weight, next_blk.conv1.stride,
                                                             next_blk.conv1.padding))
     out = _BottleneckFn.apply(x, blk, prev, pend, defer, *block_params(blk))
     src = blk.__dict__.pop("_ca_out_src", None)

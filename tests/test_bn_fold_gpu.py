@@ -74,6 +74,7 @@ def test_dgrad_bnbwd_vs_fp32(M, Cout, Cin, epi):
 def _train(fold, steps=3):
     os.environ["CLOUD_AMD_BN_FOLD"] = "1" if fold else "0"
     os.environ["CLOUD_AMD_BN_FOLD_FWD"] = "1" if fold else "0"
+    os.environ["CLOUD_AMD_BN_FOLD_ALL"] = "1"  # every site, not only the ones the default policy keeps
     from cloud_amd.models.resnet import ResNet
     from cloud_amd.ops import softmax_cross_entropy
     from cloud_amd.optim import SGD
@@ -122,6 +123,7 @@ def test_resnet_bn_fold_bitwise(monkeypatch):
     finally:
         os.environ.pop("CLOUD_AMD_BN_FOLD", None)
         os.environ.pop("CLOUD_AMD_BN_FOLD_FWD", None)
+        os.environ.pop("CLOUD_AMD_BN_FOLD_ALL", None)
     # 7 blocks: bwd folds bn3 (6 blocks get their partials from the next block) and bn1 (7);
     # fwd folds bn3 into the next conv1 (6 hand-offs) and bn2 into conv3 (all but layer 1's prw)
     assert n_fold["bwd"] > 0 and n_fold["fwd"] > 0, n_fold
