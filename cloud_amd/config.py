@@ -52,8 +52,9 @@ _VARS = [
     Var("CLOUD_AMD_OPS", str, "native", "'native' HIP kernels or 'torch' stock ops", "ops"),
     Var("CLOUD_AMD_GEMM", str, "native", "dense GEMMs: 'native' or 'torch'", "ops"),
     Var("CLOUD_AMD_CONV", str, "native", "convolutions: 'native' or 'torch'", "ops"),
-    Var("CLOUD_AMD_GEMM_CORE", str, "auto", "GEMM core: 'auto' (128x128 LDS-DMA core plus the 256x256 ring core "
-        "for large GEMMs), 'glds' (128 core only), 'v256' (256 core whenever M, N >= 256), 'glds8', 'reg' "
+    Var("CLOUD_AMD_GEMM_CORE", str, "auto", "GEMM core: 'auto' (128x128 LDS-DMA core plus the 256x256 two-phase "
+        "core of ca_gemm256p8.h for large GEMMs), 'glds_ring' (128 core plus the 256x256 ring core), 'glds' (128 "
+        "core only), 'vp8' / 'v256' (the two-phase / ring 256 core whenever M, N >= 256), 'glds8', 'reg' "
         "(register staging)", "ops"),
     Var("CLOUD_AMD_WGRAD_BLOCKS", int, 512, "convolution weight gradients: split-K so that about this many "
         "workgroups run (tiles x splits); fewer splits = less fp32 slab traffic, more = fuller CUs", "ops"),

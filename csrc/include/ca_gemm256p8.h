@@ -1,43 +1,48 @@
-// 256 x 256 x 64 MFMA GEMM core with a 4-phase-per-K-tile (8 phases per two K tiles)
-// interleave over a double-buffered LDS-DMA image (gfx950 / CDNA4).
+// 256 x 256 x 64 MFMA GEMM core over a double-buffered LDS-DMA image, two staggered wave
+// groups, counted vmcnt (gfx950 / CDNA4).
 //
 //   C[M,N] = sum_k A(m,k) * B(k,n)     bf16 operands, fp32 accumulation
 //
 // Geometry: one 512-thread workgroup per CU (2 waves per SIMD), K tile 64 deep.  The LDS
 // holds two K tiles, each as four 16 KB half tiles: A top / bottom (128 rows x 64 k) and
-// B left / right (128 columns x 64 k) -- 128 KB.  The C tile is four 128 x 128 quadrants;
-// each PHASE computes one quadrant over one K tile with all 8 waves: waves 2 (M) x 4 (N),
-// a 64 x 32 block per wave = 16 v_mfma_f32_16x16x32_bf16.  Quadrant order (0,0) (0,1)
-// (1,1) (1,0) lets each phase read only ONE new half tile of fragments (A 8 or B 4
-// ds_read_b128 per wave; the other operand's fragments stay in registers).
+// B left / right (128 columns x 64 k) -- 128 KB.  Waves are 2 (M) x 4 (N); every phase is
+// {fragment reads; s_waitcnt lgkmcnt(0); LDS-DMA of restaged half tiles (2 pieces per thread
+// each); counted vmcnt} barrier {MFMAs at s_setprio 1} barrier, and waves 4-7 run one barrier
+// behind waves 0-3, so on every SIMD one wave multiplies while its partner reads LDS and
+// issues DMA (MI355X_MICROARCH.md "Two waves per SIMD").  Because each phase retires its own
+// LDS reads before its first barrier, a half tile is restaged ONE phase after its last read;
+// a half tile's data is waited for (counted vmcnt) before the first barrier of a phase that
+// precedes the phase reading it (cdna_hip_programming.md section 5, RAW / WAR rules with the
+// stagger).  The loop never drains vmcnt to 0.
 //
-// Per phase: {fragment reads; one half tile of LDS-DMA (2 pieces per thread); [counted
-// vmcnt]} barrier {lgkmcnt(0); 16 MFMAs at s_setprio 1} barrier.  Half tiles are restaged
-// two phases after their last read and retired by ONE counted vmcnt(4) per K tile (two half
-// tiles stay in flight; the loop never drains), read one phase after the wait:
+// PHASES = 2 (default): one C HALF per phase, 32 MFMAs per wave between barriers.
+//   K tile t, buffer b = t & 1     reads (buffer b)                 DMA issued
+//     P1 top half    (qm 0)        A top, B left, B right           A bottom of t+1 (buffer b^1)
+//     P2 bottom half (qm 1)        A bottom (B held in registers)   A top, B left, B right of t+2
+//                                                                   (buffer b); vmcnt(6) -> t+1 complete
+// PHASES = 4: one C QUADRANT per phase, 16 MFMAs per wave between barriers (the layout of
+//   cdna_hip_programming.md "The 256^2 8-phase template"): quadrant order (0,0) (0,1) (1,1)
+//   (1,0), one new half tile of fragments per phase, A bottom / B left of t+1 and A top /
+//   B right of t+2 restaged two phases after their last reads, vmcnt(4) once per K tile.
 //
-//   K tile t, buffer b = t & 1      reads (buffer b)       DMA issued
-//     q0 quadrant (0,0)              A top, B left          A bottom of t+1   (buffer b^1)
-//     q1 quadrant (0,1)              B right                B left   of t+1   (buffer b^1)
-//     q2 quadrant (1,1)              A bottom               A top    of t+2   (buffer b)
-//     q3 quadrant (1,0)              B left                 B right  of t+2   (buffer b); vmcnt(4) -> t+1 complete
-//
-// Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave multiplies while its
-// partner reads LDS and issues DMA (MI355X_MICROARCH.md "Two waves per SIMD"); the two-phase
-// restage distance keeps the write-after-read order safe under that stagger.  This is the
-// structure of cdna_hip_programming.md section 5 "The 256^2 8-phase template" (measured there
-// at ~1.33 PF/s at 4096^3 and ~1.47 PF/s at 8192^3 on random operands), written for this
-// repo's loaders (GDenseKC / GDenseNC half tiles, XOR-swizzled lane-linear images) and its
-// shared epilogue (QUAD fragment mapping).
+// Measured on MI355X, one process, random operands (bin/gemm_bench, profiles/r4_gemm/):
+// PHASES 2 reaches 1,178-1,228 TF/s at 4096^3 and 1,245-1,260 at 8192^3 (MFMA busy 0.70),
+// PHASES 4 1,050-1,110 / 1,168-1,190 (busy 0.61), the ring core of ca_gemm256.h 1,097-1,158 /
+// 1,172-1,183 (busy 0.65).  Variants that waited for each half tile one phase before it is
+// read (four half tiles in flight) or rotated A bottom over three slots (144 KB) gave the
+// half-tile loads more latency budget and were NOT faster: the barrier count per MFMA, not the
+// load latency, is what the extra MFMAs per phase buy back.  Epilogue: the shared
+// gemm_epilogue with the quadrant fragment mapping (QUAD).
 #pragma once
 #include "ca_gemm256.h"
 
 namespace ca {
 
-template <template <int, int, int> class LAT, template <int, int, int> class LBT, int EPI>
+template <template <int, int, int> class LAT, template <int, int, int> class LBT, int EPI, int PHASES = 2>
 __device__ __forceinline__ void mfma_gemm_256p8(const CoreParams& P) {
+  static_assert(PHASES == 2 || PHASES == 4, "2 or 4 phases per K tile");
   constexpr int BM = 256, BN = 256, NT = 512, HR = 128;
-  constexpr int HT = HR * BK;  // shorts per half tile
+  constexpr int HT = HR * BK;   // shorts per half tile
   constexpr int SMEM = 8 * HT;  // 2 buffers x 4 half tiles = 128 KB
   static_assert(SMEM >= BM * EpiLayout<BN>::LD, "C staging must fit the operand image");
   using LA = LAT<HR, 2, NT>;
@@ -86,21 +91,23 @@ __device__ __forceinline__ void mfma_gemm_256p8(const CoreParams& P) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 af[4][2], bfr[2][2];  // this phase's fragments: A 4 rows x 2 k halves, B 2 cols x 2 k halves
+  // fragments: A 4 rows x 2 k halves of one A half tile; B 2 cols x 2 k halves of the left
+  // (bfl) and right (bfr) B half tiles (PHASES 4 uses bfl only)
+  bf16x8 af[4][2], bfl[2][2], bfr[2][2];
   auto read_a = [&](const short* half) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) af[i][kk] = read_frag_sw<HR, A_KC>(half, wm * 64 + i * 16, kk * 32, lane);
   };
-  auto read_b = [&](const short* half) {
+  auto read_b = [&](bf16x8 (&f)[2][2], const short* half) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bfr[j][kk] = read_frag_sw<HR, B_KC>(half, wn * 32 + j * 16, kk * 32, lane);
+      for (int kk = 0; kk < 2; ++kk) f[j][kk] = read_frag_sw<HR, B_KC>(half, wn * 32 + j * 16, kk * 32, lane);
   };
+  // C quadrant (qm, qn) from af and bfl: 16 MFMAs
   auto mfma_q = [&](int qm, int qn) {
-    lgkm_wait0();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
@@ -109,59 +116,121 @@ __device__ __forceinline__ void mfma_gemm_256p8(const CoreParams& P) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[qm * 4 + i][qn * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfl[j][kk], af[i][kk], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // C half qm (quadrants (qm,0), (qm,1)) from af, bfl and bfr: 32 MFMAs
+  auto mfma_h = [&](int qm) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[qm * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(j < 2 ? bfl[j][kk] : bfr[j - 2][kk], af[i][kk],
+                                                                       acc[qm * 4 + i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // prologue: all of K tile 0, and the half tiles of tile 1 that K tile -1 would have issued
-  if (nk > 0) {
-    dma(0, 0);
-    dma(0, 3);
-    dma(0, 1);
-    dma(0, 2);
-  }
-  if (nk > 1) {
-    dma(1, 0);
-    dma(1, 3);
-    vm_wait<4>();
+  if constexpr (PHASES == 2) {
+    // prologue: K tile 0, and tile 1's A top / B left / B right (what "P2 of tile -1" issues)
+    if (nk > 0) {
+      dma(0, 0);
+      dma(0, 2);
+      dma(0, 3);
+      dma(0, 1);
+    }
+    if (nk > 1) {
+      dma(1, 0);
+      dma(1, 2);
+      dma(1, 3);
+      vm_wait<6>();
+    } else {
+      vm_wait<0>();
+    }
+    bar256();
+    if (grp == 1) bar256();
+    for (int t = 0; t < nk; ++t) {
+      const int b = t & 1;
+      // P1: top C half
+      read_a(region(b, 0));
+      read_b(bfl, region(b, 2));
+      read_b(bfr, region(b, 3));
+      lgkm_wait0();
+      if (t + 1 < nk) dma(t + 1, 1);
+      bar256();
+      mfma_h(0);
+      bar256();
+      // P2: bottom C half; K tile t+1 must be complete before the next P1 reads it
+      read_a(region(b, 1));
+      lgkm_wait0();
+      if (t + 2 < nk) {
+        dma(t + 2, 0);
+        dma(t + 2, 2);
+        dma(t + 2, 3);
+        vm_wait<6>();
+      } else {
+        vm_wait<0>();
+      }
+      bar256();
+      mfma_h(1);
+      bar256();
+    }
   } else {
-    vm_wait<0>();
-  }
-  bar256();
-  if (grp == 1) bar256();
-
-  for (int t = 0; t < nk; ++t) {
-    const int b = t & 1;
-    // q0: quadrant (0,0)
-    read_a(region(b, 0));
-    read_b(region(b, 2));
-    if (t + 1 < nk) dma(t + 1, 1);
-    bar256();
-    mfma_q(0, 0);
-    bar256();
-    // q1: quadrant (0,1)
-    read_b(region(b, 3));
-    if (t + 1 < nk) dma(t + 1, 2);
-    bar256();
-    mfma_q(0, 1);
-    bar256();
-    // q2: quadrant (1,1)
-    read_a(region(b, 1));
-    if (t + 2 < nk) dma(t + 2, 0);
-    bar256();
-    mfma_q(1, 1);
-    bar256();
-    // q3: quadrant (1,0); K tile t+1 must be complete before the next q0 reads it
-    read_b(region(b, 2));
-    if (t + 2 < nk) {
-      dma(t + 2, 3);
+    // prologue: all of K tile 0, and the half tiles of tile 1 that K tile -1 would have issued
+    if (nk > 0) {
+      dma(0, 0);
+      dma(0, 3);
+      dma(0, 1);
+      dma(0, 2);
+    }
+    if (nk > 1) {
+      dma(1, 0);
+      dma(1, 3);
       vm_wait<4>();
     } else {
       vm_wait<0>();
     }
     bar256();
-    mfma_q(1, 0);
-    bar256();
+    if (grp == 1) bar256();
+    for (int t = 0; t < nk; ++t) {
+      const int b = t & 1;
+      // q0: quadrant (0,0)
+      read_a(region(b, 0));
+      read_b(bfl, region(b, 2));
+      if (t + 1 < nk) dma(t + 1, 1);
+      bar256();
+      lgkm_wait0();
+      mfma_q(0, 0);
+      bar256();
+      // q1: quadrant (0,1)
+      read_b(bfl, region(b, 3));
+      if (t + 1 < nk) dma(t + 1, 2);
+      bar256();
+      lgkm_wait0();
+      mfma_q(0, 1);
+      bar256();
+      // q2: quadrant (1,1)
+      read_a(region(b, 1));
+      if (t + 2 < nk) dma(t + 2, 0);
+      bar256();
+      lgkm_wait0();
+      mfma_q(1, 1);
+      bar256();
+      // q3: quadrant (1,0); K tile t+1 must be complete before the next q0 reads it
+      read_b(bfl, region(b, 2));
+      if (t + 2 < nk) {
+        dma(t + 2, 3);
+        vm_wait<4>();
+      } else {
+        vm_wait<0>();
+      }
+      bar256();
+      lgkm_wait0();
+      mfma_q(1, 0);
+      bar256();
+    }
   }
   if (grp == 0) bar256();
   __syncthreads();

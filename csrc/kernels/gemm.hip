@@ -62,31 +62,32 @@ __global__ void __launch_bounds__(512) dense_gemm_256_kernel(CoreParams P) {
   mfma_gemm_256<LA, LB, EPI>(P);
 }
 
-// The 256 x 256 x 64 core with the 4-phase-per-K-tile interleave (csrc/include/ca_gemm256p8.h).
+// The 256 x 256 x 64 core with two staggered wave groups and two phases per K tile
+// (csrc/include/ca_gemm256p8.h).
 template <template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
 __global__ void __launch_bounds__(512) dense_gemm_256p8_kernel(CoreParams P) {
-  mfma_gemm_256p8<LA, LB, EPI>(P);
+  mfma_gemm_256p8<LA, LB, EPI, 2>(P);
 }
 
 // CLOUD_AMD_GEMM_CORE selects the core (A/B comparisons; ca_gemm_set_core overrides it):
 // 0 "reg" = register-staged, 1 "glds" = glds single stage (4 waves) only, 2 "glds8" = glds
-// double-buffered (8 waves), 3 (default) = glds plus the 256 x 256 ring core for large
-// GEMMs (use_256 below; 4096^3: 904 -> 1126-1148 TF/s, 8192^3: 845 -> 1166-1175), 4 "v256"
-// = the 256 core for every GEMM with M, N >= 256 (tests).
-// 5 "p8" = glds plus the 8-phase 256 x 256 x 64 core (ca_gemm256p8.h) for large GEMMs, 6 "vp8"
-// = the 8-phase core for every GEMM with M, N >= 256 (tests).
+// double-buffered (8 waves), 3 "glds_ring" = glds plus the 256 x 256 ring core (ca_gemm256.h)
+// for large GEMMs, 4 "v256" = the ring core for every GEMM with M, N >= 256 (tests),
+// 5 (default) = glds plus the 256 x 256 two-phase core (ca_gemm256p8.h) for large GEMMs
+// (use_256 below; 8192^3: ring 1,172-1,183 -> 1,245-1,260 TF/s, split-K / TN weight-gradient
+// layout 1,042 -> 1,142), 6 "vp8" = the two-phase core for every GEMM with M, N >= 256 (tests).
 int g_core_kind = -1;
 int core_kind() {
   if (g_core_kind < 0) {
     const char* e = getenv("CLOUD_AMD_GEMM_CORE");
-    g_core_kind = !e ? 3
+    g_core_kind = !e ? 5
                      : (e[0] == 'r' ? 0
-                        : strcmp(e, "glds8") == 0 ? 2
-                        : strcmp(e, "glds") == 0  ? 1
-                        : strcmp(e, "v256") == 0  ? 4
-                        : strcmp(e, "p8") == 0    ? 5
-                        : strcmp(e, "vp8") == 0   ? 6
-                                                  : 3);
+                        : strcmp(e, "glds8") == 0     ? 2
+                        : strcmp(e, "glds") == 0      ? 1
+                        : strcmp(e, "glds_ring") == 0 ? 3
+                        : strcmp(e, "v256") == 0      ? 4
+                        : strcmp(e, "vp8") == 0       ? 6
+                                                      : 5);
   }
   return g_core_kind;
 }

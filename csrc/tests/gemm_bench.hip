@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "ca_gemm256.h"
+#include "ca_gemm256p8.h"
 
 using namespace ca;
 
@@ -62,6 +63,11 @@ __global__ void __launch_bounds__(512) k256(CoreParams P) {
   mfma_gemm_256<GA, GB, EPI_BF16, ST>(P);
 }
 
+template <template <int, int, int> class GA, template <int, int, int> class GB, int PHASES>
+__global__ void __launch_bounds__(512) kp8(CoreParams P) {
+  mfma_gemm_256p8<GA, GB, EPI_BF16, PHASES>(P);
+}
+
 template <template <int, int, int> class GA, template <int, int, int> class GB>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k128(CoreParams P) {
   mfma_gemm_glds<128, 128, 2, 2, GA, GB, EPI_BF16>(P);
@@ -80,6 +86,13 @@ static void launch256_t(const CoreParams& p, int layout, dim3 g, hipStream_t s) 
   else k256<GDenseNC, GDenseNC, ST><<<g, 512, 0, s>>>(p);
 }
 static void launch256(const CoreParams& p, int layout, dim3 g, hipStream_t s) { launch256_t<false>(p, layout, g, s); }
+
+template <int PHASES>
+static void launchp8(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) kp8<GDenseKC, GDenseKC, PHASES><<<g, 512, 0, s>>>(p);
+  else if (layout == 1) kp8<GDenseKC, GDenseNC, PHASES><<<g, 512, 0, s>>>(p);
+  else kp8<GDenseNC, GDenseNC, PHASES><<<g, 512, 0, s>>>(p);
+}
 
 static void launch128(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
   if (layout == 0) k128<GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
@@ -130,7 +143,10 @@ int main(int argc, char** argv) {
   }
   if (shapes.empty()) shapes = {4096, 4096, 4096, 0};
   const char* only = getenv("GB_VARIANTS");  // comma list of full variant names, e.g. "v256,glds128"
-  Variant vars[] = {{"v256", 256, 256, launch256}, {"glds128", 128, 128, launch128}};
+  Variant vars[] = {{"v256", 256, 256, launch256},
+                    {"p8q4", 256, 256, launchp8<4>},
+                    {"p8h2", 256, 256, launchp8<2>},
+                    {"glds128", 128, 128, launch128}};
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
   hipEvent_t e0, e1;

@@ -71,6 +71,42 @@ def test_dgrad_bnbwd_vs_fp32(M, Cout, Cin, epi):
         assert rel(s, gd.sum(0)) < 1e-3 and rel(q, (gd * zb.float()).sum(0)) < 1e-3
 
 
+@pytest.mark.parametrize("M,Cin,Cout", [(4096, 256, 64), (1000, 512, 128), (777, 64, 256), (300, 40, 72)])
+@pytest.mark.parametrize("mode", ["bn", "res", "resbn"])
+def test_fwd_bnapply_vs_fp32(M, Cin, Cout, mode):
+    """Forward prologue: y = relu(z*scale + shift [+ r | + bf16(r*rscale + rshift)]) applied in
+    the GEMM's operand fetch, written once (side + ReLU bitmask), out = y W^T with the BN
+    statistics epilogue -- against a plain fp32 PyTorch reference of the same op."""
+    from cloud_amd.ops import raw
+
+    torch.manual_seed(M + Cin)
+    z = torch.randn(M, Cin, device=DEV).to(torch.bfloat16)
+    r = torch.randn(M, Cin, device=DEV).to(torch.bfloat16)
+    ss = torch.cat([torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.1])
+    rss = torch.cat([torch.rand(Cin, device=DEV) + 0.5, torch.randn(Cin, device=DEV) * 0.1])
+    w = (torch.randn(Cout, 1, 1, Cin, device=DEV) * 0.05).to(torch.bfloat16)
+    pre = z.float() * ss[:Cin] + ss[Cin:]
+    if mode == "res":
+        pre = pre + r.float()
+    if mode == "resbn":
+        pre = pre + (r.float() * rss[:Cin] + rss[Cin:]).to(torch.bfloat16).float()
+    y_ref = pre.clamp_min(0.0)
+    shp = lambda t: t.view(1, 1, M, -1)  # noqa: E731
+    side = torch.empty(1, 1, M, Cin, device=DEV, dtype=torch.bfloat16)
+    mask = torch.empty(M, Cin // 8, device=DEV, dtype=torch.uint8)
+    stats = raw.stats_buffer(M, Cout, z.device)
+    out = raw.conv1x1_fwd_bnapply(shp(z), ss, w, side, mask, res=shp(r) if mode != "bn" else None,
+                                  res_ss=rss if mode == "resbn" else None, stats=stats)
+    y = side.view(M, Cin)
+    assert rel(y, y_ref) < 1e-2
+    assert torch.equal(mask, _mask_bits(y.float() > 0)), "ReLU bitmask must mark exactly the stored positives"
+    of = out.view(M, Cout).float()
+    ref = y_ref.to(torch.bfloat16).float() @ w.view(Cout, Cin).float().t()
+    assert rel(of, ref) < 2e-2, rel(of, ref)
+    st = stats.view(-1, 2, Cout)
+    assert rel(st[:, 0].sum(0), of.sum(0)) < 1e-3 and rel(st[:, 1].sum(0), (of * of).sum(0)) < 1e-3
+
+
 def _train(fold, steps=3):
     os.environ["CLOUD_AMD_BN_FOLD"] = "1" if fold else "0"
     os.environ["CLOUD_AMD_BN_FOLD_FWD"] = "1" if fold else "0"
