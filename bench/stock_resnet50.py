@@ -5,13 +5,18 @@ Plain ``torch.nn`` ResNet-50 v1.5 (no torchvision in this image, so the module
 tree is written out here), ``channels_last`` memory format, bf16 autocast with
 fp32 weights, ``torch.optim.SGD(momentum=0.9, foreach=True)``, and
 ``DistributedDataParallel`` (RCCL, default 25 MB buckets) when WORLD_SIZE > 1.
-Same synthetic data and same JSON line as ../bench.py.
+Same synthetic data and same JSON line as ../bench.py, launched the same way: through
+``cloud_amd.run()`` (``--via-run 1``, the default; one rank per GPU) or in-process.
+MIOpen compiles its kernels during the first steps (minutes at batch 1024): a heartbeat
+line every 30 s shows the run is alive.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import sys
+import threading
 import time
 
 import torch
@@ -63,14 +68,29 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1024, help="per-GPU batch (bench.py's default)")
     ap.add_argument("--layout", default="nhwc", choices=["nhwc", "nchw"])
     ap.add_argument("--precision", default="amp", choices=["amp", "bf16"])
     ap.add_argument("--benchmark", type=int, default=0, help="torch.backends.cudnn.benchmark (MIOpen find)")
+    ap.add_argument("--via-run", type=int, default=1, help="1: launch the ranks through cloud_amd.run()")
     args = ap.parse_args()
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from cloud_amd.utils import benchlaunch
+
+    if args.via_run and not benchlaunch.inside_launched_rank():
+        return benchlaunch.launch_via_run(os.path.abspath(__file__), args.gpus, tag="stock_resnet50")
     t_start = time.time()
     rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+    benchlaunch.check_world(args.gpus, world, tag="stock_resnet50")
+    phase = {"what": "setup", "t": time.time()}
+    done = threading.Event()
+
+    def heartbeat():
+        while not done.wait(30.0):
+            print("[stock_resnet50] rank %d: %s, %.0f s" % (rank, phase["what"], time.time() - phase["t"]), flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     lr = int(os.environ.get("LOCAL_RANK", 0))
     dev = torch.device("cuda", lr)
     torch.cuda.set_device(dev)
@@ -99,12 +119,15 @@ def main():
         opt.step()
         return loss
 
+    phase.update(what="first step (MIOpen kernel compilation)", t=time.time())
     step()
     torch.cuda.synchronize()
     first = time.time() - t_start
-    for _ in range(args.warmup - 1):
+    for i in range(args.warmup - 1):
+        phase.update(what="warmup step %d" % (i + 2), t=time.time())
         step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+    phase.update(what="timed steps", t=time.time())
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
@@ -124,7 +147,11 @@ def main():
                           "n_gpus": world, "ms_per_step": round(el / args.steps * 1000, 3),
                           "config": {"layout": args.layout, "precision": args.precision, "batch": args.batch,
                                      "benchmark": args.benchmark},
-                          "first_step_latency_s": round(first, 3), "loss": float(loss)}), flush=True)
+                          "first_step_latency_s": round(first, 3), "launched_via": benchlaunch.launched_via(),
+                          "run_to_first_step_s": (round(t_start + first - float(os.environ["CLOUD_AMD_RUN_T0"]), 3)
+                                                  if os.environ.get("CLOUD_AMD_RUN_T0") else None),
+                          "loss": float(loss)}), flush=True)
+    done.set()
 
 
 if __name__ == "__main__":

@@ -77,8 +77,9 @@ _VARS = [
         "with 4 x 1 waves; 0 = 128 x 64 with 2 x 2 waves", "ops"),
     Var("CLOUD_AMD_BN_GROUPS_MAX", int, 512, "BatchNorm statistics: most groups of the first-level reduction of the "
         "per-tile partial rows (1..512; ~64 rows per group)", "ops"),
-    Var("CLOUD_AMD_GEMM_LIB", str, "auto", "plain bf16 GEMMs (bias / accumulate only, no fused epilogue): 'auto' "
-        "times the in-tree kernel against hipBLASLt once per shape and keeps the faster, 'never', 'always' "
+    Var("CLOUD_AMD_GEMM_LIB", str, "never", "plain bf16 GEMMs (bias / accumulate only, no fused epilogue): 'never' "
+        "(default: every GEMM on the in-tree kernels, the same engine on every box and rank), 'auto' (diagnostic: "
+        "times the in-tree kernel against hipBLASLt once per shape and keeps the faster), 'always' "
         "(ops/raw.py PlainGemmPolicy)", "ops"),
     Var("CLOUD_AMD_GEMM_PRW", bool, True, "forward 1x1 convolutions with N = 256, K = 64 (ResNet layer-1 conv3 "
         "and shortcut): persistent resident-weight core (csrc/include/ca_gemm_prw.h); 0 = the tiled 128 core",
@@ -100,6 +101,9 @@ _VARS = [
         "(ResNet-50: bn3 -> conv3 dgrad and bn3 -> next conv1, every stage); the transform-A core re-runs the "
         "BN transform per N tile and cannot pipeline a one-K-tile GEMM, so the short-K sites (bn2 -> conv3, "
         "bn1 -> conv1 dgrad) measured slower than the separate pass (docs/performance.md, round 4)", "ops"),
+    Var("CLOUD_AMD_BN_FOLD_WGRAD", bool, True, "bn3 -> conv3 fold at 64 input channels (ResNet stage 1): conv3's weight "
+        "gradient runs in the same kernel as its input gradient (ca_gemm_xa.h mfma_gemm_xa_dw), so the BN-backward "
+        "output dz3 is never written", "ops"),
     Var("CLOUD_AMD_BN_FOLD_ALL", bool, False, "fold every BN site regardless of CLOUD_AMD_BN_FOLD_MAX_N (tests, A/B)",
         "ops"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "

@@ -286,12 +286,22 @@ class _BottleneckFn(torch.autograd.Function):
             # bn3's backward apply folded into conv3's input-gradient GEMM: dz3 is produced in
             # its operand fetch (and written once, for the weight gradient), never read back
             coef3 = bn_coef(blk.bn3, z3, s3, p3)
-            dz3, dres = torch.empty_like(z3), None
-            dy2, p2 = raw.conv1x1_dgrad_bnbwd(dout, z3, m3, coef3, blk.conv3.weight, dz3, bn=(z2, m2))
+            dres = None
+            c3 = blk.conv3
+            if config.get("CLOUD_AMD_BN_FOLD_WGRAD") and raw.dgrad_wgrad_fusable(c3.cout, c3.cin):
+                # ... and conv3's weight gradient in the same pass: dz3 never reaches memory
+                dy2, p2 = raw.conv1x1_dgrad_wgrad_bnbwd(dout, z3, m3, coef3, c3.weight, y2, c3.weight.grad,
+                                                        bn=(z2, m2), dw_beta=1.0)
+                ddp.notify_grad_ready(c3.weight)
+                dz3 = None
+            else:
+                dz3 = torch.empty_like(z3)
+                dy2, p2 = raw.conv1x1_dgrad_bnbwd(dout, z3, m3, coef3, c3.weight, dz3, bn=(z2, m2))
         else:
             dz3, dres = bn_back(blk.bn3, dout, z3, (s3, m3), want_dres=not gate_res, partials=p3)
             dy2, p2, _ = dgrad(blk.conv3, dz3, y2.shape, (z2, m2))
-        wgrad(blk.conv3, dz3, y2)
+        if dz3 is not None:
+            wgrad(blk.conv3, dz3, y2)
         del dz3
         dz2, _ = bn_back(blk.bn2, dy2, z2, (s2, m2), partials=p2)
         del dy2, p2

@@ -244,6 +244,57 @@ def conv1x1_dgrad_bnbwd(dy, z, mask, coef, w, side, out=None, beta=0.0, bn=None,
     return (dx, part, part2) if (len(bn) > 2 and bn[2] is not None) else (dx, part)
 
 
+def dgrad_wgrad_fusable(cout, cin):
+    """Shapes the fused input+weight gradient kernel (:func:`conv1x1_dgrad_wgrad_bnbwd`) takes:
+    64 input channels, <= 256 output channels in whole 64-channel steps (ResNet stage-1 conv3)."""
+    return cin == 64 and cout % 64 == 0 and cout <= 256
+
+
+def conv1x1_dgrad_wgrad_bnbwd(dy, z, mask, coef, w, y, dw, bn=None, dw_beta=1.0, blocks=None):
+    """:func:`conv1x1_dgrad_bnbwd` with the WEIGHT gradient in the same pass: the transformed
+    ``dz = A*(dy * relu'(mask)) + B*z + D`` feeds both ``dx = dz W`` and ``dw (+)= dz^T y``
+    (``y``: the convolution's input, NHWC) while it is in LDS, so it is never written
+    (``ca_gemm_xa.h mfma_gemm_xa_dw``).  ``dw`` ([Cout, 1, 1, Cin], bf16 or fp32) = dz^T y +
+    ``dw_beta`` * dw, reduced deterministically from one fp32 slab per workgroup.  Shapes:
+    :func:`dgrad_wgrad_fusable`.  Returns ``dx`` or ``(dx, partials)`` with ``bn=(z_in, mask_in)``."""
+    ext = _ext.load(required=True)
+    N, H, W, Cout = z.shape
+    Cin = w.shape[3]
+    M = N * H * W
+    assert dgrad_wgrad_fusable(Cout, Cin), (Cout, Cin)
+    assert dy.shape == z.shape and w.shape[1:3] == (1, 1) and dw.shape == w.shape and dw.is_contiguous()
+    assert dy.is_contiguous() and z.is_contiguous() and coef.numel() == 3 * Cout
+    assert y.shape == (N, H, W, Cin) and y.is_contiguous() and (mask is None or mask.shape == (M, Cout // 8))
+    dx = torch.empty((N, H, W, Cin), dtype=torch.bfloat16, device=dy.device)
+    part, zp, mp = None, 0, 0
+    if bn is not None:
+        zb, mb = bn[0], bn[1]
+        assert zb.shape == dx.shape and zb.is_contiguous() and (mb is None or mb.shape == (M, Cin // 8))
+        part = torch.empty(((M + 127) // 128, 2, Cin), dtype=torch.float32, device=dy.device)
+        zp, mp = zb.data_ptr(), _ext.ptr(mb)
+    if blocks is None:
+        blocks = 2 * _cu_count(dy.device)
+    blocks = max(1, min(int(blocks), (M + 127) // 128))
+    ws = torch.empty(blocks * Cout * Cin, dtype=torch.float32, device=dy.device)
+    cp = coef.data_ptr()
+    g = ext.gemm_xa_dw(dy.data_ptr(), z.data_ptr(), _ext.ptr(mask), cp, cp + 4 * Cout, cp + 8 * Cout, Cout,
+                       w.data_ptr(), Cin, dx.data_ptr(), Cin, M, Cin, Cout, zp, mp, _ext.ptr(part), y.data_ptr(), Cin,
+                       dw.data_ptr(), int(dw.dtype == torch.bfloat16), float(dw_beta), ws.data_ptr(), blocks,
+                       _st(dy.device))
+    _log("dgrad_wgrad1x1_xa", M, Cin, Cout, _nb(dy, z, mask, w, dx, y) + 2 * g * Cout * Cin * 4)
+    return dx if bn is None else (dx, part)
+
+
+_CU_COUNT = {}
+
+
+def _cu_count(device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _CU_COUNT:
+        _CU_COUNT[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return _CU_COUNT[idx]
+
+
 def conv1x1_fwd_bnapply(z, ss, w, side, mask_out, res=None, res_ss=None, stats=None):
     """Forward 1x1 convolution (``w`` [Cout, 1, 1, Cin]) of a BatchNorm(+residual)+ReLU output
     that is never written by a separate pass: ``y = relu(z*scale + shift [+ r | + bf16(r*rscale +
@@ -392,10 +443,11 @@ class PlainGemmPolicy:
     GELU' backward, BN statistics, split-K weight gradients into the fp32 arena) stays on
     the in-tree kernels.
 
-    ``CLOUD_AMD_GEMM_LIB``: ``auto`` (default) times both engines once per (layout, M, N, K,
+    ``CLOUD_AMD_GEMM_LIB``: ``never`` (default) = in-tree only, so every box and every rank runs
+    the same kernels; ``auto`` (a diagnostic) times both engines once per (layout, M, N, K,
     bias, beta) key on the first call -- on scratch outputs, outside any stream capture --
-    and keeps the faster (like a cuDNN benchmark cache; ``decisions`` records the timings);
-    ``never`` = in-tree only; ``always`` = library for every plain GEMM."""
+    and keeps the faster (``decisions`` records the timings); ``always`` = library for every
+    plain GEMM."""
 
     def __init__(self):
         self.mode = None

@@ -338,6 +338,12 @@ __global__ void __launch_bounds__(256) xa_gemm_kernel(CoreParams P, XaParams X) 
   mfma_gemm_xa<BM, BN, BKC, EPI, XM>(P, X);
 }
 
+template <int EPI>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) xa_dw_kernel(CoreParams P, XaParams X, const bf16_t* Y, long ldy, float* ws,
+                                                    int tiles_per_block) {
+  mfma_gemm_xa_dw<EPI>(P, X, Y, ldy, ws, tiles_per_block);
+}
+
 template <bool LB, int EPI, int XM>
 int xa_launch(const CoreParams& p0, const XaParams& x, hipStream_t s) {
   CoreParams p = p0;
@@ -550,6 +556,37 @@ int ca_gemm_xa(int layout, int mode, const bf16_t* src0, const bf16_t* src1, con
   }
   if (res_src) return xa_launch<false, EPI_BF16_BNR, XA_BN_BWD>(p, x, s);
   return xa_launch<false, EPI_BF16_BN, XA_BN_BWD>(p, x, s);
+}
+
+// XA_BN_BWD input gradient with the weight gradient in the same pass (ca_gemm_xa.h
+// mfma_gemm_xa_dw): N == 64, K % 64 == 0, K <= 256.  `blocks` workgroups each own a
+// contiguous range of 128-row tiles and write one fp32 dW slab ([K][N]) into ws
+// (blocks * K * N floats); dw (bf16 when dw_bf16, else fp32, [K][N]) = sum of the slabs +
+// dw_beta * dw.  `side` is ignored (dz is never written).  Returns the block count used.
+int ca_gemm_xa_dw(const bf16_t* src0, const bf16_t* src1, const uint8_t* mask_in, const float* c0, const float* c1,
+                  const float* c2, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N, int K,
+                  const bf16_t* bnz, const uint8_t* bnmask, float* stats, const bf16_t* Y, long ldy, void* dw,
+                  int dw_bf16, float dw_beta, float* ws, int blocks, hipStream_t s) {
+  if (M <= 0 || N != 64 || K % 64 != 0 || K > 256 || lda % 8 != 0 || ldy % 8 != 0 || !src0 || !src1 || !c0 || !c1 ||
+      !c2 || !Y || !dw || !ws || blocks <= 0)
+    return -1;
+  if (bnz && !stats) return -1;
+  CoreParams p = base_params(src0, lda, B, ldb, C, ldc, M, N, K);
+  XaParams x{src0, src1, mask_in, c0, c1, c2, nullptr, nullptr, nullptr};
+  const int tiles = (M + 127) / 128;
+  const int tpb = (tiles + blocks - 1) / blocks;
+  const int g = (tiles + tpb - 1) / tpb;
+  if (bnz) {
+    p.stats = stats;
+    p.bnz = bnz;
+    p.bnmask = bnmask;
+    xa_dw_kernel<EPI_BF16_BN><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
+  } else {
+    xa_dw_kernel<EPI_BF16><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
+  }
+  CA_LAUNCH_CHECK();
+  const int rc = ca_splitk_reduce(ws, g, (long)K * N, dw, dw_bf16, dw_beta, s);
+  return rc < 0 ? rc : g;
 }
 
 int ca_gemm_splitk_effective(int K, int splits) {

@@ -71,6 +71,40 @@ def test_dgrad_bnbwd_vs_fp32(M, Cout, Cin, epi):
         assert rel(s, gd.sum(0)) < 1e-3 and rel(q, (gd * zb.float()).sum(0)) < 1e-3
 
 
+@pytest.mark.parametrize("M,Cout", [(4096, 256), (1000, 128), (777, 64), (300, 192), (70000, 256)])
+@pytest.mark.parametrize("blocks", [None, 3])
+@pytest.mark.parametrize("dw_dtype", [torch.bfloat16, torch.float32])
+def test_dgrad_wgrad_bnbwd_vs_fp32(M, Cout, blocks, dw_dtype):
+    """Input AND weight gradient of the BN-folded 1x1 conv in one pass (mfma_gemm_xa_dw):
+    dz = A*(dy*relu') + B*z + D is never written; dx = dz W with the BN-statistics epilogue,
+    dw = dz^T y + dw_old -- each against a plain fp32 PyTorch reference."""
+    from cloud_amd.ops import raw
+
+    Cin = 64
+    torch.manual_seed(M + Cout)
+    dy = torch.randn(M, Cout, device=DEV).to(torch.bfloat16)
+    z = torch.randn(M, Cout, device=DEV).to(torch.bfloat16)
+    act = torch.rand(M, Cout, device=DEV) > 0.4
+    coef = torch.randn(3 * Cout, device=DEV) * torch.tensor([1.0, 0.1, 0.01], device=DEV).repeat_interleave(Cout)
+    w = (torch.randn(Cout, 1, 1, Cin, device=DEV) * 0.05).to(torch.bfloat16)
+    y = torch.randn(M, Cin, device=DEV).to(torch.bfloat16)
+    zb = torch.randn(M, Cin, device=DEV).to(torch.bfloat16)
+    act_b = torch.rand(M, Cin, device=DEV) > 0.5
+    dw0 = (torch.randn(Cout, 1, 1, Cin, device=DEV) * 0.1).to(dw_dtype)
+    dw = dw0.clone()
+    A, B, D = coef[:Cout], coef[Cout:2 * Cout], coef[2 * Cout:]
+    dz = (A * dy.float() * act.float() + B * z.float() + D).to(torch.bfloat16).float()
+    shp = lambda t: t.view(1, 1, M, -1)  # noqa: E731
+    dx, part = raw.conv1x1_dgrad_wgrad_bnbwd(shp(dy), shp(z), _mask_bits(act), coef, w, shp(y), dw,
+                                             bn=(shp(zb), _mask_bits(act_b)), dw_beta=1.0, blocks=blocks)
+    dx_ref = dz @ w.view(Cout, Cin).float()
+    assert rel(dx.view(M, Cin), dx_ref) < 2e-2, rel(dx.view(M, Cin), dx_ref)
+    dw_ref = dz.t() @ y.float() + dw0.view(Cout, Cin).float()
+    assert rel(dw.view(Cout, Cin), dw_ref) < 1e-2, rel(dw.view(Cout, Cin), dw_ref)
+    gd = dx.view(M, Cin).float() * act_b.float()
+    assert rel(part[:, 0].sum(0), gd.sum(0)) < 1e-3 and rel(part[:, 1].sum(0), (gd * zb.float()).sum(0)) < 1e-3
+
+
 @pytest.mark.parametrize("M,Cin,Cout", [(4096, 256, 64), (1000, 512, 128), (777, 64, 256), (300, 40, 72)])
 @pytest.mark.parametrize("mode", ["bn", "res", "resbn"])
 def test_fwd_bnapply_vs_fp32(M, Cin, Cout, mode):
@@ -107,7 +141,8 @@ def test_fwd_bnapply_vs_fp32(M, Cin, Cout, mode):
     assert rel(st[:, 0].sum(0), of.sum(0)) < 1e-3 and rel(st[:, 1].sum(0), (of * of).sum(0)) < 1e-3
 
 
-def _train(fold, steps=3):
+def _train(fold, steps=3, wgrad_fused=False):
+    os.environ["CLOUD_AMD_BN_FOLD_WGRAD"] = "1" if wgrad_fused else "0"
     os.environ["CLOUD_AMD_BN_FOLD"] = "1" if fold else "0"
     os.environ["CLOUD_AMD_BN_FOLD_FWD"] = "1" if fold else "0"
     os.environ["CLOUD_AMD_BN_FOLD_ALL"] = "1"  # every site, not only the ones the default policy keeps
@@ -160,6 +195,7 @@ def test_resnet_bn_fold_bitwise(monkeypatch):
         os.environ.pop("CLOUD_AMD_BN_FOLD", None)
         os.environ.pop("CLOUD_AMD_BN_FOLD_FWD", None)
         os.environ.pop("CLOUD_AMD_BN_FOLD_ALL", None)
+        os.environ.pop("CLOUD_AMD_BN_FOLD_WGRAD", None)
     # 7 blocks: bwd folds bn3 (6 blocks get their partials from the next block) and bn1 (7);
     # fwd folds bn3 into the next conv1 (6 hand-offs) and bn2 into conv3 (all but layer 1's prw)
     assert n_fold["bwd"] > 0 and n_fold["fwd"] > 0, n_fold
@@ -180,3 +216,31 @@ def test_resnet_bn_fold_bitwise(monkeypatch):
     for a, b in zip(l1, l0):
         assert abs(a - b) < 0.05 * abs(b) + 1e-3, (l1, l0)
     assert fused_block is not None
+
+
+def test_resnet_fused_dgrad_wgrad_close():
+    """The fused conv3 input+weight gradient (stage 1) in a trained model: step-0 gradients
+    match the unfused fold (separate weight-gradient GEMM) to bf16 / reduction-order rounding."""
+    from cloud_amd.ops import raw
+
+    calls = {"n": 0}
+    real = raw.conv1x1_dgrad_wgrad_bnbwd
+
+    def counting(*a, **k):
+        calls["n"] += 1
+        return real(*a, **k)
+
+    raw.conv1x1_dgrad_wgrad_bnbwd = counting
+    try:
+        g1, l1, names = _train(True, steps=2, wgrad_fused=True)
+        g0, l0, _ = _train(True, steps=2, wgrad_fused=False)
+    finally:
+        raw.conv1x1_dgrad_wgrad_bnbwd = real
+        for k in ("CLOUD_AMD_BN_FOLD", "CLOUD_AMD_BN_FOLD_FWD", "CLOUD_AMD_BN_FOLD_ALL", "CLOUD_AMD_BN_FOLD_WGRAD"):
+            os.environ.pop(k, None)
+    assert calls["n"] > 0
+    for ai, (x, y) in enumerate(zip(g1[0], g0[0])):
+        for n, o, k in names[ai]:
+            assert rel(x[o:o + k], y[o:o + k]) < 2e-2, (n, rel(x[o:o + k], y[o:o + k]))
+    for a, b in zip(l1, l0):
+        assert abs(a - b) < 0.05 * abs(b) + 1e-3, (l1, l0)
