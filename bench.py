@@ -109,6 +109,7 @@ def main():
     from cloud_amd.ops import softmax_cross_entropy
     from cloud_amd.optim import SGD
     from cloud_amd.parallel import strategy as strategy_mod
+    from cloud_amd.runtime import gc_control
     from cloud_amd.utils import dist_env, trace
 
     if args.device == "cpu":
@@ -191,8 +192,11 @@ def main():
             print("[bench] %s" % e, file=sys.stderr, flush=True)
     dist_env.barrier()
     sync()
+    # everything alive now (model, optimizer state, imports) leaves the collector's full passes
+    gc_frozen = gc_control.freeze()
     reducer.timing_start()
     host0 = benchlaunch.host_state()
+    step_probe = benchlaunch.StepProbe(cuda=on_gpu)
     # per-step device time from events on the compute stream and per-step host launch time
     # (no added synchronisation: events are read after the closing sync)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if on_gpu else None
@@ -206,12 +210,13 @@ def main():
         host_ms.append((time.perf_counter() - th) * 1e3)
         if evs:
             evs[i + 1].record()
+        step_probe.mark()
     sync()
     dist_env.barrier()
     t1 = time.perf_counter()
     step_stats = benchlaunch.step_stats(
         [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)] if evs else None, host_ms,
-        host0, benchlaunch.host_state())
+        host0, benchlaunch.host_state(), probe=step_probe.close())
     comm = reducer.timing_summary()
     per_rank_ms = [v / args.steps * 1000.0 for v in dist_env.all_gather_floats(t1 - t0, device)]
     elapsed = dist_env.all_reduce_max(t1 - t0, device)
@@ -267,6 +272,7 @@ def main():
                          busbw_gbs=busbw, comm_probe=probe),
             "replicas_consistent": replicas_consistent,
             "step_stats_rank0": step_stats,
+            "gc_frozen_objects": gc_frozen,
             "warnings": step_stats.pop("warnings"),
             "rank_ms_per_step": {"min": round(min(per_rank_ms), 3), "max": round(max(per_rank_ms), 3)},
             "first_step_latency_s": round(first_lat, 3),

@@ -171,6 +171,11 @@ def main():
             print("[bert] %s" % e, file=sys.stderr, flush=True)
     dist_env.barrier()
     torch.cuda.synchronize()
+    gc_frozen = None
+    if not args.stock:
+        from cloud_amd.runtime import gc_control
+
+        gc_frozen = gc_control.freeze()  # model / optimizer / imports leave the collector's full passes
     if reducer is not None:
         reducer.timing_start()
     t0 = time.perf_counter()
@@ -203,7 +208,7 @@ def main():
             "config": {"model": "bert-base" if args.layers == 12 else "bert-%dL" % args.layers,
                        "global_batch": B * world, "seq_len": S, "per_gpu_batch": B, "parallelism": "dp%d" % world,
                        "optimizer": "adamw"},
-            "impl": impl, "first_step_latency_s": round(first, 3),
+            "impl": impl, "gc_frozen_objects": gc_frozen, "first_step_latency_s": round(first, 3),
             "run_to_first_step_s": round(run_to_first, 3) if run_to_first is not None else None,
             "startup_phases_rank0": phases,
             "launched_via": benchlaunch.launched_via(), "comm": comm,

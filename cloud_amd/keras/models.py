@@ -541,6 +541,10 @@ class Model(Layer):
                 callbacks_.on_train_batch_end(step, {"loss": float(loss.detach())} if step % 50 == 0 else {})
                 step += 1
                 global_step += 1
+                if global_step == 3:  # model, optimizer state and kernel caches exist now
+                    from ..runtime import gc_control
+
+                    gc_control.freeze()
                 if self.stop_training:
                     break
             logs = self._logs()
@@ -555,6 +559,10 @@ class Model(Layer):
             if self.stop_training:
                 break
         callbacks_.on_train_end({})
+        if global_step >= 3:
+            from ..runtime import gc_control
+
+            gc_control.unfreeze()  # this fit's objects may become garbage (tuner workers run many fits)
         self.history = history
         return history
 

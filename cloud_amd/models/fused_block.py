@@ -309,7 +309,15 @@ class _BottleneckFn(torch.autograd.Function):
         wgrad(blk.conv2, dz2, y1)
         del dz2
         coef1 = None
-        if fold and p1 is not None and _fold_site(blk.conv1.cout, blk.conv1.cin):
+        c1 = blk.conv1
+        # stage 1: bn1's backward apply, conv1's input gradient AND its weight gradient in one
+        # pass (dz1 never written); elsewhere the long-K fold or the separate passes
+        fuse1 = (fold and p1 is not None and config.get("CLOUD_AMD_BN_FOLD_WGRAD1")
+                 and raw.dgrad_wgrad_fusable(c1.cout, c1.cin))
+        if fuse1:
+            coef1 = bn_coef(blk.bn1, z1, s1, p1)
+            dz1 = None
+        elif fold and p1 is not None and _fold_site(blk.conv1.cout, blk.conv1.cin):
             coef1 = bn_coef(blk.bn1, z1, s1, p1)  # bn1's apply runs in conv1's dgrad below
             dz1 = torch.empty_like(z1)
         else:
@@ -337,8 +345,13 @@ class _BottleneckFn(torch.autograd.Function):
             bn_src = ctx.prev_src
             if bn_src is not None and res1 is None:
                 bn_src = bn_src[:2]
-            r = raw.conv1x1_dgrad_bnbwd(dy1, z1, m1, coef1, blk.conv1.weight, dz1, out=dx, beta=1.0, bn=bn_src,
-                                        res=res1)
+            if fuse1:
+                r = raw.conv1x1_dgrad_wgrad_bnbwd(dy1, z1, m1, coef1, c1.weight, x, c1.weight.grad, out=dx, beta=1.0,
+                                                  bn=bn_src, res=res1, dw_beta=1.0)
+                ddp.notify_grad_ready(c1.weight)
+            else:
+                r = raw.conv1x1_dgrad_bnbwd(dy1, z1, m1, coef1, c1.weight, dz1, out=dx, beta=1.0, bn=bn_src,
+                                            res=res1)
             del dy1
             p_prev, p_prev2 = (None, None) if bn_src is None else (r[1], r[2] if len(r) > 2 else None)
         else:
@@ -347,7 +360,8 @@ class _BottleneckFn(torch.autograd.Function):
         if p_prev is not None:
             _park(dx, p_prev, p_prev2)
         ctx.prev_src = None
-        wgrad(blk.conv1, dz1, x)
+        if dz1 is not None:
+            wgrad(blk.conv1, dz1, x)
         # join: later kernels on the main stream (and DDP's bucket events recorded on it)
         # are ordered after this block's weight gradients
         side.join()

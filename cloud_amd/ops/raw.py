@@ -245,18 +245,21 @@ def conv1x1_dgrad_bnbwd(dy, z, mask, coef, w, side, out=None, beta=0.0, bn=None,
 
 
 def dgrad_wgrad_fusable(cout, cin):
-    """Shapes the fused input+weight gradient kernel (:func:`conv1x1_dgrad_wgrad_bnbwd`) takes:
-    64 input channels, <= 256 output channels in whole 64-channel steps (ResNet stage-1 conv3)."""
-    return cin == 64 and cout % 64 == 0 and cout <= 256
+    """Shapes the fused input+weight gradient kernel (:func:`conv1x1_dgrad_wgrad_bnbwd`) takes
+    (``ca_gemm_xa_dw``): 64 input channels with 64 / 128 / 256 output channels (ResNet stage-1
+    conv3), or 64 output channels with 256 input channels (stage-1 conv1)."""
+    return (cin == 64 and cout in (64, 128, 256)) or (cout == 64 and cin == 256)
 
 
-def conv1x1_dgrad_wgrad_bnbwd(dy, z, mask, coef, w, y, dw, bn=None, dw_beta=1.0, blocks=None):
+def conv1x1_dgrad_wgrad_bnbwd(dy, z, mask, coef, w, y, dw, out=None, beta=0.0, bn=None, res=None, dw_beta=1.0,
+                              blocks=None):
     """:func:`conv1x1_dgrad_bnbwd` with the WEIGHT gradient in the same pass: the transformed
     ``dz = A*(dy * relu'(mask)) + B*z + D`` feeds both ``dx = dz W`` and ``dw (+)= dz^T y``
     (``y``: the convolution's input, NHWC) while it is in LDS, so it is never written
     (``ca_gemm_xa.h mfma_gemm_xa_dw``).  ``dw`` ([Cout, 1, 1, Cin], bf16 or fp32) = dz^T y +
-    ``dw_beta`` * dw, reduced deterministically from one fp32 slab per workgroup.  Shapes:
-    :func:`dgrad_wgrad_fusable`.  Returns ``dx`` or ``(dx, partials)`` with ``bn=(z_in, mask_in)``."""
+    ``dw_beta`` * dw, reduced deterministically from one fp32 slab per workgroup.  Input-gradient
+    epilogue options and return values are :func:`conv1x1_dgrad_bnbwd`'s (``bn=`` (z, mask[, z2]),
+    ``res=``, ``out=`` / ``beta``).  Shapes: :func:`dgrad_wgrad_fusable`."""
     ext = _ext.load(required=True)
     N, H, W, Cout = z.shape
     Cin = w.shape[3]
@@ -265,24 +268,35 @@ def conv1x1_dgrad_wgrad_bnbwd(dy, z, mask, coef, w, y, dw, bn=None, dw_beta=1.0,
     assert dy.shape == z.shape and w.shape[1:3] == (1, 1) and dw.shape == w.shape and dw.is_contiguous()
     assert dy.is_contiguous() and z.is_contiguous() and coef.numel() == 3 * Cout
     assert y.shape == (N, H, W, Cin) and y.is_contiguous() and (mask is None or mask.shape == (M, Cout // 8))
-    dx = torch.empty((N, H, W, Cin), dtype=torch.bfloat16, device=dy.device)
-    part, zp, mp = None, 0, 0
+    dx = out if out is not None else torch.empty((N, H, W, Cin), dtype=torch.bfloat16, device=dy.device)
+    src, rmask, zp, mp, part, part2, z2p = 0, 0, 0, 0, None, None, 0
+    if res is not None:
+        src_t, rm_t = res
+        assert src_t.shape == dx.shape and src_t.is_contiguous()
+        src, rmask = src_t.data_ptr(), _ext.ptr(rm_t)
     if bn is not None:
         zb, mb = bn[0], bn[1]
         assert zb.shape == dx.shape and zb.is_contiguous() and (mb is None or mb.shape == (M, Cin // 8))
         part = torch.empty(((M + 127) // 128, 2, Cin), dtype=torch.float32, device=dy.device)
         zp, mp = zb.data_ptr(), _ext.ptr(mb)
+        if len(bn) > 2 and bn[2] is not None:
+            assert res is not None, "second-BN statistics need the residual-gated (res=) form"
+            part2 = torch.empty_like(part)
+            z2p = bn[2].data_ptr()
     if blocks is None:
         blocks = 2 * _cu_count(dy.device)
     blocks = max(1, min(int(blocks), (M + 127) // 128))
     ws = torch.empty(blocks * Cout * Cin, dtype=torch.float32, device=dy.device)
     cp = coef.data_ptr()
     g = ext.gemm_xa_dw(dy.data_ptr(), z.data_ptr(), _ext.ptr(mask), cp, cp + 4 * Cout, cp + 8 * Cout, Cout,
-                       w.data_ptr(), Cin, dx.data_ptr(), Cin, M, Cin, Cout, zp, mp, _ext.ptr(part), y.data_ptr(), Cin,
-                       dw.data_ptr(), int(dw.dtype == torch.bfloat16), float(dw_beta), ws.data_ptr(), blocks,
-                       _st(dy.device))
-    _log("dgrad_wgrad1x1_xa", M, Cin, Cout, _nb(dy, z, mask, w, dx, y) + 2 * g * Cout * Cin * 4)
-    return dx if bn is None else (dx, part)
+                       w.data_ptr(), Cin, dx.data_ptr(), Cin, M, Cin, Cout, float(beta), src, rmask, zp, mp,
+                       _ext.ptr(part), z2p, _ext.ptr(part2), y.data_ptr(), Cin, dw.data_ptr(),
+                       int(dw.dtype == torch.bfloat16), float(dw_beta), ws.data_ptr(), blocks, _st(dy.device))
+    _log("dgrad_wgrad1x1_xa", M, Cin, Cout, _nb(dy, z, mask, w, dx, y) + (_nb(dx) if beta else 0)
+         + 2 * g * Cout * Cin * 4)
+    if bn is None:
+        return dx
+    return (dx, part, part2) if part2 is not None else (dx, part)
 
 
 _CU_COUNT = {}

@@ -125,6 +125,66 @@ def host_state():
     return st
 
 
+class StepProbe:
+    """Host-side evidence per timed step, no device synchronisation: Python garbage-collector
+    pauses (``gc.callbacks``: time and generation of every collection), page faults of this
+    process (``getrusage`` minor / major: a major fault is a page read back from disk or
+    swap), and the PyTorch caching allocator's device allocations and frees (a new segment is
+    a hipMalloc the driver must back and clear).  ``mark()`` at every step boundary."""
+
+    def __init__(self, cuda=True):
+        import gc
+
+        self._gc = gc
+        self._cuda = cuda
+        self._t = None
+        self._gen = -1
+        self._pause = 0.0
+        self.rows = []
+        self._last = self._sample()
+        gc.callbacks.append(self._cb)
+
+    def _cb(self, phase, info):
+        import time
+
+        if phase == "start":
+            self._t = time.perf_counter()
+        elif self._t is not None:
+            self._pause += (time.perf_counter() - self._t) * 1e3
+            self._gen = max(self._gen, int(info.get("generation", -1)))
+            self._t = None
+
+    def _sample(self):
+        import resource
+
+        ru = resource.getrusage(resource.RUSAGE_SELF)
+        allocs = frees = retries = None
+        if self._cuda:
+            try:
+                import torch
+
+                ms = torch.cuda.memory_stats()
+                allocs, frees, retries = ms.get("num_device_alloc"), ms.get("num_device_free"), \
+                    ms.get("num_alloc_retries")
+            except Exception:  # noqa: BLE001 - informational
+                pass
+        return (ru.ru_minflt, ru.ru_majflt, allocs, frees, retries)
+
+    def mark(self):
+        cur = self._sample()
+        d = [None if (a is None or b is None) else b - a for a, b in zip(self._last, cur)]
+        self.rows.append({"gc_ms": round(self._pause, 3), "gc_gen": self._gen, "minflt": d[0], "majflt": d[1],
+                          "dev_alloc": d[2], "dev_free": d[3], "alloc_retry": d[4]})
+        self._last, self._pause, self._gen = cur, 0.0, -1
+
+    def close(self):
+        try:
+            self._gc.callbacks.remove(self._cb)
+        except ValueError:
+            pass
+        return self.rows
+
+
 def _mmm(v):
     s = sorted(v)
     n = len(s)
@@ -132,7 +192,7 @@ def _mmm(v):
     return {"min": round(s[0], 3), "median": round(med, 3), "max": round(s[-1], 3)}
 
 
-def step_stats(device_ms, host_ms, host_before, host_after, outlier_ratio=1.5):
+def step_stats(device_ms, host_ms, host_before, host_after, outlier_ratio=1.5, probe=None):
     """Per-step timing of the timed region (device time between step-boundary events on
     the compute stream, host time to enqueue a step) plus the host state around it.  A
     step slower than ``outlier_ratio`` x the median adds a warning, with the evidence
@@ -142,6 +202,11 @@ def step_stats(device_ms, host_ms, host_before, host_after, outlier_ratio=1.5):
     out = {"host_launch_ms": _mmm(host_ms) if host_ms else None,
            "device_ms": _mmm(device_ms) if device_ms else None,
            "host_before": host_before, "host_after": host_after, "warnings": []}
+    if host_ms:
+        out["host_launch_ms_steps"] = [round(v, 2) for v in host_ms]
+    if probe:
+        out["probe_steps"] = probe
+        out["gc_ms_total"] = round(sum(r["gc_ms"] for r in probe), 3)
     ref = device_ms or host_ms
     if ref:
         m = out["device_ms" if device_ms else "host_launch_ms"]
@@ -156,4 +221,7 @@ def step_stats(device_ms, host_ms, host_before, host_after, outlier_ratio=1.5):
                 % (slow, m["max"] / m["median"], outlier_ratio, [round(host_ms[i], 2) for i in slow if i < len(host_ms)],
                    inv, host_before.get("cpu"), host_after.get("cpu"), host_before.get("loadavg"),
                    host_after.get("loadavg")))
+            if probe:
+                out["warnings"].append("slow steps' host probe: %s" % [dict(step=i, **probe[i]) for i in slow
+                                                                         if i < len(probe)])
     return out

@@ -41,8 +41,9 @@ int ca_gemm_xa(int, int, const bf16_t*, const bf16_t*, const uint8_t*, const flo
                const float*, bf16_t*, uint8_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float, const bf16_t*,
                const uint8_t*, const bf16_t*, const uint8_t*, float*, const bf16_t*, float*, hipStream_t);
 int ca_gemm_xa_dw(const bf16_t*, const bf16_t*, const uint8_t*, const float*, const float*, const float*, long,
-                  const bf16_t*, long, bf16_t*, long, int, int, int, const bf16_t*, const uint8_t*, float*,
-                  const bf16_t*, long, void*, int, float, float*, int, hipStream_t);
+                  const bf16_t*, long, bf16_t*, long, int, int, int, float, const bf16_t*, const uint8_t*,
+                  const bf16_t*, const uint8_t*, float*, const bf16_t*, float*, const bf16_t*, long, void*, int, float,
+                  float*, int, hipStream_t);
 int ca_dgrad_gemm(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float, const bf16_t*,
                   const uint8_t*, const bf16_t*, const uint8_t*, float*, hipStream_t, const bf16_t*, float*);
 int ca_conv_dgrad_bnstats(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
@@ -214,13 +215,15 @@ PYBIND11_MODULE(_C, m) {
           "gemm_xa");
   });
   m.def("gemm_xa_dw", [](u64 src0, u64 src1, u64 mask_in, u64 c0, u64 c1, u64 c2, long lda, u64 B, long ldb, u64 C,
-                         long ldc, int M, int N, int K, u64 z, u64 mask, u64 stats, u64 y, long ldy, u64 dw,
-                         int dw_bf16, float dw_beta, u64 ws, int blocks, u64 s) {
+                         long ldc, int M, int N, int K, float beta, u64 res, u64 res_mask, u64 z, u64 mask, u64 stats,
+                         u64 z2, u64 stats2, u64 y, long ldy, u64 dw, int dw_bf16, float dw_beta, u64 ws, int blocks,
+                         u64 s) {
     const int g = ca_gemm_xa_dw(P(const bf16_t*, src0), P(const bf16_t*, src1), P(const uint8_t*, mask_in),
                                 P(const float*, c0), P(const float*, c1), P(const float*, c2), lda,
-                                P(const bf16_t*, B), ldb, P(bf16_t*, C), ldc, M, N, K, P(const bf16_t*, z),
-                                P(const uint8_t*, mask), P(float*, stats), P(const bf16_t*, y), ldy, P(void*, dw),
-                                dw_bf16, dw_beta, P(float*, ws), blocks, S(s));
+                                P(const bf16_t*, B), ldb, P(bf16_t*, C), ldc, M, N, K, beta, P(const bf16_t*, res),
+                                P(const uint8_t*, res_mask), P(const bf16_t*, z), P(const uint8_t*, mask),
+                                P(float*, stats), P(const bf16_t*, z2), P(float*, stats2), P(const bf16_t*, y), ldy,
+                                P(void*, dw), dw_bf16, dw_beta, P(float*, ws), blocks, S(s));
     check(g < 0 ? g : 0, "gemm_xa_dw");
     return g;
   });

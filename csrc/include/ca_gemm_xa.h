@@ -234,40 +234,44 @@ __device__ __forceinline__ void mfma_gemm_xa(const CoreParams& P, const XaParams
 }
 
 // ----------------------------------------------------------------------------------------
-// XA_BN_BWD with the WEIGHT gradient in the same pass (ResNet stage-1 conv3: K = 4c = 256,
-// N = c = 64).  The unfused schedule writes dz (the BN-backward apply, [M][K]) once as the
-// side output of the input-gradient GEMM and reads it back in the split-K weight-gradient
-// GEMM; here each workgroup owns a contiguous range of 128-row tiles and, for every K step
-// of every tile, runs BOTH products on the transformed dz chunk while it is in LDS:
+// XA_BN_BWD with the WEIGHT gradient in the same pass (ResNet stage-1 1x1 convolutions:
+// conv3, K = 4c = 256 -> N = c = 64; conv1, K = c = 64 -> N = 4c = 256).  The unfused
+// schedule writes dz (the BN-backward apply, [M][K]) and reads it back in the split-K
+// weight-gradient GEMM (and, at the short-K conv1, in a separate input-gradient GEMM);
+// here each workgroup owns a contiguous range of 128-row tiles and, while a transformed dz
+// chunk is in LDS, runs BOTH products on it:
 //
-//   dx[m, n]  = sum_k dz[m, k] W[k, n]        (per tile; the usual dgrad epilogues)
+//   dx[m, n]  = sum_k dz[m, k] W[k, n]        (per tile; the dgrad epilogues: BN statistics,
+//                                             residual-gated / plain beta accumulate)
 //   dW[k, n] += sum_m dz[m, k] y[m, n]        (accumulated in registers over ALL the
 //                                             workgroup's tiles; y = the conv's input)
 //
-// so dz never reaches memory (2 x M x K x 2 bytes less HBM traffic).  dW leaves as one fp32
-// slab per workgroup ([K][N], deterministic; reduced by ca_splitk_reduce).  The dz chunk is
-// read twice from the same LDS image: as the dgrad A operand (row m, 8 consecutive k) and,
-// through ds_read_b64_tr_b16, as the wgrad A operand (row k, 8 consecutive m) -- the
-// read_frag_sw N-contiguous read with this image's (m & 7) chunk swizzle.
-template <int EPI>
+// so dz never reaches memory.  Steps: KS K chunks x NC N chunks of 64 (KS == 1 or NC == 1,
+// KS * NC <= 4: the dW block K x N <= 16K floats = 64 per thread).  With NC > 1 the dz tile
+// (K = 64) is transformed once and reused by every N chunk; each N chunk runs its epilogue.
+// dW leaves as one fp32 slab per workgroup ([K][N], deterministic; ca_splitk_reduce sums
+// them).  The dz chunk is read twice from one LDS image: as the dgrad A operand (row m, 8
+// consecutive k) and, through ds_read_b64_tr_b16, as the wgrad A operand (row k, 8
+// consecutive m) -- the read_frag_sw N-contiguous read with this image's (m & 7) swizzle.
+template <int EPI, int KS, int NC>
 __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaParams& X, const bf16_t* Y, long ldy,
                                                 float* ws, int tiles_per_block) {
+  static_assert((KS == 1 || NC == 1) && KS * NC <= 4 && KS >= 1 && NC >= 1, "dW block <= 256 x 64 / 64 x 256");
   constexpr int BM = 128, BN = 64, WM = 2, WN = 2, NT = 256;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // dgrad: 4 x 2 fragments per wave
-  constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK, Y_ELEMS = BM * BN;
-  constexpr int EPI_LD = EpiLayout<BN>::LD;
-  constexpr int KMAX = 256;           // dW rows held in registers: K <= 256
-  constexpr int KS = KMAX / BK;       // K steps (64-row dW chunks)
-  constexpr int MAIN = A_ELEMS + B_ELEMS + Y_ELEMS;
-  constexpr int SMEM = MAIN > BM * EPI_LD ? MAIN : BM * EPI_LD;
-  constexpr int COEF = 3 * KMAX * 2;  // [A | B | D] fp32 coefficients, resident (shorts)
+  constexpr int A_ELEMS = BM * BK, B_ELEMS = BK * BN, Y_ELEMS = BM * BN;
   constexpr int CPA = A_ELEMS / 8 / NT, CPB = B_ELEMS / 8 / NT, CPY = Y_ELEMS / 8 / NT;
   constexpr int RSTEP = NT / 8;
-  __shared__ __attribute__((aligned(16))) short smem[SMEM + COEF];
-  float* const Cf = reinterpret_cast<float*>(smem + SMEM);
+  constexpr int K = KS * BK, N = NC * BN, STEPS = KS * NC;
+  // LDS: As (dz chunk) | Bs (W chunk) | Ys (y chunk) | coefficients.  The epilogue stages
+  // C and its statistics rows in Bs + Ys (free between the steps' barriers), never in As.
+  constexpr int EPI_SH = B_ELEMS + Y_ELEMS;
+  static_assert(BM * EpiLayout<BN>::LD <= EPI_SH, "C staging must fit Bs + Ys");
+  __shared__ __attribute__((aligned(16))) short smem[A_ELEMS + EPI_SH + 3 * K * 2];
   short* const As = smem;
   short* const Bs = smem + A_ELEMS;
-  short* const Ys = smem + A_ELEMS + B_ELEMS;
+  short* const Ys = Bs + B_ELEMS;
+  float* const Cf = reinterpret_cast<float*>(Ys + Y_ELEMS);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -275,27 +279,27 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
   const int t_beg = blockIdx.x * tiles_per_block;
   int t_end = t_beg + tiles_per_block;
   if (t_end > tiles_m) t_end = tiles_m;
-  const int nk = P.K / BK;  // host: K % 64 == 0, K <= KMAX, N == 64
-  const int K8 = P.K >> 3;
+  constexpr int K8 = K >> 3;
 
   const auto rbw = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(P.B), (short)0,
-                                                     (int)buf_span((long)P.K * P.ldb * 2), 0x00020000);
+                                                     (int)buf_span((long)K * P.ldb * 2), 0x00020000);
   const int arow = tid >> 3, c8 = tid & 7;
 
-  f4v accw[KS][2][2];  // dW: per K chunk, a 32 (k) x 32 (n) block per wave
+  f4v accw[STEPS][2][2];  // dW: per (K chunk, N chunk) step, a 32 (k) x 32 (n) block per wave
 #pragma unroll
-  for (int c = 0; c < KS; ++c)
+  for (int c = 0; c < STEPS; ++c)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) accw[c][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
+  for (int i = tid; i < 3 * K; i += NT) {
+    const int q = i / K, k = i - q * K;
+    Cf[i] = (q == 0 ? X.c0 : (q == 1 ? X.c1 : X.c2))[k];
+  }
+
   s8v a0[CPA], a1[CPA], bw[CPB], yv[CPY];
   uint32_t mb[CPA];
-  for (int i = tid; i < 3 * P.K; i += NT) {
-    const int q = i / P.K, k = i - q * P.K;
-    Cf[q * KMAX + k] = (q == 0 ? X.c0 : (q == 1 ? X.c1 : X.c2))[k];
-  }
 
 #pragma unroll 1
   for (int tm = t_beg; tm < t_end; ++tm) {
@@ -306,14 +310,13 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
                                                        (int)span, 0x00020000);
     const auto r1s = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X.src1 + (long)m0 * P.lda), (short)0,
                                                        (int)span, 0x00020000);
-    const uint32_t mspan = buf_span(rows_left * K8);
     const auto rms = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(X.mask_in ? X.mask_in + (long)m0 * K8 : reinterpret_cast<const uint8_t*>(ca_zero16)),
-        (short)0, X.mask_in ? (int)mspan : 0, 0x00020000);
+        (short)0, X.mask_in ? (int)buf_span(rows_left * K8) : 0, 0x00020000);
     const auto rys = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Y + (long)m0 * ldy), (short)0,
                                                        (int)buf_span(rows_left * ldy * 2), 0x00020000);
 
-    auto gload = [&](int t) {
+    auto load_a = [&](int t) {  // dz sources of K chunk t
       const int k = t * BK + 8 * c8;
 #pragma unroll
       for (int i = 0; i < CPA; ++i) {
@@ -322,20 +325,30 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
         a1[i] = __builtin_bit_cast(s8v, __builtin_amdgcn_raw_buffer_load_b128(r1s, (int)off, 0, 0));
         mb[i] = __builtin_amdgcn_raw_buffer_load_b8(rms, (int)((arow + i * RSTEP) * K8 + (k >> 3)), 0, 0);
       }
+    };
+    auto load_w = [&](int t, int nc) {  // W [K][N] rows k of chunk t, columns of chunk nc
 #pragma unroll
-      for (int i = 0; i < CPB; ++i) {  // W [K][N] rows: chunk (k row, 8-n group)
+      for (int i = 0; i < CPB; ++i) {
         const int c = tid + i * NT, lr = c / (BN / 8), lc = c % (BN / 8);
-        const long off = (long)(t * BK + lr) * P.ldb + 8 * lc;
+        const long off = (long)(t * BK + lr) * P.ldb + nc * BN + 8 * lc;
         bw[i] = __builtin_bit_cast(s8v, __builtin_amdgcn_raw_buffer_load_b128(rbw, (int)(off * 2), 0, 0));
       }
     };
-    auto transform_store = [&](int t) {
+    auto load_y = [&](int nc) {  // conv input rows of this tile, columns of chunk nc (rows past M: zeros)
+#pragma unroll
+      for (int i = 0; i < CPY; ++i) {
+        const int c = tid + i * NT, lr = c / (BN / 8), lc = c % (BN / 8);
+        yv[i] = __builtin_bit_cast(s8v, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rys, (int)(((long)lr * ldy + nc * BN + 8 * lc) * 2), 0, 0));
+      }
+    };
+    auto store_a = [&](int t) {  // transform: dz = A*(dy*relu') + B*z + D  (bn_bwd_apply_kernel)
       const int k = t * BK + 8 * c8;
       f4v cf[3][2];
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        cf[q][0] = *reinterpret_cast<const f4v*>(Cf + q * KMAX + k);
-        cf[q][1] = *reinterpret_cast<const f4v*>(Cf + q * KMAX + k + 4);
+        cf[q][0] = *reinterpret_cast<const f4v*>(Cf + q * K + k);
+        cf[q][1] = *reinterpret_cast<const f4v*>(Cf + q * K + k + 4);
       }
 #pragma unroll
       for (int i = 0; i < CPA; ++i) {
@@ -350,28 +363,26 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
         }
         *reinterpret_cast<s8v*>(As + row * BK + ((c8 ^ (row & 7)) << 3)) = o;
       }
+    };
+    auto store_w = [&]() {
 #pragma unroll
       for (int i = 0; i < CPB; ++i) {
         const int c = tid + i * NT, lr = c / (BN / 8), lc = c % (BN / 8);
         *reinterpret_cast<s8v*>(Bs + lr * BN + ((lc ^ nc_swz<BN>(lr)) << 3)) = bw[i];
       }
     };
+    auto store_y = [&]() {
+#pragma unroll
+      for (int i = 0; i < CPY; ++i) {
+        const int c = tid + i * NT, lr = c / (BN / 8), lc = c % (BN / 8);
+        *reinterpret_cast<s8v*>(Ys + lr * BN + ((lc ^ nc_swz<BN>(lr)) << 3)) = yv[i];
+      }
+    };
 
-    // this tile's conv-input rows y[m0 .. m0+127][0 .. 63] (rows past M read zeros: their dz
-    // rows, = D, then add nothing to dW) and the first K step's operands
-#pragma unroll
-    for (int i = 0; i < CPY; ++i) {
-      const int c = tid + i * NT, lr = c / (BN / 8), lc = c % (BN / 8);
-      yv[i] = __builtin_bit_cast(
-          s8v, __builtin_amdgcn_raw_buffer_load_b128(rys, (int)(((long)lr * ldy + 8 * lc) * 2), 0, 0));
-    }
-    gload(0);
+    load_y(0);
+    load_a(0);
+    load_w(0, 0);
     if (tm == t_beg) __syncthreads();  // the coefficient table is in LDS
-#pragma unroll
-    for (int i = 0; i < CPY; ++i) {
-      const int c = tid + i * NT, lr = c / (BN / 8), lc = c % (BN / 8);
-      *reinterpret_cast<s8v*>(Ys + lr * BN + ((lc ^ nc_swz<BN>(lr)) << 3)) = yv[i];
-    }
 
     f4v acc[FM][FN];
 #pragma unroll
@@ -380,70 +391,81 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
       for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
-    for (int t = 0; t < KS; ++t) {
-      if (t < nk) {
-        transform_store(t);
-        if (t + 1 < nk) gload(t + 1);
-        lgkm_wait0();
-        bar256();
-        // dgrad: dx tile += dz chunk (rows m) x W chunk (loops kept rolled: hoisting every
-        // fragment read of the step would not fit next to the two accumulator sets)
+    for (int s = 0; s < STEPS; ++s) {
+      const int t = s % KS, nc = s / KS;
+      // stage this step's operands (the previous step's readers passed its closing barrier)
+      if (NC == 1 || s == 0) store_a(t);
+      store_w();
+      if (t == 0) store_y();
+      if (s + 1 < STEPS) {  // next step's loads fly during this step's MFMAs (and epilogue)
+        const int t1 = (s + 1) % KS, n1 = (s + 1) / KS;
+        if (NC == 1) load_a(t1);
+        load_w(t1, n1);
+        if (t1 == 0) load_y(n1);
+      }
+      lgkm_wait0();
+      bar256();
+      // dgrad: dx chunk += dz chunk (rows m) x W chunk (loops kept rolled: hoisting every
+      // fragment read of the step would not fit next to the two accumulator sets)
 #pragma unroll 1
-        for (int kk = 0; kk < BK; kk += 32) {
-          bf16x8 af[FM], bfr[FN];
+      for (int kk = 0; kk < BK; kk += 32) {
+        bf16x8 af[FM], bfr[FN];
 #pragma unroll
-          for (int i = 0; i < FM; ++i) af[i] = read_frag_sw<BM, true>(As, wm * (BM / WM) + i * 16, kk, lane);
+        for (int i = 0; i < FM; ++i) af[i] = read_frag_sw<BM, true>(As, wm * (BM / WM) + i * 16, kk, lane);
 #pragma unroll
-          for (int j = 0; j < FN; ++j) bfr[j] = read_frag_sw<BN, false>(Bs, wn * (BN / WN) + j * 16, kk, lane);
-          mfma_acc<FM, FN>(acc, af, bfr);
-        }
-        // wgrad: dW chunk t += dz chunk^T (rows k) x y (rows m); reduction over the tile's 128 rows
+        for (int j = 0; j < FN; ++j) bfr[j] = read_frag_sw<BN, false>(Bs, wn * (BN / WN) + j * 16, kk, lane);
+        mfma_acc<FM, FN>(acc, af, bfr);
+      }
+      // wgrad: dW (chunk t, chunk nc) += dz chunk^T (rows k) x y chunk (rows m), over the tile's rows
 #pragma unroll 1
-        for (int mk = 0; mk < BM; mk += 32) {
-          bf16x8 dzt[2], yf[2];
+      for (int mk = 0; mk < BM; mk += 32) {
+        bf16x8 dzt[2], yf[2];
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            // N-contiguous read of the [m][k] dz image (chunk swizzle m & 7): row k, 8 consecutive m
-            const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-            const int mr = mk + 8 * g + q;
-            const int lc = ((wm * 32 + i * 16) >> 3) + (pp >> 1);
-            const int sub = 4 * (pp & 1);
-            const short* b0 = As + mr * BK + ((lc ^ (mr & 7)) << 3) + sub;
-            const short* b1 = As + (mr + 4) * BK + ((lc ^ ((mr + 4) & 7)) << 3) + sub;
-            s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b0));
-            s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b1));
-            dzt[i] = __builtin_bit_cast(bf16x8, s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
-          }
-#pragma unroll
-          for (int j = 0; j < 2; ++j) yf[j] = read_frag_sw<BN, false>(Ys, wn * 32 + j * 16, mk, lane);
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              accw[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yf[j], dzt[i], accw[t][i][j], 0, 0, 0);
+        for (int i = 0; i < 2; ++i) {
+          // N-contiguous read of the [m][k] dz image (chunk swizzle m & 7): row k, 8 consecutive m
+          const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+          const int mr = mk + 8 * g + q;
+          const int lc = ((wm * 32 + i * 16) >> 3) + (pp >> 1);
+          const int sub = 4 * (pp & 1);
+          const short* b0 = As + mr * BK + ((lc ^ (mr & 7)) << 3) + sub;
+          const short* b1 = As + (mr + 4) * BK + ((lc ^ ((mr + 4) & 7)) << 3) + sub;
+          s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b0));
+          s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b1));
+          dzt[i] = __builtin_bit_cast(bf16x8, s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
         }
-        lgkm_wait0();
-        bar256();
+#pragma unroll
+        for (int j = 0; j < 2; ++j) yf[j] = read_frag_sw<BN, false>(Ys, wn * 32 + j * 16, mk, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            accw[s][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yf[j], dzt[i], accw[s][i][j], 0, 0, 0);
+      }
+      lgkm_wait0();
+      bar256();
+      if (t == KS - 1) {  // dx chunk nc complete
+        gemm_epilogue<BM, BN, WM, WN, EPI, EPI_SH, 1>(P, acc, Bs, m0, nc * BN, tm, tid);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
       }
     }
-    vm_wait<0>();
-    gemm_epilogue<BM, BN, WM, WN, EPI, SMEM, 1>(P, acc, smem, m0, 0, tm, tid);
-    __syncthreads();
   }
-  // dW slab of this workgroup: accw[c][i][j][r] = dW[64c + 32 wm + 16 i + (lane & 15)][32 wn + 16 j + 4 (lane >> 4) + r]
-  float* slab = ws + (long)blockIdx.x * P.K * BN;
+  // dW slab of this workgroup: accw[s][i][j][r] = dW[64 t + 32 wm + 16 i + (lane & 15)][64 nc + 32 wn + 16 j + 4 (lane >> 4) + r]
+  float* slab = ws + (long)blockIdx.x * K * N;
 #pragma unroll
-  for (int c = 0; c < KS; ++c) {
-    if (c < nk) {
+  for (int s = 0; s < STEPS; ++s) {
+    const int t = s % KS, nc = s / KS;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int k = c * BK + wm * 32 + i * 16 + (lane & 15);
-          const int n = wn * 32 + j * 16 + 4 * (lane >> 4);
-          *reinterpret_cast<f4v*>(slab + (long)k * BN + n) = accw[c][i][j];
-        }
-    }
+      for (int j = 0; j < 2; ++j) {
+        const int k = t * BK + wm * 32 + i * 16 + (lane & 15);
+        const int n = nc * BN + wn * 32 + j * 16 + 4 * (lane >> 4);
+        *reinterpret_cast<f4v*>(slab + (long)k * N + n) = accw[s][i][j];
+      }
   }
 }
 

@@ -338,10 +338,28 @@ __global__ void __launch_bounds__(256) xa_gemm_kernel(CoreParams P, XaParams X) 
   mfma_gemm_xa<BM, BN, BKC, EPI, XM>(P, X);
 }
 
-template <int EPI>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) xa_dw_kernel(CoreParams P, XaParams X, const bf16_t* Y, long ldy, float* ws,
-                                                    int tiles_per_block) {
-  mfma_gemm_xa_dw<EPI>(P, X, Y, ldy, ws, tiles_per_block);
+template <int EPI, int KS, int NC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) xa_dw_kernel(
+    CoreParams P, XaParams X, const bf16_t* Y, long ldy, float* ws, int tiles_per_block) {
+  mfma_gemm_xa_dw<EPI, KS, NC>(P, X, Y, ldy, ws, tiles_per_block);
+}
+
+template <int KS, int NC>
+int xa_dw_launch(const CoreParams& p, const XaParams& x, const bf16_t* Y, long ldy, float* ws, int g, int tpb,
+                 hipStream_t s) {
+  if (p.bnz2) {
+    if constexpr (KS == 1) xa_dw_kernel<EPI_BF16_BNR2, KS, NC><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
+    else return -2;
+  } else if (p.res_src) {
+    if constexpr (KS == 1) xa_dw_kernel<EPI_BF16_BNR, KS, NC><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
+    else return -2;
+  } else if (p.bnz) {
+    xa_dw_kernel<EPI_BF16_BN, KS, NC><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
+  } else {
+    xa_dw_kernel<EPI_BF16, KS, NC><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
+  }
+  CA_LAUNCH_CHECK();
+  return 0;
 }
 
 template <bool LB, int EPI, int XM>
@@ -559,33 +577,43 @@ int ca_gemm_xa(int layout, int mode, const bf16_t* src0, const bf16_t* src1, con
 }
 
 // XA_BN_BWD input gradient with the weight gradient in the same pass (ca_gemm_xa.h
-// mfma_gemm_xa_dw): N == 64, K % 64 == 0, K <= 256.  `blocks` workgroups each own a
-// contiguous range of 128-row tiles and write one fp32 dW slab ([K][N]) into ws
-// (blocks * K * N floats); dw (bf16 when dw_bf16, else fp32, [K][N]) = sum of the slabs +
-// dw_beta * dw.  `side` is ignored (dz is never written).  Returns the block count used.
+// mfma_gemm_xa_dw).  Shapes: N == 64 with K in {64, 128, 256} (conv3), or K == 64 with
+// N == 256 (conv1); the dgrad epilogues of ca_gemm_xa layout 1 (BN statistics bnz/bnmask/
+// stats, residual-gated res_src/res_mask, second BN bnz2/stats2 -- the last two at K == 64
+// only) and a plain beta accumulate into C.  `blocks` workgroups each own a contiguous range
+// of 128-row tiles and write one fp32 dW slab ([K][N]) into ws (blocks * K * N floats);
+// dw (bf16 when dw_bf16, else fp32, [K][N]) = sum of the slabs + dw_beta * dw.  dz is never
+// written.  Returns the workgroup count used (>= 1) or a negative code.
 int ca_gemm_xa_dw(const bf16_t* src0, const bf16_t* src1, const uint8_t* mask_in, const float* c0, const float* c1,
                   const float* c2, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N, int K,
-                  const bf16_t* bnz, const uint8_t* bnmask, float* stats, const bf16_t* Y, long ldy, void* dw,
-                  int dw_bf16, float dw_beta, float* ws, int blocks, hipStream_t s) {
-  if (M <= 0 || N != 64 || K % 64 != 0 || K > 256 || lda % 8 != 0 || ldy % 8 != 0 || !src0 || !src1 || !c0 || !c1 ||
-      !c2 || !Y || !dw || !ws || blocks <= 0)
+                  float beta, const bf16_t* res_src, const uint8_t* res_mask, const bf16_t* bnz,
+                  const uint8_t* bnmask, float* stats, const bf16_t* bnz2, float* stats2, const bf16_t* Y, long ldy,
+                  void* dw, int dw_bf16, float dw_beta, float* ws, int blocks, hipStream_t s) {
+  if (M <= 0 || lda % 8 != 0 || ldy % 8 != 0 || ldc % 8 != 0 || !src0 || !src1 || !c0 || !c1 || !c2 || !Y || !dw ||
+      !ws || blocks <= 0)
     return -1;
-  if (bnz && !stats) return -1;
+  if ((bnz && !stats) || (bnz2 && (!bnz || !stats2 || !res_src))) return -1;
   CoreParams p = base_params(src0, lda, B, ldb, C, ldc, M, N, K);
+  p.beta = beta;
+  p.res_src = res_src;
+  p.res_mask = res_mask;
+  p.bnz = bnz;
+  p.bnmask = bnmask;
+  p.stats = stats;
+  p.bnz2 = bnz2;
+  p.stats2 = stats2;
   XaParams x{src0, src1, mask_in, c0, c1, c2, nullptr, nullptr, nullptr};
   const int tiles = (M + 127) / 128;
   const int tpb = (tiles + blocks - 1) / blocks;
   const int g = (tiles + tpb - 1) / tpb;
-  if (bnz) {
-    p.stats = stats;
-    p.bnz = bnz;
-    p.bnmask = bnmask;
-    xa_dw_kernel<EPI_BF16_BN><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
-  } else {
-    xa_dw_kernel<EPI_BF16><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
-  }
-  CA_LAUNCH_CHECK();
-  const int rc = ca_splitk_reduce(ws, g, (long)K * N, dw, dw_bf16, dw_beta, s);
+  int rc;
+  if (N == 64 && K == 64) rc = xa_dw_launch<1, 1>(p, x, Y, ldy, ws, g, tpb, s);
+  else if (N == 64 && K == 128) rc = xa_dw_launch<2, 1>(p, x, Y, ldy, ws, g, tpb, s);
+  else if (N == 64 && K == 256) rc = xa_dw_launch<4, 1>(p, x, Y, ldy, ws, g, tpb, s);
+  else if (K == 64 && N == 256) rc = xa_dw_launch<1, 4>(p, x, Y, ldy, ws, g, tpb, s);
+  else return -1;
+  if (rc < 0) return rc;
+  rc = ca_splitk_reduce(ws, g, (long)K * N, dw, dw_bf16, dw_beta, s);
   return rc < 0 ? rc : g;
 }
 

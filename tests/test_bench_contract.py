@@ -44,6 +44,10 @@ def test_bench_two_ranks_via_run_cpu(tmp_path):
     ss = j["step_stats_rank0"]
     assert ss["host_launch_ms"]["min"] <= ss["host_launch_ms"]["median"] <= ss["host_launch_ms"]["max"]
     assert ss["host_before"]["n_affinity"] >= 1 and isinstance(j["warnings"], list)
+    # per-step host evidence for slow-step diagnosis: GC pauses, page faults, allocator segments
+    assert len(ss["probe_steps"]) == 2 and len(ss["host_launch_ms_steps"]) == 2
+    assert {"gc_ms", "gc_gen", "minflt", "majflt", "dev_alloc"} <= set(ss["probe_steps"][0])
+    assert j["gc_frozen_objects"] > 0  # runtime.gc_control.freeze() ran after warmup
     job = os.listdir(tmp_path / "jobs")
     assert len(job) == 1
     meta = json.load(open(tmp_path / "jobs" / job[0] / "job.json"))
@@ -64,3 +68,35 @@ def test_bench_world_mismatch_is_an_error(tmp_path):
                        cwd=str(tmp_path))
     assert r.returncode == 3, r.stderr[-2000:]
     assert "WORLD_SIZE=1" in r.stderr and not _json_lines(r.stdout)
+
+
+def test_step_stats_names_gc_pause_of_slow_step():
+    """A slow step's warning carries the probe row of that step (here: a 3 s GC pause)."""
+    sys.path.insert(0, ROOT)
+    from cloud_amd.utils import benchlaunch
+
+    dev = [70.0] * 5 + [3100.0] + [70.0] * 4
+    host = [60.0] * 5 + [3300.0] + [60.0] * 4
+    probe = [{"gc_ms": 0.0, "gc_gen": -1, "minflt": 10, "majflt": 0, "dev_alloc": 0, "dev_free": 0,
+              "alloc_retry": 0} for _ in dev]
+    probe[5].update(gc_ms=3050.0, gc_gen=2, majflt=812)
+    st = benchlaunch.step_stats(dev, host, {"ctx_involuntary": 1}, {"ctx_involuntary": 2}, probe=probe)
+    assert len(st["warnings"]) == 2 and "slow steps [5]" in st["warnings"][0]
+    assert "'gc_ms': 3050.0" in st["warnings"][1] and "'majflt': 812" in st["warnings"][1]
+    assert st["gc_ms_total"] == 3050.0
+
+
+def test_gc_freeze_control(monkeypatch):
+    import gc
+
+    sys.path.insert(0, ROOT)
+    from cloud_amd.runtime import gc_control
+
+    monkeypatch.setenv("CLOUD_AMD_GC_FREEZE", "0")
+    assert gc_control.freeze() == 0
+    monkeypatch.setenv("CLOUD_AMD_GC_FREEZE", "1")
+    try:
+        assert gc_control.freeze() > 0 and gc.get_freeze_count() > 0
+    finally:
+        gc_control.unfreeze()
+    assert gc.get_freeze_count() == 0

@@ -71,17 +71,22 @@ def test_dgrad_bnbwd_vs_fp32(M, Cout, Cin, epi):
         assert rel(s, gd.sum(0)) < 1e-3 and rel(q, (gd * zb.float()).sum(0)) < 1e-3
 
 
-@pytest.mark.parametrize("M,Cout", [(4096, 256), (1000, 128), (777, 64), (300, 192), (70000, 256)])
+DW_CASES = [(4096, 256, 64, "bn"), (1000, 128, 64, "bn"), (777, 64, 64, "plain"), (70000, 256, 64, "bn"),
+            (4096, 256, 64, "plain"), (3000, 64, 256, "res2"), (1000, 64, 256, "res"), (777, 64, 256, "bn"),
+            (300, 64, 64, "res"), (5000, 64, 256, "plain")]
+
+
+@pytest.mark.parametrize("M,Cout,Cin,epi", DW_CASES)
 @pytest.mark.parametrize("blocks", [None, 3])
 @pytest.mark.parametrize("dw_dtype", [torch.bfloat16, torch.float32])
-def test_dgrad_wgrad_bnbwd_vs_fp32(M, Cout, blocks, dw_dtype):
+def test_dgrad_wgrad_bnbwd_vs_fp32(M, Cout, Cin, epi, blocks, dw_dtype):
     """Input AND weight gradient of the BN-folded 1x1 conv in one pass (mfma_gemm_xa_dw):
-    dz = A*(dy*relu') + B*z + D is never written; dx = dz W with the BN-statistics epilogue,
-    dw = dz^T y + dw_old -- each against a plain fp32 PyTorch reference."""
+    dz = A*(dy*relu') + B*z + D is never written; dx = dz W (+ beta * old / residual-gated
+    source) with the BN-statistics epilogues, dw = dz^T y + dw_old -- each against a plain fp32
+    PyTorch reference.  conv3 shapes (Cin 64, K chunks) and conv1 shapes (Cout 64, N chunks)."""
     from cloud_amd.ops import raw
 
-    Cin = 64
-    torch.manual_seed(M + Cout)
+    torch.manual_seed(M + Cout + Cin)
     dy = torch.randn(M, Cout, device=DEV).to(torch.bfloat16)
     z = torch.randn(M, Cout, device=DEV).to(torch.bfloat16)
     act = torch.rand(M, Cout, device=DEV) > 0.4
@@ -89,20 +94,39 @@ def test_dgrad_wgrad_bnbwd_vs_fp32(M, Cout, blocks, dw_dtype):
     w = (torch.randn(Cout, 1, 1, Cin, device=DEV) * 0.05).to(torch.bfloat16)
     y = torch.randn(M, Cin, device=DEV).to(torch.bfloat16)
     zb = torch.randn(M, Cin, device=DEV).to(torch.bfloat16)
+    z2 = torch.randn(M, Cin, device=DEV).to(torch.bfloat16)
     act_b = torch.rand(M, Cin, device=DEV) > 0.5
+    src = torch.randn(M, Cin, device=DEV).to(torch.bfloat16)
+    act_r = torch.rand(M, Cin, device=DEV) > 0.5
+    old = torch.randn(M, Cin, device=DEV).to(torch.bfloat16)
     dw0 = (torch.randn(Cout, 1, 1, Cin, device=DEV) * 0.1).to(dw_dtype)
     dw = dw0.clone()
     A, B, D = coef[:Cout], coef[Cout:2 * Cout], coef[2 * Cout:]
     dz = (A * dy.float() * act.float() + B * z.float() + D).to(torch.bfloat16).float()
     shp = lambda t: t.view(1, 1, M, -1)  # noqa: E731
-    dx, part = raw.conv1x1_dgrad_wgrad_bnbwd(shp(dy), shp(z), _mask_bits(act), coef, w, shp(y), dw,
-                                             bn=(shp(zb), _mask_bits(act_b)), dw_beta=1.0, blocks=blocks)
-    dx_ref = dz @ w.view(Cout, Cin).float()
-    assert rel(dx.view(M, Cin), dx_ref) < 2e-2, rel(dx.view(M, Cin), dx_ref)
+    kw = {}
+    want = dz @ w.view(Cout, Cin).float()
+    if epi in ("bn", "res", "res2"):
+        kw["bn"] = (shp(zb), _mask_bits(act_b)) + ((shp(z2),) if epi == "res2" else ())
+    if epi in ("res", "res2"):
+        kw.update(res=(shp(src), _mask_bits(act_r)), beta=1.0)
+        want = want + src.float() * act_r.float()
+    if epi == "plain":  # beta accumulate into the existing dx (the projection block's shortcut gradient)
+        kw.update(out=shp(old.clone()), beta=1.0)
+        want = want + old.float()
+    r = raw.conv1x1_dgrad_wgrad_bnbwd(shp(dy), shp(z), _mask_bits(act), coef, w, shp(y), dw, dw_beta=1.0,
+                                      blocks=blocks, **kw)
+    dx = r[0] if isinstance(r, tuple) else r
+    assert rel(dx.view(M, Cin), want) < 2e-2, rel(dx.view(M, Cin), want)
     dw_ref = dz.t() @ y.float() + dw0.view(Cout, Cin).float()
     assert rel(dw.view(Cout, Cin), dw_ref) < 1e-2, rel(dw.view(Cout, Cin), dw_ref)
-    gd = dx.view(M, Cin).float() * act_b.float()
-    assert rel(part[:, 0].sum(0), gd.sum(0)) < 1e-3 and rel(part[:, 1].sum(0), (gd * zb.float()).sum(0)) < 1e-3
+    if "bn" in kw:
+        gd = dx.view(M, Cin).float() * act_b.float()
+        part = r[1]
+        assert rel(part[:, 0].sum(0), gd.sum(0)) < 1e-3 and rel(part[:, 1].sum(0), (gd * zb.float()).sum(0)) < 1e-3
+        if epi == "res2":
+            p2 = r[2]
+            assert rel(p2[:, 0].sum(0), gd.sum(0)) < 1e-3 and rel(p2[:, 1].sum(0), (gd * z2.float()).sum(0)) < 1e-3
 
 
 @pytest.mark.parametrize("M,Cin,Cout", [(4096, 256, 64), (1000, 512, 128), (777, 64, 256), (300, 40, 72)])
@@ -143,6 +167,7 @@ def test_fwd_bnapply_vs_fp32(M, Cin, Cout, mode):
 
 def _train(fold, steps=3, wgrad_fused=False):
     os.environ["CLOUD_AMD_BN_FOLD_WGRAD"] = "1" if wgrad_fused else "0"
+    os.environ["CLOUD_AMD_BN_FOLD_WGRAD1"] = "1" if wgrad_fused else "0"
     os.environ["CLOUD_AMD_BN_FOLD"] = "1" if fold else "0"
     os.environ["CLOUD_AMD_BN_FOLD_FWD"] = "1" if fold else "0"
     os.environ["CLOUD_AMD_BN_FOLD_ALL"] = "1"  # every site, not only the ones the default policy keeps
@@ -196,6 +221,7 @@ def test_resnet_bn_fold_bitwise(monkeypatch):
         os.environ.pop("CLOUD_AMD_BN_FOLD_FWD", None)
         os.environ.pop("CLOUD_AMD_BN_FOLD_ALL", None)
         os.environ.pop("CLOUD_AMD_BN_FOLD_WGRAD", None)
+        os.environ.pop("CLOUD_AMD_BN_FOLD_WGRAD1", None)
     # 7 blocks: bwd folds bn3 (6 blocks get their partials from the next block) and bn1 (7);
     # fwd folds bn3 into the next conv1 (6 hand-offs) and bn2 into conv3 (all but layer 1's prw)
     assert n_fold["bwd"] > 0 and n_fold["fwd"] > 0, n_fold
@@ -236,7 +262,8 @@ def test_resnet_fused_dgrad_wgrad_close():
         g0, l0, _ = _train(True, steps=2, wgrad_fused=False)
     finally:
         raw.conv1x1_dgrad_wgrad_bnbwd = real
-        for k in ("CLOUD_AMD_BN_FOLD", "CLOUD_AMD_BN_FOLD_FWD", "CLOUD_AMD_BN_FOLD_ALL", "CLOUD_AMD_BN_FOLD_WGRAD"):
+        for k in ("CLOUD_AMD_BN_FOLD", "CLOUD_AMD_BN_FOLD_FWD", "CLOUD_AMD_BN_FOLD_ALL", "CLOUD_AMD_BN_FOLD_WGRAD",
+                  "CLOUD_AMD_BN_FOLD_WGRAD1"):
             os.environ.pop(k, None)
     assert calls["n"] > 0
     for ai, (x, y) in enumerate(zip(g1[0], g0[0])):
