@@ -288,7 +288,8 @@ class _BottleneckFn(torch.autograd.Function):
             coef3 = bn_coef(blk.bn3, z3, s3, p3)
             dres = None
             c3 = blk.conv3
-            if config.get("CLOUD_AMD_BN_FOLD_WGRAD") and raw.dgrad_wgrad_fusable(c3.cout, c3.cin):
+            if (config.get("CLOUD_AMD_BN_FOLD_WGRAD") and raw.dgrad_wgrad_fusable(c3.cout, c3.cin)
+                    and (c3.cin == 64 or config.get("CLOUD_AMD_BN_FOLD_WGRAD2"))):
                 # ... and conv3's weight gradient in the same pass: dz3 never reaches memory
                 dy2, p2 = raw.conv1x1_dgrad_wgrad_bnbwd(dout, z3, m3, coef3, c3.weight, y2, c3.weight.grad,
                                                         bn=(z2, m2), dw_beta=1.0)

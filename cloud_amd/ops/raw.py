@@ -247,8 +247,9 @@ def conv1x1_dgrad_bnbwd(dy, z, mask, coef, w, side, out=None, beta=0.0, bn=None,
 def dgrad_wgrad_fusable(cout, cin):
     """Shapes the fused input+weight gradient kernel (:func:`conv1x1_dgrad_wgrad_bnbwd`) takes
     (``ca_gemm_xa_dw``): 64 input channels with 64 / 128 / 256 output channels (ResNet stage-1
-    conv3), or 64 output channels with 256 input channels (stage-1 conv1)."""
-    return (cin == 64 and cout in (64, 128, 256)) or (cout == 64 and cin == 256)
+    conv3), 64 output channels with 256 input channels (stage-1 conv1), 128 input channels with
+    512 output channels (stage-2 conv3, 8-wave workgroups)."""
+    return (cin == 64 and cout in (64, 128, 256)) or (cout == 64 and cin == 256) or (cin == 128 and cout == 512)
 
 
 def conv1x1_dgrad_wgrad_bnbwd(dy, z, mask, coef, w, y, dw, out=None, beta=0.0, bn=None, res=None, dw_beta=1.0,
@@ -283,8 +284,8 @@ def conv1x1_dgrad_wgrad_bnbwd(dy, z, mask, coef, w, y, dw, out=None, beta=0.0, b
             assert res is not None, "second-BN statistics need the residual-gated (res=) form"
             part2 = torch.empty_like(part)
             z2p = bn[2].data_ptr()
-    if blocks is None:
-        blocks = 2 * _cu_count(dy.device)
+    if blocks is None:  # 4-wave workgroups two per CU, 8-wave (Cin 128) one per CU
+        blocks = (1 if Cin == 128 else 2) * _cu_count(dy.device)
     blocks = max(1, min(int(blocks), (M + 127) // 128))
     ws = torch.empty(blocks * Cout * Cin, dtype=torch.float32, device=dy.device)
     cp = coef.data_ptr()

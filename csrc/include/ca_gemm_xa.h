@@ -253,11 +253,17 @@ __device__ __forceinline__ void mfma_gemm_xa(const CoreParams& P, const XaParams
 // them).  The dz chunk is read twice from one LDS image: as the dgrad A operand (row m, 8
 // consecutive k) and, through ds_read_b64_tr_b16, as the wgrad A operand (row k, 8
 // consecutive m) -- the read_frag_sw N-contiguous read with this image's (m & 7) swizzle.
-template <int EPI, int KS, int NC>
+//
+// BN = 64 with 4 waves (stage 1), or BN = 128 with 8 waves (stage 2 conv3: K = 512 -> N = 128,
+// a 512 x 128 dW block = 128 fp32 per lane, one workgroup per CU): waves 2 (M) x BN/32 (N) for
+// the dgrad tile, 2 (k) x BN/32 (n) 32 x 32 blocks of each dW chunk.
+template <int EPI, int KS, int NC, int BN = 64, int NT = 256>
 __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaParams& X, const bf16_t* Y, long ldy,
                                                 float* ws, int tiles_per_block) {
-  static_assert((KS == 1 || NC == 1) && KS * NC <= 4 && KS >= 1 && NC >= 1, "dW block <= 256 x 64 / 64 x 256");
-  constexpr int BM = 128, BN = 64, WM = 2, WN = 2, NT = 256;
+  static_assert((KS == 1 || NC == 1) && KS >= 1 && NC >= 1, "K chunks or N chunks, not both");
+  static_assert(KS * NC * 16 <= (NT == 512 ? 128 : 64), "dW block: <= 64 (4 waves) / 128 (8 waves) fp32 per lane");
+  static_assert((BN == 64 && NT == 256) || (BN == 128 && NT == 512), "4 waves x 64 columns or 8 waves x 128");
+  constexpr int BM = 128, WN = BN / 32, WM = NT / 64 / WN;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // dgrad: 4 x 2 fragments per wave
   constexpr int A_ELEMS = BM * BK, B_ELEMS = BK * BN, Y_ELEMS = BM * BN;
   constexpr int CPA = A_ELEMS / 8 / NT, CPB = B_ELEMS / 8 / NT, CPY = Y_ELEMS / 8 / NT;

@@ -338,25 +338,25 @@ __global__ void __launch_bounds__(256) xa_gemm_kernel(CoreParams P, XaParams X) 
   mfma_gemm_xa<BM, BN, BKC, EPI, XM>(P, X);
 }
 
-template <int EPI, int KS, int NC>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) xa_dw_kernel(
+template <int EPI, int KS, int NC, int BN, int NT>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) xa_dw_kernel(
     CoreParams P, XaParams X, const bf16_t* Y, long ldy, float* ws, int tiles_per_block) {
-  mfma_gemm_xa_dw<EPI, KS, NC>(P, X, Y, ldy, ws, tiles_per_block);
+  mfma_gemm_xa_dw<EPI, KS, NC, BN, NT>(P, X, Y, ldy, ws, tiles_per_block);
 }
 
-template <int KS, int NC>
+template <int KS, int NC, int BN = 64, int NT = 256>
 int xa_dw_launch(const CoreParams& p, const XaParams& x, const bf16_t* Y, long ldy, float* ws, int g, int tpb,
                  hipStream_t s) {
   if (p.bnz2) {
-    if constexpr (KS == 1) xa_dw_kernel<EPI_BF16_BNR2, KS, NC><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
+    if constexpr (KS == 1) xa_dw_kernel<EPI_BF16_BNR2, KS, NC, BN, NT><<<g, NT, 0, s>>>(p, x, Y, ldy, ws, tpb);
     else return -2;
   } else if (p.res_src) {
-    if constexpr (KS == 1) xa_dw_kernel<EPI_BF16_BNR, KS, NC><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
+    if constexpr (KS == 1) xa_dw_kernel<EPI_BF16_BNR, KS, NC, BN, NT><<<g, NT, 0, s>>>(p, x, Y, ldy, ws, tpb);
     else return -2;
   } else if (p.bnz) {
-    xa_dw_kernel<EPI_BF16_BN, KS, NC><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
+    xa_dw_kernel<EPI_BF16_BN, KS, NC, BN, NT><<<g, NT, 0, s>>>(p, x, Y, ldy, ws, tpb);
   } else {
-    xa_dw_kernel<EPI_BF16, KS, NC><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
+    xa_dw_kernel<EPI_BF16, KS, NC, BN, NT><<<g, NT, 0, s>>>(p, x, Y, ldy, ws, tpb);
   }
   CA_LAUNCH_CHECK();
   return 0;
@@ -577,8 +577,8 @@ int ca_gemm_xa(int layout, int mode, const bf16_t* src0, const bf16_t* src1, con
 }
 
 // XA_BN_BWD input gradient with the weight gradient in the same pass (ca_gemm_xa.h
-// mfma_gemm_xa_dw).  Shapes: N == 64 with K in {64, 128, 256} (conv3), or K == 64 with
-// N == 256 (conv1); the dgrad epilogues of ca_gemm_xa layout 1 (BN statistics bnz/bnmask/
+// mfma_gemm_xa_dw).  Shapes: N == 64 with K in {64, 128, 256} (stage-1 conv3), K == 64 with
+// N == 256 (stage-1 conv1), N == 128 with K == 512 (stage-2 conv3, 8-wave workgroups); the dgrad epilogues of ca_gemm_xa layout 1 (BN statistics bnz/bnmask/
 // stats, residual-gated res_src/res_mask, second BN bnz2/stats2 -- the last two at K == 64
 // only) and a plain beta accumulate into C.  `blocks` workgroups each own a contiguous range
 // of 128-row tiles and write one fp32 dW slab ([K][N]) into ws (blocks * K * N floats);
@@ -611,6 +611,7 @@ int ca_gemm_xa_dw(const bf16_t* src0, const bf16_t* src1, const uint8_t* mask_in
   else if (N == 64 && K == 128) rc = xa_dw_launch<2, 1>(p, x, Y, ldy, ws, g, tpb, s);
   else if (N == 64 && K == 256) rc = xa_dw_launch<4, 1>(p, x, Y, ldy, ws, g, tpb, s);
   else if (K == 64 && N == 256) rc = xa_dw_launch<1, 4>(p, x, Y, ldy, ws, g, tpb, s);
+  else if (N == 128 && K == 512) rc = xa_dw_launch<8, 1, 128, 512>(p, x, Y, ldy, ws, g, tpb, s);
   else return -1;
   if (rc < 0) return rc;
   rc = ca_splitk_reduce(ws, g, (long)K * N, dw, dw_bf16, dw_beta, s);

@@ -73,7 +73,8 @@ def test_dgrad_bnbwd_vs_fp32(M, Cout, Cin, epi):
 
 DW_CASES = [(4096, 256, 64, "bn"), (1000, 128, 64, "bn"), (777, 64, 64, "plain"), (70000, 256, 64, "bn"),
             (4096, 256, 64, "plain"), (3000, 64, 256, "res2"), (1000, 64, 256, "res"), (777, 64, 256, "bn"),
-            (300, 64, 64, "res"), (5000, 64, 256, "plain")]
+            (300, 64, 64, "res"), (5000, 64, 256, "plain"), (5000, 512, 128, "bn"), (777, 512, 128, "plain"),
+            (100000, 512, 128, "bn")]
 
 
 @pytest.mark.parametrize("M,Cout,Cin,epi", DW_CASES)
