@@ -511,6 +511,11 @@ class Model(Layer):
         from ..utils import faults
 
         global_step = 0
+        from ..runtime import gc_control
+
+        if getattr(self, "_ca_gc_frozen", False):  # a previous fit ended by an exception
+            gc_control.unfreeze()
+            self._ca_gc_frozen = False
         for epoch in range(initial_epoch, epochs):
             self._reset_metrics()
             callbacks_.on_epoch_begin(epoch, {})
@@ -542,9 +547,7 @@ class Model(Layer):
                 step += 1
                 global_step += 1
                 if global_step == 3:  # model, optimizer state and kernel caches exist now
-                    from ..runtime import gc_control
-
-                    gc_control.freeze()
+                    self._ca_gc_frozen = gc_control.freeze() > 0
                 if self.stop_training:
                     break
             logs = self._logs()
@@ -559,10 +562,9 @@ class Model(Layer):
             if self.stop_training:
                 break
         callbacks_.on_train_end({})
-        if global_step >= 3:
-            from ..runtime import gc_control
-
+        if getattr(self, "_ca_gc_frozen", False):
             gc_control.unfreeze()  # this fit's objects may become garbage (tuner workers run many fits)
+            self._ca_gc_frozen = False
         self.history = history
         return history
 

@@ -25,3 +25,15 @@ def test_knobs(monkeypatch):
     assert _fold_site(256, 64) and not _fold_site(512, 128)
     monkeypatch.setenv("CLOUD_AMD_BN_FOLD_ALL", "1")
     assert _fold_site(64, 256) and _fold_site(512, 128)
+
+
+def test_fused_weight_gradient_shapes():
+    """One-pass input + weight gradient (ca_gemm_xa_dw): the dW block must fit the
+    registers of a workgroup -- stage-1 conv3 (K 256 -> N 64) and conv1 (K 64 -> N 256) with
+    4 waves, stage-2 conv3 (K 512 -> N 128) with 8 waves; nothing wider."""
+    from cloud_amd.ops.raw import dgrad_wgrad_fusable
+
+    assert dgrad_wgrad_fusable(256, 64) and dgrad_wgrad_fusable(64, 256) and dgrad_wgrad_fusable(64, 64)
+    assert dgrad_wgrad_fusable(512, 128)
+    assert not dgrad_wgrad_fusable(1024, 256) and not dgrad_wgrad_fusable(128, 512)
+    assert not dgrad_wgrad_fusable(2048, 512) and not dgrad_wgrad_fusable(256, 1024)
