@@ -110,6 +110,7 @@ def main():
     from cloud_amd.optim import SGD
     from cloud_amd.parallel import strategy as strategy_mod
     from cloud_amd.runtime import gc_control
+    from cloud_amd.runtime.step_pacer import StepPacer
     from cloud_amd.utils import dist_env, trace
 
     if args.device == "cpu":
@@ -179,8 +180,12 @@ def main():
     # (HIP-graph capture of this step measured slower than eager on ROCm 7.2 at b256/b512:
     # kernel boundaries cost the same in a graph; not offered here -- docs/performance.md)
     step_fn = train_step
+    # at most CLOUD_AMD_MAX_STEPS_IN_FLIGHT steps queued ahead of the GPU (warmup and timed
+    # steps alike), so the caching allocator's pool is complete before the timed region
+    pacer = StepPacer(device)
     for _ in range(max(args.warmup - 1, 0)):
         loss = step_fn()
+        pacer.step_done()
     # desync check once after warmup (world > 1): every replica must hold identical
     # all-reduced gradients (fp64 fingerprint over all arenas, all-gathered)
     replicas_consistent = None
@@ -207,9 +212,10 @@ def main():
     for i in range(args.steps):
         th = time.perf_counter()
         loss = step_fn()
-        host_ms.append((time.perf_counter() - th) * 1e3)
         if evs:
             evs[i + 1].record()
+        pacer.step_done()
+        host_ms.append((time.perf_counter() - th) * 1e3)
         step_probe.mark()
     sync()
     dist_env.barrier()
@@ -273,6 +279,7 @@ def main():
             "replicas_consistent": replicas_consistent,
             "step_stats_rank0": step_stats,
             "gc_frozen_objects": gc_frozen,
+            "max_steps_in_flight": pacer.depth if pacer.enabled else None,
             "warnings": step_stats.pop("warnings"),
             "rank_ms_per_step": {"min": round(min(per_rank_ms), 3), "max": round(max(per_rank_ms), 3)},
             "first_step_latency_s": round(first_lat, 3),

@@ -65,6 +65,8 @@ _VARS = [
     Var("CLOUD_AMD_DENSE_WGRAD_BLOCKS", int, 1024, "dense-layer weight gradients (BERT): split-K workgroup target "
         "(1024 with the split-major XCD mapping: 6,210 / 6,231 vs 6,153 / 6,131 seq/s at 512)",
         "ops"),
+    Var("CLOUD_AMD_DENSE_WGRAD_256", bool, True, "dense-layer weight gradients whose 256 x 256 tiles times a split "
+        "count fill one round of the chip (BERT QKV / FFN) run on the two-phase 256 core with that split", "ops"),
     Var("CLOUD_AMD_TAPMASK", bool, True, "convolutions: tap-mask / incremental buffer-mode gather loaders; 0 keeps "
         "the general per-chunk decode loaders (A/B runs)", "ops"),
     Var("CLOUD_AMD_SPLIT_XCD", bool, True, "split-K GEMM/conv grids: give each XCD contiguous (split, tile) "
@@ -110,6 +112,9 @@ _VARS = [
         "bn1's backward apply (K = 64 -> N = 256: dz1 never written, four output chunks per tile)", "ops"),
     Var("CLOUD_AMD_BN_FOLD_ALL", bool, False, "fold every BN site regardless of CLOUD_AMD_BN_FOLD_MAX_N (tests, A/B)",
         "ops"),
+    Var("CLOUD_AMD_MAX_STEPS_IN_FLIGHT", int, 2, "training loops (benches, Keras fit) let the host enqueue at most this "
+        "many steps ahead of the GPU (runtime.step_pacer); bounds the memory in flight so the caching allocator "
+        "stops requesting segments after warmup; 0 = unbounded", "runtime"),
     Var("CLOUD_AMD_GC_FREEZE", bool, True, "training loops (benches, Keras fit) call runtime.gc_control.freeze() after "
         "their first steps: objects alive then are excluded from Python's full collections", "runtime"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "

@@ -513,6 +513,9 @@ class Model(Layer):
         global_step = 0
         from ..runtime import gc_control
 
+        from ..runtime.step_pacer import StepPacer
+
+        pacer = StepPacer(s.device)  # at most CLOUD_AMD_MAX_STEPS_IN_FLIGHT steps queued ahead of the GPU
         if getattr(self, "_ca_gc_frozen", False):  # a previous fit ended by an exception
             gc_control.unfreeze()
             self._ca_gc_frozen = False
@@ -539,6 +542,7 @@ class Model(Layer):
                 world = s.num_replicas_in_sync
                 w = (n_local * world / n_global) if world > 1 else 1.0
                 loss = self.train_step(xb, yb, loss_weight=w, n_real=n_local)
+                pacer.step_done()
                 if mon:  # host-side step period (the device queue evens it out over steps)
                     now = time.perf_counter()
                     monitoring.observe(monitoring.STEP_TIME, (now - t_prev) * 1e3)

@@ -631,6 +631,25 @@ class deferred_finalize:
         return False
 
 
+def _wgrad_splits_256(n_out, k_in, kred):
+    """Split count that puts a dense weight gradient on ONE round of the two-phase 256 x 256
+    core (csrc/kernels/gemm.hip use_256: 224-256 workgroups of 256 x 256 tiles, >= 512
+    reduction rows each), e.g. BERT's QKV (27 tiles x 9 splits), FFN1 / FFN2 (36 x 7); 0 when
+    the shape does not fit one round (``CLOUD_AMD_DENSE_WGRAD_256=0``: never)."""
+    from .. import config
+
+    if not config.get("CLOUD_AMD_DENSE_WGRAD_256"):
+        return 0
+    t256 = -(-n_out // 256) * -(-k_in // 256)
+    if t256 > 128:
+        return 0
+    ext = _ext.load(required=True)
+    s = ext.gemm_splitk_effective(kred, 256 // t256)
+    if not 224 <= t256 * s <= 256 or kred // s < 512:
+        return 0
+    return s
+
+
 def wgrad_into(dy, x, out, beta=1.0):
     """out[N_out, K_in] (+)= dy[M, N_out]^T @ x[M, K_in] (split-K over M), bf16 or fp32 out."""
     global _DENSE_WGRAD_BLOCKS
@@ -642,8 +661,10 @@ def wgrad_into(dy, x, out, beta=1.0):
     M, n_out = dy.shape
     k_in = x.shape[1]
     # dense layers: K = tokens is moderate, so fewer/larger K slices (less slab traffic).
-    # (A one-round 256 x 256 ring-core variant measured slower on BERT and was removed.)
     splits = ext.gemm_splitk_effective(M, wgrad_splits(n_out, k_in, M, target_blocks=_DENSE_WGRAD_BLOCKS, min_k=1024))
+    s256 = _wgrad_splits_256(n_out, k_in, M)
+    if s256:
+        splits = s256
     ws = torch.empty(splits * n_out * k_in, dtype=torch.float32, device=dy.device)
     fb = _FIN_BATCH
     ext.gemm_splitk(TN, dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
