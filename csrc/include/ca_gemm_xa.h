@@ -307,20 +307,30 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
   s8v a0[CPA], a1[CPA], bw[CPB], yv[CPY];
   uint32_t mb[CPA];
 
+  // per-tile operand windows (buffer resources; rows past M read zeros), switched to the NEXT
+  // tile during the last step of the current one so that tile's first loads fly during this
+  // tile's last MFMAs and its epilogue
+  __amdgpu_buffer_rsrc_t r0s, r1s, rms, rys;
+  auto set_tile = [&](int t) {
+    const int mt = t * BM;
+    const long rl = (long)P.M - mt;
+    const uint32_t span = buf_span(rl * P.lda * 2);
+    r0s = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X.src0 + (long)mt * P.lda), (short)0, (int)span,
+                                            0x00020000);
+    r1s = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X.src1 + (long)mt * P.lda), (short)0, (int)span,
+                                            0x00020000);
+    rms = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(X.mask_in ? X.mask_in + (long)mt * K8 : reinterpret_cast<const uint8_t*>(ca_zero16)),
+        (short)0, X.mask_in ? (int)buf_span(rl * K8) : 0, 0x00020000);
+    rys = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Y + (long)mt * ldy), (short)0,
+                                            (int)buf_span(rl * ldy * 2), 0x00020000);
+  };
+  bool prefetched = false;
+
 #pragma unroll 1
   for (int tm = t_beg; tm < t_end; ++tm) {
     const int m0 = tm * BM;
-    const long rows_left = (long)P.M - m0;
-    const uint32_t span = buf_span(rows_left * P.lda * 2);
-    const auto r0s = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X.src0 + (long)m0 * P.lda), (short)0,
-                                                       (int)span, 0x00020000);
-    const auto r1s = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X.src1 + (long)m0 * P.lda), (short)0,
-                                                       (int)span, 0x00020000);
-    const auto rms = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(X.mask_in ? X.mask_in + (long)m0 * K8 : reinterpret_cast<const uint8_t*>(ca_zero16)),
-        (short)0, X.mask_in ? (int)buf_span(rows_left * K8) : 0, 0x00020000);
-    const auto rys = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Y + (long)m0 * ldy), (short)0,
-                                                       (int)buf_span(rows_left * ldy * 2), 0x00020000);
+    if (!prefetched) set_tile(tm);
 
     auto load_a = [&](int t) {  // dz sources of K chunk t
       const int k = t * BK + 8 * c8;
@@ -385,9 +395,12 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
       }
     };
 
-    load_y(0);
-    load_a(0);
-    load_w(0, 0);
+    if (!prefetched) {
+      load_y(0);
+      load_a(0);
+      load_w(0, 0);
+    }
+    prefetched = false;
     if (tm == t_beg) __syncthreads();  // the coefficient table is in LDS
 
     f4v acc[FM][FN];
@@ -408,6 +421,12 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
         if (NC == 1) load_a(t1);
         load_w(t1, n1);
         if (t1 == 0) load_y(n1);
+      } else if (tm + 1 < t_end) {  // the next tile's first step
+        set_tile(tm + 1);
+        load_y(0);
+        load_a(0);
+        load_w(0, 0);
+        prefetched = true;
       }
       lgkm_wait0();
       bar256();
