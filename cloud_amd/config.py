@@ -65,8 +65,9 @@ _VARS = [
     Var("CLOUD_AMD_DENSE_WGRAD_BLOCKS", int, 1024, "dense-layer weight gradients (BERT): split-K workgroup target "
         "(1024 with the split-major XCD mapping: 6,210 / 6,231 vs 6,153 / 6,131 seq/s at 512)",
         "ops"),
-    Var("CLOUD_AMD_DENSE_WGRAD_256", bool, True, "dense-layer weight gradients whose 256 x 256 tiles times a split "
-        "count fill one round of the chip (BERT QKV / FFN) run on the two-phase 256 core with that split", "ops"),
+    Var("CLOUD_AMD_DENSE_WGRAD_256", bool, False, "dense-layer weight gradients whose 256 x 256 tiles times a split "
+        "count fill one round of the chip (BERT QKV / FFN) run on the two-phase 256 core with that split (measured "
+        "3 % slower on BERT than the 128 core's 1024-workgroup split: 6,749 / 6,754 vs 6,952 / 6,940 seq/s)", "ops"),
     Var("CLOUD_AMD_TAPMASK", bool, True, "convolutions: tap-mask / incremental buffer-mode gather loaders; 0 keeps "
         "the general per-chunk decode loaders (A/B runs)", "ops"),
     Var("CLOUD_AMD_SPLIT_XCD", bool, True, "split-K GEMM/conv grids: give each XCD contiguous (split, tile) "
