@@ -237,4 +237,101 @@ __device__ __forceinline__ void mfma_gemm_256p8(const CoreParams& P) {
   gemm_epilogue<BM, BN, 2, 4, EPI, SMEM, 1, FM, FN, true>(P, acc, smem, m0, n0, tm, tid);
 }
 
+// 256 x 128 x 64 variant for GEMMs whose 256 x 256 grid does not fill whole rounds of the chip
+// but whose 256 x 128 grid does (BERT-base at M = 8192: N = 3072 -> 768 tiles = 3 rounds, where
+// 256 x 256 gives 384 = 1.5).  Same two staggered 4-wave groups; ONE phase per K tile (the
+// whole 256 x 128 tile, 32 MFMAs per wave: waves 4 (M) x 2 (N), 64 x 64 each) and THREE LDS
+// buffers of one K tile (A 32 KB + B 16 KB each, 144 KB): K tile t+2 is restaged into the
+// buffer K tile t-1 used, one phase after its reads retired, and ONE counted vmcnt(6) per K
+// tile (t+2's six loads per thread still in flight) completes t+1 before the phase that reads it.
+template <template <int, int, int> class LAT, template <int, int, int> class LBT, int EPI>
+__device__ __forceinline__ void mfma_gemm_256x128(const CoreParams& P) {
+  constexpr int BM = 256, BN = 128, NT = 512, WM = 4, WN = 2;
+  constexpr int AT = BM * BK, BT = BN * BK, ST = AT + BT;  // shorts per buffer
+  constexpr int SMEM = 3 * ST;                              // 144 KB
+  static_assert(SMEM >= BM * EpiLayout<BN>::LD, "C staging must fit the operand image");
+  using LA = LAT<BM, 4, NT>;
+  using LB = LBT<BN, 2, NT>;
+  static_assert(!loader_stateful<LA>::value && !loader_stateful<LB>::value, "stateless loaders only");
+  constexpr bool A_KC = LA::KC, B_KC = LB::KC;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // 4 x 4
+  __shared__ __attribute__((aligned(16))) short smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int grp = __builtin_amdgcn_readfirstlane(wave) >> 2;
+  const int tiles_m = (P.M + BM - 1) / BM, tiles_n = (P.N + BN - 1) / BN;
+  const BlkPos bp = blk_pos(P);
+  int tm, tn;
+  tile256_coords(bp.tile, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = bp.split * P.k_per_split;
+  int kend = kbeg + P.k_per_split;
+  if (kend > P.K) kend = P.K;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  const LA la(P, true, m0, tid);
+  const LB lb(P, false, n0, tid);
+  const auto ra = loader_rsrc(la);
+  const auto rb = loader_rsrc(lb);
+  auto dma = [&](int t) {
+    const int k0 = kbeg + t * BK;
+    short* As = smem + (t % 3) * ST;
+    short* Bs = As + AT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) CA_DMA_CHUNK(LA, la, ra, i, k0, As + (i * NT + wave * 64) * 8);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) CA_DMA_CHUNK(LB, lb, rb, i, k0, Bs + (i * NT + wave * 64) * 8);
+  };
+
+  f4v acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) dma(0);
+  if (nk > 1) {
+    dma(1);
+    vm_wait<6>();
+  } else {
+    vm_wait<0>();
+  }
+  bar256();
+  if (grp == 1) bar256();
+  for (int t = 0; t < nk; ++t) {
+    const short* As = smem + (t % 3) * ST;
+    const short* Bs = As + AT;
+    bf16x8 af[FM][2], bfr[FN][2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j][kk] = read_frag_sw<BN, B_KC>(Bs, wn * (BN / WN) + j * 16, kk * 32, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i][kk] = read_frag_sw<BM, A_KC>(As, wm * (BM / WM) + i * 16, kk * 32, lane);
+    }
+    lgkm_wait0();
+    if (t + 2 < nk) {  // into the buffer K tile t-1 used (its reads retired before the last barrier)
+      dma(t + 2);
+      vm_wait<6>();
+    } else {
+      vm_wait<0>();
+    }
+    bar256();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar256();
+  }
+  if (grp == 0) bar256();
+  __syncthreads();
+  gemm_epilogue<BM, BN, WM, WN, EPI, SMEM, 1>(P, acc, smem, m0, n0, tm, tid);
+}
+
 }  // namespace ca

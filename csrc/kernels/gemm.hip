@@ -69,6 +69,12 @@ __global__ void __launch_bounds__(512) dense_gemm_256p8_kernel(CoreParams P) {
   mfma_gemm_256p8<LA, LB, EPI, 2>(P);
 }
 
+// Its 256 x 128 single-phase, three-buffer variant (same header).
+template <template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
+__global__ void __launch_bounds__(512) dense_gemm_256x128_kernel(CoreParams P) {
+  mfma_gemm_256x128<LA, LB, EPI>(P);
+}
+
 // CLOUD_AMD_GEMM_CORE selects the core (A/B comparisons; ca_gemm_set_core overrides it):
 // 0 "reg" = register-staged, 1 "glds" = glds single stage (4 waves) only, 2 "glds8" = glds
 // double-buffered (8 waves), 3 "glds_ring" = glds plus the 256 x 256 ring core (ca_gemm256.h)
@@ -250,6 +256,20 @@ static bool use_256(const CoreParams& p, int splits) {
   return t >= 256 && (tile_balance(t) >= 0.999 || (t >= 512 && tile_balance(t) >= 0.85));
 }
 
+// 256 x 128 tiles where 256 x 256 tiles do not fill whole rounds but 256 x 128 tiles do
+// (BERT-base FFN1 forward / FFN2 input gradient at M = 8192: N = 3072 -> 768 tiles = 3 rounds;
+// 256 x 256 gives 384 = 1.5).  CLOUD_AMD_GEMM_256X128=0 keeps them on the 128 core.
+static bool use_256x128(const CoreParams& p, int splits) {
+  static int en = -1;
+  if (en < 0) {
+    const char* e = getenv("CLOUD_AMD_GEMM_256X128");
+    en = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!en || !core_p8() || splits != 1 || p.M < 256 || p.N < 128 || p.K < 512) return false;
+  const long t = (long)((p.M + 255) / 256) * ((p.N + 127) / 128);
+  return t >= 256 && (tile_balance(t) >= 0.999 || (t >= 512 && tile_balance(t) >= 0.85));
+}
+
 template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB,
           template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
 int launch(const CoreParams& p0, int splits, hipStream_t s) {
@@ -282,6 +302,18 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
         dense_gemm_256_kernel<GDenseKC32, GDenseNC, EPI><<<dim3(t256, 1, splits), 512, 0, s>>>(p);
       else if constexpr (!AK && !BKC)
         dense_gemm_256_kernel<GDenseNC, GDenseNC, EPI><<<dim3(t256, 1, splits), 512, 0, s>>>(p);
+      else
+        return -2;
+      CA_LAUNCH_CHECK();
+      return 0;
+    }
+    if (use_256x128(p, splits)) {
+      const int t = ((p.M + 255) / 256) * ((p.N + 127) / 128);
+      constexpr bool AK = GA<BM, 1, 256>::KC, BKC = GB<BN, 1, 256>::KC;
+      if constexpr (AK && BKC)
+        dense_gemm_256x128_kernel<GDenseKC, GDenseKC, EPI><<<dim3(t, 1, 1), 512, 0, s>>>(p);
+      else if constexpr (AK && !BKC)
+        dense_gemm_256x128_kernel<GDenseKC, GDenseNC, EPI><<<dim3(t, 1, 1), 512, 0, s>>>(p);
       else
         return -2;
       CA_LAUNCH_CHECK();

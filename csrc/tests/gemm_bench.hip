@@ -69,6 +69,11 @@ __global__ void __launch_bounds__(512) kp8(CoreParams P) {
 }
 
 template <template <int, int, int> class GA, template <int, int, int> class GB>
+__global__ void __launch_bounds__(512) k256x128(CoreParams P) {
+  mfma_gemm_256x128<GA, GB, EPI_BF16>(P);
+}
+
+template <template <int, int, int> class GA, template <int, int, int> class GB>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k128(CoreParams P) {
   mfma_gemm_glds<128, 128, 2, 2, GA, GB, EPI_BF16>(P);
 }
@@ -92,6 +97,12 @@ static void launchp8(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
   if (layout == 0) kp8<GDenseKC, GDenseKC, PHASES><<<g, 512, 0, s>>>(p);
   else if (layout == 1) kp8<GDenseKC, GDenseNC, PHASES><<<g, 512, 0, s>>>(p);
   else kp8<GDenseNC, GDenseNC, PHASES><<<g, 512, 0, s>>>(p);
+}
+
+static void launch256x128(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) k256x128<GDenseKC, GDenseKC><<<g, 512, 0, s>>>(p);
+  else if (layout == 1) k256x128<GDenseKC, GDenseNC><<<g, 512, 0, s>>>(p);
+  else k256x128<GDenseNC, GDenseNC><<<g, 512, 0, s>>>(p);
 }
 
 static void launch128(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
@@ -146,6 +157,7 @@ int main(int argc, char** argv) {
   Variant vars[] = {{"v256", 256, 256, launch256},
                     {"p8q4", 256, 256, launchp8<4>},
                     {"p8h2", 256, 256, launchp8<2>},
+                    {"w256x128", 256, 128, launch256x128},
                     {"glds128", 128, 128, launch128}};
   hipStream_t s;
   CHECK(hipStreamCreate(&s));

@@ -90,3 +90,33 @@ def test_default_dispatch_selects_256_on_large_gemm():
         assert _rel(y[:1024], a[:1024].float() @ w.float().t()) < 5e-3
     finally:
         ext.gemm_set_core(prev)
+
+
+@pytest.mark.parametrize("M,N,K", [(8192, 3072, 768), (8000, 1000, 700), (4096, 2048, 4096)])
+def test_256x128_core_default_dispatch(M, N, K):
+    """The 256 x 128 single-phase core (ca_gemm256p8.h mfma_gemm_256x128), picked by the default
+    dispatch when 256 x 128 tiles fill whole rounds (BERT FFN1 forward / FFN2 input gradient
+    shape first; ragged M / N / K last): forward with bias + GELU + pre-activation, input
+    gradient with GELU' -- against fp32 references."""
+    from cloud_amd.ops import raw
+
+    torch.manual_seed(M + N + K)
+    a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda") * 0.1
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    y = raw.gemm(a, w, bias=b, act="gelu", preact=pre)
+    ref = a.float() @ w.float().t() + b
+    assert _rel(pre, ref) < 5e-3
+    assert _rel(y, torch.nn.functional.gelu(pre.float())) < 1e-2
+    w2 = (torch.randn(K, N, device="cuda") * 0.05).to(torch.bfloat16)  # NN: dx[M, N] = dy[M, K] @ w2[K, N]
+    dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    dx = raw.gemm(dy, w2, layout=raw.NN, act="gelu", dact_src=pre)
+    ref2 = (dy.float() @ w2.float()) * _gelu_grad(pre.float())
+    assert _rel(dx, ref2) < 1e-2, _rel(dx, ref2)
+
+
+def _gelu_grad(x):
+    cdf = 0.5 * (1.0 + torch.erf(x / 2 ** 0.5))
+    pdf = torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+    return cdf + x * pdf
