@@ -10,7 +10,7 @@ out=gpurun_out/$tag; mkdir -p $out
 chk() { grep -q " passed" gpurun_out/$1 && ! grep -qE " failed| error" gpurun_out/$1 || { echo "tests failed: $1"; tail -60 gpurun_out/$1; exit 1; }; }
 $S 300 ${tag}_g256_tests.log python -u -m pytest tests/test_gemm256_gpu.py tests/test_plain_gemm_policy_gpu.py -x -q --timeout 120 --timeout-method thread || exit 1
 chk ${tag}_g256_tests.log
-timeout -k 10 240 bin/gemm_bench 20 8192,3072,768,0 8192,3072,768,1 8192,2304,768,0 4096,4096,4096,0 8192,8192,8192,0 8000,1000,700,0 > $out/gemm_bench.txt 2>&1 || { echo "gemm_bench failed"; cat $out/gemm_bench.txt; exit 1; }
+timeout -k 10 240 bin/gemm_bench 20 8192,3072,768,0 8192,3072,768,1 8192,2304,768,0 4096,4096,4096,0 8192,8192,8192,0 8000,1000,704,0 > $out/gemm_bench.txt 2>&1 || { echo "gemm_bench failed"; cat $out/gemm_bench.txt; exit 1; }
 grep -h '"variant"' $out/gemm_bench.txt | python3 -c "
 import sys,json
 for l in sys.stdin:
