@@ -65,6 +65,9 @@ _VARS = [
     Var("CLOUD_AMD_DENSE_WGRAD_BLOCKS", int, 1024, "dense-layer weight gradients (BERT): split-K workgroup target "
         "(1024 with the split-major XCD mapping: 6,210 / 6,231 vs 6,153 / 6,131 seq/s at 512)",
         "ops"),
+    Var("CLOUD_AMD_GEMM_256X128", bool, False, "GEMMs whose 256 x 128 grid fills whole rounds (and 256 x 256 does "
+        "not) on the 256 x 128 single-phase core (csrc/include/ca_gemm256p8.h); measured slower than the 128 core "
+        "on BERT's shapes", "ops"),
     Var("CLOUD_AMD_DENSE_WGRAD_256", bool, False, "dense-layer weight gradients whose 256 x 256 tiles times a split "
         "count fill one round of the chip (BERT QKV / FFN) run on the two-phase 256 core with that split (measured "
         "3 % slower on BERT than the 128 core's 1024-workgroup split: 6,749 / 6,754 vs 6,952 / 6,940 seq/s)", "ops"),

@@ -258,12 +258,15 @@ static bool use_256(const CoreParams& p, int splits) {
 
 // 256 x 128 tiles where 256 x 256 tiles do not fill whole rounds but 256 x 128 tiles do
 // (BERT-base FFN1 forward / FFN2 input gradient at M = 8192: N = 3072 -> 768 tiles = 3 rounds;
-// 256 x 256 gives 384 = 1.5).  CLOUD_AMD_GEMM_256X128=0 keeps them on the 128 core.
+// 256 x 256 gives 384 = 1.5).  Opt-in (CLOUD_AMD_GEMM_256X128=1): measured 669 vs 830 TF/s for
+// the 128 core on 8192 x 3072 x 768 and BERT 6,286 / 6,328 vs 6,863 / 6,875 seq/s
+// (profiles/r4_s18/) -- one barrier pair per K tile with 16 fragment reads per wave does not
+// keep the MFMA pipe as busy as the two-phase 256 x 256 schedule.
 static bool use_256x128(const CoreParams& p, int splits) {
   static int en = -1;
   if (en < 0) {
     const char* e = getenv("CLOUD_AMD_GEMM_256X128");
-    en = (e && e[0] == '0') ? 0 : 1;
+    en = (e && e[0] == '1') ? 1 : 0;
   }
   if (!en || !core_p8() || splits != 1 || p.M < 256 || p.N < 128 || p.K < 512) return false;
   const long t = (long)((p.M + 255) / 256) * ((p.N + 127) / 128);

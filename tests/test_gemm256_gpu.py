@@ -93,12 +93,15 @@ def test_default_dispatch_selects_256_on_large_gemm():
 
 
 @pytest.mark.parametrize("M,N,K", [(8192, 3072, 768), (8000, 1000, 704), (4096, 2048, 4096)])
-def test_256x128_core_default_dispatch(M, N, K):
-    """The 256 x 128 single-phase core (ca_gemm256p8.h mfma_gemm_256x128), picked by the default
-    dispatch when 256 x 128 tiles fill whole rounds (BERT FFN1 forward / FFN2 input gradient
-    shape first; ragged M / N / K last): forward with bias + GELU + pre-activation, input
+def test_256x128_core_dispatch(M, N, K, monkeypatch):
+    """The 256 x 128 single-phase core (ca_gemm256p8.h mfma_gemm_256x128, opt-in with
+    CLOUD_AMD_GEMM_256X128=1, read once per process -- so this test also covers whatever the
+    process decided) where 256 x 128 tiles fill whole rounds (BERT FFN1 forward / FFN2 input
+    gradient shape first; ragged M / N / K): forward with bias + GELU + pre-activation, input
     gradient with GELU' -- against fp32 references."""
     from cloud_amd.ops import raw
+
+    monkeypatch.setenv("CLOUD_AMD_GEMM_256X128", "1")
 
     torch.manual_seed(M + N + K)
     a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
