@@ -261,9 +261,10 @@ template <int EPI, int KS, int NC, int BN = 64, int NT = 256>
 __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaParams& X, const bf16_t* Y, long ldy,
                                                 float* ws, int tiles_per_block) {
   static_assert((KS == 1 || NC == 1) && KS >= 1 && NC >= 1, "K chunks or N chunks, not both");
-  static_assert(KS * NC * 16 <= (NT == 512 ? 128 : 64), "dW block: <= 64 (4 waves) / 128 (8 waves) fp32 per lane");
-  static_assert((BN == 64 && NT == 256) || (BN == 128 && NT == 512), "4 waves x 64 columns or 8 waves x 128");
-  constexpr int BM = 128, WN = BN / 32, WM = NT / 64 / WN;
+  static_assert((BN == 64 && (NT == 256 || NT == 512)) || (BN == 128 && NT == 512), "64 columns (4 or 8 waves), 128 (8)");
+  constexpr int BM = 128, WM = 2, WN = NT / 64 / WM;
+  constexpr int WNB = BN / WN, FNW = WNB / 16;  // a wave's dW / dgrad columns, its 16-wide fragments
+  static_assert(KS * NC * 8 * FNW <= 64 * (NT / 256), "dW block per lane: <= 64 fp32 (4 waves) / 128 (8 waves)");
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // dgrad: 4 x 2 fragments per wave
   constexpr int A_ELEMS = BM * BK, B_ELEMS = BK * BN, Y_ELEMS = BM * BN;
   constexpr int CPA = A_ELEMS / 8 / NT, CPB = B_ELEMS / 8 / NT, CPY = Y_ELEMS / 8 / NT;
@@ -271,13 +272,15 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
   constexpr int K = KS * BK, N = NC * BN, STEPS = KS * NC;
   // LDS: As (dz chunk) | Bs (W chunk) | Ys (y chunk) | coefficients.  The epilogue stages
   // C and its statistics rows in Bs + Ys (free between the steps' barriers), never in As.
-  constexpr int EPI_SH = B_ELEMS + Y_ELEMS;
+  // (the statistics epilogues reduce up to three fp32 rows per thread group: 3 * NT/(BN/8) * BN floats)
+  constexpr int SRED = 3 * (NT / (BN / 8)) * BN * 2;
+  constexpr int EPI_SH = (B_ELEMS + Y_ELEMS) > SRED ? (B_ELEMS + Y_ELEMS) : SRED;
   static_assert(BM * EpiLayout<BN>::LD <= EPI_SH, "C staging must fit Bs + Ys");
   __shared__ __attribute__((aligned(16))) short smem[A_ELEMS + EPI_SH + 3 * K * 2];
   short* const As = smem;
   short* const Bs = smem + A_ELEMS;
   short* const Ys = Bs + B_ELEMS;
-  float* const Cf = reinterpret_cast<float*>(Ys + Y_ELEMS);
+  float* const Cf = reinterpret_cast<float*>(Bs + EPI_SH);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -291,13 +294,13 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
                                                      (int)buf_span((long)K * P.ldb * 2), 0x00020000);
   const int arow = tid >> 3, c8 = tid & 7;
 
-  f4v accw[STEPS][2][2];  // dW: per (K chunk, N chunk) step, a 32 (k) x 32 (n) block per wave
+  f4v accw[STEPS][2][FNW];  // dW: per (K chunk, N chunk) step, a 32 (k) x WNB (n) block per wave
 #pragma unroll
   for (int c = 0; c < STEPS; ++c)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) accw[c][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < FNW; ++j) accw[c][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
   for (int i = tid; i < 3 * K; i += NT) {
     const int q = i / K, k = i - q * K;
@@ -444,7 +447,7 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
       // wgrad: dW (chunk t, chunk nc) += dz chunk^T (rows k) x y chunk (rows m), over the tile's rows
 #pragma unroll 1
       for (int mk = 0; mk < BM; mk += 32) {
-        bf16x8 dzt[2], yf[2];
+        bf16x8 dzt[2], yf[FNW];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           // N-contiguous read of the [m][k] dz image (chunk swizzle m & 7): row k, 8 consecutive m
@@ -459,11 +462,11 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
           dzt[i] = __builtin_bit_cast(bf16x8, s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) yf[j] = read_frag_sw<BN, false>(Ys, wn * 32 + j * 16, mk, lane);
+        for (int j = 0; j < FNW; ++j) yf[j] = read_frag_sw<BN, false>(Ys, wn * WNB + j * 16, mk, lane);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < FNW; ++j)
             accw[s][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yf[j], dzt[i], accw[s][i][j], 0, 0, 0);
       }
       lgkm_wait0();
@@ -478,7 +481,7 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
       }
     }
   }
-  // dW slab of this workgroup: accw[s][i][j][r] = dW[64 t + 32 wm + 16 i + (lane & 15)][64 nc + 32 wn + 16 j + 4 (lane >> 4) + r]
+  // dW slab of this workgroup: accw[s][i][j][r] = dW[64 t + 32 wm + 16 i + (lane & 15)][64 nc + WNB wn + 16 j + 4 (lane >> 4) + r]
   float* slab = ws + (long)blockIdx.x * K * N;
 #pragma unroll
   for (int s = 0; s < STEPS; ++s) {
@@ -486,9 +489,9 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < FNW; ++j) {
         const int k = t * BK + wm * 32 + i * 16 + (lane & 15);
-        const int n = nc * BN + wn * 32 + j * 16 + 4 * (lane >> 4);
+        const int n = nc * BN + wn * WNB + j * 16 + 4 * (lane >> 4);
         *reinterpret_cast<f4v*>(slab + (long)k * N + n) = accw[s][i][j];
       }
   }

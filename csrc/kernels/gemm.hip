@@ -373,9 +373,13 @@ __global__ void __launch_bounds__(256) xa_gemm_kernel(CoreParams P, XaParams X) 
   mfma_gemm_xa<BM, BN, BKC, EPI, XM>(P, X);
 }
 
+// two waves per SIMD: two 4-wave or one 8-wave workgroup per CU.  (Two 8-wave workgroups at
+// 64 columns would need <= 128 registers per lane: the compiler spilled 135 of them there, 47
+// at a 168 budget -- not used.)
 template <int EPI, int KS, int NC, int BN, int NT>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2))) xa_dw_kernel(
-    CoreParams P, XaParams X, const bf16_t* Y, long ldy, float* ws, int tiles_per_block) {
+__global__ void __launch_bounds__(NT)
+    __attribute__((amdgpu_waves_per_eu(2))) xa_dw_kernel(
+        CoreParams P, XaParams X, const bf16_t* Y, long ldy, float* ws, int tiles_per_block) {
   mfma_gemm_xa_dw<EPI, KS, NC, BN, NT>(P, X, Y, ldy, ws, tiles_per_block);
 }
 
@@ -644,7 +648,15 @@ int ca_gemm_xa_dw(const bf16_t* src0, const bf16_t* src1, const uint8_t* mask_in
   int rc;
   if (N == 64 && K == 64) rc = xa_dw_launch<1, 1>(p, x, Y, ldy, ws, g, tpb, s);
   else if (N == 64 && K == 128) rc = xa_dw_launch<2, 1>(p, x, Y, ldy, ws, g, tpb, s);
-  else if (N == 64 && K == 256) rc = xa_dw_launch<4, 1>(p, x, Y, ldy, ws, g, tpb, s);
+  else if (N == 64 && K == 256) {
+    // 4-wave workgroups, two per CU; CLOUD_AMD_XA_DW_WAVES=8: one 8-wave workgroup per CU
+    static int w8 = -1;
+    if (w8 < 0) {
+      const char* e = getenv("CLOUD_AMD_XA_DW_WAVES");
+      w8 = (e && e[0] == '8') ? 1 : 0;
+    }
+    rc = w8 ? xa_dw_launch<4, 1, 64, 512>(p, x, Y, ldy, ws, g, tpb, s) : xa_dw_launch<4, 1>(p, x, Y, ldy, ws, g, tpb, s);
+  }
   else if (K == 64 && N == 256) rc = xa_dw_launch<1, 4>(p, x, Y, ldy, ws, g, tpb, s);
   else if (N == 128 && K == 512) rc = xa_dw_launch<8, 1, 128, 512>(p, x, Y, ldy, ws, g, tpb, s);
   else return -1;
