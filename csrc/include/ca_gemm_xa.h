@@ -57,14 +57,19 @@ struct XaTraits {
   static constexpr int NCOEF = XM == XA_BN_BWD ? 3 : (XM == XA_BN_RESBN_RELU ? 4 : 2);
 };
 
-template <int BM, int BN, bool B_KC, int EPI, int XM>
+// NT = 256 (4 waves, 2 x 2) or 512 (8 waves, 2 x 4: half the registers per lane, so two
+// workgroups -- 16 waves -- per CU keep twice the loads in flight)
+template <int BM, int BN, bool B_KC, int EPI, int XM, int NT = 256>
 __device__ __forceinline__ void mfma_gemm_xa(const CoreParams& P, const XaParams& X) {
-  constexpr int WM = 2, WN = 2, NT = 256;
+  constexpr int WM = 2, WN = NT / 128;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  static_assert(FN >= 1, "at least one 16-column fragment per wave");
   constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;
   constexpr int STAGE = A_ELEMS + B_ELEMS;
   constexpr int EPI_LD = EpiLayout<BN>::LD;
-  constexpr int SMEM = (STAGE > BM * EPI_LD ? STAGE : BM * EPI_LD);
+  constexpr int SRED = 2 * (NT / (BN / 8)) * BN * 2;  // two fp32 statistics rows per thread group
+  constexpr int SMEM0 = (STAGE > BM * EPI_LD ? STAGE : BM * EPI_LD);
+  constexpr int SMEM = SMEM0 > SRED ? SMEM0 : SRED;
   constexpr int CPA = A_ELEMS / 8 / NT;  // A chunks (16 B) per thread and K step
   constexpr int CPB = B_ELEMS / 8 / NT;
   constexpr int RSTEP = NT / 8;          // tile rows between a thread's A chunks

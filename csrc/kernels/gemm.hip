@@ -373,6 +373,23 @@ __global__ void __launch_bounds__(256) xa_gemm_kernel(CoreParams P, XaParams X) 
   mfma_gemm_xa<BM, BN, BKC, EPI, XM>(P, X);
 }
 
+// 8-wave form: <= 128 registers per lane so two workgroups (16 waves) fit a CU
+template <int BM, int BN, bool BKC, int EPI, int XM>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) xa_gemm8_kernel(CoreParams P,
+                                                                                              XaParams X) {
+  mfma_gemm_xa<BM, BN, BKC, EPI, XM, 512>(P, X);
+}
+
+// CLOUD_AMD_XA_WAVES=8: the 128 x 128 transform-A GEMMs on 8-wave workgroups
+static bool xa_waves8() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_XA_WAVES");
+    v = (e && e[0] == '8') ? 1 : 0;
+  }
+  return v != 0;
+}
+
 // two waves per SIMD: two 4-wave or one 8-wave workgroup per CU.  (Two 8-wave workgroups at
 // 64 columns would need <= 128 registers per lane: the compiler spilled 135 of them there, 47
 // at a 168 budget -- not used.)
@@ -409,7 +426,14 @@ int xa_launch(const CoreParams& p0, const XaParams& x, hipStream_t s) {
   if (want_small_n(p, 1)) {
     xa_gemm_kernel<128, 64, LB, EPI, XM><<<tm * ((p.N + 63) / 64), 256, 0, s>>>(p, x);
   } else {
-    xa_gemm_kernel<128, 128, LB, EPI, XM><<<tm * ((p.N + 127) / 128), 256, 0, s>>>(p, x);
+    if (xa_waves8()) {
+      if constexpr (EPI != EPI_BF16_BNR2)  // its three statistics rows do not fit the 8-wave LDS image
+        xa_gemm8_kernel<128, 128, LB, EPI, XM><<<tm * ((p.N + 127) / 128), 512, 0, s>>>(p, x);
+      else
+        xa_gemm_kernel<128, 128, LB, EPI, XM><<<tm * ((p.N + 127) / 128), 256, 0, s>>>(p, x);
+    } else {
+      xa_gemm_kernel<128, 128, LB, EPI, XM><<<tm * ((p.N + 127) / 128), 256, 0, s>>>(p, x);
+    }
   }
   CA_LAUNCH_CHECK();
   return 0;
