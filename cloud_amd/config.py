@@ -114,6 +114,8 @@ _VARS = [
         "(K = 512 -> N = 128, 8-wave workgroups holding the 512 x 128 dW block)", "ops"),
     Var("CLOUD_AMD_BN_FOLD_WGRAD1", bool, False, "the same one-pass input + weight gradient for stage 1's conv1 with "
         "bn1's backward apply (K = 64 -> N = 256: dz1 never written, four output chunks per tile)", "ops"),
+    Var("CLOUD_AMD_XA_WAVES", int, 8, "128 x 128 transform-A GEMMs (BN folded into the 1x1 convs): 8-wave "
+        "workgroups (<= 128 registers, two per CU) or 4", "ops"),
     Var("CLOUD_AMD_XA_DW_WAVES", int, 4, "stage-1 conv3 fused input+weight gradient: 4-wave workgroups (two per "
         "CU) or 8 (one per CU)", "ops"),
     Var("CLOUD_AMD_BN_FOLD_ALL", bool, False, "fold every BN site regardless of CLOUD_AMD_BN_FOLD_MAX_N (tests, A/B)",

@@ -380,12 +380,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) x
   mfma_gemm_xa<BM, BN, BKC, EPI, XM, 512>(P, X);
 }
 
-// CLOUD_AMD_XA_WAVES=8: the 128 x 128 transform-A GEMMs on 8-wave workgroups
+// The 128 x 128 transform-A GEMMs on 8-wave workgroups (default; CLOUD_AMD_XA_WAVES=4: the
+// 4-wave form).  ResNet-50 b1024: xa kernels 11.2 -> 10.8 ms/step, 14,614 / 14,617 / 14,560 ->
+// 14,668 / 14,650 / 14,582 img/s interleaved (profiles/r4_s20/).
 static bool xa_waves8() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("CLOUD_AMD_XA_WAVES");
-    v = (e && e[0] == '8') ? 1 : 0;
+    v = (e && e[0] == '4') ? 0 : 1;
   }
   return v != 0;
 }
