@@ -262,12 +262,13 @@ __device__ __forceinline__ void mfma_gemm_xa(const CoreParams& P, const XaParams
 // BN = 64 with 4 waves (stage 1), or BN = 128 with 8 waves (stage 2 conv3: K = 512 -> N = 128,
 // a 512 x 128 dW block = 128 fp32 per lane, one workgroup per CU): waves 2 (M) x BN/32 (N) for
 // the dgrad tile, 2 (k) x BN/32 (n) 32 x 32 blocks of each dW chunk.
-template <int EPI, int KS, int NC, int BN = 64, int NT = 256>
+template <int EPI, int KS, int NC, int BN = 64, int NT = 256, int BM = 128>
 __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaParams& X, const bf16_t* Y, long ldy,
                                                 float* ws, int tiles_per_block) {
   static_assert((KS == 1 || NC == 1) && KS >= 1 && NC >= 1, "K chunks or N chunks, not both");
   static_assert((BN == 64 && (NT == 256 || NT == 512)) || (BN == 128 && NT == 512), "64 columns (4 or 8 waves), 128 (8)");
-  constexpr int BM = 128, WM = 2, WN = NT / 64 / WM;
+  static_assert(BM == 128 || BM == 64, "128- or 64-row tiles");
+  constexpr int WM = 2, WN = NT / 64 / WM;
   constexpr int WNB = BN / WN, FNW = WNB / 16;  // a wave's dW / dgrad columns, its 16-wide fragments
   static_assert(KS * NC * 8 * FNW <= 64 * (NT / 256), "dW block per lane: <= 64 fp32 (4 waves) / 128 (8 waves)");
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // dgrad: 4 x 2 fragments per wave

@@ -394,12 +394,12 @@ static bool xa_waves8() {
 
 // two waves per SIMD: two 4-wave or one 8-wave workgroup per CU.  (Two 8-wave workgroups at
 // 64 columns would need <= 128 registers per lane: the compiler spilled 135 of them there, 47
-// at a 168 budget -- not used.)
-template <int EPI, int KS, int NC, int BN, int NT>
+// at a 168 budget; 64-row tiles at a 168 budget spilled 19 -- not used.)
+template <int EPI, int KS, int NC, int BN, int NT, int BM = 128>
 __global__ void __launch_bounds__(NT)
     __attribute__((amdgpu_waves_per_eu(2))) xa_dw_kernel(
         CoreParams P, XaParams X, const bf16_t* Y, long ldy, float* ws, int tiles_per_block) {
-  mfma_gemm_xa_dw<EPI, KS, NC, BN, NT>(P, X, Y, ldy, ws, tiles_per_block);
+  mfma_gemm_xa_dw<EPI, KS, NC, BN, NT, BM>(P, X, Y, ldy, ws, tiles_per_block);
 }
 
 template <int KS, int NC, int BN = 64, int NT = 256>
