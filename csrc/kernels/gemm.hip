@@ -383,6 +383,15 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) x
 // The 128 x 128 transform-A GEMMs on 8-wave workgroups (default; CLOUD_AMD_XA_WAVES=4: the
 // 4-wave form).  ResNet-50 b1024: xa kernels 11.2 -> 10.8 ms/step, 14,614 / 14,617 / 14,560 ->
 // 14,668 / 14,650 / 14,582 img/s interleaved (profiles/r4_s20/).
+// ... and the 128 x 64 ones (stage 1) with CLOUD_AMD_XA_WAVES_N64=1 (A/B)
+static bool xa_waves8_n64() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_XA_WAVES_N64");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v != 0;
+}
 static bool xa_waves8() {
   static int v = -1;
   if (v < 0) {
@@ -426,7 +435,14 @@ int xa_launch(const CoreParams& p0, const XaParams& x, hipStream_t s) {
   p.split_xcd = 0;
   const int tm = (p.M + 127) / 128;
   if (want_small_n(p, 1)) {
-    xa_gemm_kernel<128, 64, LB, EPI, XM><<<tm * ((p.N + 63) / 64), 256, 0, s>>>(p, x);
+    bool w8 = false;
+    if constexpr (EPI != EPI_BF16_BNR2) {  // its three statistics rows do not fit the 8-wave LDS image
+      if (xa_waves8() && xa_waves8_n64()) {
+        xa_gemm8_kernel<128, 64, LB, EPI, XM><<<tm * ((p.N + 63) / 64), 512, 0, s>>>(p, x);
+        w8 = true;
+      }
+    }
+    if (!w8) xa_gemm_kernel<128, 64, LB, EPI, XM><<<tm * ((p.N + 63) / 64), 256, 0, s>>>(p, x);
   } else {
     if (xa_waves8()) {
       if constexpr (EPI != EPI_BF16_BNR2)  // its three statistics rows do not fit the 8-wave LDS image
