@@ -116,6 +116,8 @@ _VARS = [
         "bn1's backward apply (K = 64 -> N = 256: dz1 never written, four output chunks per tile)", "ops"),
     Var("CLOUD_AMD_XA_WAVES", int, 8, "128 x 128 transform-A GEMMs (BN folded into the 1x1 convs): 8-wave "
         "workgroups (<= 128 registers, two per CU) or 4", "ops"),
+    Var("CLOUD_AMD_XA_WAVES_N64", bool, True, "the 128 x 64 transform-A GEMMs (stage 1) on 8-wave workgroups too "
+        "(with CLOUD_AMD_XA_WAVES=8)", "ops"),
     Var("CLOUD_AMD_XA_DW_WAVES", int, 4, "stage-1 conv3 fused input+weight gradient: 4-wave workgroups (two per "
         "CU) or 8 (one per CU)", "ops"),
     Var("CLOUD_AMD_BN_FOLD_ALL", bool, False, "fold every BN site regardless of CLOUD_AMD_BN_FOLD_MAX_N (tests, A/B)",

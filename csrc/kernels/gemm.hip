@@ -383,12 +383,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) x
 // The 128 x 128 transform-A GEMMs on 8-wave workgroups (default; CLOUD_AMD_XA_WAVES=4: the
 // 4-wave form).  ResNet-50 b1024: xa kernels 11.2 -> 10.8 ms/step, 14,614 / 14,617 / 14,560 ->
 // 14,668 / 14,650 / 14,582 img/s interleaved (profiles/r4_s20/).
-// ... and the 128 x 64 ones (stage 1) with CLOUD_AMD_XA_WAVES_N64=1 (A/B)
+// ... and the 128 x 64 ones (stage 1; CLOUD_AMD_XA_WAVES_N64=0: 4 waves): 85-108 registers;
+// 14,775 / 14,784 / 14,767 -> 14,874 / 14,796 / 14,826 img/s interleaved (profiles/r4_s22/)
 static bool xa_waves8_n64() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("CLOUD_AMD_XA_WAVES_N64");
-    v = (e && e[0] == '1') ? 1 : 0;
+    v = (e && e[0] == '0') ? 0 : 1;
   }
   return v != 0;
 }
