@@ -110,6 +110,8 @@ _VARS = [
     Var("CLOUD_AMD_BN_FOLD_WGRAD", bool, True, "bn3 -> conv3 fold at 64 input channels (ResNet stage 1): conv3's weight "
         "gradient runs in the same kernel as its input gradient (ca_gemm_xa.h mfma_gemm_xa_dw), so the BN-backward "
         "output dz3 is never written", "ops"),
+    Var("CLOUD_AMD_BN_FOLD_WGRAD_DS", bool, True, "stage-1 projection shortcut: its BN backward (gated by the block "
+        "output's ReLU mask), the shortcut conv's input gradient and its weight gradient in one pass", "ops"),
     Var("CLOUD_AMD_BN_FOLD_WGRAD2", bool, False, "the same one-pass input + weight gradient for stage 2's conv3 "
         "(K = 512 -> N = 128, 8-wave workgroups holding the 512 x 128 dW block)", "ops"),
     Var("CLOUD_AMD_BN_FOLD_WGRAD1", bool, False, "the same one-pass input + weight gradient for stage 1's conv1 with "

@@ -327,15 +327,25 @@ class _BottleneckFn(torch.autograd.Function):
         del p1
         if ds is not None:
             zd, sd = saved[12], saved[13]
-            if gate_res:
-                dzd, _ = bn_back(ds["bn"], dout, zd, (sd, None), gate=m3, partials=p_short)
-            else:
-                dzd, _ = bn_back(ds["bn"], dres, zd, (sd, None))
-            del dres
             c = ds["conv"]
-            dx = raw.conv_dgrad(dzd, c.weight, x.shape, c.stride, c.padding)
-            wgrad(c, dzd, x)
-            del dzd
+            if (fold and gate_res and p_short is not None and config.get("CLOUD_AMD_BN_FOLD_WGRAD_DS")
+                    and raw.is_gemm_conv(c.weight, c.stride, c.padding) and raw.dgrad_wgrad_fusable(c.cout, c.cin)):
+                # stage-1 projection shortcut: its BN backward (gated by the block output's ReLU),
+                # the shortcut conv's input gradient and its weight gradient in one pass -- the
+                # shortcut's dz is never written
+                coefd = bn_coef(ds["bn"], zd, sd, p_short)
+                dx = raw.conv1x1_dgrad_wgrad_bnbwd(dout, zd, m3, coefd, c.weight, x, c.weight.grad, dw_beta=1.0)
+                ddp.notify_grad_ready(c.weight)
+                del dres
+            else:
+                if gate_res:
+                    dzd, _ = bn_back(ds["bn"], dout, zd, (sd, None), gate=m3, partials=p_short)
+                else:
+                    dzd, _ = bn_back(ds["bn"], dres, zd, (sd, None))
+                del dres
+                dx = raw.conv_dgrad(dzd, c.weight, x.shape, c.stride, c.padding)
+                wgrad(c, dzd, x)
+                del dzd
         elif gate_res:
             dx = torch.empty_like(x)  # = conv1's input gradient + dout * relu'(m3), one epilogue
         else:
