@@ -169,6 +169,7 @@ def test_fwd_bnapply_vs_fp32(M, Cin, Cout, mode):
 def _train(fold, steps=3, wgrad_fused=False):
     os.environ["CLOUD_AMD_BN_FOLD_WGRAD"] = "1" if wgrad_fused else "0"
     os.environ["CLOUD_AMD_BN_FOLD_WGRAD1"] = "1" if wgrad_fused else "0"
+    os.environ["CLOUD_AMD_BN_FOLD_WGRAD_DS"] = "1" if wgrad_fused else "0"
     os.environ["CLOUD_AMD_BN_FOLD"] = "1" if fold else "0"
     os.environ["CLOUD_AMD_BN_FOLD_FWD"] = "1" if fold else "0"
     os.environ["CLOUD_AMD_BN_FOLD_ALL"] = "1"  # every site, not only the ones the default policy keeps
@@ -223,6 +224,7 @@ def test_resnet_bn_fold_bitwise(monkeypatch):
         os.environ.pop("CLOUD_AMD_BN_FOLD_ALL", None)
         os.environ.pop("CLOUD_AMD_BN_FOLD_WGRAD", None)
         os.environ.pop("CLOUD_AMD_BN_FOLD_WGRAD1", None)
+        os.environ.pop("CLOUD_AMD_BN_FOLD_WGRAD_DS", None)
     # 7 blocks: bwd folds bn3 (6 blocks get their partials from the next block) and bn1 (7);
     # fwd folds bn3 into the next conv1 (6 hand-offs) and bn2 into conv3 (all but layer 1's prw)
     assert n_fold["bwd"] > 0 and n_fold["fwd"] > 0, n_fold
@@ -267,7 +269,7 @@ def test_resnet_fused_dgrad_wgrad_close():
     finally:
         raw.conv1x1_dgrad_wgrad_bnbwd = real
         for k in ("CLOUD_AMD_BN_FOLD", "CLOUD_AMD_BN_FOLD_FWD", "CLOUD_AMD_BN_FOLD_ALL", "CLOUD_AMD_BN_FOLD_WGRAD",
-                  "CLOUD_AMD_BN_FOLD_WGRAD1"):
+                  "CLOUD_AMD_BN_FOLD_WGRAD1", "CLOUD_AMD_BN_FOLD_WGRAD_DS"):
             os.environ.pop(k, None)
     assert calls["n"] > 0
     for ai, (x, y) in enumerate(zip(g1[0], g0[0])):
