@@ -121,7 +121,10 @@ _VARS = [
     Var("CLOUD_AMD_XA_WAVES_N64", bool, True, "the 128 x 64 transform-A GEMMs (stage 1) on 8-wave workgroups too "
         "(with CLOUD_AMD_XA_WAVES=8)", "ops"),
     Var("CLOUD_AMD_XA_DW_WAVES", int, 4, "stage-1 conv3 fused input+weight gradient: 4-wave workgroups (two per "
-        "CU) or 8 (one per CU)", "ops"),
+        "CU) or 8 (one per CU); 8 selects the one-step form", "ops"),
+    Var("CLOUD_AMD_XA_DW_DEPTH", int, 1, "stage-1 fused input+weight gradient (K 256 -> N 64): 0 = one-step form; "
+        "1, 2, 4 = deep form (weights resident in LDS, epilogue operands ahead of the next tile's) with that many "
+        "source steps in flight per workgroup (1: two workgroups per CU, 2 and 4: one)", "ops"),
     Var("CLOUD_AMD_BN_FOLD_ALL", bool, False, "fold every BN site regardless of CLOUD_AMD_BN_FOLD_MAX_N (tests, A/B)",
         "ops"),
     Var("CLOUD_AMD_MAX_STEPS_IN_FLIGHT", int, 2, "training loops (benches, Keras fit) let the host enqueue at most this "

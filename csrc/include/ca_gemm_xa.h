@@ -503,4 +503,300 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
   }
 }
 
+// ----------------------------------------------------------------------------------------
+// mfma_gemm_xa_dw with a deeper operand stream, for the shape that carries ResNet-50's
+// stage-1 traffic (K = 4 x 64 -> N = 64, NC == 1: conv3 and the projection shortcut).  The
+// form above keeps one K step of dz sources in flight per workgroup (~33 KB; two workgroups
+// per CU) and runs at ~3.5 TB/s.  Here:
+//   * the whole K x 64 weight block is copied to LDS once per workgroup (it is the same for
+//     every tile), so the step stream carries only dy, z and the ReLU mask;
+//   * the sources of step g + PD load while step g runs (PD register sets; set = step % PD,
+//     static since KS % PD == 0), across tile boundaries: the next tile's y and first steps
+//     are in flight during this tile's last steps and its epilogue;
+//   * one buffer window per tensor covers the workgroup's tile range, so the "next tile"
+//     past the range reads nothing (hardware range check) and no load sits behind a branch;
+//   * the BN-statistics epilogue's operands (z, ReLU mask of the consuming BN) are loaded in
+//     the stream BEFORE the next tile's sources: vmcnt retires in issue order, so a load
+//     issued after them would make the epilogue wait for the next tile.
+// The epilogue (bf16 dx, optional BN-backward statistics) is gemm_epilogue's arithmetic in
+// its order, staged in As + Ys.  beta = 0, no residual / second BN: the host checks.
+// Registers: PD = 1 fits two workgroups per CU (256); PD = 2 / 4 run one workgroup per CU
+// (waves_per_eu(1)), with 2 / 4 steps (66 / 132 KB) in flight.
+template <int EPI, int KS, int PD>
+__device__ __forceinline__ void mfma_gemm_xa_dw_deep(const CoreParams& P, const XaParams& X, const bf16_t* Y,
+                                                     long ldy, float* ws, int tiles_per_block) {
+  static_assert(EPI == EPI_BF16 || EPI == EPI_BF16_BN, "plain or BN-statistics epilogue");
+  static_assert(KS % PD == 0 && PD >= 1 && PD <= KS, "step sets tile the K chunks");
+  constexpr int BM = 128, BN = 64, NT = 256, WM = 2, WN = 2;
+  constexpr int WNB = BN / WN, FNW = WNB / 16;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  constexpr int A_ELEMS = BM * BK, Y_ELEMS = BM * BN, W_ELEMS = KS * BK * BN;
+  constexpr int CPA = A_ELEMS / 8 / NT, CPY = Y_ELEMS / 8 / NT, CPW = W_ELEMS / 8 / NT;
+  constexpr int RSTEP = NT / 8;
+  constexpr int K = KS * BK, N = BN, STEPS = KS, K8 = K >> 3;
+  constexpr bool BNS = EPI == EPI_BF16_BN;
+  constexpr int IT = BM * BN / 8 / NT;  // epilogue rows per thread (one 8-column group each)
+  constexpr int PARTS = NT / (BN / 8);
+  using EL = EpiLayout<BN>;
+  static_assert(BM * EL::LD <= A_ELEMS + Y_ELEMS && 2 * PARTS * BN * 2 <= A_ELEMS + Y_ELEMS,
+                "epilogue staging fits As + Ys");
+  // LDS: As (dz chunk) | Ys (y tile) | Ws (all of W, 64-row chunks) | coefficients
+  __shared__ __attribute__((aligned(16))) short smem[A_ELEMS + Y_ELEMS + W_ELEMS + 3 * K * 2];
+  short* const As = smem;
+  short* const Ys = smem + A_ELEMS;
+  short* const Ws = Ys + Y_ELEMS;
+  float* const Cf = reinterpret_cast<float*>(Ws + W_ELEMS);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_m = (P.M + BM - 1) / BM;
+  const int t_beg = blockIdx.x * tiles_per_block;
+  int t_end = t_beg + tiles_per_block;
+  if (t_end > tiles_m) t_end = tiles_m;
+  const int arow = tid >> 3, c8 = tid & 7;
+  const int ecol = (tid % (BN / 8)) * 8;  // the epilogue's 8-column group
+
+#pragma unroll
+  for (int i = 0; i < CPW; ++i) {  // W [K][N] -> one swizzled 64 x 64 image per K chunk
+    const int c = tid + i * NT, kr = c / (BN / 8), lc = c % (BN / 8);
+    const int lr = kr % BK;
+    const s8v v = *reinterpret_cast<const s8v*>(P.B + (long)kr * P.ldb + 8 * lc);
+    *reinterpret_cast<s8v*>(Ws + (kr / BK) * (BK * BN) + lr * BN + ((lc ^ nc_swz<BN>(lr)) << 3)) = v;
+  }
+  for (int i = tid; i < 3 * K; i += NT) {
+    const int q = i / K, k = i - q * K;
+    Cf[i] = (q == 0 ? X.c0 : (q == 1 ? X.c1 : X.c2))[k];
+  }
+
+  // operand windows over the workgroup's whole tile range [t_beg, t_end) (rows past M or past
+  // the range read zeros)
+  const long r0 = (long)t_beg * BM;
+  long rl = (long)P.M - r0;
+  if (rl > (long)(t_end - t_beg) * BM) rl = (long)(t_end - t_beg) * BM;
+  const auto r0s = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X.src0 + r0 * P.lda), (short)0,
+                                                     (int)buf_span(rl * P.lda * 2), 0x00020000);
+  const auto r1s = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X.src1 + r0 * P.lda), (short)0,
+                                                     (int)buf_span(rl * P.lda * 2), 0x00020000);
+  const auto rms = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(X.mask_in ? X.mask_in + r0 * K8 : reinterpret_cast<const uint8_t*>(ca_zero16)), (short)0,
+      X.mask_in ? (int)buf_span(rl * K8) : 0, 0x00020000);
+  const auto rys = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Y + r0 * ldy), (short)0,
+                                                     (int)buf_span(rl * ldy * 2), 0x00020000);
+  const auto rzs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(BNS ? P.bnz + r0 * P.ldc : ca_zero16), (short)0, BNS ? (int)buf_span(rl * P.ldc * 2) : 0,
+      0x00020000);
+  const bool has_bnmask = BNS && P.bnmask != nullptr;
+  const auto rbm = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(has_bnmask ? P.bnmask + r0 * (N / 8) : reinterpret_cast<const uint8_t*>(ca_zero16)),
+      (short)0, has_bnmask ? (int)buf_span(rl * (N / 8)) : 0, 0x00020000);
+
+  f4v accw[STEPS][2][FNW];
+#pragma unroll
+  for (int c = 0; c < STEPS; ++c)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < FNW; ++j) accw[c][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  s8v a0[PD][CPA], a1[PD][CPA], yv[CPY], zp[BNS ? IT : 1];
+  uint32_t mb[PD][CPA], mk[BNS ? IT : 1];
+
+  auto load_a = [&](int p, int lt, int t) {  // set p <- dz sources of K chunk t of range tile lt
+    const int k = t * BK + 8 * c8;
+#pragma unroll
+    for (int i = 0; i < CPA; ++i) {
+      const int row = lt * BM + arow + i * RSTEP;
+      const uint32_t off = (uint32_t)(((long)row * P.lda + k) * 2);
+      a0[p][i] = __builtin_bit_cast(s8v, __builtin_amdgcn_raw_buffer_load_b128(r0s, (int)off, 0, 0));
+      a1[p][i] = __builtin_bit_cast(s8v, __builtin_amdgcn_raw_buffer_load_b128(r1s, (int)off, 0, 0));
+      mb[p][i] = __builtin_amdgcn_raw_buffer_load_b8(rms, row * K8 + (k >> 3), 0, 0);
+    }
+  };
+  auto load_y = [&](int lt) {
+#pragma unroll
+    for (int i = 0; i < CPY; ++i) {
+      const int c = tid + i * NT, lr = c / (BN / 8), lc = c % (BN / 8);
+      yv[i] = __builtin_bit_cast(
+          s8v, __builtin_amdgcn_raw_buffer_load_b128(rys, (int)(((long)(lt * BM + lr) * ldy + 8 * lc) * 2), 0, 0));
+    }
+  };
+  auto load_epi = [&](int lt) {  // z and ReLU mask of the BN that consumes dx, this thread's IT rows
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+      const int row = lt * BM + (tid + u * NT) / (BN / 8);
+      zp[u] = __builtin_bit_cast(
+          s8v, __builtin_amdgcn_raw_buffer_load_b128(rzs, (int)(((long)row * P.ldc + ecol) * 2), 0, 0));
+      mk[u] = has_bnmask ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rbm, row * (N / 8) + (ecol >> 3), 0, 0)
+                         : 0xffu;
+    }
+  };
+  auto store_a = [&](int p, int t) {  // dz = A*(dy*relu') + B*z + D  (bn_bwd_apply_kernel)
+    const int k = t * BK + 8 * c8;
+    f4v cf[3][2];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      cf[q][0] = *reinterpret_cast<const f4v*>(Cf + q * K + k);
+      cf[q][1] = *reinterpret_cast<const f4v*>(Cf + q * K + k + 4);
+    }
+#pragma unroll
+    for (int i = 0; i < CPA; ++i) {
+      const int row = arow + i * RSTEP;
+      s8v o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d = bf2f((bf16_t)a0[p][i][j]);
+        if (X.mask_in) d = ((mb[p][i] >> j) & 1u) ? d : 0.f;
+        o[j] = (short)f2bf(cf[0][j >> 2][j & 3] * d + cf[1][j >> 2][j & 3] * bf2f((bf16_t)a1[p][i][j]) +
+                           cf[2][j >> 2][j & 3]);
+      }
+      *reinterpret_cast<s8v*>(As + row * BK + ((c8 ^ (row & 7)) << 3)) = o;
+    }
+  };
+  auto store_y = [&]() {
+#pragma unroll
+    for (int i = 0; i < CPY; ++i) {
+      const int c = tid + i * NT, lr = c / (BN / 8), lc = c % (BN / 8);
+      *reinterpret_cast<s8v*>(Ys + lr * BN + ((lc ^ nc_swz<BN>(lr)) << 3)) = yv[i];
+    }
+  };
+
+  load_y(0);
+#pragma unroll
+  for (int p = 0; p < PD; ++p) load_a(p, 0, p);
+  __syncthreads();  // W and the coefficient table are in LDS
+
+  bf16_t* Cg = reinterpret_cast<bf16_t*>(P.C);
+#pragma unroll 1
+  for (int tm = t_beg; tm < t_end; ++tm) {
+    const int lt = tm - t_beg, m0 = tm * BM;
+    f4v acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      store_a(s % PD, s);
+      if (s == 0) store_y();
+      // PD == KS: every refill is the next tile's, so this tile's epilogue operands go first
+      if (BNS && PD == STEPS && s == 0) load_epi(lt);
+      const int s2 = s + PD;  // refill the set just consumed
+      if (s2 < STEPS) {
+        load_a(s2 % PD, lt, s2);
+        if (BNS && s2 == STEPS - 1) load_epi(lt);
+      } else {
+        if (s2 == STEPS) load_y(lt + 1);
+        load_a(s2 % PD, lt + 1, s2 - STEPS);
+      }
+      lgkm_wait0();
+      bar256();
+      const short* Bs = Ws + s * (BK * BN);
+#pragma unroll 1
+      for (int kk = 0; kk < BK; kk += 32) {
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = read_frag_sw<BM, true>(As, wm * (BM / WM) + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = read_frag_sw<BN, false>(Bs, wn * (BN / WN) + j * 16, kk, lane);
+        mfma_acc<FM, FN>(acc, af, bfr);
+      }
+#pragma unroll 1
+      for (int mk0 = 0; mk0 < BM; mk0 += 32) {
+        bf16x8 dzt[2], yf[FNW];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+          const int mr = mk0 + 8 * g + q;
+          const int lc = ((wm * 32 + i * 16) >> 3) + (pp >> 1);
+          const int sub = 4 * (pp & 1);
+          const short* b0 = As + mr * BK + ((lc ^ (mr & 7)) << 3) + sub;
+          const short* b1 = As + (mr + 4) * BK + ((lc ^ ((mr + 4) & 7)) << 3) + sub;
+          s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b0));
+          s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b1));
+          dzt[i] = __builtin_bit_cast(bf16x8, s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+        }
+#pragma unroll
+        for (int j = 0; j < FNW; ++j) yf[j] = read_frag_sw<BN, false>(Ys, wn * WNB + j * 16, mk0, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < FNW; ++j)
+            accw[s][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yf[j], dzt[i], accw[s][i][j], 0, 0, 0);
+      }
+      lgkm_wait0();
+      bar256();
+    }
+
+    // epilogue (gemm_epilogue, EPI_BF16 / EPI_BF16_BN at beta 0): C tile -> LDS (As + Ys) as bf16
+    {
+      short* Cs = As;
+      const int rbase = wm * (BM / WM) + (lane & 15), cbase = wn * (BN / WN) + 4 * (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          s4v pk;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pk[r] = (short)f2bf(acc[i][j][r]);
+          *reinterpret_cast<s4v*>(Cs + EL::idx(rbase + i * 16, cbase + j * 16)) = pk;
+        }
+      __syncthreads();
+      float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, bzsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      (void)bsum;
+      (void)bzsum;
+#pragma unroll
+      for (int u = 0; u < IT; ++u) {
+        const int row = (tid + u * NT) / (BN / 8), gm = m0 + row;
+        if (gm >= P.M) continue;
+        const s8v v = *reinterpret_cast<const s8v*>(Cs + EL::idx(row, ecol));
+        *reinterpret_cast<s8v*>(Cg + (long)gm * P.ldc + ecol) = v;
+        if constexpr (BNS) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float g = ((mk[u] >> j) & 1u) ? bf2f((bf16_t)v[j]) : 0.f;
+            bsum[j] += g;
+            bzsum[j] += g * bf2f((bf16_t)zp[u][j]);
+          }
+        }
+      }
+      if constexpr (BNS) {
+        const int cg = tid % (BN / 8), part = tid / (BN / 8);
+        __syncthreads();  // Cs consumed (sred aliases it)
+        float* sred = reinterpret_cast<float*>(smem);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sred[part * BN + cg * 8 + j] = bsum[j];
+          sred[(PARTS + part) * BN + cg * 8 + j] = bzsum[j];
+        }
+        __syncthreads();
+        for (int c = tid; c < BN; c += NT) {
+          float ts = 0.f, tq = 0.f;
+          for (int pp = 0; pp < PARTS; ++pp) {
+            ts += sred[pp * BN + c];
+            tq += sred[(PARTS + pp) * BN + c];
+          }
+          float* st = P.stats + (long)tm * 2 * P.N;
+          st[c] = ts;
+          st[P.N + c] = tq;
+        }
+      }
+      __syncthreads();  // As / Ys free for the next tile's stores
+    }
+  }
+  vm_wait<0>();  // the range's last refill reads nothing, but let it retire before the slab stores
+
+  float* slab = ws + (long)blockIdx.x * K * N;
+#pragma unroll
+  for (int s = 0; s < STEPS; ++s)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < FNW; ++j) {
+        const int k = s * BK + wm * 32 + i * 16 + (lane & 15);
+        const int n = wn * WNB + j * 16 + 4 * (lane >> 4);
+        *reinterpret_cast<f4v*>(slab + (long)k * N + n) = accw[s][i][j];
+      }
+}
+
 }  // namespace ca

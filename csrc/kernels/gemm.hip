@@ -412,6 +412,37 @@ __global__ void __launch_bounds__(NT)
   mfma_gemm_xa_dw<EPI, KS, NC, BN, NT, BM>(P, X, Y, ldy, ws, tiles_per_block);
 }
 
+// the deep-stream form (ca_gemm_xa.h mfma_gemm_xa_dw_deep): PD = 1 two workgroups per CU,
+// PD = 2 / 4 one
+template <int EPI, int KS, int PD>
+__global__ void __launch_bounds__(256)
+    __attribute__((amdgpu_waves_per_eu(PD == 1 ? 2 : 1))) xa_dw_deep_kernel(
+        CoreParams P, XaParams X, const bf16_t* Y, long ldy, float* ws, int tiles_per_block) {
+  mfma_gemm_xa_dw_deep<EPI, KS, PD>(P, X, Y, ldy, ws, tiles_per_block);
+}
+
+// CLOUD_AMD_XA_DW_DEPTH: the K = 256 -> N = 64 kernel (0 = the one-step form above; 1, 2 or 4 =
+// the deep form with that many source steps in flight per workgroup).  Stage-1 conv3 shape,
+// M = 3.2M (bench/xa_dw_bench.py, profiles/r4_s26/): 1.43 / 0.99 / 1.05 / 1.05 ms with the
+// BN-statistics epilogue -- depth 1 at two workgroups per CU is the default.
+inline int xa_dw_depth() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_XA_DW_DEPTH");
+    v = (e && (e[0] == '0' || e[0] == '1' || e[0] == '2' || e[0] == '4')) ? e[0] - '0' : 1;
+  }
+  return v;
+}
+
+template <int PD>
+int xa_dw_deep_launch(const CoreParams& p, const XaParams& x, const bf16_t* Y, long ldy, float* ws, int g, int tpb,
+                      hipStream_t s) {
+  if (p.bnz) xa_dw_deep_kernel<EPI_BF16_BN, 4, PD><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
+  else xa_dw_deep_kernel<EPI_BF16, 4, PD><<<g, 256, 0, s>>>(p, x, Y, ldy, ws, tpb);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
 template <int KS, int NC, int BN = 64, int NT = 256>
 int xa_dw_launch(const CoreParams& p, const XaParams& x, const bf16_t* Y, long ldy, float* ws, int g, int tpb,
                  hipStream_t s) {
@@ -686,19 +717,26 @@ int ca_gemm_xa_dw(const bf16_t* src0, const bf16_t* src1, const uint8_t* mask_in
   p.stats2 = stats2;
   XaParams x{src0, src1, mask_in, c0, c1, c2, nullptr, nullptr, nullptr};
   const int tiles = (M + 127) / 128;
+  const int depth = (N == 64 && K == 256) ? xa_dw_depth() : 0;
+  static int w8 = -1;  // CLOUD_AMD_XA_DW_WAVES=8: one 8-wave workgroup per CU (one-step form)
+  if (w8 < 0) {
+    const char* e = getenv("CLOUD_AMD_XA_DW_WAVES");
+    w8 = (e && e[0] == '8') ? 1 : 0;
+  }
+  // deep form: beta 0, no residual / second BN, statistics exactly with a BN input
+  const bool deep = depth > 0 && !w8 && beta == 0.f && !res_src && !bnz2 && (bnz != nullptr) == (stats != nullptr);
+  // deep forms at one workgroup per CU: one tile range per CU
+  if (deep && depth >= 2 && blocks > cu_count()) blocks = cu_count();
   const int tpb = (tiles + blocks - 1) / blocks;
   const int g = (tiles + tpb - 1) / tpb;
   int rc;
   if (N == 64 && K == 64) rc = xa_dw_launch<1, 1>(p, x, Y, ldy, ws, g, tpb, s);
   else if (N == 64 && K == 128) rc = xa_dw_launch<2, 1>(p, x, Y, ldy, ws, g, tpb, s);
   else if (N == 64 && K == 256) {
-    // 4-wave workgroups, two per CU; CLOUD_AMD_XA_DW_WAVES=8: one 8-wave workgroup per CU
-    static int w8 = -1;
-    if (w8 < 0) {
-      const char* e = getenv("CLOUD_AMD_XA_DW_WAVES");
-      w8 = (e && e[0] == '8') ? 1 : 0;
-    }
-    rc = w8 ? xa_dw_launch<4, 1, 64, 512>(p, x, Y, ldy, ws, g, tpb, s) : xa_dw_launch<4, 1>(p, x, Y, ldy, ws, g, tpb, s);
+    if (deep && depth == 1) rc = xa_dw_deep_launch<1>(p, x, Y, ldy, ws, g, tpb, s);
+    else if (deep && depth == 2) rc = xa_dw_deep_launch<2>(p, x, Y, ldy, ws, g, tpb, s);
+    else if (deep) rc = xa_dw_deep_launch<4>(p, x, Y, ldy, ws, g, tpb, s);
+    else rc = w8 ? xa_dw_launch<4, 1, 64, 512>(p, x, Y, ldy, ws, g, tpb, s) : xa_dw_launch<4, 1>(p, x, Y, ldy, ws, g, tpb, s);
   }
   else if (K == 64 && N == 256) rc = xa_dw_launch<1, 4>(p, x, Y, ldy, ws, g, tpb, s);
   else if (N == 128 && K == 512) rc = xa_dw_launch<8, 1, 128, 512>(p, x, Y, ldy, ws, g, tpb, s);
