@@ -74,7 +74,9 @@ def test_dgrad_bnbwd_vs_fp32(M, Cout, Cin, epi):
 DW_CASES = [(4096, 256, 64, "bn"), (1000, 128, 64, "bn"), (777, 64, 64, "plain"), (70000, 256, 64, "bn"),
             (4096, 256, 64, "plain"), (3000, 64, 256, "res2"), (1000, 64, 256, "res"), (777, 64, 256, "bn"),
             (300, 64, 64, "res"), (5000, 64, 256, "plain"), (5000, 512, 128, "bn"), (777, 512, 128, "plain"),
-            (100000, 512, 128, "bn")]
+            (100000, 512, 128, "bn"), (777, 256, 64, "bn"), (777, 256, 64, "plain0"), (70000, 256, 64, "plain0")]
+# K 256 -> N 64 with beta 0 ("bn", "plain0": a fresh output, the projection shortcut's form) runs
+# the deep-stream kernel (mfma_gemm_xa_dw_deep); the other epilogues the one-step form
 
 
 @pytest.mark.parametrize("M,Cout,Cin,epi", DW_CASES)
@@ -112,7 +114,7 @@ def test_dgrad_wgrad_bnbwd_vs_fp32(M, Cout, Cin, epi, blocks, dw_dtype):
     if epi in ("res", "res2"):
         kw.update(res=(shp(src), _mask_bits(act_r)), beta=1.0)
         want = want + src.float() * act_r.float()
-    if epi == "plain":  # beta accumulate into the existing dx (the projection block's shortcut gradient)
+    if epi == "plain":  # beta accumulate into an existing dx
         kw.update(out=shp(old.clone()), beta=1.0)
         want = want + old.float()
     r = raw.conv1x1_dgrad_wgrad_bnbwd(shp(dy), shp(z), _mask_bits(act), coef, w, shp(y), dw, dw_beta=1.0,
@@ -277,3 +279,30 @@ def test_resnet_fused_dgrad_wgrad_close():
             assert rel(x[o:o + k], y[o:o + k]) < 2e-2, (n, rel(x[o:o + k], y[o:o + k]))
     for a, b in zip(l1, l0):
         assert abs(a - b) < 0.05 * abs(b) + 1e-3, (l1, l0)
+
+
+@pytest.mark.gpu
+def test_deep_fused_gradient_matches_one_step_form():
+    """The deep-stream fused input+weight gradient (CLOUD_AMD_XA_DW_DEPTH=1, the default) against
+    the one-step form (=0) on the stage-1 conv3 shape: the same dx bits as the one-step plain
+    kernel, repeatable bits for dx and the BN statistics, weight gradients equal up to the slab
+    summation order (bench/xa_dw_bench.py in one process per form: the form is read once)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for d in ("0", "1"):
+        env = dict(os.environ, CLOUD_AMD_XA_DW_DEPTH=d)
+        r = subprocess.run([sys.executable, os.path.join(root, "bench", "xa_dw_bench.py"), "--batch", "8",
+                            "--iters", "2"], env=env, capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[d] = json.loads(r.stdout.strip().splitlines()[-1])
+    deep, one = out["1"], out["0"]
+    assert deep["dx_repeat_equal"] and deep["stats_repeat_equal"] and deep["dx_bn_vs_plain_equal"]
+    assert deep["plain"]["dx_sum"] == one["plain"]["dx_sum"] and deep["bn"]["dx_sum"] == one["plain"]["dx_sum"]
+    for k in ("plain", "bn"):
+        assert abs(deep[k]["dw_sum"] - one[k]["dw_sum"]) <= 1e-4 * one[k]["dw_abs"]
+    assert abs(deep["bn"]["stats_sum"] - one["bn"]["stats_sum"]) <= 1e-5 * abs(one["bn"]["stats_sum"]) + 1e-3
