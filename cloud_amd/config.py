@@ -103,10 +103,12 @@ _VARS = [
     Var("CLOUD_AMD_BN_FOLD_FWD", bool, True, "ResNet block forward: bn2's apply runs in conv3's operand fetch and "
         "bn3's (+ residual) in the next block's conv1 (ca_gemm_xa.h); the applied tensors are written once, by "
         "those GEMMs", "ops"),
-    Var("CLOUD_AMD_BN_FOLD_MAX_N", int, 4096, "BN fold sites kept: only GEMMs with K >= 2N and N <= this "
-        "(ResNet-50: bn3 -> conv3 dgrad and bn3 -> next conv1, every stage); the transform-A core re-runs the "
-        "BN transform per N tile and cannot pipeline a one-K-tile GEMM, so the short-K sites (bn2 -> conv3, "
-        "bn1 -> conv1 dgrad) measured slower than the separate pass (docs/performance.md, round 4)", "ops"),
+    Var("CLOUD_AMD_BN_FOLD_MAX_N", int, 128, "BN fold sites kept: only GEMMs with K >= 2N and N <= this "
+        "(ResNet-50 default: bn3 -> conv3 dgrad and bn3 -> next conv1 at stages 1-2; 4096 = every stage); the "
+        "transform-A core re-runs the BN transform per N tile and cannot pipeline a one-K-tile GEMM, so the short-K "
+        "sites (bn2 -> conv3, bn1 -> conv1 dgrad) measured slower than the separate pass, and at stages 3-4 (N 256 / "
+        "512: 2-4 N tiles re-transform each A tile) the fold is 0.4 % slower end to end (docs/performance.md, "
+        "round 4)", "ops"),
     Var("CLOUD_AMD_BN_FOLD_WGRAD", bool, True, "bn3 -> conv3 fold at 64 input channels (ResNet stage 1): conv3's weight "
         "gradient runs in the same kernel as its input gradient (ca_gemm_xa.h mfma_gemm_xa_dw), so the BN-backward "
         "output dz3 is never written", "ops"),
