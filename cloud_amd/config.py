@@ -81,6 +81,8 @@ _VARS = [
         "the workgroups (one contiguous sweep); 0 = one contiguous row chunk per workgroup", "ops"),
     Var("CLOUD_AMD_CONV_TALL", bool, True, "<= 64-channel 3x3 convolutions (fwd, stride-1 dgrad): 256 x 64 tiles "
         "with 4 x 1 waves; 0 = 128 x 64 with 2 x 2 waves", "ops"),
+    Var("CLOUD_AMD_STEM_TALL", bool, True, "space-to-depth stem convolution on the tall 256 x 64 tiles too (0.88 -> "
+        "0.72 ms per call at b1024); 0 = 128 x 64 tiles (A/B runs)", "ops"),
     Var("CLOUD_AMD_BN_GROUPS_MAX", int, 512, "BatchNorm statistics: most groups of the first-level reduction of the "
         "per-tile partial rows (1..512; ~64 rows per group)", "ops"),
     Var("CLOUD_AMD_GEMM_LIB", str, "never", "plain bf16 GEMMs (bias / accumulate only, no fused epilogue): 'never' "

@@ -789,6 +789,17 @@ bool tall_tiles() {
   return v != 0;
 }
 
+// The space-to-depth stem (K = 3 row tiles, N = 64) on the tall 256 x 64 tiles as well: 0.88 ->
+// 0.72 ms per call at b1024 (profiles/r4_s34/); CLOUD_AMD_STEM_TALL=0 keeps 128 x 64 (A/B runs)
+bool stem_tall() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_STEM_TALL");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
+}
+
 // CLOUD_AMD_GEMM_CORE=reg selects the register-staged core (A/B comparisons).
 // 0 = register-staged, 1 = glds single stage (4 waves), 2 = glds double-buffered (8 waves)
 int core_kind() {
@@ -899,6 +910,9 @@ int ca_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   if (sh == 1 && sw == 1 && ph == 0 && pw == 0 && KW * Cin == BK && tapmask_loaders() && use_glds() &&
       (long)Nb * H * W * Cin * 2 < (long)BUF_CAP) {
     // one K tile per kernel row (the space-to-depth stem): row-segment loader
+    if (Cout <= 64 && stem_tall())
+      return stats ? launch_n64<ConvFwdA, DenseKC, GConvRowA, GDenseKC, EPI_BF16_ST>(p, s)
+                   : launch_n64<ConvFwdA, DenseKC, GConvRowA, GDenseKC, EPI_BF16>(p, s);
     if (Cout <= 64)
       return stats ? launch<128, 64, ConvFwdA, DenseKC, GConvRowA, GDenseKC, EPI_BF16_ST>(p, 1, s)
                    : launch<128, 64, ConvFwdA, DenseKC, GConvRowA, GDenseKC, EPI_BF16>(p, 1, s);
