@@ -62,8 +62,9 @@ _VARS = [
         "(ResNet stem, layers 1-2): split-K workgroup target", "ops"),
     Var("CLOUD_AMD_STEM_WGRAD_BLOCKS", int, 2048, "space-to-depth stem weight gradient (the last kernel of the "
         "backward pass): split-K workgroup target", "ops"),
-    Var("CLOUD_AMD_DENSE_WGRAD_BLOCKS", int, 1024, "dense-layer weight gradients (BERT): split-K workgroup target "
-        "(1024 with the split-major XCD mapping: 6,210 / 6,231 vs 6,153 / 6,131 seq/s at 512)",
+    Var("CLOUD_AMD_DENSE_WGRAD_BLOCKS", int, 640, "dense-layer weight gradients (BERT): split-K workgroup target "
+        "(round 4, same box: 640 -> 6,993 / 6,993 seq/s, 768 -> 6,962 / 6,952, 1024 -> 6,892 / 6,911, 512 -> "
+        "6,865 / 6,896; profiles/r4_s36/)",
         "ops"),
     Var("CLOUD_AMD_GEMM_256X128", bool, False, "GEMMs whose 256 x 128 grid fills whole rounds (and 256 x 256 does "
         "not) on the 256 x 128 single-phase core (csrc/include/ca_gemm256p8.h); measured slower than the 128 core "
