@@ -724,7 +724,14 @@ int ca_gemm_xa_dw(const bf16_t* src0, const bf16_t* src1, const uint8_t* mask_in
     w8 = (e && e[0] == '8') ? 1 : 0;
   }
   // deep form: beta 0, no residual / second BN, statistics exactly with a BN input
-  const bool deep = depth > 0 && !w8 && beta == 0.f && !res_src && !bnz2 && (bnz != nullptr) == (stats != nullptr);
+  bool deep = depth > 0 && !w8 && beta == 0.f && !res_src && !bnz2 && (bnz != nullptr) == (stats != nullptr);
+  {  // the deep form reads each tensor through ONE buffer window over a workgroup's tile range
+    const int b = (depth >= 2 && blocks > cu_count()) ? cu_count() : blocks;
+    const long rows = (long)((tiles + b - 1) / b) * 128;
+    long ld = lda > ldy ? lda : ldy;
+    if (ldc > ld) ld = ldc;
+    if (rows * ld * 2 >= (long)BUF_CAP) deep = false;
+  }
   // deep forms at one workgroup per CU: one tile range per CU
   if (deep && depth >= 2 && blocks > cu_count()) blocks = cu_count();
   const int tpb = (tiles + blocks - 1) / blocks;
