@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from .. import config
 from . import _ext
 
 
@@ -148,12 +149,24 @@ class _StemTailFn(torch.autograd.Function):
         N, H, W, C = z.shape
         OH, OW = y.shape[1], y.shape[2]
         dev = z.device
-        g = torch.empty_like(z)
+        dy = dy.contiguous()
+        st = _ext.stream_handle(dev)
         parts = torch.empty((ext.maxpool_bnstats_parts(N, H, W, C), 2, C), dtype=torch.float32, device=dev)
-        ext.maxpool_bwd_s2k3_bnstats(dy.contiguous().data_ptr(), y.data_ptr(), idx.data_ptr(), z.data_ptr(),
-                                     g.data_ptr(), parts.data_ptr(), N, H, W, C, OH, OW, _ext.stream_handle(dev))
         dgamma = torch.empty(C, dtype=torch.float32, device=dev) if gamma is not None else None
         dbeta = torch.empty(C, dtype=torch.float32, device=dev) if ctx.has_beta else None
+        if config.get("CLOUD_AMD_STEM_BWD_RECOMPUTE"):
+            # statistics pass, then the apply pass recomputes the pooled gradient g per 2x2 block:
+            # g (N x H x W x C) is never written or read back
+            ext.maxpool_bwd_s2k3_bnstats(dy.data_ptr(), y.data_ptr(), idx.data_ptr(), z.data_ptr(), 0,
+                                         parts.data_ptr(), N, H, W, C, OH, OW, st)
+            coef = raw.bn_bwd_coef(C, N * H * W, gamma, stats, parts, dgamma=dgamma, dbeta=dbeta)
+            dz = torch.empty_like(z)
+            ext.maxpool_bwd_s2k3_bnapply(dy.data_ptr(), y.data_ptr(), idx.data_ptr(), z.data_ptr(), coef.data_ptr(),
+                                         dz.data_ptr(), N, H, W, C, OH, OW, st)
+            return dz, dgamma, dbeta, None, None, None, None, None
+        g = torch.empty_like(z)
+        ext.maxpool_bwd_s2k3_bnstats(dy.data_ptr(), y.data_ptr(), idx.data_ptr(), z.data_ptr(),
+                                     g.data_ptr(), parts.data_ptr(), N, H, W, C, OH, OW, st)
         dz, _ = raw.bn_bwd(g, None, z, gamma, stats, False, dgamma=dgamma, dbeta=dbeta, partials=parts)
         return dz, dgamma, dbeta, None, None, None, None, None
 

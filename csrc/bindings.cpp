@@ -68,6 +68,8 @@ int ca_bn_relu_maxpool_s2k3(const bf16_t*, const float*, bf16_t*, uint8_t*, int,
 int ca_maxpool_bnstats_parts(int, int, int, int);
 int ca_maxpool_bwd_s2k3_bnstats(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, bf16_t*, float*, int, int,
                                 int, int, int, int, hipStream_t);
+int ca_maxpool_bwd_s2k3_bnapply(const bf16_t*, const bf16_t*, const uint8_t*, const bf16_t*, const float*, bf16_t*, int,
+                                int, int, int, int, int, hipStream_t);
 int ca_conv_fwd_ex(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int,
                    const float*, int, hipStream_t);
 int ca_conv_fwd(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int, float*,
@@ -299,6 +301,13 @@ PYBIND11_MODULE(_C, m) {
     check(ca_maxpool_bwd_s2k3_bnstats(P(const bf16_t*, dy), P(const bf16_t*, yp), P(const uint8_t*, idx),
                                       P(const bf16_t*, z), P(bf16_t*, g), P(float*, part), N, H, W, C, OH, OW, S(s)),
           "maxpool_bwd_s2k3_bnstats");
+  });
+  m.def("maxpool_bwd_s2k3_bnapply", [](u64 dy, u64 yp, u64 idx, u64 z, u64 coef, u64 dz, int N, int H, int W, int C,
+                                       int OH, int OW, u64 s) {
+    check(ca_maxpool_bwd_s2k3_bnapply(P(const bf16_t*, dy), P(const bf16_t*, yp), P(const uint8_t*, idx),
+                                      P(const bf16_t*, z), P(const float*, coef), P(bf16_t*, dz), N, H, W, C, OH, OW,
+                                      S(s)),
+          "maxpool_bwd_s2k3_bnapply");
   });
   m.def("conv_fwd_ex", [](u64 x, u64 w, u64 y, int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh,
                           int sw, int ph, int pw, u64 bias, int act, u64 s) {

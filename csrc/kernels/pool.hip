@@ -367,6 +367,59 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_s2k3_kernel(const bf16_t*
 // per-block channel partials [sum g | sum g*z] -- the BN backward skips its statistics
 // pass over g and z.  The grid is fixed (grid-stride loop); 256 % (C/8) == 0 keeps each
 // thread on one channel group.
+//
+// WRITE_G = false: statistics only; maxpool_bwd_s2k3_bnapply_kernel then recomputes g from
+// the pooled gradient (0.6 GB of dy / pooled output / argmax instead of the 1.6 GB g written
+// and read back at b1024) and applies the BN backward to it -- g never reaches memory.
+
+// g of the 2x2 stem-pixel block (bi, bj) of image n, channels 8 vc .. 8 vc + 7, rounded to
+// bf16 as the stored tensor was
+__device__ __forceinline__ void stem_block_grad(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ ypool,
+                                                const uint8_t* __restrict__ idx, int n, int bi, int bj, int vc,
+                                                int C, int OH, int OW, float (&acc)[2][2][8]) {
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[a][b][j] = 0.f;
+#pragma unroll
+  for (int wy = 0; wy < 2; ++wy) {
+    const int oh = bi + wy;
+    if (oh >= OH) continue;
+#pragma unroll
+    for (int wx = 0; wx < 2; ++wx) {
+      const int ow = bj + wx;
+      if (ow >= OW) continue;
+      const long oo = (((long)n * OH + oh) * OW + ow) * C + vc * 8;
+      const us8 gv = *reinterpret_cast<const us8*>(dy + oo);
+      const us8 yv = *reinterpret_cast<const us8*>(ypool + oo);
+      const uint64_t id = *reinterpret_cast<const uint64_t*>(idx + oo);
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int kh = a + 1 - 2 * wy;
+        if (kh < 0 || kh > 2) continue;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int kw = b + 1 - 2 * wx;
+          if (kw < 0 || kw > 2) continue;
+          const uint32_t want = (uint32_t)(kh * 3 + kw);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (((id >> (8 * j)) & 0xff) == want && bf2f(yv[j]) > 0.f) acc[a][b][j] += bf2f(gv[j]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[a][b][j] = bf2f(f2bf(acc[a][b][j]));
+}
+
+template <bool WRITE_G>
 __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnstats_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ ypool, const uint8_t* __restrict__ idx,
     const bf16_t* __restrict__ z, bf16_t* __restrict__ g, float* __restrict__ part, int N, int H, int W, int C,
@@ -386,40 +439,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnstats_kernel(
     const int bi = (int)(r % Hb);
     const int n = (int)(r / Hb);
     float acc[2][2][8];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[a][b][j] = 0.f;
-#pragma unroll
-    for (int wy = 0; wy < 2; ++wy) {
-      const int oh = bi + wy;
-      if (oh >= OH) continue;
-#pragma unroll
-      for (int wx = 0; wx < 2; ++wx) {
-        const int ow = bj + wx;
-        if (ow >= OW) continue;
-        const long oo = (((long)n * OH + oh) * OW + ow) * C + vc * 8;
-        const us8 gv = *reinterpret_cast<const us8*>(dy + oo);
-        const us8 yv = *reinterpret_cast<const us8*>(ypool + oo);
-        const uint64_t id = *reinterpret_cast<const uint64_t*>(idx + oo);
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-          const int kh = a + 1 - 2 * wy;
-          if (kh < 0 || kh > 2) continue;
-#pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            const int kw = b + 1 - 2 * wx;
-            if (kw < 0 || kw > 2) continue;
-            const uint32_t want = (uint32_t)(kh * 3 + kw);
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (((id >> (8 * j)) & 0xff) == want && bf2f(yv[j]) > 0.f) acc[a][b][j] += bf2f(gv[j]);
-          }
-        }
-      }
-    }
+    stem_block_grad(dy, ypool, idx, n, bi, bj, vc, C, OH, OW, acc);
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
       const int h = 2 * bi + a;
@@ -434,11 +454,11 @@ __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnstats_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           o[j] = f2bf(acc[a][b][j]);
-          const float gr = bf2f(o[j]);  // the stored (bf16) gradient, as the BN backward reads it
+          const float gr = acc[a][b][j];  // the stored (bf16) gradient, as the BN backward reads it
           s1[j] += gr;
           s2[j] += gr * bf2f(zv[j]);
         }
-        *reinterpret_cast<us8*>(g + off) = o;
+        if constexpr (WRITE_G) *reinterpret_cast<us8*>(g + off) = o;
       }
     }
   }
@@ -454,6 +474,49 @@ __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnstats_kernel(
     float tsum = 0.f;
     for (int th = vc; th < 256; th += CT) tsum += red[th][8 * k + j];
     part[(long)blockIdx.x * 2 * C + c] = tsum;
+  }
+}
+
+// dz = A*g + B*z + D (bn_bwd_apply_kernel<false, false>) with g recomputed per 2x2 block
+__global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnapply_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ ypool, const uint8_t* __restrict__ idx,
+    const bf16_t* __restrict__ z, const float* __restrict__ coef, bf16_t* __restrict__ dz, int N, int H, int W,
+    int C, int OH, int OW) {
+  const int CT = C / 8;
+  const int Hb = (H + 1) / 2, Wb = (W + 1) / 2;
+  const long total = (long)N * Hb * Wb * CT;
+  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (long t = t0; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int vc = (int)(t % CT);
+    long r = t / CT;
+    const int bj = (int)(r % Wb); r /= Wb;
+    const int bi = (int)(r % Hb);
+    const int n = (int)(r / Hb);
+    float A[8], B[8], D[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      A[j] = coef[vc * 8 + j];
+      B[j] = coef[C + vc * 8 + j];
+      D[j] = coef[2 * C + vc * 8 + j];
+    }
+    float acc[2][2][8];
+    stem_block_grad(dy, ypool, idx, n, bi, bj, vc, C, OH, OW, acc);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int h = 2 * bi + a;
+      if (h >= H) continue;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int w = 2 * bj + b;
+        if (w >= W) continue;
+        const long off = (((long)n * H + h) * W + w) * C + vc * 8;
+        const us8 zv = *reinterpret_cast<const us8*>(z + off);
+        us8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(A[j] * acc[a][b][j] + B[j] * bf2f(zv[j]) + D[j]);
+        *reinterpret_cast<us8*>(dz + off) = o;
+      }
+    }
   }
 }
 
@@ -479,11 +542,26 @@ int ca_maxpool_bnstats_parts(int N, int H, int W, int C) {
 int ca_maxpool_bwd_s2k3_bnstats(const bf16_t* dy, const bf16_t* ypool, const uint8_t* idx, const bf16_t* z, bf16_t* g,
                                 float* part, int N, int H, int W, int C, int OH, int OW, hipStream_t st) {
   if (C % 8 != 0 || 256 % (C / 8) != 0 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
-  maxpool_bwd_s2k3_bnstats_kernel<<<ca_maxpool_bnstats_parts(N, H, W, C), 256, 0, st>>>(dy, ypool, idx, z, g, part,
-                                                                                         N, H, W, C, OH, OW);
+  const int grid = ca_maxpool_bnstats_parts(N, H, W, C);
+  if (g) maxpool_bwd_s2k3_bnstats_kernel<true><<<grid, 256, 0, st>>>(dy, ypool, idx, z, g, part, N, H, W, C, OH, OW);
+  else maxpool_bwd_s2k3_bnstats_kernel<false><<<grid, 256, 0, st>>>(dy, ypool, idx, z, g, part, N, H, W, C, OH, OW);
   CA_LAUNCH_CHECK();
   return 0;
 }
+
+// dz[N,H,W,C] = the BN backward (coef = [A | B | D] from the statistics finalize) of the stem
+// max-pool gradient, recomputed from the pooled gradient / output / argmax (see above).
+int ca_maxpool_bwd_s2k3_bnapply(const bf16_t* dy, const bf16_t* ypool, const uint8_t* idx, const bf16_t* z,
+                                const float* coef, bf16_t* dz, int N, int H, int W, int C, int OH, int OW,
+                                hipStream_t st) {
+  if (C % 8 != 0 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
+  const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+  maxpool_bwd_s2k3_bnapply_kernel<<<ca_stream_grid(total, 256), 256, 0, st>>>(dy, ypool, idx, z, coef, dz, N, H, W,
+                                                                              C, OH, OW);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
 
 int ca_stem_s2d(const bf16_t* x, bf16_t* y, int N, int H, int W, int C, int Hs, int Ws, int pad, hipStream_t st) {
   if (C < 1 || C > 4) return -1;
