@@ -84,11 +84,11 @@ _VARS = [
         "with 4 x 1 waves; 0 = 128 x 64 with 2 x 2 waves", "ops"),
     Var("CLOUD_AMD_STEM_TALL", bool, True, "space-to-depth stem convolution on the tall 256 x 64 tiles too (0.88 -> "
         "0.72 ms per call at b1024); 0 = 128 x 64 tiles (A/B runs)", "ops"),
-    Var("CLOUD_AMD_STEM_BWD_RECOMPUTE", bool, False, "ResNet stem tail backward: a statistics-only max-pool "
+    Var("CLOUD_AMD_STEM_BWD_RECOMPUTE", bool, True, "ResNet stem tail backward: a statistics-only max-pool "
         "backward pass, then the BN-backward apply recomputes the pooled gradient per 2x2 block (the 112x112 "
-        "gradient is never written).  Saves 3.3 GB per step at b1024 but the two window-gather passes run at "
-        "3.1 / 4.1 TB/s: 0.86 + 1.05 ms against 0.97 + 0.91 for write-then-apply (neutral end to end, "
-        "profiles/r4_s42/); off by default", "ops"),
+        "gradient is never written: 3.3 GB fewer per step at b1024).  With the window loads issued ahead of "
+        "any branch: 0.65 + 0.90 ms against 1.09 + 0.94 for write-then-apply, +0.8 % end to end "
+        "(profiles/r4_s44/); 0 = write g and run the separate apply pass", "ops"),
     Var("CLOUD_AMD_BN_GROUPS_MAX", int, 512, "BatchNorm statistics: most groups of the first-level reduction of the "
         "per-tile partial rows (1..512; ~64 rows per group)", "ops"),
     Var("CLOUD_AMD_GEMM_LIB", str, "never", "plain bf16 GEMMs (bias / accumulate only, no fused epilogue): 'never' "

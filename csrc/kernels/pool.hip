@@ -330,20 +330,31 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_s2k3_kernel(const bf16_t*
       best[j] = -INFINITY;
       bi[j] = 0;
     }
+    // all nine window loads first (clamped addresses, border taps masked after): no load
+    // sits behind a branch, so the nine round trips overlap instead of running in sequence
+    us8 v[3][3];
+    bool ok[3][3];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
       const int h = oh * 2 - 1 + kh;
-      if (h < 0 || h >= H) continue;
+      const int hc = h < 0 ? 0 : (h >= H ? H - 1 : h);
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
         const int w = ow * 2 - 1 + kw;
-        if (w < 0 || w >= W) continue;
-        us8 v = *reinterpret_cast<const us8*>(z + (((long)n * H + h) * W + w) * C + vc * 8);
+        const int wc = w < 0 ? 0 : (w >= W ? W - 1 : w);
+        ok[kh][kw] = h >= 0 && h < H && w >= 0 && w < W;
+        v[kh][kw] = *reinterpret_cast<const us8*>(z + (((long)n * H + hc) * W + wc) * C + vc * 8);
+      }
+    }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float f = fmaxf(bf2f(v[j]) * sc[j] + sh[j], 0.f);
+          float f = fmaxf(bf2f(v[kh][kw][j]) * sc[j] + sh[j], 0.f);
           f = bf2f(f2bf(f));
-          if (f > best[j]) { best[j] = f; bi[j] = (uint8_t)(kh * 3 + kw); }
+          if (ok[kh][kw] && f > best[j]) { best[j] = f; bi[j] = (uint8_t)(kh * 3 + kw); }
         }
       }
     }
@@ -383,6 +394,19 @@ __device__ __forceinline__ void stem_block_grad(const bf16_t* __restrict__ dy, c
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[a][b][j] = 0.f;
+  // the four windows' loads first (clamped, masked after): none behind a branch
+  us8 gvs[2][2], yvs[2][2];
+  uint64_t ids[2][2];
+#pragma unroll
+  for (int wy = 0; wy < 2; ++wy)
+#pragma unroll
+    for (int wx = 0; wx < 2; ++wx) {
+      const int oh = bi + wy < OH ? bi + wy : OH - 1, ow = bj + wx < OW ? bj + wx : OW - 1;
+      const long oo = (((long)n * OH + oh) * OW + ow) * C + vc * 8;
+      gvs[wy][wx] = *reinterpret_cast<const us8*>(dy + oo);
+      yvs[wy][wx] = *reinterpret_cast<const us8*>(ypool + oo);
+      ids[wy][wx] = *reinterpret_cast<const uint64_t*>(idx + oo);
+    }
 #pragma unroll
   for (int wy = 0; wy < 2; ++wy) {
     const int oh = bi + wy;
@@ -391,10 +415,9 @@ __device__ __forceinline__ void stem_block_grad(const bf16_t* __restrict__ dy, c
     for (int wx = 0; wx < 2; ++wx) {
       const int ow = bj + wx;
       if (ow >= OW) continue;
-      const long oo = (((long)n * OH + oh) * OW + ow) * C + vc * 8;
-      const us8 gv = *reinterpret_cast<const us8*>(dy + oo);
-      const us8 yv = *reinterpret_cast<const us8*>(ypool + oo);
-      const uint64_t id = *reinterpret_cast<const uint64_t*>(idx + oo);
+      const us8 gv = gvs[wy][wx];
+      const us8 yv = yvs[wy][wx];
+      const uint64_t id = ids[wy][wx];
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
         const int kh = a + 1 - 2 * wy;
@@ -438,6 +461,14 @@ __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnstats_kernel(
     const int bj = (int)(r % Wb); r /= Wb;
     const int bi = (int)(r % Hb);
     const int n = (int)(r / Hb);
+    us8 zvs[2][2];  // z of the block, loaded up front (clamped) with the windows' operands
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int h = 2 * bi + a < H ? 2 * bi + a : H - 1, w = 2 * bj + b < W ? 2 * bj + b : W - 1;
+        zvs[a][b] = *reinterpret_cast<const us8*>(z + (((long)n * H + h) * W + w) * C + vc * 8);
+      }
     float acc[2][2][8];
     stem_block_grad(dy, ypool, idx, n, bi, bj, vc, C, OH, OW, acc);
 #pragma unroll
@@ -449,7 +480,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnstats_kernel(
         const int w = 2 * bj + b;
         if (w >= W) continue;
         const long off = (((long)n * H + h) * W + w) * C + vc * 8;
-        const us8 zv = *reinterpret_cast<const us8*>(z + off);
+        const us8 zv = zvs[a][b];
         us8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
