@@ -313,61 +313,73 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_s2k3_kernel(const bf16_t*
                                                                   const float* __restrict__ ss,
                                                                   bf16_t* __restrict__ y, uint8_t* __restrict__ idx,
                                                                   int N, int H, int W, int C, int OH, int OW) {
+  // one thread: two horizontally adjacent outputs (ow, ow + 1), 8 channels -- their windows
+  // share a column, so 15 loads instead of 18, all issued before any is used (clamped
+  // addresses, border taps masked after)
   const int CT = C / 8;
-  const long total = (long)N * OH * OW * CT;
+  const int OW2 = (OW + 1) / 2;
+  const long total = (long)N * OH * OW2 * CT;
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
     const int vc = (int)(t % CT);
     long r = t / CT;
-    const int ow = (int)(r % OW); r /= OW;
+    const int ow0 = 2 * (int)(r % OW2); r /= OW2;
     const int oh = (int)(r % OH);
     const int n = (int)(r / OH);
-    float sc[8], sh[8], best[8];
-    uint8_t bi[8];
+    float sc[8], sh[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       sc[j] = ss[vc * 8 + j];
       sh[j] = ss[C + vc * 8 + j];
-      best[j] = -INFINITY;
-      bi[j] = 0;
     }
-    // all nine window loads first (clamped addresses, border taps masked after): no load
-    // sits behind a branch, so the nine round trips overlap instead of running in sequence
-    us8 v[3][3];
-    bool ok[3][3];
+    us8 v[3][5];
+    bool ok[3][5];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
       const int h = oh * 2 - 1 + kh;
       const int hc = h < 0 ? 0 : (h >= H ? H - 1 : h);
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int w = ow * 2 - 1 + kw;
+      for (int kx = 0; kx < 5; ++kx) {
+        const int w = ow0 * 2 - 1 + kx;
         const int wc = w < 0 ? 0 : (w >= W ? W - 1 : w);
-        ok[kh][kw] = h >= 0 && h < H && w >= 0 && w < W;
-        v[kh][kw] = *reinterpret_cast<const us8*>(z + (((long)n * H + hc) * W + wc) * C + vc * 8);
+        ok[kh][kx] = h >= 0 && h < H && w >= 0 && w < W;
+        v[kh][kx] = *reinterpret_cast<const us8*>(z + (((long)n * H + hc) * W + wc) * C + vc * 8);
       }
     }
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
+    for (int q = 0; q < 2; ++q) {
+      const int ow = ow0 + q;
+      if (ow >= OW) continue;
+      float best[8];
+      uint8_t bi[8];
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
+      for (int j = 0; j < 8; ++j) {
+        best[j] = -INFINITY;
+        bi[j] = 0;
+      }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float f = fmaxf(bf2f(v[kh][kw][j]) * sc[j] + sh[j], 0.f);
-          f = bf2f(f2bf(f));
-          if (ok[kh][kw] && f > best[j]) { best[j] = f; bi[j] = (uint8_t)(kh * 3 + kw); }
+      for (int kh = 0; kh < 3; ++kh) {
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int kx = 2 * q + kw;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float f = fmaxf(bf2f(v[kh][kx][j]) * sc[j] + sh[j], 0.f);
+            f = bf2f(f2bf(f));
+            if (ok[kh][kx] && f > best[j]) { best[j] = f; bi[j] = (uint8_t)(kh * 3 + kw); }
+          }
         }
       }
-    }
-    us8 o;
-    uint64_t packed = 0;
+      us8 o;
+      uint64_t packed = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      o[j] = f2bf(best[j]);
-      packed |= (uint64_t)bi[j] << (8 * j);
+      for (int j = 0; j < 8; ++j) {
+        o[j] = f2bf(best[j]);
+        packed |= (uint64_t)bi[j] << (8 * j);
+      }
+      const long oo = (((long)n * OH + oh) * OW + ow) * C + vc * 8;
+      *reinterpret_cast<us8*>(y + oo) = o;
+      *reinterpret_cast<uint64_t*>(idx + oo) = packed;
     }
-    const long oo = (((long)n * OH + oh) * OW + ow) * C + vc * 8;
-    *reinterpret_cast<us8*>(y + oo) = o;
-    *reinterpret_cast<uint64_t*>(idx + oo) = packed;
   }
 }
 
@@ -556,7 +568,7 @@ extern "C" {
 int ca_bn_relu_maxpool_s2k3(const bf16_t* z, const float* ss, bf16_t* y, uint8_t* idx, int N, int H, int W, int C,
                             int OH, int OW, hipStream_t st) {
   if (C % 8 != 0 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
-  const long total = (long)N * OH * OW * (C / 8);
+  const long total = (long)N * OH * ((OW + 1) / 2) * (C / 8);
   const int grid = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
   bn_relu_maxpool_s2k3_kernel<<<grid, 256, 0, st>>>(z, ss, y, idx, N, H, W, C, OH, OW);
   CA_LAUNCH_CHECK();
