@@ -110,7 +110,6 @@ def main():
     from cloud_amd.optim import SGD
     from cloud_amd.parallel import strategy as strategy_mod
     from cloud_amd.runtime import gc_control
-    from cloud_amd.runtime.step_pacer import StepPacer
     from cloud_amd.utils import dist_env, trace
 
     if args.device == "cpu":
@@ -180,12 +179,12 @@ def main():
     # (HIP-graph capture of this step measured slower than eager on ROCm 7.2 at b256/b512:
     # kernel boundaries cost the same in a graph; not offered here -- docs/performance.md)
     step_fn = train_step
-    # at most CLOUD_AMD_MAX_STEPS_IN_FLIGHT steps queued ahead of the GPU (warmup and timed
-    # steps alike), so the caching allocator's pool is complete before the timed region
-    pacer = StepPacer(device)
+    # the fused optimizer's step() keeps at most CLOUD_AMD_MAX_STEPS_IN_FLIGHT steps queued ahead
+    # of the GPU (warmup and timed steps alike, runtime/step_pacer.py), so the caching allocator's
+    # pool is complete before the timed region
+    pacer = opt.pacer
     for _ in range(max(args.warmup - 1, 0)):
         loss = step_fn()
-        pacer.step_done()
     # desync check once after warmup (world > 1): every replica must hold identical
     # all-reduced gradients (fp64 fingerprint over all arenas, all-gathered)
     replicas_consistent = None
@@ -206,23 +205,25 @@ def main():
     # (no added synchronisation: events are read after the closing sync)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if on_gpu else None
     host_ms = []
+    paced_ms = []  # per step: host time blocked in the run-ahead bound (host_ms minus this = launch time)
     t0 = time.perf_counter()
     if evs:
         evs[0].record()
     for i in range(args.steps):
         th = time.perf_counter()
+        w0 = pacer.wait_ms if pacer is not None else 0.0
         loss = step_fn()
         if evs:
             evs[i + 1].record()
-        pacer.step_done()
         host_ms.append((time.perf_counter() - th) * 1e3)
+        paced_ms.append((pacer.wait_ms if pacer is not None else 0.0) - w0)
         step_probe.mark()
     sync()
     dist_env.barrier()
     t1 = time.perf_counter()
     step_stats = benchlaunch.step_stats(
         [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)] if evs else None, host_ms,
-        host0, benchlaunch.host_state(), probe=step_probe.close())
+        host0, benchlaunch.host_state(), probe=step_probe.close(), paced_ms=paced_ms)
     comm = reducer.timing_summary()
     per_rank_ms = [v / args.steps * 1000.0 for v in dist_env.all_gather_floats(t1 - t0, device)]
     elapsed = dist_env.all_reduce_max(t1 - t0, device)
@@ -279,7 +280,7 @@ def main():
             "replicas_consistent": replicas_consistent,
             "step_stats_rank0": step_stats,
             "gc_frozen_objects": gc_frozen,
-            "max_steps_in_flight": pacer.depth if pacer.enabled else None,
+            "max_steps_in_flight": pacer.depth if (pacer is not None and pacer.enabled) else None,
             "warnings": step_stats.pop("warnings"),
             "rank_ms_per_step": {"min": round(min(per_rank_ms), 3), "max": round(max(per_rank_ms), 3)},
             "first_step_latency_s": round(first_lat, 3),

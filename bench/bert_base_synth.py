@@ -160,15 +160,10 @@ def main():
     phases = benchlaunch.startup_phases(T_START, t_first_done)
     run_t0 = os.environ.get("CLOUD_AMD_RUN_T0")
     run_to_first = (time.time() - float(run_t0)) if run_t0 else None
-    pacer = None
-    if not args.stock:
-        from cloud_amd.runtime.step_pacer import StepPacer
-
-        pacer = StepPacer(device)  # bounded host run-ahead (allocator pool complete after warmup)
+    # (cloud_amd: the fused optimizer's step() bounds the host run-ahead, runtime/step_pacer.py,
+    # so the allocator's pool is complete after warmup)
     for _ in range(max(args.warmup - 1, 0)):
         loss = train_step()
-        if pacer is not None:
-            pacer.step_done()
     replicas_consistent = None
     if world > 1 and reducer is not None:
         try:
@@ -188,8 +183,6 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = train_step()
-        if pacer is not None:
-            pacer.step_done()
     torch.cuda.synchronize()
     dist_env.barrier()
     dt = time.perf_counter() - t0

@@ -12,7 +12,9 @@ ends up best completed).  Synthetic MNIST (no network).
 ``--pool 1`` (default): the scheduler runs on a warm ``WorkerPool`` -- worker processes
 that imported torch / cloud_amd once and serve study after study.  The pool is started
 first (``pool_warm_s``), then ``--studies`` studies run back to back on it; ``value`` /
-``time_to_best_s`` are the first warm study's, ``cold_*`` include the pool's start-up.
+``time_to_best_s`` are COLD figures (from before the pool spawn: interpreter start and imports
+counted, as in every earlier round); ``warm_value`` / ``warm_time_to_best_s`` are the first
+study's on the already-warm pool, and ``studies`` lists every study's warm figures.
 ``--pool 0``: one process per worker per study (spawned, gated standbys).  The CNN is the
 reference's ``mnist_example_using_fit.py`` model with tuned filters / dense
 width / learning rate.
@@ -115,10 +117,18 @@ def main():
     out = outs[0]
     out["pool"] = bool(args.pool)
     if args.pool:
+        # `value` / `time_to_best_s` stay COLD (interpreter start, imports and pool spawn counted),
+        # comparable with every earlier round; the warm-pool figures are separate labelled fields
         out["pool_warm_s"] = round(pool_warm, 2)
-        out["cold_wall_s"] = round(runs[0][1] + runs[0][2] - t_cold, 2)
-        out["cold_time_to_best_s"] = (round(out["time_to_best_s"] + runs[0][1] - t_cold, 2)
-                                      if out["time_to_best_s"] is not None else None)
+        cold_wall = runs[0][1] + runs[0][2] - t_cold
+        out["warm_value"] = out["value"]
+        out["warm_wall_s"] = out["wall_s"]
+        out["warm_time_to_best_s"] = out["time_to_best_s"]
+        out["value"] = round(out["trials_completed"] / cold_wall * 3600.0, 2)
+        out["wall_s"] = round(cold_wall, 2)
+        out["time_to_best_s"] = (round(out["warm_time_to_best_s"] + runs[0][1] - t_cold, 2)
+                                 if out["warm_time_to_best_s"] is not None else None)
+        out["value_basis"] = "cold: from before the pool spawn (imports and interpreter start included)"
         out["studies"] = [{k: o[k] for k in ("value", "wall_s", "time_to_best_s", "trials_completed",
                                              "best_val_accuracy")} for o in outs]
     print(json.dumps(out), flush=True)

@@ -174,7 +174,8 @@ _VARS = [
         "ready only when backward ends: its all-reduce is exposed)", "distributed"),
     Var("CLOUD_AMD_GRAD_REDUCE_DTYPE", str, "auto", "wire dtype of the gradient all-reduce: 'bf16' (every "
         "bucket, fp32 arenas through a bf16 copy: half the bytes), 'fp32' (every bucket through fp32), 'native' "
-        "(each arena in its own dtype), 'auto' (bf16 for mixed-precision models, native for all-fp32 ones)",
+        "(each arena in its own dtype), 'auto' (= native: fp32 master-weight gradients keep fp32 sums; 'bf16' is "
+        "the opt-in)",
         "distributed"),
     Var("CLOUD_AMD_RCCL_ENV", bool, True, "launcher sets the xGMI RCCL defaults (NCCL_MIN_NCHANNELS, "
         "HSA_NO_SCRATCH_RECLAIM) for multi-GPU jobs", "distributed"),

@@ -313,7 +313,8 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
                    "--output-format", "csv", "--"] + cmd
         logf = open(os.path.join(job_dir, "logs", log_name(info)), "w")
         p = subprocess.Popen(cmd, cwd=app_dir, env=env, stdout=logf, stderr=subprocess.STDOUT,
-                             start_new_session=True, preexec_fn=_pin(cpus))
+                             start_new_session=True)
+        _pin(p.pid, cpus)
         logf.close()
         procs.append(p)
     job = Job(job_id, job_dir, procs, ranks, meta)
@@ -327,20 +328,17 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
     return job
 
 
-def _pin(cpus):
-    """preexec_fn of a rank: set its CPU affinity in the child, before exec (the launcher
-    never initialises HIP, so nothing GPU-side is forked)."""
+def _pin(pid, cpus):
+    """Pin a freshly spawned rank to its CPU set from the parent (``sched_setaffinity(pid)``):
+    no ``preexec_fn``, which Python documents as unsafe when the launching process has
+    threads.  Popen returns after the child's exec, and the interpreter creates its worker
+    threads (OpenMP, HIP) only later, at ``import torch``, so they inherit this mask."""
     if not cpus:
-        return None
-    cpus = list(cpus)
-
-    def fn():
-        try:
-            os.sched_setaffinity(0, cpus)
-        except OSError:
-            pass
-
-    return fn
+        return
+    try:
+        os.sched_setaffinity(pid, list(cpus))
+    except OSError:
+        pass
 
 
 def deploy_job(job_id, job_dir, target, chief_config, worker_count, worker_config, entry_point_args,

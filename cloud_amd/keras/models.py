@@ -296,6 +296,7 @@ class Model(Layer):
         from ..parallel.ddp import GradAllReducer
 
         self._reducer = GradAllReducer(impl.arenas) if world > 1 else None
+        impl.reducer = self._reducer
         if self._reducer is not None:
             self._reducer.broadcast_parameters()
             self._broadcast_buffers()
@@ -513,9 +514,7 @@ class Model(Layer):
         global_step = 0
         from ..runtime import gc_control
 
-        from ..runtime.step_pacer import StepPacer
-
-        pacer = StepPacer(s.device)  # at most CLOUD_AMD_MAX_STEPS_IN_FLIGHT steps queued ahead of the GPU
+        # (the fused optimizer's step() bounds the host run-ahead: runtime/step_pacer.py)
         if getattr(self, "_ca_gc_frozen", False):  # a previous fit ended by an exception
             gc_control.unfreeze()
             self._ca_gc_frozen = False
@@ -542,7 +541,6 @@ class Model(Layer):
                 world = s.num_replicas_in_sync
                 w = (n_local * world / n_global) if world > 1 else 1.0
                 loss = self.train_step(xb, yb, loss_weight=w, n_real=n_local)
-                pacer.step_done()
                 if mon:  # host-side step period (the device queue evens it out over steps)
                     now = time.perf_counter()
                     monitoring.observe(monitoring.STEP_TIME, (now - t_prev) * 1e3)
@@ -550,7 +548,10 @@ class Model(Layer):
                 callbacks_.on_train_batch_end(step, {"loss": float(loss.detach())} if step % 50 == 0 else {})
                 step += 1
                 global_step += 1
-                if global_step == 3:  # model, optimizer state and kernel caches exist now
+                if global_step == 3 and gc_control.frozen_count() == 0:
+                    # model, optimizer state and kernel caches exist now.  Only when nothing is
+                    # frozen yet: gc.unfreeze() at the end is process-wide and must not hand back
+                    # objects the caller froze itself (e.g. to keep pages shared after fork)
                     self._ca_gc_frozen = gc_control.freeze() > 0
                 if self.stop_training:
                     break

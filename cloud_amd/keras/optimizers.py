@@ -78,15 +78,23 @@ class Optimizer:
     def apply_gradients(self, grads_and_vars):
         """Custom-training-loop update (``optimizer.apply_gradients(zip(grads, vars))``).
 
-        On first use the variables move into flat arenas and the fused HIP
-        optimizer is created with ``grad_scale = 1``: as under TF's
-        MirroredStrategy, per-replica gradients are SUMMED across replicas (the
-        loss is already divided by the global batch via
-        ``compute_average_loss``).  Under a multi-replica strategy the arena is
-        all-reduced in buckets (RCCL / gloo) before the fused update.
+        On first use the variables move into flat arenas, replicas adopt rank 0's
+        weights (TF mirrors variables at creation; here before the first update), and the
+        fused HIP optimizer is created with ``grad_scale = 1``: as under TF's
+        MirroredStrategy, per-replica gradients are SUMMED across replicas (the loss is
+        already divided by the global batch via ``compute_average_loss``).
+
+        The optimizer's :class:`~cloud_amd.parallel.ddp.GradAllReducer` is the hook-driven,
+        backward-overlapped one that ``fit`` uses.  Gradients from ``tf.GradientTape`` over
+        arena-resident variables arrive already reduced (the tape joined the buckets) and as
+        views of the arena: no copy, no second reduction.  Any other gradient tensor is
+        copied into its arena slot (a variable given ``None`` gets a zero gradient), and the
+        arena is all-reduced here unless the tape already did.
+        Reference: ``TFC/core/tests/testdata/mnist_example_using_ctl.py:124-129,150-157``.
         """
         pairs = [(g, v) for g, v in grads_and_vars]
-        if self._impl is None:
+        first = self._impl is None
+        if first:
             self._impl = self.fused_cls([v for _, v in pairs], learning_rate=self.learning_rate, grad_scale=1.0,
                                         clipnorm=self.clipnorm, **self.kw)
             self._reducer = None
@@ -95,16 +103,26 @@ class Optimizer:
             if get_strategy().num_replicas_in_sync > 1:
                 from ..parallel.ddp import GradAllReducer
 
-                self._reducer = GradAllReducer(self._impl.arenas, overlap=False)
+                self._reducer = GradAllReducer(self._impl.arenas)
+                self._reducer.broadcast_parameters()
+                self._impl.reducer = self._reducer
         impl = self._impl
-        impl.zero_grad()
-        for g, v in pairs:
-            if g is None:
-                continue
-            v.grad.copy_(g.detach().to(v.grad.dtype).reshape(v.grad.shape))
         red = getattr(self, "_reducer", None)
+        reduced = red is not None and red.tape_reduced
+        for g, v in pairs:
+            slot = v.grad
+            if g is None:
+                if slot is not None:
+                    slot.zero_()  # TF skips such a variable; a zero gradient is the closest
+                continue
+            if slot is not None and g.data_ptr() == slot.data_ptr() and g.dtype == slot.dtype \
+                    and g.numel() == slot.numel():
+                continue  # the tape's in-arena gradient: already in place
+            slot.copy_(g.detach().to(slot.dtype).reshape(slot.shape))
         if red is not None:
-            red.finish()
+            if not reduced:
+                red.finish()
+            red.tape_reduced = False
         impl.step()
         return impl.iterations
 

@@ -381,6 +381,14 @@ class _BottleneckFn(torch.autograd.Function):
         return (dx, None, None) + (None,) * (len(ctx.needs_input_grad) - 3)
 
 
+def _global_hooks():
+    """Module hooks registered for EVERY module (``register_module_forward_hook`` / ``_pre_hook``)
+    would see a deferred block output before the next block's conv1 writes it."""
+    from torch.nn.modules import module as _m
+
+    return bool(_m._global_forward_hooks or _m._global_forward_pre_hooks)
+
+
 def bottleneck_forward(blk, x, next_blk=None):
     """Run ``blk`` as one autograd node.  ``next_blk``: the fused block that will consume this
     block's output next (ResNet.forward passes it): this block's bn3 apply is then left to that
@@ -388,7 +396,8 @@ def bottleneck_forward(blk, x, next_blk=None):
     prev = getattr(x, "_ca_bn_src", None) if config.get("CLOUD_AMD_BN_BWD_EPILOGUE") else None
     pend = x.__dict__.pop("_ca_pending", None)
     defer = (next_blk is not None and config.get("CLOUD_AMD_BN_FOLD_FWD") and not blk._forward_hooks
-             and not next_blk._forward_pre_hooks and getattr(next_blk, "fused_block", False)
+             and not next_blk._forward_pre_hooks and not _global_hooks()
+             and getattr(next_blk, "fused_block", False)
              and can_fuse(next_blk, x) and _fold_site(next_blk.conv1.cin, next_blk.conv1.cout)
              and raw.is_gemm_conv(next_blk.conv1.weight, next_blk.conv1.stride,
                                                             next_blk.conv1.padding))

@@ -86,10 +86,14 @@ class ResNet(nn.Module):
             if self.stem_cin != self.in_channels:
                 x = torch.nn.functional.pad(x, (0, self.stem_cin - self.in_channels))
             x = self._stem_tail(self.conv1(x, stats=True))
-        blocks = list(self.layers)
-        for i, blk in enumerate(blocks):
-            # a fused block hands its bn3 apply to the next fused block's conv1 (fused_block)
-            x = blk(x, blocks[i + 1] if i + 1 < len(blocks) else None)
+        if self.layers._forward_hooks or self.layers._forward_pre_hooks:
+            # hooks on the block Sequential: call it (they fire; no cross-block BN fold)
+            x = self.layers(x)
+        else:
+            blocks = list(self.layers)
+            for i, blk in enumerate(blocks):
+                # a fused block hands its bn3 apply to the next fused block's conv1 (fused_block)
+                x = blk(x, blocks[i + 1] if i + 1 < len(blocks) else None)
         return self.fc(self.pool(x))
 
     def _stem_tail(self, out):

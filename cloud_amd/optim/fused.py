@@ -20,6 +20,7 @@ a schedule callable ``lr(step)``.
 from __future__ import annotations
 
 import math
+import weakref
 
 import torch
 
@@ -47,6 +48,21 @@ class FusedOptimizer:
         self._hp = {}
         self.fuse_zero_grad = True
         self._grads_clean = True  # arenas are allocated zeroed
+        # gradient all-reduce engine attached by the training loop that owns this optimizer
+        # (Keras fit, apply_gradients); tf.GradientTape finds it through the parameters
+        self.reducer = None
+        owner = weakref.ref(self)
+        for a in self.arenas:
+            for s in a.slots:
+                s.param._ca_opt = owner
+        # Bounded host run-ahead as a property of the step itself (runtime/step_pacer.py):
+        # every loop that steps this optimizer -- Keras fit, custom loops, strategy.run,
+        # user scripts -- queues at most CLOUD_AMD_MAX_STEPS_IN_FLIGHT steps ahead of the GPU.
+        self.pacer = None
+        if self.arenas and self.arenas[0].master.is_cuda:
+            from ..runtime.step_pacer import StepPacer
+
+            self.pacer = StepPacer(self.arenas[0].device)
 
     # -- hyper-parameters ---------------------------------------------------
     @property
@@ -121,6 +137,8 @@ class FusedOptimizer:
             for lo, hi, wd in self._segments(a):
                 self._update(ai, a, lo, hi, None, [float(v) for v in self._hp_values(wd)])
         self._after_update()
+        if self.pacer is not None:
+            self.pacer.step_done()
         return loss
 
     def _zero_in_kernel(self, a):

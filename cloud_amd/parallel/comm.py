@@ -9,6 +9,13 @@ by an event, so the DP engine (:mod:`cloud_amd.parallel.ddp`) can overlap
 bucket all-reduces with the rest of backward and ``join`` the compute stream
 only before the optimizer step.
 
+Robustness: the bootstrap has a deadline (``CLOUD_AMD_COMM_INIT_TIMEOUT_S``, default 300 s):
+a non-root rank waits for the unique id with ``store.wait(..., timeout)``, and the C++
+init runs ``ncclCommInitRankConfig`` non-blocking, polled until every peer joined or the
+deadline passed -- then the half-built communicator is aborted and ``TimeoutError`` is
+raised, so a peer that HANGS before joining fails the job promptly instead of stalling
+every rank until the launcher's timeout.  ``init_seconds`` records how long the init took.
+
 Selection: ``CLOUD_AMD_COMM=rccl`` (native communicator) or ``torch`` (default:
 ``torch.distributed`` with the RCCL backend).  The native path is opt-in until
 it has been validated on a multi-GPU node; both run RCCL underneath.
@@ -39,8 +46,30 @@ def _stream(device=None):
     return torch.cuda.current_stream(device).cuda_stream
 
 
+def init_timeout_s() -> float:
+    return float(os.environ.get("CLOUD_AMD_COMM_INIT_TIMEOUT_S", "300"))
+
+
+def exchange_unique_id(store, key, rank, make_uid, timeout_s):
+    """Rank 0 publishes ``make_uid()`` under ``key``; every other rank waits for it at most
+    ``timeout_s`` seconds (``TimeoutError`` naming the key otherwise -- rank 0 hung or died
+    before publishing).  ``store`` is any c10d-style store (``set`` / ``get`` / ``wait``)."""
+    import datetime
+
+    if rank == 0:
+        uid = make_uid()
+        store.set(key, uid)
+        return bytes(uid)
+    try:
+        store.wait([key], datetime.timedelta(seconds=timeout_s))
+    except Exception as e:  # c10d raises RuntimeError / DistStoreError on its deadline
+        raise TimeoutError("rank %d: RCCL unique id %r not published by rank 0 within %.1f s (%s)"
+                           % (rank, key, timeout_s, e)) from e
+    return bytes(store.get(key))
+
+
 class RcclComm:
-    def __init__(self, rank=None, world=None, device=None, store=None, tag=None):
+    def __init__(self, rank=None, world=None, device=None, store=None, tag=None, timeout_s=None):
         ext = load()
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if world is None else world
@@ -48,17 +77,15 @@ class RcclComm:
         if dev.index is None:
             dev = torch.device("cuda", torch.cuda.current_device())
         self.device = dev
+        self.timeout_s = init_timeout_s() if timeout_s is None else float(timeout_s)
         key = "cloud_amd/rccl_uid/%s" % (tag if tag is not None else next(_ctr))
-        if self.world > 1:
+        if self.world > 1 and store is not False:
             store = store or dist.distributed_c10d._get_default_store()
-            if self.rank == 0:
-                uid = ext.unique_id()
-                store.set(key, uid)
-            else:
-                uid = store.get(key)
+            uid = exchange_unique_id(store, key, self.rank, ext.unique_id, self.timeout_s)
         else:
             uid = ext.unique_id()
-        self.c = ext.Comm(self.world, self.rank, bytes(uid), self.device.index)
+        self.c = ext.Comm(self.world, self.rank, bytes(uid), self.device.index, self.timeout_s)
+        self.init_seconds = float(self.c.init_seconds)
 
     def _args(self, t):
         assert t.is_cuda and t.is_contiguous(), "collectives need contiguous device tensors"

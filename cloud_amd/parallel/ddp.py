@@ -131,14 +131,17 @@ class GradAllReducer:
         #             copy cast back into the fp32 gradient -- half the xGMI bytes of fp32;
         #   fp32   -- every bucket reduced in fp32 (bf16 arenas through an fp32 copy);
         #   native -- each arena in its own dtype;
-        #   auto   -- bf16 for a mixed-precision model (it has a bf16 arena), native for an
-        #             all-fp32 one (a user who trains in fp32 keeps fp32 gradient sums).
+        #   auto   -- native: bf16 arenas on a bf16 wire, fp32 arenas (master-weight gradients:
+        #             BatchNorm / LayerNorm parameters, BERT's word-embedding table) in fp32, as
+        #             the reference's MirroredStrategy reduces each gradient in its variable's
+        #             dtype.  The all-bf16 wire (half the fp32 arenas' xGMI bytes, ~3 bf16 ulp of
+        #             error on their sums) is an explicit opt-in.
         # The casts run on the comm stream, next to the collective, into a wire buffer kept
         # per bucket (allocated once).  RCCL adds bf16 operands in fp32 and rounds each hop's
         # partial sum to bf16 (error: tests/test_grad_reduce_precision.py).
         rd = reduce_dtype if reduce_dtype is not None else os.environ.get("CLOUD_AMD_GRAD_REDUCE_DTYPE", "auto")
         if rd == "auto":
-            rd = "bf16" if any(a.grad.dtype == torch.bfloat16 for a in arenas) else "native"
+            rd = "native"
         if isinstance(rd, str):
             rd = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
                   "bfloat16": torch.bfloat16, "native": None}[rd]
@@ -180,6 +183,7 @@ class GradAllReducer:
         self._next = 0
         self._seen = set()
         self._sync_enabled = True
+        self.tape_reduced = False  # tf.GradientTape joined this step's buckets (cloud_amd/tf.py)
         self._hooks = []
         self._build()
         if self.world > 1 and overlap:

@@ -31,6 +31,11 @@ def freeze():
     return gc.get_freeze_count()
 
 
+def frozen_count():
+    """Objects in the permanent generation now (someone -- this runtime or the caller -- froze)."""
+    return gc.get_freeze_count()
+
+
 def unfreeze():
     """Return the frozen objects to the collector (e.g. before tearing a model down)."""
     gc.unfreeze()

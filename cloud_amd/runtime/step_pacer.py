@@ -15,6 +15,12 @@ the event of the step ``depth`` steps back, so at most ``depth`` steps are ever 
 in flight is bounded and reaches its steady state during warmup.  With the GPU the bottleneck
 (70 ms steps, ~10 ms of host launch time) the wait costs nothing.  ``CLOUD_AMD_MAX_STEPS_IN_FLIGHT``
 (default 2; 0 = unbounded).
+
+Since round 5 every :class:`cloud_amd.optim.FusedOptimizer` owns one and calls
+:meth:`StepPacer.step_done` at the end of ``step()``: the bound is a property of the runtime,
+not of the loop, so custom training loops (``tf.GradientTape`` + ``apply_gradients``),
+``strategy.run`` and user scripts get it too.  ``wait_ms`` accumulates the time the host spent
+blocked in the bound, so a caller can report its unpaced launch time.
 """
 from __future__ import annotations
 
@@ -33,6 +39,7 @@ class StepPacer:
             device is None or getattr(device, "type", str(device)).startswith("cuda"))
         self._events = collections.deque()
         self.waits = 0
+        self.wait_ms = 0.0
 
     def step_done(self):
         """Call after enqueueing a step: records its end and blocks until at most
@@ -45,5 +52,9 @@ class StepPacer:
         while len(self._events) > self.depth:
             old = self._events.popleft()
             if not old.query():
+                import time
+
                 self.waits += 1
+                t0 = time.perf_counter()
                 old.synchronize()
+                self.wait_ms += (time.perf_counter() - t0) * 1e3

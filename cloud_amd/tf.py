@@ -31,7 +31,29 @@ from .version import __version__  # noqa: F401
 
 
 class GradientTape:
-    """``with tf.GradientTape() as tape: ...; tape.gradient(loss, vars)`` on autograd."""
+    """``with tf.GradientTape() as tape: ...; tape.gradient(loss, vars)`` on autograd.
+
+    Variables that live in a fused optimizer's flat arenas (after the first
+    ``optimizer.apply_gradients``) take the runtime's training-step path:
+
+    * the native Dense / Conv2D backward writes their weight gradients straight into the
+      arena (``ops/dense.py``), so ``gradient()`` first zeroes the owning optimizer's
+      gradient arena and then runs ``backward(inputs=sources)``, which accumulates every
+      other gradient into the same arena slices;
+    * under a multi-replica strategy the optimizer's bucketed all-reduce
+      (:class:`cloud_amd.parallel.ddp.GradAllReducer`) launches each bucket from the backward
+      hooks as its gradients complete (overlapped with the rest of backward) and is joined
+      before ``gradient()`` returns -- the returned gradients are the cross-replica SUM, as
+      Horovod's ``DistributedGradientTape`` returns them, and ``apply_gradients`` does not
+      reduce them again;
+    * the returned tensors are views of the arena (``v.grad``): no copy, and
+      ``apply_gradients`` recognises them.  They are valid until the next ``gradient()``
+      over the same variables; ``tf.identity``-style copies (``g.clone()``) keep them.
+
+    Other sources (plain tensors, variables before the optimizer's first step) get
+    ``torch.autograd.grad`` results (zeros for unconnected sources).  Reference pattern:
+    ``TFC/core/tests/testdata/mnist_example_using_ctl.py:124-129``.
+    """
 
     def __init__(self, persistent=False, watch_accessed_variables=True):
         self.persistent = persistent
@@ -46,11 +68,48 @@ class GradientTape:
         if isinstance(tensor, torch.Tensor) and not tensor.requires_grad:
             tensor.requires_grad_(True)
 
-    def gradient(self, target, sources):
+    @staticmethod
+    def _owners(srcs):
+        owners = {}
+        for s in srcs:
+            ref = getattr(s, "_ca_opt", None) if getattr(s, "_ca_arena", False) else None
+            opt = ref() if ref is not None else None
+            if opt is not None:
+                owners[id(opt)] = opt
+        return list(owners.values())
+
+    def gradient(self, target, sources, output_gradients=None):
         single = isinstance(sources, torch.Tensor)
         srcs = [sources] if single else list(sources)
-        grads = torch.autograd.grad(target, srcs, allow_unused=True, retain_graph=self.persistent)
-        out = [g if g is not None else torch.zeros_like(s) for g, s in zip(grads, srcs)]
+        owners = self._owners(srcs)
+        for opt in owners:
+            opt.zero_grad()  # the arena slots are accumulated into in place
+        reducers = [o.reducer for o in owners if getattr(o, "reducer", None) is not None and o.reducer.world > 1]
+        if owners and all(getattr(s, "_ca_arena", False) and s.grad is not None for s in srcs):
+            target.backward(gradient=output_gradients, inputs=srcs, retain_graph=self.persistent)
+            for r in reducers:
+                r.finish()  # buckets launched during backward; the compute stream joins them
+                r.tape_reduced = True
+            out = [s.grad for s in srcs]
+            return out[0] if single else out
+        # mixed / non-arena sources: no bucket may launch while autograd.grad runs (the copies
+        # apply_gradients makes would race a reduction already in flight); the optimizer
+        # reduces the whole arena in apply_gradients instead
+        prev = [(r, r._sync_enabled) for r in reducers]
+        for r, _ in prev:
+            r._sync_enabled = False
+        try:
+            grads = torch.autograd.grad(target, srcs, grad_outputs=output_gradients, allow_unused=True,
+                                        retain_graph=self.persistent)
+        finally:
+            for r, was in prev:
+                r._sync_enabled = was
+                r.reset()
+        out = []
+        for g, s in zip(grads, srcs):
+            if g is None and getattr(s, "_ca_arena", False) and s.grad is not None:
+                g = s.grad  # written in place by a native backward (autograd saw no gradient)
+            out.append(g if g is not None else torch.zeros_like(s))
         return out[0] if single else out
 
 

@@ -127,6 +127,32 @@ def _worker_body(target, tuner_id, device, env, gate_file, tl):
     getattr(importlib.import_module(mod), fn)(tuner_id, device)
 
 
+def _release_gpu_state():
+    """Between pooled jobs: return every cached segment a job left to the driver and reset
+    the peak-memory counters of every device this process touched, so the next study's
+    footprint probe (``max_memory_reserved``) measures that study alone and packing by
+    measured footprint never counts a previous job's pool."""
+    try:
+        import torch
+    except Exception:  # pragma: no cover
+        return
+    if not (torch.cuda.is_available() and torch.cuda.is_initialized()):
+        return
+    import gc
+
+    gc.collect()  # the job's tensors (a finished trial's model) become free blocks first
+    for d in range(torch.cuda.device_count()):
+        try:
+            if torch.cuda.memory_reserved(d) == 0 and torch.cuda.max_memory_reserved(d) == 0:
+                continue  # never touched: do not create a context there
+            with torch.cuda.device(d):
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()
+            torch.cuda.reset_peak_memory_stats(d)
+        except Exception as e:  # pragma: no cover - a failing device must not kill the pool
+            print("[cloud_amd pool] releasing cuda:%d: %r" % (d, e), file=sys.stderr, flush=True)
+
+
 def _pool_main(idx, jobs, done, preload, env):
     """A pooled tuner worker: imports once, then runs scheduler jobs until told to stop.
     Each job is (target, tuner_id, device, env, timeline_file); the job's env is applied for
@@ -149,6 +175,7 @@ def _pool_main(idx, jobs, done, preload, env):
             code = 1
             print("[cloud_amd pool] %s failed: %r" % (tuner_id, e), file=sys.stderr, flush=True)
         finally:
+            _release_gpu_state()
             if tl is not None:
                 _mark(tl, "exited")
                 tmp = tl_file + ".tmp"

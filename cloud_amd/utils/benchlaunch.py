@@ -192,18 +192,23 @@ def _mmm(v):
     return {"min": round(s[0], 3), "median": round(med, 3), "max": round(s[-1], 3)}
 
 
-def step_stats(device_ms, host_ms, host_before, host_after, outlier_ratio=1.5, probe=None):
+def step_stats(device_ms, host_ms, host_before, host_after, outlier_ratio=1.5, probe=None, paced_ms=None):
     """Per-step timing of the timed region (device time between step-boundary events on
     the compute stream, host time to enqueue a step) plus the host state around it.  A
     step slower than ``outlier_ratio`` x the median adds a warning, with the evidence
     needed to name the cause: the host launch time (a starved / descheduled host makes
     host time ~ device time), involuntary context switches (another process on our
-    cores), the CPU the rank ran on before and after (migration), the load average."""
+    cores), the CPU the rank ran on before and after (migration), the load average.
+    ``paced_ms`` (per step: time blocked in the optimizer's run-ahead bound) splits the host
+    time into the UNPACED launch time (``host_unpaced_ms``) and the pacing wait."""
     out = {"host_launch_ms": _mmm(host_ms) if host_ms else None,
            "device_ms": _mmm(device_ms) if device_ms else None,
            "host_before": host_before, "host_after": host_after, "warnings": []}
     if host_ms:
         out["host_launch_ms_steps"] = [round(v, 2) for v in host_ms]
+    if host_ms and paced_ms and len(paced_ms) == len(host_ms):
+        out["host_unpaced_ms"] = _mmm([max(h - p, 0.0) for h, p in zip(host_ms, paced_ms)])
+        out["pacer_wait_ms_total"] = round(sum(paced_ms), 3)
     if probe:
         out["probe_steps"] = probe
         out["gc_ms_total"] = round(sum(r["gc_ms"] for r in probe), 3)

@@ -172,6 +172,9 @@ def comm_probe(device, sizes_mb=(16, 64), iters=5, dtype=torch.bfloat16):
         if device.type == "cuda":
             torch.cuda.synchronize(device)
 
+    from ..parallel import comm as _comm
+
+    out["bench_transport"] = _comm.backend()  # the data plane the timed steps used (CLOUD_AMD_COMM)
     bufs = {mb: torch.ones((mb << 20) // torch.tensor([], dtype=dtype).element_size(), dtype=dtype, device=device)
             for mb in sizes_mb}
     out["torch"] = {str(mb): timed(lambda t: dist.all_reduce(t), t, dev_sync) for mb, t in bufs.items()}
@@ -182,6 +185,7 @@ def comm_probe(device, sizes_mb=(16, 64), iters=5, dtype=torch.bfloat16):
             c = RcclComm(tag="comm_probe", device=device)
             try:
                 out["rccl"] = {str(mb): timed(lambda t: c.all_reduce(t), t, c.synchronize) for mb, t in bufs.items()}
+                out["rccl"]["init_s"] = round(all_reduce_max(c.init_seconds, device), 3)
             finally:
                 c.close()
         except Exception as e:  # noqa: BLE001 - a probe reports, it never fails the bench

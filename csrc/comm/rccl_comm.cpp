@@ -8,14 +8,21 @@
 //
 // Bootstrap: rank 0 calls unique_id() and publishes the 128-byte id through the
 // rendezvous store (cloud_amd/parallel/comm.py); every rank then constructs
-// Comm(nranks, rank, id, device) -> ncclCommInitRank.
+// Comm(nranks, rank, id, device, timeout_s) -> ncclCommInitRankConfig in NON-BLOCKING mode,
+// polled with ncclCommGetAsyncError until it settles or the deadline passes; past the
+// deadline the half-built communicator is aborted (ncclCommAbort) and the constructor
+// raises TimeoutError -- a peer that hangs before joining (rather than exiting) no longer
+// stalls every rank until the launcher's job timeout.  In non-blocking mode any call may
+// return ncclInProgress; settle() polls it to completion with the GIL released.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <rccl/rccl.h>
 #include <stdint.h>
 
+#include <chrono>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 namespace py = pybind11;
 
@@ -54,9 +61,14 @@ ncclRedOp_t op_of(int code) {
 hipStream_t S(uint64_t s) { return reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(s)); }
 void* P(uint64_t p) { return reinterpret_cast<void*>(static_cast<uintptr_t>(p)); }
 
+struct InitTimeout : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
 class Comm {
  public:
-  Comm(int nranks, int rank, py::bytes uid, int device) : nranks_(nranks), rank_(rank), device_(device) {
+  Comm(int nranks, int rank, py::bytes uid, int device, double timeout_s)
+      : nranks_(nranks), rank_(rank), device_(device) {
     std::string u = uid;
     if (u.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("unique id must be 128 bytes");
     ncclUniqueId id;
@@ -67,9 +79,42 @@ class Comm {
     hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "hipStreamCreateWithPriority");
     hip_check(hipEventCreateWithFlags(&ready_, hipEventDisableTiming), "hipEventCreate");
     hip_check(hipEventCreateWithFlags(&done_, hipEventDisableTiming), "hipEventCreate");
+    auto t0 = std::chrono::steady_clock::now();
+    ncclResult_t state = ncclSuccess;
     {
-      py::gil_scoped_release nogil;  // init blocks until every rank joined
-      nccl_check(ncclCommInitRank(&comm_, nranks, id, rank), "ncclCommInitRank");
+      py::gil_scoped_release nogil;  // init completes only when every rank joined
+      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+      cfg.blocking = 0;
+      ncclResult_t r = ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg);
+      if (r != ncclSuccess && r != ncclInProgress) {
+        comm_ = nullptr;
+        destroy();
+        nccl_check(r, "ncclCommInitRankConfig");
+      }
+      state = r;
+      while (state == ncclInProgress) {
+        if (ncclCommGetAsyncError(comm_, &state) != ncclSuccess) break;
+        if (state != ncclInProgress) break;
+        double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (timeout_s > 0 && el > timeout_s) {
+          ncclCommAbort(comm_);  // unblocks the init threads; frees the partial communicator
+          comm_ = nullptr;
+          break;
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(2));
+      }
+    }
+    init_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!comm_) {
+      destroy();
+      throw InitTimeout("ncclCommInitRankConfig: rank " + std::to_string(rank) + " of " + std::to_string(nranks) +
+                        " not joined by all peers within " + std::to_string(timeout_s) + " s (aborted)");
+    }
+    if (state != ncclSuccess) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+      destroy();
+      nccl_check(state, "ncclCommInitRankConfig (async)");
     }
   }
 
@@ -78,6 +123,12 @@ class Comm {
   void destroy() {
     if (comm_) {
       hipStreamSynchronize(stream_);
+      // non-blocking communicator: finalize (flush) and let it settle before the destroy
+      ncclResult_t st = ncclCommFinalize(comm_);
+      while (st == ncclInProgress) {
+        std::this_thread::yield();
+        if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) break;
+      }
       ncclCommDestroy(comm_);
       comm_ = nullptr;
     }
@@ -105,23 +156,23 @@ class Comm {
 
   void all_reduce(uint64_t buf, size_t count, int dtype, int op, uint64_t compute) {
     after(compute);
-    nccl_check(ncclAllReduce(P(buf), P(buf), count, dtype_of(dtype), op_of(op), comm_, stream_), "ncclAllReduce");
+    settle(ncclAllReduce(P(buf), P(buf), count, dtype_of(dtype), op_of(op), comm_, stream_), "ncclAllReduce");
   }
 
   void broadcast(uint64_t buf, size_t count, int dtype, int root, uint64_t compute) {
     after(compute);
-    nccl_check(ncclBroadcast(P(buf), P(buf), count, dtype_of(dtype), root, comm_, stream_), "ncclBroadcast");
+    settle(ncclBroadcast(P(buf), P(buf), count, dtype_of(dtype), root, comm_, stream_), "ncclBroadcast");
   }
 
   void reduce_scatter(uint64_t send, uint64_t recv, size_t recvcount, int dtype, int op, uint64_t compute) {
     after(compute);
-    nccl_check(ncclReduceScatter(P(send), P(recv), recvcount, dtype_of(dtype), op_of(op), comm_, stream_),
-               "ncclReduceScatter");
+    settle(ncclReduceScatter(P(send), P(recv), recvcount, dtype_of(dtype), op_of(op), comm_, stream_),
+           "ncclReduceScatter");
   }
 
   void all_gather(uint64_t send, uint64_t recv, size_t sendcount, int dtype, uint64_t compute) {
     after(compute);
-    nccl_check(ncclAllGather(P(send), P(recv), sendcount, dtype_of(dtype), comm_, stream_), "ncclAllGather");
+    settle(ncclAllGather(P(send), P(recv), sendcount, dtype_of(dtype), comm_, stream_), "ncclAllGather");
   }
 
   // compute stream waits for every collective issued so far
@@ -145,6 +196,7 @@ class Comm {
   }
 
   uint64_t stream() const { return reinterpret_cast<uintptr_t>(stream_); }
+  double init_seconds() const { return init_s_; }
   int rank() const { return rank_; }
   int nranks() const { return nranks_; }
   int device() const { return device_; }
@@ -153,6 +205,19 @@ class Comm {
   void live() const {
     if (!comm_) throw std::runtime_error("communicator destroyed or aborted");
   }
+  // a non-blocking communicator may answer ncclInProgress: the call is enqueued once its
+  // state settles (the watchdog aborts a communicator whose peer failed, which ends this)
+  void settle(ncclResult_t r, const char* what) {
+    if (r == ncclInProgress) {
+      py::gil_scoped_release nogil;
+      do {
+        std::this_thread::yield();
+        if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) break;
+      } while (r == ncclInProgress);
+    }
+    nccl_check(r, what);
+  }
+  double init_s_ = 0.0;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t ready_ = nullptr, done_ = nullptr;
@@ -173,9 +238,10 @@ PYBIND11_MODULE(_comm, m) {
     ncclGetVersion(&v);
     return v;
   });
+  py::register_exception<InitTimeout>(m, "InitTimeout", PyExc_TimeoutError);
   py::class_<Comm>(m, "Comm")
-      .def(py::init<int, int, py::bytes, int>(), py::arg("nranks"), py::arg("rank"), py::arg("uid"),
-           py::arg("device"))
+      .def(py::init<int, int, py::bytes, int, double>(), py::arg("nranks"), py::arg("rank"), py::arg("uid"),
+           py::arg("device"), py::arg("timeout_s") = 600.0)
       .def("all_reduce", &Comm::all_reduce)
       .def("broadcast", &Comm::broadcast)
       .def("reduce_scatter", &Comm::reduce_scatter)
@@ -186,6 +252,7 @@ PYBIND11_MODULE(_comm, m) {
       .def("abort", &Comm::abort)
       .def("destroy", &Comm::destroy)
       .def_property_readonly("stream", &Comm::stream)
+      .def_property_readonly("init_seconds", &Comm::init_seconds)
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("nranks", &Comm::nranks)
       .def_property_readonly("device", &Comm::device);

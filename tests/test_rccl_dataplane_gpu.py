@@ -16,6 +16,15 @@ deterministic), for bf16 and fp32 wires.  The step must add no host synchronisat
 (``torch.cuda.set_sync_debug_mode`` counts every synchronising call), and the timing
 summary must be finite with the exposed communication inside the step.
 
+What each wire case can and cannot see: with the bf16 wire the bf16 arenas are reduced IN
+PLACE, and an in-place all-reduce over one rank is a no-op -- a collective ordered too early
+against its producers would still leave the right bytes.  Only the fp32-wire case checks
+producer -> collective -> consumer ordering for the bf16 arenas, because their gradients go
+through the comm stream's copy into the fp32 wire buffer and back: a copy that ran before the
+producing kernels (or a copy back after the optimizer read) changes the bits.  The fp32-wire
+case is therefore mandatory for both transports; the bf16 case covers the fp32 arenas'
+bf16 round trip and the launch / timing branches.
+
 Reference: the MirroredStrategy / MWMS gradient all-reduce the reference relies on,
 ``/root/reference/src/python/tensorflow_cloud/core/preprocess.py:137-146`` and
 ``core/tests/testdata/mnist_example_using_ctl.py:129,155-157``.
