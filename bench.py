@@ -139,6 +139,8 @@ def main():
     opt = SGD(model, learning_rate=args.lr, momentum=0.9, weight_decay=5e-5, grad_scale=1.0 / world)
     reducer = strategy.gradient_reducer(opt.arenas, bucket_mb=args.bucket_mb, reduce_dtype=args.grad_reduce_dtype)
     reducer.broadcast_parameters()
+    # world > 1 (RCCL): bucket k's fused update runs as its all-reduce completes
+    sliced = reducer.attach_optimizer(opt)
 
     gen = torch.Generator(device=device)
     gen.manual_seed(1000 + rank)
@@ -199,6 +201,7 @@ def main():
     # everything alive now (model, optimizer state, imports) leaves the collector's full passes
     gc_frozen = gc_control.freeze()
     reducer.timing_start()
+    reducer.probe_readiness()  # per-bucket gradient-ready events -> overlap budget (any world size)
     host0 = benchlaunch.host_state()
     step_probe = benchlaunch.StepProbe(cuda=on_gpu)
     # per-step device time from events on the compute stream and per-step host launch time
@@ -225,6 +228,7 @@ def main():
         [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)] if evs else None, host_ms,
         host0, benchlaunch.host_state(), probe=step_probe.close(), paced_ms=paced_ms)
     comm = reducer.timing_summary()
+    budget = reducer.overlap_budget()
     per_rank_ms = [v / args.steps * 1000.0 for v in dist_env.all_gather_floats(t1 - t0, device)]
     elapsed = dist_env.all_reduce_max(t1 - t0, device)
     ms = elapsed / args.steps * 1000.0
@@ -276,7 +280,8 @@ def main():
             "strategy": strategy.name,
             "comm": dict(reducer.describe(), allreduce_ms=comm["allreduce_ms"],
                          exposed_comm_ms=comm["exposed_comm_ms"], timing=comm.get("timing"),
-                         busbw_gbs=busbw, comm_probe=probe),
+                         busbw_gbs=busbw, comm_probe=probe, sliced_optimizer=sliced),
+            "overlap_budget": budget,
             "replicas_consistent": replicas_consistent,
             "step_stats_rank0": step_stats,
             "gc_frozen_objects": gc_frozen,

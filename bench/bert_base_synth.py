@@ -142,6 +142,7 @@ def main():
         reducer = strategy.gradient_reducer(opt.arenas, bucket_mb=args.bucket_mb,
                                             reduce_dtype=args.grad_reduce_dtype)
         reducer.broadcast_parameters()
+        reducer.attach_optimizer(opt)  # world > 1: AdamW per bucket as each all-reduce completes
 
         def train_step():
             opt.zero_grad()
@@ -180,6 +181,7 @@ def main():
         gc_frozen = gc_control.freeze()  # model / optimizer / imports leave the collector's full passes
     if reducer is not None:
         reducer.timing_start()
+        reducer.probe_readiness()  # per-bucket gradient-ready events -> overlap budget
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = train_step()
@@ -199,7 +201,8 @@ def main():
         t = reducer.timing_summary()
         comm = dict(reducer.describe(), allreduce_ms=dist_env.all_reduce_max(t["allreduce_ms"], device),
                     exposed_comm_ms=dist_env.all_reduce_max(t["exposed_comm_ms"], device), timing=t.get("timing"),
-                    busbw_gbs=busbw, comm_probe=probe)
+                    busbw_gbs=busbw, comm_probe=probe, sliced_optimizer=reducer.optimizer is not None,
+                    overlap_budget=reducer.overlap_budget())
     if rank == 0:
         print(json.dumps(_finite({
             "metric": "sequences/sec BERT-base fine-tune synthetic GLUE (seq %d)" % S,

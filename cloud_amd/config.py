@@ -172,6 +172,9 @@ _VARS = [
         "projection that fed it (no separate column-sum pass)", "ops"),
     Var("CLOUD_AMD_TAIL_BUCKET_MB", float, 1.0, "cap on the last gradient bucket (the first layers' gradients, "
         "ready only when backward ends: its all-reduce is exposed)", "distributed"),
+    Var("CLOUD_AMD_SLICED_OPT", bool, True, "multi-GPU: run the fused optimizer update per gradient bucket as "
+        "each bucket's all-reduce completes (overlapping the next bucket's), instead of once after the last one",
+        "distributed"),
     Var("CLOUD_AMD_GRAD_REDUCE_DTYPE", str, "auto", "wire dtype of the gradient all-reduce: 'bf16' (every "
         "bucket, fp32 arenas through a bf16 copy: half the bytes), 'fp32' (every bucket through fp32), 'native' "
         "(each arena in its own dtype), 'auto' (= native: fp32 master-weight gradients keep fp32 sums; 'bf16' is "

@@ -298,6 +298,7 @@ class Model(Layer):
         self._reducer = GradAllReducer(impl.arenas) if world > 1 else None
         impl.reducer = self._reducer
         if self._reducer is not None:
+            self._reducer.attach_optimizer(impl)  # RCCL: the update runs per bucket as it joins
             self._reducer.broadcast_parameters()
             self._broadcast_buffers()
         sm = self._final_softmax_layer()

@@ -28,6 +28,23 @@ from ..ops import _ext
 from .arena import build_arenas, reattach_grads, zero_grads
 
 
+class _OwnerRef:
+    """``param._ca_opt``: a weak reference to the optimizer whose arenas hold the parameter.
+    Pickles (model save via cloudpickle, checkpoints) as a dead reference: an optimizer is
+    never serialised through its parameters."""
+
+    __slots__ = ("_ref",)
+
+    def __init__(self, opt=None):
+        self._ref = weakref.ref(opt) if opt is not None else None
+
+    def __call__(self):
+        return self._ref() if self._ref is not None else None
+
+    def __reduce__(self):
+        return (_OwnerRef, ())
+
+
 class FusedOptimizer:
     kind = "base"
 
@@ -51,7 +68,7 @@ class FusedOptimizer:
         # gradient all-reduce engine attached by the training loop that owns this optimizer
         # (Keras fit, apply_gradients); tf.GradientTape finds it through the parameters
         self.reducer = None
-        owner = weakref.ref(self)
+        owner = _OwnerRef(self)
         for a in self.arenas:
             for s in a.slots:
                 s.param._ca_opt = owner
@@ -128,8 +145,41 @@ class FusedOptimizer:
                 self._update(ai, a, lo, hi, hp, None)
         self._after_update()
 
+    # -- per-slice update (driven by the DP engine, parallel/ddp.attach_optimizer) ------------
+    def sliced_begin(self):
+        """Open a step whose update is issued slice by slice: count the iteration and freeze
+        this step's hyper-parameters (one host computation per distinct weight decay)."""
+        self.iterations += 1
+        self._slice_hv = {}
+        self._slice_ai = {id(a): i for i, a in enumerate(self.arenas)}
+
+    def sliced_update(self, arena, lo, hi):
+        """Update elements [lo, hi) of ``arena`` (a gradient bucket) on the current stream;
+        a slice that straddles the decayed / non-decayed boundary is split there."""
+        ai = self._slice_ai[id(arena)]
+        for slo, shi, wd in self._segments(arena):
+            a, b = max(lo, slo), min(hi, shi)
+            if a >= b:
+                continue
+            hv = self._slice_hv.get(wd)
+            if hv is None:
+                hv = self._slice_hv[wd] = [float(v) for v in self._hp_values(wd)]
+            self._update(ai, arena, a, b, None, hv)
+
+    def sliced_end_pending(self):
+        """Every slice of this step has been issued: the next ``step()`` only closes it."""
+        self._sliced_done = True
+
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        if getattr(self, "_sliced_done", False):
+            # the DP engine already issued this step's update bucket by bucket (and the compute
+            # stream joined it); only the bookkeeping and the run-ahead bound remain
+            self._sliced_done = False
+            self._after_update()
+            if self.pacer is not None:
+                self.pacer.step_done()
+            return loss
         if self.clipnorm is not None:
             self._clip()
         self.iterations += 1

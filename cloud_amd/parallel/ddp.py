@@ -96,7 +96,7 @@ class _TorchTransport:
 
 class Bucket:
     __slots__ = ("arena", "lo", "hi", "slots", "pending", "work", "launched", "index", "wire", "wire_buf", "ev",
-                 "span")
+                 "span", "ready_ev")
 
     def __init__(self, arena, lo, hi, slots, index):
         self.arena, self.lo, self.hi, self.slots, self.index = arena, lo, hi, slots, index
@@ -107,6 +107,7 @@ class Bucket:
         self.wire_buf = None  # persistent storage of that copy (allocated on first use)
         self.ev = None     # (start, end) timing events of this step's collective (GPU)
         self.span = None   # [start_s, end_s] host clock of this step's collective (gloo / CPU)
+        self.ready_ev = None  # compute-stream event: this step's last gradient of the bucket produced
 
     @property
     def tensor(self):
@@ -185,6 +186,15 @@ class GradAllReducer:
         self._sync_enabled = True
         self.tape_reduced = False  # tf.GradientTape joined this step's buckets (cloud_amd/tf.py)
         self._hooks = []
+        # overlap budget (bench JSON): per bucket, a compute-stream event when its last gradient
+        # was produced, and one at the end of backward -- recorded at ANY world size
+        self._probe = False
+        self._ready_log = []
+        # per-slice optimizer (attach_optimizer): bucket k's fused update runs on its own
+        # stream as soon as bucket k's collective completes, overlapping bucket k+1's
+        self.optimizer = None
+        self._opt_stream = None
+        self._sliced_step = False
         self._build()
         if self.world > 1 and overlap:
             self._install_hooks()
@@ -237,7 +247,12 @@ class GradAllReducer:
             return
         b.pending -= 1
         if b.pending <= 0:
-            self._launch_ready()
+            if self._probe:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(torch.cuda.current_stream(b.tensor.device))
+                b.ready_ev = ev
+            if self.world > 1 or not self._probe:  # world 1: hooks exist for the readiness probe only
+                self._launch_ready()
 
     def _wire(self, b):
         """The tensor this bucket's collective reduces; runs on the comm stream."""
@@ -268,6 +283,7 @@ class GradAllReducer:
                     b.tensor.copy_(b.wire)
                 if self.timing:
                     b.ev[1].record(self._comm_stream)
+            self._update_slice(b, self._comm_stream)
         elif self._side is not None:
             # Explicit ordering: the collective is issued from a dedicated comm stream that
             # first waits on an event recorded on the compute stream (where the kernels that
@@ -296,6 +312,8 @@ class GradAllReducer:
                         b.ev[1].record(self._side)
                 elif self.timing:
                     self._host_span(b)
+            if self._device_timed:
+                self._update_slice(b, self._side)
         else:
             b.work = self.transport.all_reduce(self._wire(b))
             if self.timing:
@@ -320,7 +338,10 @@ class GradAllReducer:
 
     def finish(self):
         """Launch remaining buckets in order and join them onto the compute stream."""
+        if self._probe:
+            self._log_ready()
         if self.world <= 1:
+            self.reset()
             return
         dev_timed = self.timing and self._device_timed
         if self.timing:  # backward done (compute stream) -> comm joined = exposed communication
@@ -334,6 +355,7 @@ class GradAllReducer:
             self._next += 1
         if self.comm is not None:
             self.comm.join()  # compute stream waits for the comm stream (collectives + copies)
+            self._join_sliced()
         elif self._side is not None:
             with torch.cuda.stream(self._side):
                 for b in self.buckets:
@@ -343,6 +365,7 @@ class GradAllReducer:
                         if b.wire is not None:
                             b.tensor.copy_(b.wire)
             torch.cuda.current_stream(self._side.device).wait_stream(self._side)
+            self._join_sliced()
         else:
             for b in self.buckets:
                 if b.work is not None:
@@ -388,15 +411,19 @@ class GradAllReducer:
 
     def check_consistency(self, rtol=0.0):
         """Desync detector: after the all-reduce every replica must hold
-        the same gradients.  Compares an fp64 (sum, sum of squares, sum of |x|) fingerprint
-        of every arena across ranks; raises RuntimeError on mismatch.  Cheap -- meant to
+        the same gradients, and every replica the same master weights.  Compares an fp64
+        (sum, sum of squares, sum of |x|) fingerprint of every arena's gradients and master
+        weights across ranks; raises RuntimeError on mismatch.  Cheap -- meant to
         run every N steps (``CLOUD_AMD_GRAD_CHECK_EVERY``)."""
         if self.world <= 1:
             return True
         fp = []
         for a in self.arenas:
-            g = a.grad.double()
-            fp += [g.sum(), (g * g).sum(), g.abs().sum()]
+            # the master weights are compared too: after a fused step the gradient arena is
+            # zero (the update kernel clears it), while the weights must agree at all times
+            for t in (a.grad, a.master):
+                t = t.double()
+                fp += [t.sum(), (t * t).sum(), t.abs().sum()]
         mine = torch.stack(fp)
         allfp = [torch.empty_like(mine) for _ in range(self.world)]
         dist.all_gather(allfp, mine, group=self.pg)
@@ -417,6 +444,7 @@ class GradAllReducer:
             b.wire = None
             b.ev = None
             b.span = None
+            b.ready_ev = None
         self._next = 0
 
     def _drain_to_monitoring(self):
@@ -475,6 +503,91 @@ class GradAllReducer:
                 "reduce_dtype": wire[0] if len(wire) == 1 else "mixed(%s)" % ",".join(wire),
                 "grad_dtypes": sorted({name(a.grad.dtype) for a in self.arenas}),
                 "wire_mb_per_step": round(wire_mb, 2), "transport": transport, "world": self.world}
+
+    # -- per-slice optimizer ---------------------------------------------------------
+    def attach_optimizer(self, optimizer):
+        """Run ``optimizer``'s fused update per bucket, as each bucket's collective completes
+        (RCCL transports): bucket k's update runs on a dedicated stream while bucket k+1 is
+        still on the wire and backward is still running, so after the last collective only the
+        last bucket's update remains -- for BERT that is the word-embedding tail instead of the
+        whole-arena AdamW.  The elementwise update is the same per element, so the weights are
+        bitwise those of the whole-arena ``step()`` (tests/test_rccl_dataplane_gpu.py).
+        ``optimizer.step()`` after ``finish()`` then only closes the step.  Off when the
+        transport is not stream-ordered (gloo / CPU), with ``clipnorm`` (needs the global norm
+        first), or with ``CLOUD_AMD_SLICED_OPT=0``.  Returns True when enabled."""
+        from .. import config
+
+        ok = (self.world > 1 and self._device_timed and getattr(optimizer, "clipnorm", None) is None
+              and config.get("CLOUD_AMD_SLICED_OPT") and hasattr(optimizer, "sliced_begin"))
+        self.optimizer = optimizer if ok else None
+        if ok and self._opt_stream is None:
+            self._opt_stream = torch.cuda.Stream(self.arenas[0].grad.device)
+        return bool(ok)
+
+    def _update_slice(self, b, after_stream):
+        opt = self.optimizer
+        if opt is None:
+            return
+        if not self._sliced_step:
+            opt.sliced_begin()  # iteration count / hyper-parameters of this step, once
+            self._sliced_step = True
+        done = torch.cuda.Event()
+        done.record(after_stream)
+        self._opt_stream.wait_event(done)
+        with torch.cuda.stream(self._opt_stream):
+            opt.sliced_update(b.arena, b.lo, b.hi)
+
+    def _join_sliced(self):
+        if self.optimizer is not None and self._sliced_step:
+            torch.cuda.current_stream(self._opt_stream.device).wait_stream(self._opt_stream)
+            self.optimizer.sliced_end_pending()
+            self._sliced_step = False
+
+    # -- overlap budget ------------------------------------------------------------------
+    def probe_readiness(self, on=True):
+        """Record, for every following step, when each bucket's gradients were complete on the
+        compute stream and when backward ended (device events, no sync; any world size -- at
+        world 1 the hooks are installed for the probe only).  Read with :meth:`overlap_budget`."""
+        self._probe = bool(on) and bool(self.arenas) and self.arenas[0].grad.is_cuda
+        self._ready_log = []
+        if self._probe and not self._hooks:
+            self._install_hooks()
+            _ACTIVE.add(self)
+
+    def _log_ready(self):
+        end = torch.cuda.Event(enable_timing=True)
+        end.record(torch.cuda.current_stream(self.arenas[0].grad.device))
+        self._ready_log.append((end, [b.ready_ev for b in self.buckets]))
+        self._ready_log = self._ready_log[-64:]
+
+    def overlap_budget(self, busbw_gbs=(150.0, 300.0), world=None):
+        """Per bucket: wire MB and how many ms before the end of backward its gradients were
+        ready (mean over the probed steps; 0 for buckets completed only by ``finish``), and the
+        exposed communication PREDICTED for a serial comm path at each bus bandwidth (nccl-tests
+        convention: a bucket of B bytes takes B * 2(n-1)/n / busbw) with n = ``world`` (default:
+        this job's world, 8 at world 1).  Call after a device synchronize."""
+        if not self._ready_log:
+            return None
+        n = world or (self.world if self.world > 1 else 8)
+        nb = len(self.buckets)
+        before = [0.0] * nb
+        for end, evs in self._ready_log:
+            for i, ev in enumerate(evs):
+                if ev is not None:
+                    before[i] += max(ev.elapsed_time(end), 0.0)
+        before = [v / len(self._ready_log) for v in before]
+        mb = [(b.hi - b.lo) * (self.reduce_dtype or b.tensor.dtype).itemsize / 2 ** 20 for b in self.buckets]
+        pred = {}
+        for bw in busbw_gbs:
+            t_end = None
+            for i in range(nb):  # launch order = bucket order
+                dur = mb[i] * 2 ** 20 * 2.0 * (n - 1) / n / (bw * 1e9) * 1e3
+                start = -before[i] if t_end is None else max(-before[i], t_end)
+                t_end = start + dur
+            pred["%g" % bw] = round(max(t_end or 0.0, 0.0), 3)
+        return {"world_predicted": n, "steps": len(self._ready_log),
+                "buckets": [{"mb": round(m, 2), "ready_before_bwd_end_ms": round(v, 3)} for m, v in zip(mb, before)],
+                "predicted_exposed_comm_ms": pred}
 
     def broadcast_parameters(self, src=0):
         """C2: make every rank start from rank ``src``'s weights (one call per arena)."""

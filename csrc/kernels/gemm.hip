@@ -214,6 +214,45 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
+// Split-K reduce of a LARGE output (>= 64 x 512 float4 columns): one float4 column per thread,
+// every slab's load issued back to back (S loads of 16 B in flight per thread instead of the
+// tree kernel's 1-2), summed in slab order 0..S-1.  The tree kernel above reached ~2.5 TB/s on
+// BERT's weight gradients (6 slabs of 2304 x 768: 1-2 dependent loads per thread, two LDS
+// barriers per 1 KB of output); this form streams.  The small-output case keeps the tree
+// (slab-lanes give it the parallelism its few columns lack).
+template <bool OUT_BF16>
+__global__ void __launch_bounds__(256) splitk_reduce_cols_kernel(const float* __restrict__ ws, int S, long MN,
+                                                                void* __restrict__ out, float beta) {
+  const long n4 = MN / 4;
+  const long v = (long)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n4) return;
+  const f4v* p = reinterpret_cast<const f4v*>(ws) + v;
+  f4v acc = p[0];
+  int s = 1;
+  for (; s + 4 <= S; s += 4) {
+    const f4v a = p[(long)s * n4], b = p[(long)(s + 1) * n4], c = p[(long)(s + 2) * n4], d = p[(long)(s + 3) * n4];
+    acc += a;
+    acc += b;
+    acc += c;
+    acc += d;
+  }
+  for (; s < S; ++s) acc += p[(long)s * n4];
+  if (OUT_BF16) {
+    bf16_t* o = reinterpret_cast<bf16_t*>(out) + v * 4;
+    if (beta != 0.f) {
+      us4 old = *reinterpret_cast<const us4*>(o);
+      for (int j = 0; j < 4; ++j) acc[j] += beta * bf2f(old[j]);
+    }
+    us4 r;
+    for (int j = 0; j < 4; ++j) r[j] = f2bf(acc[j]);
+    *reinterpret_cast<us4*>(o) = r;
+  } else {
+    float* o = reinterpret_cast<float*>(out) + v * 4;
+    if (beta != 0.f) acc += beta * *reinterpret_cast<const f4v*>(o);
+    *reinterpret_cast<f4v*>(o) = acc;
+  }
+}
+
 // Split-K reduce for a skinny dense layer (Keras Flatten -> Dense: small batch, long K):
 // out[m][n] = act(sum_s ws[s][m][n] + bias[n]) in bf16 -- the fp32 sum, bias add, activation
 // and cast of the layer in one pass (no fp32 output tensor, no elementwise kernels).
@@ -545,8 +584,14 @@ int ca_splitk_bias_act(const float* ws, int splits, long M, int N, const float* 
 int ca_splitk_reduce(const float* ws, int splits, long MN, void* out, int out_bf16, float beta, hipStream_t s) {
   if (MN % 4) return -3;
   const long n4 = MN / 4;
-  int CB = 64;
-  if (n4 < 64L * 512) CB = 16;
+  if (n4 >= 64L * 512) {  // large output: streaming column kernel (same rule in gradfin.hip)
+    const int g = (int)((n4 + 255) / 256);
+    if (out_bf16) splitk_reduce_cols_kernel<true><<<g, 256, 0, s>>>(ws, splits, MN, out, beta);
+    else splitk_reduce_cols_kernel<false><<<g, 256, 0, s>>>(ws, splits, MN, out, beta);
+    CA_LAUNCH_CHECK();
+    return 0;
+  }
+  int CB = 16;
   if (n4 < 16L * 512) CB = 4;
   const int grid = (int)((n4 + CB - 1) / CB);
   if (out_bf16) splitk_reduce_kernel<true><<<grid, 256, 0, s>>>(ws, splits, MN, out, beta, CB);

@@ -38,6 +38,39 @@ struct FinArgs {
   int nj;
 };
 
+// large outputs (cb == 0): one float4 column per thread, slabs summed in order 0..S-1 with
+// every load issued back to back -- bitwise gemm.hip splitk_reduce_cols_kernel
+__device__ void fin_splitk_cols(const FinJob& J, int vb) {
+  const long n4 = J.n / 4;
+  const long v = (long)vb * 256 + threadIdx.x;
+  if (v >= n4) return;
+  const f4* p = reinterpret_cast<const f4*>(J.src) + v;
+  f4 acc = p[0];
+  int s = 1;
+  for (; s + 4 <= J.nparts; s += 4) {
+    const f4 a = p[(long)s * n4], b = p[(long)(s + 1) * n4], c = p[(long)(s + 2) * n4], d = p[(long)(s + 3) * n4];
+    acc += a;
+    acc += b;
+    acc += c;
+    acc += d;
+  }
+  for (; s < J.nparts; ++s) acc += p[(long)s * n4];
+  if (J.out_bf16) {
+    bf16_t* o = reinterpret_cast<bf16_t*>(J.out0) + v * 4;
+    if (J.beta != 0.f) {
+      const us4 old = *reinterpret_cast<const us4*>(o);
+      for (int j = 0; j < 4; ++j) acc[j] += J.beta * bf2f(old[j]);
+    }
+    us4 r;
+    for (int j = 0; j < 4; ++j) r[j] = f2bf(acc[j]);
+    *reinterpret_cast<us4*>(o) = r;
+  } else {
+    float* o = reinterpret_cast<float*>(J.out0) + v * 4;
+    if (J.beta != 0.f) acc += J.beta * *reinterpret_cast<const f4*>(o);
+    *reinterpret_cast<f4*>(o) = acc;
+  }
+}
+
 __device__ void fin_splitk(const FinJob& J, int vb, f4* red) {
   const long n4 = J.n / 4;
   const int CB = J.cb, SL = 256 / CB;
@@ -101,7 +134,8 @@ __global__ void __launch_bounds__(256) grad_fin_kernel(FinArgs a) {
   int j = 0;
   while (j + 1 < a.nj && b >= a.start[j + 1]) ++j;
   const int vb = b - a.start[j];
-  if (a.j[j].kind == 0) fin_splitk(a.j[j], vb, red);
+  if (a.j[j].kind == 0 && a.j[j].cb == 0) fin_splitk_cols(a.j[j], vb);
+  else if (a.j[j].kind == 0) fin_splitk(a.j[j], vb, red);
   else fin_cols(a.j[j], vb, reinterpret_cast<float(*)[17]>(red));
 }
 
@@ -133,8 +167,8 @@ int ca_grad_finalize_multi(const uint64_t* jobs, const float* betas, int n, hipS
       if (J.kind == 0) {
         if (J.n % 4) return -3;
         const long n4 = J.n / 4;
-        J.cb = n4 < 16L * 512 ? 4 : (n4 < 64L * 512 ? 16 : 64);  // as ca_splitk_reduce
-        J.nblocks = (int)((n4 + J.cb - 1) / J.cb);
+        J.cb = n4 < 16L * 512 ? 4 : (n4 < 64L * 512 ? 16 : 0);  // as ca_splitk_reduce (0: column kernel)
+        J.nblocks = J.cb ? (int)((n4 + J.cb - 1) / J.cb) : (int)((n4 + 255) / 256);
       } else if (J.kind == 1) {
         const long total = J.out2 ? 3 * J.n : (J.out1 ? 2 * J.n : J.n);
         J.nblocks = (int)((total + 15) / 16);

@@ -40,7 +40,11 @@ def test_bench_two_ranks_via_run_cpu(tmp_path):
     assert j["comm"]["buckets"] >= 1 and j["comm"]["allreduce_ms"] > 0
     assert j["backend"] == "gloo" and j["config"]["global_batch"] == 8
     probe = j["comm"]["comm_probe"]  # both transports measured on the same buffers
-    assert set(probe) == {"torch"} and probe["torch"]["16"]["busbw_gbs"] > 0  # CPU: no native RCCL
+    assert set(probe) == {"torch", "bench_transport"} and probe["torch"]["16"]["busbw_gbs"] > 0  # CPU: no RCCL
+    assert probe["bench_transport"] == "torch"
+    # overlap budget: per-bucket readiness needs device events -> none on CPU ranks
+    assert "overlap_budget" in j and j["overlap_budget"] is None
+    assert j["comm"]["sliced_optimizer"] is False  # gloo is not stream-ordered
     ss = j["step_stats_rank0"]
     assert ss["host_launch_ms"]["min"] <= ss["host_launch_ms"]["median"] <= ss["host_launch_ms"]["max"]
     assert ss["host_before"]["n_affinity"] >= 1 and isinstance(j["warnings"], list)

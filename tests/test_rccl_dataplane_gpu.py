@@ -63,7 +63,7 @@ def _count_syncs(fn):
     return sum("synchroniz" in str(x.message).lower() for x in w)
 
 
-def _worker(rank, port, out_path, transport, wire):
+def _worker(rank, port, out_path, transport, wire, sliced=False):
     os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       CLOUD_AMD_COMM=transport, CLOUD_AMD_GRAD_REDUCE_DTYPE=wire)
     sys.path.insert(0, ROOT)
@@ -113,6 +113,8 @@ def _worker(rank, port, out_path, transport, wire):
     info = {"describe": red.describe(), "side": red._side is not None, "native": red.comm is not None,
             "device_timed": red._device_timed, "buckets": len(red.buckets)}
     red.broadcast_parameters()  # C2 over the same transport (one rank: identity)
+    info["sliced"] = red.attach_optimizer(o1) if sliced else False
+    red.probe_readiness()
     launched = []
     step(m1, o1, red, 0)  # first collective: communicator setup outside the timed steps
     red.timing_start()
@@ -130,6 +132,7 @@ def _worker(rank, port, out_path, transport, wire):
     torch.cuda.synchronize()
     ms_per_step = t0.elapsed_time(t1) / 3
     summary = red.timing_summary()
+    info["budget"] = red.overlap_budget()
     got = [a.master.detach().cpu().clone() for a in o1.arenas]
     syncs_dp = _count_syncs(lambda: step(m1, o1, red, 0))
     if red.comm is not None:
@@ -140,13 +143,21 @@ def _worker(rank, port, out_path, transport, wire):
 
 
 @pytest.mark.parametrize("transport", ["torch", "rccl"])
-@pytest.mark.parametrize("wire", ["bf16", "fp32"])
-def test_rccl_data_plane_world1_forced_multirank(tmp_path, transport, wire):
+@pytest.mark.parametrize("wire,sliced", [("bf16", True), ("fp32", True), ("fp32", False)])
+def test_rccl_data_plane_world1_forced_multirank(tmp_path, transport, wire, sliced):
+    """``sliced``: the fused SGD runs per bucket on its own stream as each bucket's collective
+    completes (``attach_optimizer``, the multi-GPU default); the weights must still be BITWISE
+    those of the whole-arena step without DP."""
     out = str(tmp_path / "r.pt")
-    mp.spawn(_worker, args=(_free_port(), out, transport, wire), nprocs=1, join=True)
+    mp.spawn(_worker, args=(_free_port(), out, transport, wire, sliced), nprocs=1, join=True)
     r = torch.load(out, weights_only=True)
     info = r["info"]
     assert info["device_timed"] is True
+    assert info["sliced"] is sliced
+    b = info["budget"]  # overlap budget: per-bucket readiness before the end of backward
+    assert b is not None and b["steps"] == 4 and len(b["buckets"]) == info["buckets"]
+    assert any(x["ready_before_bwd_end_ms"] > 0 for x in b["buckets"])
+    assert all(math.isfinite(v) and v >= 0 for v in b["predicted_exposed_comm_ms"].values())
     if transport == "rccl":
         assert info["native"] and info["describe"]["transport"] == "native RcclComm"
     else:
