@@ -41,6 +41,7 @@ class Slot:
     offset: int
     numel: int
     decay: bool
+    seq: int = 0  # position in reverse registration order (~ the order backward produces gradients)
 
 
 @dataclass
@@ -70,8 +71,10 @@ def build_arenas(named_params, decay_fn=default_decay):
     """Move ``named_params`` (list of (name, Parameter)) into flat arenas, one per dtype."""
     named_params = [(n, p) for n, p in named_params if p.requires_grad]
     groups: dict = {}
-    for name, p in reversed(named_params):
+    seq = {}
+    for i, (name, p) in enumerate(reversed(named_params)):
         groups.setdefault((p.dtype, p.device), []).append((name, p))
+        seq[id(p)] = i
     arenas = []
     for (dtype, device), items in groups.items():
         a = Arena(dtype=dtype, device=device)
@@ -79,7 +82,7 @@ def build_arenas(named_params, decay_fn=default_decay):
         off = 0
         for name, p in ordered:
             d = decay_fn(name, p)
-            a.slots.append(Slot(p, name, off, p.numel(), d))
+            a.slots.append(Slot(p, name, off, p.numel(), d, seq[id(p)]))
             off += _pad(p.numel())
             if d:
                 a.n_decay = off

@@ -224,6 +224,16 @@ class GradAllReducer:
                     self.buckets.append(Bucket(a, lo, cut, cur[:k], len(self.buckets)))
                     cur, lo = cur[k:], cut
                 self.buckets.append(Bucket(a, lo, a.n, cur, len(self.buckets)))
+        # Launch order = the order buckets COMPLETE in backward (their last slot in reverse
+        # registration order), across arenas -- not arena by arena: BERT's fp32 arena starts
+        # with the word-embedding table, whose gradient is the very last one backward produces,
+        # and a strictly ordered launch would hold every bf16 bucket behind it (nothing
+        # overlapped; overlap_budget showed ~1.5 ms exposed at 300 GB/s).  Every rank builds the
+        # same order from the same model.
+        if os.environ.get("CLOUD_AMD_BUCKET_ORDER", "ready") == "ready":
+            self.buckets.sort(key=lambda b: (max(s.seq for s in b.slots), b.index))
+            for i, b in enumerate(self.buckets):
+                b.index = i
         for b in self.buckets:
             for s in b.slots:
                 self._param_bucket[id(s.param)] = b
