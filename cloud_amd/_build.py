@@ -186,6 +186,21 @@ def build_monitoring_test(verbose=False) -> Path:
     return out
 
 
+def build_gemm_bench(verbose=False) -> Path:
+    """bin/gemm_bench: the standalone GEMM-core benchmark + fp32-reference check
+    (csrc/tests/gemm_bench.hip; no Python on the GPU side)."""
+    out = PKG.parent / "bin" / "gemm_bench"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    cmd = [_hipcc(), *[f for f in HIP_FLAGS if f != "-fPIC"], f"-I{CSRC / 'include'}",
+           str(CSRC / "tests" / "gemm_bench.hip"), "-o", str(out)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"gemm_bench build failed\n{r.stdout}\n{r.stderr}")
+    return out
+
+
 def build_all(verbose=False):
     outs = [build_kernels(verbose)]
     if (CSRC / "comm" / "rccl_comm.cpp").exists():
@@ -198,5 +213,8 @@ def build_all(verbose=False):
 
 
 if __name__ == "__main__":
-    for p in build_all(verbose="-v" in sys.argv):
-        print(p)
+    if "gemm_bench" in sys.argv:
+        print(build_gemm_bench(verbose="-v" in sys.argv))
+    else:
+        for p in build_all(verbose="-v" in sys.argv):
+            print(p)

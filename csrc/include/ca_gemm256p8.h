@@ -38,6 +38,125 @@
 
 namespace ca {
 
+// The two-phase K loop for ONE 256 x 256 tile at (m0, n0) over K elements [kbeg, kend), into
+// `acc` (zeroed here), on the 128-KB operand image `smem`.  Returns with both wave groups
+// re-aligned and every LDS read retired (__syncthreads): the caller may reuse the LDS.  Used
+// by the data-parallel kernel below (one tile per workgroup) and by the stream-K kernel
+// (mfma_gemm_256p8_sk: several tile segments per workgroup).
+template <template <int, int, int> class LAT, template <int, int, int> class LBT>
+struct P8Loop {
+__device__ static __forceinline__ void run(const CoreParams& P, int m0, int n0, int kbeg, int kend, short* smem,
+                                           f4v (&acc)[8][4]) {
+  constexpr int NT = 512, HR = 128;
+  constexpr int HT = HR * BK;  // shorts per half tile
+  using LA = LAT<HR, 2, NT>;
+  using LB = LBT<HR, 2, NT>;
+  static_assert(!loader_stateful<LA>::value && !loader_stateful<LB>::value, "stateless loaders only");
+  constexpr bool A_KC = LA::KC, B_KC = LB::KC;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / 4, wn = wave % 4;
+  const int grp = __builtin_amdgcn_readfirstlane(wave) >> 2;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  const LA la0(P, true, m0, tid), la1(P, true, m0 + HR, tid);
+  const LB lb0(P, false, n0, tid), lb1(P, false, n0 + HR, tid);
+  const auto ra0 = loader_rsrc(la0), ra1 = loader_rsrc(la1);
+  const auto rb0 = loader_rsrc(lb0), rb1 = loader_rsrc(lb1);
+
+  // half tile h of buffer b: 0 A top, 1 A bottom, 2 B left, 3 B right
+  auto region = [&](int b, int h) { return smem + (b * 4 + h) * HT; };
+  auto dma = [&](int t, int h) {
+    const int k0 = kbeg + t * BK;
+    short* dst = region(t & 1, h);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      short* d = dst + (i * NT + wave * 64) * 8;
+      if (h == 0) CA_DMA_CHUNK(LA, la0, ra0, i, k0, d);
+      else if (h == 1) CA_DMA_CHUNK(LA, la1, ra1, i, k0, d);
+      else if (h == 2) CA_DMA_CHUNK(LB, lb0, rb0, i, k0, d);
+      else CA_DMA_CHUNK(LB, lb1, rb1, i, k0, d);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  // fragments: A 4 rows x 2 k halves of one A half tile; B 2 cols x 2 k halves of the left
+  // (bfl) and right (bfr) B half tiles
+  bf16x8 af[4][2], bfl[2][2], bfr[2][2];
+  auto read_a = [&](const short* half) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = read_frag_sw<HR, A_KC>(half, wm * 64 + i * 16, kk * 32, lane);
+  };
+  auto read_b = [&](bf16x8 (&f)[2][2], const short* half) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) f[j][kk] = read_frag_sw<HR, B_KC>(half, wn * 32 + j * 16, kk * 32, lane);
+  };
+  // C half qm (quadrants (qm,0), (qm,1)) from af, bfl and bfr: 32 MFMAs
+  auto mfma_h = [&](int qm) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[qm * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(j < 2 ? bfl[j][kk] : bfr[j - 2][kk], af[i][kk],
+                                                                       acc[qm * 4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // prologue: K tile 0, and tile 1's A top / B left / B right (what "P2 of tile -1" issues)
+  if (nk > 0) {
+    dma(0, 0);
+    dma(0, 2);
+    dma(0, 3);
+    dma(0, 1);
+  }
+  if (nk > 1) {
+    dma(1, 0);
+    dma(1, 2);
+    dma(1, 3);
+    vm_wait<6>();
+  } else {
+    vm_wait<0>();
+  }
+  bar256();
+  if (grp == 1) bar256();
+  for (int t = 0; t < nk; ++t) {
+    const int b = t & 1;
+    // P1: top C half
+    read_a(region(b, 0));
+    read_b(bfl, region(b, 2));
+    read_b(bfr, region(b, 3));
+    lgkm_wait0();
+    if (t + 1 < nk) dma(t + 1, 1);
+    bar256();
+    mfma_h(0);
+    bar256();
+    // P2: bottom C half; K tile t+1 must be complete before the next P1 reads it
+    read_a(region(b, 1));
+    lgkm_wait0();
+    if (t + 2 < nk) {
+      dma(t + 2, 0);
+      dma(t + 2, 2);
+      dma(t + 2, 3);
+      vm_wait<6>();
+    } else {
+      vm_wait<0>();
+    }
+    bar256();
+    mfma_h(1);
+    bar256();
+  }
+  if (grp == 0) bar256();
+  __syncthreads();
+}
+};
+
 template <template <int, int, int> class LAT, template <int, int, int> class LBT, int EPI, int PHASES = 2>
 __device__ __forceinline__ void mfma_gemm_256p8(const CoreParams& P) {
   static_assert(PHASES == 2 || PHASES == 4, "2 or 4 phases per K tile");
@@ -134,49 +253,9 @@ __device__ __forceinline__ void mfma_gemm_256p8(const CoreParams& P) {
   };
 
   if constexpr (PHASES == 2) {
-    // prologue: K tile 0, and tile 1's A top / B left / B right (what "P2 of tile -1" issues)
-    if (nk > 0) {
-      dma(0, 0);
-      dma(0, 2);
-      dma(0, 3);
-      dma(0, 1);
-    }
-    if (nk > 1) {
-      dma(1, 0);
-      dma(1, 2);
-      dma(1, 3);
-      vm_wait<6>();
-    } else {
-      vm_wait<0>();
-    }
-    bar256();
-    if (grp == 1) bar256();
-    for (int t = 0; t < nk; ++t) {
-      const int b = t & 1;
-      // P1: top C half
-      read_a(region(b, 0));
-      read_b(bfl, region(b, 2));
-      read_b(bfr, region(b, 3));
-      lgkm_wait0();
-      if (t + 1 < nk) dma(t + 1, 1);
-      bar256();
-      mfma_h(0);
-      bar256();
-      // P2: bottom C half; K tile t+1 must be complete before the next P1 reads it
-      read_a(region(b, 1));
-      lgkm_wait0();
-      if (t + 2 < nk) {
-        dma(t + 2, 0);
-        dma(t + 2, 2);
-        dma(t + 2, 3);
-        vm_wait<6>();
-      } else {
-        vm_wait<0>();
-      }
-      bar256();
-      mfma_h(1);
-      bar256();
-    }
+    P8Loop<LAT, LBT>::run(P, m0, n0, kbeg, kend, smem, acc);
+    gemm_epilogue<BM, BN, 2, 4, EPI, SMEM, 1, FM, FN, true>(P, acc, smem, m0, n0, tm, tid);
+    return;
   } else {
     // prologue: all of K tile 0, and the half tiles of tile 1 that K tile -1 would have issued
     if (nk > 0) {
@@ -235,6 +314,129 @@ __device__ __forceinline__ void mfma_gemm_256p8(const CoreParams& P) {
   if (grp == 0) bar256();
   __syncthreads();
   gemm_epilogue<BM, BN, 2, 4, EPI, SMEM, 1, FM, FN, true>(P, acc, smem, m0, n0, tm, tid);
+}
+
+// ---------------------------------------------------------------------------------------
+// Stream-K over the two-phase core, for GEMMs whose 256 x 256 grid is less than a few rounds
+// of the chip (BERT-base at M = 8192: QKV 288 tiles, FFN1 forward / FFN2 input gradient 384,
+// FFN2 forward / FFN1 and QKV input gradients 96, attention output 96 -- 1.1-1.5 rounds or
+// less, which left up to half the CUs idle in the last round and sent these shapes to the 128
+// core, with twice the L2 -> LDS traffic per MFMA).
+//
+// The (tile, K iteration) space -- tiles x ipt iterations of BK = 64 -- is cut into gridDim.x
+// equal contiguous ranges, one per workgroup (one 128-KB workgroup per CU).  Ranges are dealt
+// to XCDs contiguously (xcd_remap), tiles in the 256-core's grouped order, so the workgroups
+// that share a tile's K range are neighbours on one XCD.  A workgroup runs its range as
+// segments of P8Loop::run; a tile covered by one segment goes straight to the epilogue.  A split
+// tile has a static OWNER: the workgroup whose segment holds the tile's first K iteration
+// (the last segment of its range, so it is normally the last to reach the tile).  Every other
+// contributor stores its fp32 partial tile (16-B stores, [32 fragments][512 threads]) and
+// publishes it with the agent-scope release recipe of cdna_hip_programming.md section 5 (all
+// waves retire their stores, barrier, one lane: release fence, wait, relaxed agent-scope
+// atomic add on the tile's ticket).  The owner polls the ticket (relaxed agent-scope loads)
+// until every contributor arrived, acquires, adds the partials in contributor order to its own
+// accumulator (a fixed order: the result does not depend on timing), resets the ticket for the
+// next launch and runs the ordinary epilogue (bias / activation / pre-activation / act').
+// No contributor ever waits except an owner, and every contributor it waits for has already
+// finished its MFMAs or is running: the grid is gridDim.x <= CU count single-workgroup CUs.
+struct SkParams {
+  float* part;    // [gridDim.x][256 * 256] partial tiles, slot w = range w's first segment
+  int* ticket;    // [tiles] arrival counts, zero between launches (the owner resets its tile's);
+                  // ticket[err_index] = 1 if an owner's bounded wait ever ran out
+  int ipt;        // K iterations per tile
+  int err_index;
+  long total;     // tiles * ipt
+};
+
+__device__ __forceinline__ long sk_start(long w, long total, int G) { return w * total / G; }
+
+// the range index whose [start, next start) holds iteration x
+__device__ __forceinline__ int sk_owner_of(long x, long total, int G) {
+  int w = (int)(x * G / total);
+  while (w + 1 < G && sk_start(w + 1, total, G) <= x) ++w;
+  while (w > 0 && sk_start(w, total, G) > x) --w;
+  return w;
+}
+
+template <template <int, int, int> class LAT, template <int, int, int> class LBT, int EPI>
+__device__ __forceinline__ void mfma_gemm_256p8_sk(const CoreParams& P, const SkParams& S) {
+  constexpr int BM = 256, BN = 256, HR = 128;
+  constexpr int SMEM = 8 * HR * BK;  // 128 KB, as mfma_gemm_256p8
+  constexpr int FM = 8, FN = 4, NF = FM * FN;
+  __shared__ __attribute__((aligned(16))) short smem[SMEM];
+  int* flag = reinterpret_cast<int*>(smem);  // owner broadcast through the one LDS array
+
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;
+  const int lid = xcd_remap(blockIdx.x, G);
+  const int tiles_m = (P.M + BM - 1) / BM, tiles_n = (P.N + BN - 1) / BN;
+  long it = sk_start(lid, S.total, G);
+  const long end = sk_start(lid + 1, S.total, G);
+  f4v acc[FM][FN];
+  while (it < end) {
+    const int tile = (int)(it / S.ipt);
+    const int k0 = (int)(it - (long)tile * S.ipt);
+    const int k1 = (int)((long)S.ipt < (long)k0 + (end - it) ? (long)S.ipt : (long)k0 + (end - it));
+    int tm, tn;
+    tile256_coords(tile, tiles_m, tiles_n, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kend = k1 * BK < P.K ? k1 * BK : P.K;
+    P8Loop<LAT, LBT>::run(P, m0, n0, k0 * BK, kend, smem, acc);
+    if (k0 != 0 || k1 != S.ipt) {
+      const long t_beg = (long)tile * S.ipt;
+      const int first = sk_owner_of(t_beg, S.total, G);
+      const int last = sk_owner_of(t_beg + S.ipt - 1, S.total, G);
+      if (k0 != 0) {
+        // contributor: its range STARTS inside this tile, so this is its first segment and the
+        // only partial it ever stores (slot lid); publish it, then the ticket (release)
+        f4v* dst = reinterpret_cast<f4v*>(S.part) + (long)lid * NF * 512;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) dst[(i * FN + j) * 512 + tid] = acc[i][j];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_fetch_add(S.ticket + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        // owner: wait for the (last - first) other contributors, then add their partials in order
+        if (tid == 0) {
+          // bounded: a contributor that never arrives (it cannot, with the grid <= the CU count
+          // and no other stream-K launch beside this one) ends the wait after ~0.5 s with an
+          // error code for the host instead of hanging the GPU
+          const int want = last - first;
+          int spins = 0;
+          while (__hip_atomic_load(S.ticket + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+            __builtin_amdgcn_s_sleep(8);
+            if (++spins == (1 << 20)) {
+              __hip_atomic_store(S.ticket + S.err_index, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          __hip_atomic_store(S.ticket + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          flag[0] = want;
+        }
+        __syncthreads();
+        for (int w = first + 1; w <= last; ++w) {
+          const f4v* src = reinterpret_cast<const f4v*>(S.part) + (long)w * NF * 512;
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] += src[(i * FN + j) * 512 + tid];
+        }
+        __syncthreads();  // flag word read by nobody after this; the epilogue may stage C over it
+        gemm_epilogue<BM, BN, 2, 4, EPI, SMEM, 1, FM, FN, true>(P, acc, smem, m0, n0, tm, tid);
+      }
+    } else {
+      gemm_epilogue<BM, BN, 2, 4, EPI, SMEM, 1, FM, FN, true>(P, acc, smem, m0, n0, tm, tid);
+    }
+    __syncthreads();  // the next segment's DMA overwrites the epilogue's C staging
+    it += k1 - k0;
+  }
 }
 
 // 256 x 128 x 64 variant for GEMMs whose 256 x 256 grid does not fill whole rounds of the chip

@@ -69,6 +69,13 @@ __global__ void __launch_bounds__(512) dense_gemm_256p8_kernel(CoreParams P) {
   mfma_gemm_256p8<LA, LB, EPI, 2>(P);
 }
 
+// Stream-K form of the same core (ca_gemm256p8.h mfma_gemm_256p8_sk): one workgroup per CU,
+// each an equal range of the (tile, K iteration) space.
+template <template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
+__global__ void __launch_bounds__(512) dense_gemm_256p8_sk_kernel(CoreParams P, SkParams S) {
+  mfma_gemm_256p8_sk<LA, LB, EPI>(P, S);
+}
+
 // Its 256 x 128 single-phase, three-buffer variant (same header).
 template <template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
 __global__ void __launch_bounds__(512) dense_gemm_256x128_kernel(CoreParams P) {
@@ -312,6 +319,67 @@ static bool use_256x128(const CoreParams& p, int splits) {
   return t >= 256 && (tile_balance(t) >= 0.999 || (t >= 512 && tile_balance(t) >= 0.85));
 }
 
+// Stream-K (ca_gemm256p8.h) for plain bf16-epilogue GEMMs whose 256 x 256 grid is between
+// 3/8 of a round and two rounds of the chip and not whole rounds: BERT-base's M = 8192 forward
+// and input-gradient GEMMs (96-384 tiles).  Below ~96 tiles a tile's K range is shared by so
+// many workgroups that its owner's partial reads dominate; at two rounds and more the
+// data-parallel grids already fill the chip.  CLOUD_AMD_GEMM_STREAMK=0 turns it off,
+// =2 forces it wherever the operands allow (tests, A/B runs).
+static int g_streamk = -1;
+static int streamk_mode() {
+  if (g_streamk < 0) {
+    const char* e = getenv("CLOUD_AMD_GEMM_STREAMK");
+    g_streamk = e ? atoi(e) : 1;
+  }
+  return g_streamk;
+}
+
+static bool use_streamk(const CoreParams& p, int splits) {
+  const int mode = streamk_mode();
+  if (!mode || !core_p8() || splits != 1 || p.M < 256 || p.N < 256 || p.stats || p.K < 2 * BK) return false;
+  if (mode == 2) return true;
+  const long t = (long)((p.M + 255) / 256) * ((p.N + 255) / 256);
+  const long cus = cu_count();
+  return t * 8 >= cus * 3 && t < 2 * cus && tile_balance(t) < 0.999;
+}
+
+// Per-stream stream-K workspace: cu_count() fp32 partial tiles (256 KB each) and the tile
+// tickets (+1 error word), allocated once per stream and zeroed once -- the owners leave
+// their tickets at zero for the next launch, which is ordered after this one on the stream.
+struct SkWorkspace {
+  float* part = nullptr;
+  int* ticket = nullptr;
+  int nticket = 0;
+};
+
+static int streamk_workspace(hipStream_t s, int tiles, SkParams& S) {
+  static SkWorkspace slots[8];
+  static hipStream_t keys[8];
+  static int used = 0;
+  int k = 0;
+  while (k < used && keys[k] != s) ++k;
+  if (k == used) {
+    if (used == 8) return -4;
+    keys[used++] = s;
+  }
+  SkWorkspace& w = slots[k];
+  if (!w.part && hipMalloc(&w.part, (size_t)cu_count() * 256 * 256 * 4) != hipSuccess) return -5;
+  if (w.nticket < tiles + 1) {
+    if (w.ticket) {
+      hipStreamSynchronize(s);  // the old tickets may still be in use by a queued launch
+      hipFree(w.ticket);
+    }
+    const int n = tiles + 1 > 1024 ? tiles + 1 : 1024;
+    if (hipMalloc(&w.ticket, (size_t)n * 4) != hipSuccess) return -5;
+    hipMemsetAsync(w.ticket, 0, (size_t)n * 4, s);
+    w.nticket = n;
+  }
+  S.part = w.part;
+  S.ticket = w.ticket;
+  S.err_index = w.nticket - 1;
+  return 0;
+}
+
 template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB,
           template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
 int launch(const CoreParams& p0, int splits, hipStream_t s) {
@@ -322,6 +390,28 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
   // (ca_mfma_core.h BUF_CAP): rows of a tile (KC) or one split's K range (NC)
   const long span = (long)(p.k_per_split + BK > 256 ? p.k_per_split + BK : 256) * (p.lda > p.ldb ? p.lda : p.ldb) * 2;
   if (use_glds() && span >= (long)BUF_CAP) return -3;
+  if constexpr (BM == 128 && BN == 128 && EPI == EPI_BF16) {
+    if (use_streamk(p, splits)) {
+      SkParams S{};
+      const int t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+      const int rc = streamk_workspace(s, t256, S);
+      if (rc) return rc;
+      S.ipt = (p.K + BK - 1) / BK;
+      S.total = (long)t256 * S.ipt;
+      const int nwg = cu_count();
+      constexpr bool AK = GA<BM, 1, 256>::KC, BKC = GB<BN, 1, 256>::KC;
+      if constexpr (AK && BKC)
+        dense_gemm_256p8_sk_kernel<GDenseKC, GDenseKC, EPI><<<nwg, 512, 0, s>>>(p, S);
+      else if constexpr (AK && !BKC)
+        dense_gemm_256p8_sk_kernel<GDenseKC, GDenseNC, EPI><<<nwg, 512, 0, s>>>(p, S);
+      else if constexpr (!AK && !BKC)
+        dense_gemm_256p8_sk_kernel<GDenseNC, GDenseNC, EPI><<<nwg, 512, 0, s>>>(p, S);
+      else
+        return -2;
+      CA_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   if constexpr (BM == 128 && BN == 128 && (EPI == EPI_BF16 || EPI == EPI_F32_PARTIAL || EPI == EPI_BF16_ST)) {
     if (use_256(p, splits)) {
       const int t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
@@ -530,7 +620,8 @@ int xa_launch(const CoreParams& p0, const XaParams& x, hipStream_t s) {
 
 template <int EPI>
 int dispatch(int layout, const CoreParams& p, int splits, hipStream_t s) {
-  const bool small_n = want_small_n(p, splits);
+  // stream-K runs on 256 x 256 tiles whatever the 128-tile grid's balance (launch<128, 128>)
+  const bool small_n = !(EPI == EPI_BF16 && use_streamk(p, splits)) && want_small_n(p, splits);
   switch (layout) {
     case 0:
       return small_n ? launch<128, 64, DenseKC, DenseKC, GDenseKC, GDenseKC, EPI>(p, splits, s)
@@ -567,6 +658,13 @@ int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long l
 
 // Select the GEMM core for this process (values as CLOUD_AMD_GEMM_CORE above); returns
 // the previous one.
+// Stream-K mode (CLOUD_AMD_GEMM_STREAMK: 0 off, 1 auto, 2 wherever allowed); returns the previous.
+int ca_gemm_set_streamk(int mode) {
+  const int prev = streamk_mode();
+  if (mode >= 0 && mode <= 2) g_streamk = mode;
+  return prev;
+}
+
 int ca_gemm_set_core(int kind) {
   const int prev = core_kind();
   if (kind >= 0 && kind <= 6) g_core_kind = kind;

@@ -3,7 +3,7 @@
 // same process on the same random operands (uniform [-1, 1), cdna_hip_programming.md
 // §5.4 rules 24/25) and checked against an fp32 reference GEMM computed on the GPU.
 //
-//   build:  python scripts/build_gemm_bench.py        (-> bin/gemm_bench)
+//   build:  python -m cloud_amd._build gemm_bench      (-> bin/gemm_bench)
 //   run:    bin/gemm_bench [iters] M,N,K,layout ...   layout 0 = NT (fwd), 1 = NN (dgrad), 2 = TN (wgrad)
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -69,6 +69,11 @@ __global__ void __launch_bounds__(512) kp8(CoreParams P) {
 }
 
 template <template <int, int, int> class GA, template <int, int, int> class GB>
+__global__ void __launch_bounds__(512) kp8sk(CoreParams P, SkParams S) {
+  mfma_gemm_256p8_sk<GA, GB, EPI_BF16>(P, S);
+}
+
+template <template <int, int, int> class GA, template <int, int, int> class GB>
 __global__ void __launch_bounds__(512) k256x128(CoreParams P) {
   mfma_gemm_256x128<GA, GB, EPI_BF16>(P);
 }
@@ -97,6 +102,31 @@ static void launchp8(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
   if (layout == 0) kp8<GDenseKC, GDenseKC, PHASES><<<g, 512, 0, s>>>(p);
   else if (layout == 1) kp8<GDenseKC, GDenseNC, PHASES><<<g, 512, 0, s>>>(p);
   else kp8<GDenseNC, GDenseNC, PHASES><<<g, 512, 0, s>>>(p);
+}
+
+// stream-K: one workgroup per CU over all (tile, K iteration) pairs; the grid argument is
+// ignored (the 256 x 256 tile count comes from p)
+static void launchp8sk(const CoreParams& p, int layout, dim3, hipStream_t s) {
+  static float* part = nullptr;
+  static int* ticket = nullptr;
+  int dev = 0, cus = 256;
+  CHECK(hipGetDevice(&dev));
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  if (!part) {
+    CHECK(hipMalloc(&part, (size_t)cus * 256 * 256 * 4));
+    CHECK(hipMalloc(&ticket, 65536 * 4));
+    CHECK(hipMemset(ticket, 0, 65536 * 4));
+  }
+  SkParams S{};
+  const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  S.part = part;
+  S.ticket = ticket;
+  S.err_index = 65535;
+  S.ipt = (p.K + 63) / 64;
+  S.total = (long)tiles * S.ipt;
+  if (layout == 0) kp8sk<GDenseKC, GDenseKC><<<cus, 512, 0, s>>>(p, S);
+  else if (layout == 1) kp8sk<GDenseKC, GDenseNC><<<cus, 512, 0, s>>>(p, S);
+  else kp8sk<GDenseNC, GDenseNC><<<cus, 512, 0, s>>>(p, S);
 }
 
 static void launch256x128(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
@@ -157,6 +187,7 @@ int main(int argc, char** argv) {
   Variant vars[] = {{"v256", 256, 256, launch256},
                     {"p8q4", 256, 256, launchp8<4>},
                     {"p8h2", 256, 256, launchp8<2>},
+                    {"p8sk", 256, 256, launchp8sk},
                     {"w256x128", 256, 128, launch256x128},
                     {"glds128", 128, 128, launch128}};
   hipStream_t s;
