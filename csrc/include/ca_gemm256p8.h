@@ -345,14 +345,17 @@ struct SkParams {
                   // ticket[err_index] = 1 if an owner's bounded wait ever ran out
   int ipt;        // K iterations per tile
   int err_index;
-  long total;     // tiles * ipt
+  int total;      // tiles * ipt (< 2^31 / CU count: host-checked)
 };
 
-__device__ __forceinline__ long sk_start(long w, long total, int G) { return w * total / G; }
+// 32-bit range arithmetic (the scalar registers are as scarce as the vector ones here)
+__device__ __forceinline__ int sk_start(int w, int total, int G) {
+  return (int)(((unsigned long long)(unsigned)w * (unsigned)total) / (unsigned)G);
+}
 
 // the range index whose [start, next start) holds iteration x
-__device__ __forceinline__ int sk_owner_of(long x, long total, int G) {
-  int w = (int)(x * G / total);
+__device__ __forceinline__ int sk_owner_of(int x, int total, int G) {
+  int w = (int)(((unsigned long long)(unsigned)x * (unsigned)G) / (unsigned)total);
   while (w + 1 < G && sk_start(w + 1, total, G) <= x) ++w;
   while (w > 0 && sk_start(w, total, G) > x) --w;
   return w;
@@ -364,76 +367,80 @@ __device__ __forceinline__ void mfma_gemm_256p8_sk(const CoreParams& P, const Sk
   constexpr int SMEM = 8 * HR * BK;  // 128 KB, as mfma_gemm_256p8
   constexpr int FM = 8, FN = 4, NF = FM * FN;
   __shared__ __attribute__((aligned(16))) short smem[SMEM];
-  int* flag = reinterpret_cast<int*>(smem);  // owner broadcast through the one LDS array
 
   const int tid = threadIdx.x;
   const int G = gridDim.x;
   const int lid = xcd_remap(blockIdx.x, G);
   const int tiles_m = (P.M + BM - 1) / BM, tiles_n = (P.N + BN - 1) / BN;
-  long it = sk_start(lid, S.total, G);
-  const long end = sk_start(lid + 1, S.total, G);
+  int it = sk_start(lid, S.total, G);
+  const int end = sk_start(lid + 1, S.total, G);
   f4v acc[FM][FN];
   while (it < end) {
-    const int tile = (int)(it / S.ipt);
-    const int k0 = (int)(it - (long)tile * S.ipt);
-    const int k1 = (int)((long)S.ipt < (long)k0 + (end - it) ? (long)S.ipt : (long)k0 + (end - it));
+    const int tile = it / S.ipt;
+    const int k0 = it - tile * S.ipt;
+    const int k1 = S.ipt < k0 + (end - it) ? S.ipt : k0 + (end - it);
     int tm, tn;
     tile256_coords(tile, tiles_m, tiles_n, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
     const int kend = k1 * BK < P.K ? k1 * BK : P.K;
     P8Loop<LAT, LBT>::run(P, m0, n0, k0 * BK, kend, smem, acc);
-    if (k0 != 0 || k1 != S.ipt) {
-      const long t_beg = (long)tile * S.ipt;
-      const int first = sk_owner_of(t_beg, S.total, G);
-      const int last = sk_owner_of(t_beg + S.ipt - 1, S.total, G);
-      if (k0 != 0) {
-        // contributor: its range STARTS inside this tile, so this is its first segment and the
-        // only partial it ever stores (slot lid); publish it, then the ticket (release)
-        f4v* dst = reinterpret_cast<f4v*>(S.part) + (long)lid * NF * 512;
+    bool finish = true;  // this workgroup runs the tile's epilogue (one call site: register budget)
+    if (k0 != 0) {
+      // contributor: its range STARTS inside this tile, so this is its first segment and the
+      // only partial it ever stores (slot lid); publish it, then the ticket (release)
+      // the lane offset passes through an empty asm so its 32 store addresses are formed
+      // here, not hoisted out of the segment loop (64 live VGPRs -> spills)
+      uint32_t off = (uint32_t)(lid * NF * 512 + tid) * 16u;
+      asm volatile("" : "+v"(off));
+      char* dst = reinterpret_cast<char*>(S.part) + off;
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j) dst[(i * FN + j) * 512 + tid] = acc[i][j];
+        for (int j = 0; j < FN; ++j) *reinterpret_cast<f4v*>(dst + (i * FN + j) * 512 * 16) = acc[i][j];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_fetch_add(S.ticket + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      } else {
-        // owner: wait for the (last - first) other contributors, then add their partials in order
-        if (tid == 0) {
-          // bounded: a contributor that never arrives (it cannot, with the grid <= the CU count
-          // and no other stream-K launch beside this one) ends the wait after ~0.5 s with an
-          // error code for the host instead of hanging the GPU
-          const int want = last - first;
-          int spins = 0;
-          while (__hip_atomic_load(S.ticket + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-            __builtin_amdgcn_s_sleep(8);
-            if (++spins == (1 << 20)) {
-              __hip_atomic_store(S.ticket + S.err_index, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-          }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          __hip_atomic_store(S.ticket + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          flag[0] = want;
-        }
-        __syncthreads();
-        for (int w = first + 1; w <= last; ++w) {
-          const f4v* src = reinterpret_cast<const f4v*>(S.part) + (long)w * NF * 512;
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j) acc[i][j] += src[(i * FN + j) * 512 + tid];
-        }
-        __syncthreads();  // flag word read by nobody after this; the epilogue may stage C over it
-        gemm_epilogue<BM, BN, 2, 4, EPI, SMEM, 1, FM, FN, true>(P, acc, smem, m0, n0, tm, tid);
+        __hip_atomic_fetch_add(S.ticket + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-    } else {
-      gemm_epilogue<BM, BN, 2, 4, EPI, SMEM, 1, FM, FN, true>(P, acc, smem, m0, n0, tm, tid);
+      finish = false;
+    } else if (k1 != S.ipt) {
+      // owner of a split tile: wait for the other contributors, add their partials in order
+      const int last = sk_owner_of(tile * S.ipt + S.ipt - 1, S.total, G);
+      if (tid == 0) {
+        // bounded: a contributor that never arrives (it cannot: the grid is <= the CU count,
+        // every range non-empty, and no other stream-K launch runs beside this one) ends the
+        // wait after ~0.2 s with an error word for the host instead of hanging the GPU
+        const int want = last - lid;
+        int spins = 0;
+        while (__hip_atomic_load(S.ticket + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+          __builtin_amdgcn_s_sleep(8);
+          if (++spins == (1 << 20)) {
+            __hip_atomic_store(S.ticket + S.err_index, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_store(S.ticket + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      for (int w = lid + 1; w <= last; ++w) {
+        uint32_t off = (uint32_t)(w * NF * 512 + tid) * 16u;
+        asm volatile("" : "+v"(off));
+        const char* src = reinterpret_cast<const char*>(S.part) + off;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          f4v v[FN];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) v[j] = *reinterpret_cast<const f4v*>(src + (i * FN + j) * 512 * 16);
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] += v[j];
+          asm volatile("" ::: "memory");  // at most one fragment row of loads in flight
+        }
+      }
     }
+    if (finish) gemm_epilogue<BM, BN, 2, 4, EPI, SMEM, 1, FM, FN, true>(P, acc, smem, m0, n0, tm, tid);
     __syncthreads();  // the next segment's DMA overwrites the epilogue's C staging
     it += k1 - k0;
   }

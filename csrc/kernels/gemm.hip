@@ -397,8 +397,9 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
       const int rc = streamk_workspace(s, t256, S);
       if (rc) return rc;
       S.ipt = (p.K + BK - 1) / BK;
-      S.total = (long)t256 * S.ipt;
-      const int nwg = cu_count();
+      S.total = t256 * S.ipt;
+      // every range non-empty: an empty one would be counted as a contributor by the owner
+      const int nwg = (int)(S.total < cu_count() ? S.total : cu_count());
       constexpr bool AK = GA<BM, 1, 256>::KC, BKC = GB<BN, 1, 256>::KC;
       if constexpr (AK && BKC)
         dense_gemm_256p8_sk_kernel<GDenseKC, GDenseKC, EPI><<<nwg, 512, 0, s>>>(p, S);

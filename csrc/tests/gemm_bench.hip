@@ -123,10 +123,11 @@ static void launchp8sk(const CoreParams& p, int layout, dim3, hipStream_t s) {
   S.ticket = ticket;
   S.err_index = 65535;
   S.ipt = (p.K + 63) / 64;
-  S.total = (long)tiles * S.ipt;
-  if (layout == 0) kp8sk<GDenseKC, GDenseKC><<<cus, 512, 0, s>>>(p, S);
-  else if (layout == 1) kp8sk<GDenseKC, GDenseNC><<<cus, 512, 0, s>>>(p, S);
-  else kp8sk<GDenseNC, GDenseNC><<<cus, 512, 0, s>>>(p, S);
+  S.total = tiles * S.ipt;
+  const int g = (int)(S.total < cus ? S.total : cus);
+  if (layout == 0) kp8sk<GDenseKC, GDenseKC><<<g, 512, 0, s>>>(p, S);
+  else if (layout == 1) kp8sk<GDenseKC, GDenseNC><<<g, 512, 0, s>>>(p, S);
+  else kp8sk<GDenseNC, GDenseNC><<<g, 512, 0, s>>>(p, S);
 }
 
 static void launch256x128(const CoreParams& p, int layout, dim3 g, hipStream_t s) {

@@ -1,0 +1,25 @@
+#!/usr/bin/env bash
+# Round-5 session 4: stream-K GEMM without spills (isolated A/B + numerics), LN backward 8-wave A/B.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+S=scripts/gpu_step.sh
+tag=${1:-r5s4}
+chk() { grep -q " passed" gpurun_out/$1 && ! grep -qE " failed| error" gpurun_out/$1 || { echo "tests failed: $1"; tail -60 gpurun_out/$1; exit 1; }; }
+GB_VARIANTS=p8h2,p8sk,glds128 $S 240 ${tag}_gb.log bin/gemm_bench 20 8192,2304,768,0 8192,3072,768,0 8192,768,3072,0 8192,768,768,0 8192,768,2304,1 8192,3072,768,1 8192,768,3072,1 8192,768,768,1 4096,4096,4096,0 1000,600,776,1 || exit 1
+grep -h '"variant"' gpurun_out/${tag}_gb.log | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); print('%-9s %5d %5d %5d L%d %8.1f us %7.1f TF bad=%d rel=%.2e' % (d['variant'],d['M'],d['N'],d['K'],d['layout'],d['us'],d['TF'],d['bad'],d['rel_l2']))"
+$S 300 ${tag}_sk.log python -u -m pytest tests/test_gemm_streamk_gpu.py tests/test_gemm256_gpu.py -x -q --timeout 120 --timeout-method thread || exit 1
+chk ${tag}_sk.log
+$S 300 ${tag}_bt.log python -u -m pytest tests/test_bert_hf_parity.py tests/test_transformer_gpu.py -x -q --timeout 120 --timeout-method thread || exit 1
+chk ${tag}_bt.log
+for r in 1 2; do
+CLOUD_AMD_GEMM_STREAMK=0 CLOUD_AMD_LN_BWD8=0 $S 200 ${tag}_bert_base_${r}.log python bench/bert_base_synth.py --steps 20 --warmup 5 || exit 1
+CLOUD_AMD_GEMM_STREAMK=0 CLOUD_AMD_LN_BWD8=1 $S 200 ${tag}_bert_ln8_${r}.log python bench/bert_base_synth.py --steps 20 --warmup 5 || exit 1
+CLOUD_AMD_GEMM_STREAMK=1 CLOUD_AMD_LN_BWD8=1 $S 200 ${tag}_bert_sk_${r}.log python bench/bert_base_synth.py --steps 20 --warmup 5 || exit 1
+done
+tail -2 gpurun_out/${tag}_sk.log
+for f in gpurun_out/${tag}_bert_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f | tail -1)"; done
+echo SESSION_DONE
