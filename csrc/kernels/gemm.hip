@@ -321,15 +321,17 @@ static bool use_256x128(const CoreParams& p, int splits) {
 
 // Stream-K (ca_gemm256p8.h) for plain bf16-epilogue GEMMs whose 256 x 256 grid is between
 // 3/8 of a round and two rounds of the chip and not whole rounds: BERT-base's M = 8192 forward
-// and input-gradient GEMMs (96-384 tiles).  Below ~96 tiles a tile's K range is shared by so
-// many workgroups that its owner's partial reads dominate; at two rounds and more the
-// data-parallel grids already fill the chip.  CLOUD_AMD_GEMM_STREAMK=0 turns it off,
-// =2 forces it wherever the operands allow (tests, A/B runs).
+// and input-gradient GEMMs (96-384 tiles).  OFF by default (CLOUD_AMD_GEMM_STREAMK=1: those
+// shapes, =2: wherever the operands allow -- tests): measured slower than the 128 x 128 core
+// it would replace on every BERT shape (bin/gemm_bench, profiles/r5_s4/: QKV forward 57.4 vs
+// 42.1 us, FFN2 forward 75.0 vs 59.8, attention output 48.4 vs 19.6) and BERT 5,365 vs 6,866
+// seq/s -- the two-phase core's per-iteration rate on short segments plus one 256-KB fp32
+// partial store and load per split tile cost more than the last round's idle CUs.
 static int g_streamk = -1;
 static int streamk_mode() {
   if (g_streamk < 0) {
     const char* e = getenv("CLOUD_AMD_GEMM_STREAMK");
-    g_streamk = e ? atoi(e) : 1;
+    g_streamk = e ? atoi(e) : 0;
   }
   return g_streamk;
 }

@@ -222,120 +222,6 @@ __global__ void __launch_bounds__(LN_BLK) ln_bwd_kernel(const bf16_t* __restrict
   }
 }
 
-// LayerNorm backward, 8 waves per block and TWO rows per wave per trip (both rows' dy / h
-// loads issued before either is reduced).  At BERT's M = 8192 x C = 768 the 4-wave kernel
-// above runs 2,048 waves (2 per SIMD) of 4 rows each, one row's loads in flight behind the row
-// being reduced: 19-24 us for ~55 MB.  This form runs 4,096 waves of 2 rows with the same
-// 512 blocks (so the same [nblk][3][C] partials for col_finalize), reducing the 8 waves' column
-// sums through 4 LDS slots in two steps (the 12 C floats of dynamic LDS the 4-wave kernel uses).
-template <int NV>
-__global__ void __launch_bounds__(512) ln_bwd8_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
-                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                     const float* __restrict__ gamma, bf16_t* __restrict__ dh,
-                                                     bf16_t* __restrict__ dx, float* __restrict__ part, long M,
-                                                     int C, DropCfg din, DropCfg dout) {
-  extern __shared__ float red[];  // [4 slots][3][C]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int C4 = C >> 2;
-  float ag[NV][4], ab[NV][4], ax[NV][4], g[NV][4];
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c4 = lane + 64 * i;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ag[i][j] = ab[i][j] = ax[i][j] = 0.f;
-      g[i][j] = c4 < C4 ? gamma[4 * c4 + j] : 0.f;
-    }
-  }
-  const float invC = 1.f / (float)C;
-  for (long r0 = (long)blockIdx.x * 16 + wave * 2; r0 < M; r0 += (long)gridDim.x * 16) {
-    float d[2][NV][4], xh[2][NV][4], mu[2], rs[2];
-    bool live[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const long r = r0 + q;
-      live[q] = r < M;
-      mu[q] = live[q] ? mean[r] : 0.f;
-      rs[q] = live[q] ? rstd[r] : 0.f;
-#pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int c4 = lane + 64 * i;
-        if (live[q] && c4 < C4) {
-          load4(dy + r * C + 4 * c4, d[q][i]);
-          load4(h + r * C + 4 * c4, xh[q][i]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) d[q][i][j] = xh[q][i][j] = 0.f;
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (!live[q]) continue;
-      const long base = (r0 + q) * C;
-      float sa = 0.f, sb = 0.f;
-#pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int c4 = lane + 64 * i;
-        if (c4 < C4) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (dout.on) d[q][i][j] *= drop_mul(dout, base + 4 * c4 + j);
-            xh[q][i][j] = (xh[q][i][j] - mu[q]) * rs[q];
-            ag[i][j] += d[q][i][j] * xh[q][i][j];
-            ab[i][j] += d[q][i][j];
-            const float gd = g[i][j] * d[q][i][j];
-            sa += gd;
-            sb += gd * xh[q][i][j];
-          }
-        }
-      }
-      const float a = wave_sum(sa) * invC, b = wave_sum(sb) * invC;
-#pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int c4 = lane + 64 * i;
-        if (c4 >= C4) continue;
-        float o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = rs[q] * (g[i][j] * d[q][i][j] - a - xh[q][i][j] * b);
-        store4(dh + base + 4 * c4, o);
-        if (dx) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] *= din.on ? drop_mul(din, base + 4 * c4 + j) : 1.f;
-          store4(dx + base + 4 * c4, o);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ax[i][j] += o[j];
-      }
-    }
-  }
-  // column sums: waves 4-7 store into slots 0-3, waves 0-3 add theirs, then 4 slots -> partial
-  const int slot = wave & 3;
-  for (int step = 0; step < 2; ++step) {
-    if ((wave >> 2) == 1 - step) {
-#pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int c4 = lane + 64 * i;
-        if (c4 >= C4) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float* r = red + slot * 3 * C + 4 * c4 + j;
-          r[0] = step ? r[0] + ag[i][j] : ag[i][j];
-          r[C] = step ? r[C] + ab[i][j] : ab[i][j];
-          r[2 * C] = step ? r[2 * C] + ax[i][j] : ax[i][j];
-        }
-      }
-    }
-    __syncthreads();
-  }
-  for (int c = threadIdx.x; c < 3 * C; c += 512) {
-    float t = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) t += red[w * 3 * C + c];
-    part[(long)blockIdx.x * 3 * C + c] = t;
-  }
-}
-
 // out[c] (+)= sum_p part[p*stride + c], for c < N; out2 / out3 (optional) get columns
 // N..2N-1 / 2N..3N-1.  Block = 16 columns x 16 part-lanes (enough waves in flight to
 // hide the partial-slab reads; deterministic fixed-order tree).
@@ -637,31 +523,19 @@ int ln_fwd_launch(const bf16_t* x, const bf16_t* res, const float* g, const floa
   return 0;
 }
 
-// 8-wave LayerNorm backward (ln_bwd8_kernel; CLOUD_AMD_LN_BWD8=0: the 4-wave kernel)
-bool ln_bwd8() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CLOUD_AMD_LN_BWD8");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v != 0;
-}
-
 template <int NV>
 int ln_bwd_launch(const bf16_t* dy, const bf16_t* h, const float* mu, const float* rs, const float* g, bf16_t* dh,
                   bf16_t* dx, float* part, int nblk, long M, int C, DropCfg din, DropCfg dout, hipStream_t s) {
-  if (ln_bwd8())
-    ln_bwd8_kernel<NV><<<nblk, 512, 12 * C * sizeof(float), s>>>(dy, h, mu, rs, g, dh, dx, part, M, C, din, dout);
-  else
-    ln_bwd_kernel<NV><<<nblk, LN_BLK, 12 * C * sizeof(float), s>>>(dy, h, mu, rs, g, dh, dx, part, M, C, din, dout);
+  ln_bwd_kernel<NV><<<nblk, LN_BLK, 12 * C * sizeof(float), s>>>(dy, h, mu, rs, g, dh, dx, part, M, C, din, dout);
   return 0;
 }
 
-// LayerNorm-backward blocks (each block leaves one [3][C] partial row for col_finalize): 4-wave
-// blocks take 4 rows per trip, 8-wave blocks 16.  Measured at M = 8192, C = 768 (4-wave):
-// 512 blocks 19-23 us, 1024 blocks 25-26 us.
+// LayerNorm-backward blocks (4 rows each per trip; each block leaves one [3][C] partial row
+// for col_finalize).  Measured at M = 8192, C = 768: 512 blocks 19-23 us, 1024 blocks 25-26 us.
+// (An 8-wave block taking two rows per wave per trip -- 4,096 waves instead of 2,048 -- made
+// BERT 1.5 % SLOWER: 6,774 / 6,790 vs 6,866 / 6,899 seq/s, profiles/r5_s4/.)
 int ln_nblk(long M) {
-  long b = ln_bwd8() ? (M + 15) / 16 : (M + 3) / 4;
+  long b = (M + 3) / 4;
   return (int)(b < 512 ? b : 512);
 }
 

@@ -13,7 +13,7 @@ for l in sys.stdin:
     d=json.loads(l); print('%-9s %5d %5d %5d L%d %8.1f us %7.1f TF bad=%d rel=%.2e' % (d['variant'],d['M'],d['N'],d['K'],d['layout'],d['us'],d['TF'],d['bad'],d['rel_l2']))"
 $S 300 ${tag}_sk.log python -u -m pytest tests/test_gemm_streamk_gpu.py tests/test_gemm256_gpu.py -x -q --timeout 120 --timeout-method thread || exit 1
 chk ${tag}_sk.log
-$S 300 ${tag}_bt.log python -u -m pytest tests/test_bert_hf_parity.py tests/test_transformer_gpu.py -x -q --timeout 120 --timeout-method thread || exit 1
+$S 300 ${tag}_bt.log python -u -m pytest tests/test_bert_hf_parity.py tests/test_transformer_gpu.py tests/test_no_library_fallback_gpu.py -x -q --timeout 120 --timeout-method thread || exit 1
 chk ${tag}_bt.log
 for r in 1 2; do
 CLOUD_AMD_GEMM_STREAMK=0 CLOUD_AMD_LN_BWD8=0 $S 200 ${tag}_bert_base_${r}.log python bench/bert_base_synth.py --steps 20 --warmup 5 || exit 1
