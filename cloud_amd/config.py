@@ -102,6 +102,13 @@ _VARS = [
         "forward 1x1 convs, BERT bias/GELU/GELU'/beta dense layers): 4 staged output rows in flight per trip", "ops"),
     Var("CLOUD_AMD_ATTN_FUSED_BWD", bool, True, "attention at S = 64 / 128: one workgroup per (batch, head) for "
         "the forward and a single fused backward kernel; 0 keeps the 64-query-block kernels", "ops"),
+    Var("CLOUD_AMD_GEMM_STREAMK", int, 0, "two-phase 256 x 256 GEMM: 0 off (default; measured slower than the "
+        "128 x 128 core on BERT's M = 8192 shapes), 1 stream-K on under-filled grids, 2 wherever allowed (tests)", "ops"),
+    Var("CLOUD_AMD_LN_BWD8", bool, False, "retired round-5 A/B knob (8-wave LayerNorm backward, measured 1.5 % slower "
+        "and removed); ignored", "ops"),
+    Var("CLOUD_AMD_CONV_HALO", bool, True, "3x3 / stride-1 / 64-channel convolutions at width 56 (ResNet-50 "
+        "stage 1) forward and input gradient on the LDS-resident kernel (ca_conv_halo.h: input patch and all 9 taps "
+        "in LDS, persistent grid); 0 = implicit-GEMM tiles (A/B runs)", "ops"),
     Var("CLOUD_AMD_CONV_EPI_PF", bool, True, "implicit-GEMM forward convolutions with the BN-statistics epilogue: "
         "read 2 staged output rows from LDS before storing", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "
@@ -233,6 +240,10 @@ _VARS = [
     Var("CLOUD_AMD_DATA", str, None, "directory of real .npz datasets (else synthetic)", "data"),
     # benchmarks / examples
     Var("CLOUD_AMD_BENCH_BATCH", int, 1024, "per-GPU batch of bench.py (41 GB of the 288 GB HBM)", "bench"),
+    Var("CLOUD_AMD_BUCKET_ORDER", str, "ready", "gradient buckets launch in backward-completion order across "
+        "arenas ('ready', default) or in arena order ('arena')", "distributed"),
+    Var("CLOUD_AMD_COMM_INIT_TIMEOUT_S", float, 300.0, "deadline for the native communicator's bootstrap (unique-id "
+        "exchange + non-blocking init); past it the communicator is aborted and TimeoutError raised", "distributed"),
     Var("CLOUD_AMD_EXAMPLE_CPU", bool, False, "examples: launch CPU ranks instead of GPUs", "examples"),
     Var("CLOUD_AMD_EXAMPLE_SMALL", bool, False, "examples: tiny datasets (tests)", "examples"),
     Var("CLOUD_AMD_EXAMPLE_OUT", str, None, "examples: output directory", "examples"),

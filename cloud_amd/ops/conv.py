@@ -214,7 +214,7 @@ def conv2d_nhwc(x, w, bias=None, stride=1, padding=0, stats=False):
         param = w if (w.is_leaf and w.requires_grad) else None
         OH, OW = _out(H, KH, stride, padding), _out(W, KW, stride, padding)
         if stats:
-            part = stats_buffer(N * OH * OW, Cout, x.device)
+            part = raw.conv_stats_buffer(x.shape, w, stride, padding, x.device)
         y = _ConvFn.apply(x, w.detach() if param is not None else w, param, stride, padding, part)
         if bias is not None:
             y = y + bias

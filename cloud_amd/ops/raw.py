@@ -66,6 +66,9 @@ def conv_stats_buffer(x_shape, w, stride, padding, device):
     Cout, KH, KW, _ = w.shape
     if is_gemm_conv(w, stride, padding):
         return gemm_stats_buffer(N * H * W, Cout, Cin, device)
+    if device.type == "cuda":  # the kernel that will run decides (one row per workgroup on the halo kernel)
+        rows = _ext.load(required=True).conv_stat_rows(N, H, W, Cin, Cout, KH, KW, stride, stride, padding, padding)
+        return torch.empty((rows, 2, Cout), dtype=torch.float32, device=device)
     return stats_buffer(N * out_hw(H, KH, stride, padding) * out_hw(W, KW, stride, padding), Cout, device)
 
 
@@ -150,7 +153,8 @@ def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res
                                   float(beta), z.data_ptr(), _ext.ptr(mask), part.data_ptr(), _st(dy.device))
             _log("dgrad1x1_bn", N * H * W, Cin, Cout, _nb(dy, w, dx, z, mask) + (_nb(dx) if beta else 0))
         else:
-            rows = ext.conv_dgrad_stat_tiles(N, H, W, stride, stride)
+            rows = ext.conv_dgrad_stat_rows(N, H, W, Cin, Cout, KH, KW, stride, stride, padding, padding,
+                                            float(beta))
             part = torch.empty((rows, 2, Cin), dtype=torch.float32, device=dy.device)
             ext.conv_dgrad_bnstats(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, KH, KW, stride,
                                    stride, padding, padding, float(beta), z.data_ptr(), _ext.ptr(mask),

@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "ca_conv_halo.h"
 #include "ca_mfma_core.h"
 
 namespace {
@@ -875,6 +876,49 @@ int launch_n64(const CoreParams& p0, hipStream_t s) {
   return 0;
 }
 
+// 3x3 / s1 / p1 / 64-channel convolutions at width 56 (ResNet-50 stage-1 conv2, forward and
+// input gradient) on the LDS-resident patch + filter kernel (csrc/include/ca_conv_halo.h);
+// CLOUD_AMD_CONV_HALO=0 keeps them on the implicit-GEMM kernels (A/B runs).
+template <bool STATS>
+__global__ void __launch_bounds__(HALO_NT) conv3x3_halo_kernel(HaloParams P) {
+  conv3x3_halo<STATS>(P);
+}
+
+bool halo_shape(int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw) {
+  static int en = -1;
+  if (en < 0) {
+    const char* e = getenv("CLOUD_AMD_CONV_HALO");
+    en = (e && e[0] == '0') ? 0 : 1;
+  }
+  return en && KH == 3 && KW == 3 && sh == 1 && sw == 1 && ph == 1 && pw == 1 && Cin == HALO_C && Cout == HALO_C &&
+         W == 56 && H % HALO_TR == 0 && use_glds();
+}
+
+// persistent grid: one workgroup per CU (the 148-KB LDS image), at most one per tile
+int halo_grid(int Nb, int H) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+           prop.multiProcessorCount > 0) ? prop.multiProcessorCount : 256;
+  }
+  const long tiles = (long)Nb * (H / HALO_TR);
+  return (int)(tiles < cus ? tiles : cus);
+}
+
+int halo_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int W, float* stats, const bf16_t* bnz,
+                const uint8_t* bnmask, int dgrad, hipStream_t s) {
+  HaloParams hp{};
+  hp.x = x; hp.w = w; hp.y = y; hp.stats = stats; hp.bnz = bnz; hp.bnmask = bnmask;
+  hp.N = Nb; hp.H = H; hp.W = W; hp.dgrad = dgrad;
+  const int g = halo_grid(Nb, H);
+  if (stats) conv3x3_halo_kernel<true><<<g, HALO_NT, 0, s>>>(hp);
+  else conv3x3_halo_kernel<false><<<g, HALO_NT, 0, s>>>(hp);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
 CoreParams conv_params(int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw) {
   CoreParams p{};
   p.Nb = Nb; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout; p.KH = KH; p.KW = KW;
@@ -904,6 +948,8 @@ int ca_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
                 int KW, int sh, int sw, int ph, int pw, float* stats, hipStream_t s) {
   CoreParams p = conv_params(Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw);
   if (!geom_ok(Cin, Cout, (long)Nb * H * W)) return -1;
+  if (halo_shape(H, W, Cin, Cout, KH, KW, sh, sw, ph, pw))
+    return halo_launch(x, w, y, Nb, H, W, stats, nullptr, nullptr, 0, s);
   p.A = x; p.B = w; p.lda = Cin; p.ldb = (long)KH * KW * Cin; p.C = y; p.ldc = Cout;
   p.M = Nb * p.OH * p.OW; p.N = Cout; p.K = KH * KW * Cin; p.k_per_split = p.K;
   p.stats = stats;
@@ -951,6 +997,24 @@ int ca_conv_fwd_ex(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, i
 
 // Rows of the BN-backward statistics partials ca_conv_dgrad_bnstats writes: one per
 // 128-row GEMM tile, summed over the output-parity classes of a strided dgrad.
+long ca_conv_dgrad_stat_tiles(int Nb, int H, int W, int sh, int sw);
+
+// Rows of the BN-forward statistics partials ca_conv_fwd(stats != null) writes: one per
+// 128 output pixels on the implicit-GEMM kernels, one per workgroup on the halo kernel.
+long ca_conv_stat_rows(int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw) {
+  if (halo_shape(H, W, Cin, Cout, KH, KW, sh, sw, ph, pw)) return halo_grid(Nb, H);
+  const long oh = (H + 2 * ph - KH) / sh + 1, ow = (W + 2 * pw - KW) / sw + 1;
+  return ((long)Nb * oh * ow + 127) / 128;
+}
+
+// Rows of ca_conv_dgrad_bnstats' partials for the full geometry (the halo kernel writes one
+// per workgroup; beta must be 0 for it to run).
+long ca_conv_dgrad_stat_rows(int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw,
+                             float beta) {
+  if (beta == 0.f && halo_shape(H, W, Cin, Cout, KH, KW, sh, sw, ph, pw)) return halo_grid(Nb, H);
+  return ca_conv_dgrad_stat_tiles(Nb, H, W, sh, sw);
+}
+
 long ca_conv_dgrad_stat_tiles(int Nb, int H, int W, int sh, int sw) {
   if ((sh == 1 && sw == 1) || !use_glds()) return ((long)Nb * H * W + 127) / 128;
   long t = 0;
@@ -990,6 +1054,8 @@ static int conv_dgrad_impl(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb
                            const uint8_t* bnmask, float* stats, hipStream_t s) {
   CoreParams p = conv_params(Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw);
   if (!geom_ok(Cin, Cout, (long)Nb * H * W)) return -1;
+  if (beta == 0.f && halo_shape(H, W, Cin, Cout, KH, KW, sh, sw, ph, pw))
+    return halo_launch(dy, w, dx, Nb, H, W, bnz ? stats : nullptr, bnz, bnmask, 1, s);
   p.A = dy; p.B = w; p.C = dx; p.ldc = Cin;
   p.M = Nb * H * W; p.N = Cin; p.K = KH * KW * Cout; p.k_per_split = p.K;
   p.beta = beta;
