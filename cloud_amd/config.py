@@ -106,6 +106,9 @@ _VARS = [
         "128 x 128 core on BERT's M = 8192 shapes), 1 stream-K on under-filled grids, 2 wherever allowed (tests)", "ops"),
     Var("CLOUD_AMD_LN_BWD8", bool, False, "retired round-5 A/B knob (8-wave LayerNorm backward, measured 1.5 % slower "
         "and removed); ignored", "ops"),
+    Var("CLOUD_AMD_BN_FIN_MERGED", bool, True, "BatchNorm statistics from many partial rows: group reduction and "
+        "per-channel finalize in ONE launch (last block per 64 channels finalizes, agent-scope ticket); 0 = two "
+        "launches (A/B runs)", "ops"),
     Var("CLOUD_AMD_CONV_HALO", bool, True, "3x3 / stride-1 / 64-channel convolutions at width 56 (ResNet-50 "
         "stage 1) forward and input gradient on the LDS-resident kernel (ca_conv_halo.h: input patch and all 9 taps "
         "in LDS, persistent grid); 0 = implicit-GEMM tiles (A/B runs)", "ops"),

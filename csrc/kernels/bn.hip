@@ -15,6 +15,8 @@
 // combined in double precision by the finalize kernel.
 #include "ca_common.h"
 
+#include <mutex>
+
 namespace {
 
 constexpr int BLK = 256;
@@ -206,33 +208,38 @@ __global__ void __launch_bounds__(BLK) bn_stats_kernel(const bf16_t* __restrict_
 //   save_mean/save_rstd : fp32 [C] (needed by backward)
 //   scale/shift         : fp32 [C], y = x*scale + shift
 //   running stats updated in place when non-null (unbiased variance).
+struct FwdFin {
+  long M;
+  const float *gamma, *beta;
+  float eps, momentum;
+  float *run_mean, *run_var, *save_mean, *save_rstd, *scale, *shift;
+  __device__ void operator()(int c, double s, double q) const {
+    const double mean = s / (double)M;
+    double var = q / (double)M - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma ? gamma[c] : 1.f;
+    const float b = beta ? beta[c] : 0.f;
+    save_mean[c] = (float)mean;
+    save_rstd[c] = rstd;
+    scale[c] = g * rstd;
+    shift[c] = b - (float)mean * g * rstd;
+    if (run_mean) {
+      const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+      run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+    }
+  }
+};
+
 __global__ void bn_fwd_finalize_kernel(const float* __restrict__ ws, int nchunks, long stride_k, long off_q,
-                                       long M, int C,
-                                       const float* __restrict__ gamma, const float* __restrict__ beta,
-                                       float eps, float momentum,
-                                       float* __restrict__ run_mean, float* __restrict__ run_var,
-                                       float* __restrict__ save_mean, float* __restrict__ save_rstd,
-                                       float* __restrict__ scale, float* __restrict__ shift) {
+                                       int C, const FwdFin F) {
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
   double s, q;
   wave_chunk_sum(ws, nchunks, stride_k, off_q, c, s, q);
   if ((threadIdx.x & 63) != 0) return;
-  const double mean = s / (double)M;
-  double var = q / (double)M - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float g = gamma ? gamma[c] : 1.f;
-  const float b = beta ? beta[c] : 0.f;
-  save_mean[c] = (float)mean;
-  save_rstd[c] = rstd;
-  scale[c] = g * rstd;
-  shift[c] = b - (float)mean * g * rstd;
-  if (run_mean) {
-    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
-  }
+  F(c, s, q);
 }
 
 // y = act(x*scale + shift [+ res]); with a ReLU, optionally also the ReLU
@@ -401,29 +408,83 @@ __global__ void __launch_bounds__(BLK) bn_bwd_reduce_kernel(const bf16_t* __rest
 
 // dgamma = sum(dz*xhat), dbeta = sum(dz); coefficients so that
 // dx = A*dz + B*x + D.
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ ws, int nchunks, long stride_k, long off_q, long M,
-                                       int C,
-                                       const float* __restrict__ gamma, const float* __restrict__ mean,
-                                       const float* __restrict__ rstd, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta, float* __restrict__ coef, int accum,
-                                       int raw_moments) {
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (c >= C) return;
-  double sd, sdx;
-  wave_chunk_sum(ws, nchunks, stride_k, off_q, c, sd, sdx);
-  if ((threadIdx.x & 63) != 0) return;
-  // partials from a GEMM epilogue hold sum(dz*x): sum(dz*xhat) = rstd*(sum(dz*x) - mean*sum(dz))
-  if (raw_moments) sdx = (double)rstd[c] * (sdx - (double)mean[c] * sd);
-  // accum: parameter grads are summed into (flat arena slots), not overwritten
-  if (dgamma) dgamma[c] = (float)sdx + (accum ? dgamma[c] : 0.f);
-  if (dbeta) dbeta[c] = (float)sd + (accum ? dbeta[c] : 0.f);
-  const double g = gamma ? gamma[c] : 1.0;
-  const double rs = rstd[c], mu = mean[c];
-  const double k1 = g * rs;
-  const double a = sd / (double)M, b = sdx / (double)M;
-  coef[c] = (float)k1;                               // A
-  coef[C + c] = (float)(-k1 * b * rs);               // B
-  coef[2 * C + c] = (float)(-k1 * a + k1 * b * rs * mu);  // D
+struct BwdFin {
+  long M;
+  int C;
+  const float *gamma, *mean, *rstd;
+  float *dgamma, *dbeta, *coef;
+  int accum, raw_moments;
+  __device__ void operator()(int c, double sd, double sdx) const {
+    // partials from a GEMM epilogue hold sum(dz*x): sum(dz*xhat) = rstd*(sum(dz*x) - mean*sum(dz))
+    if (raw_moments) sdx = (double)rstd[c] * (sdx - (double)mean[c] * sd);
+    // accum: parameter grads are summed into (flat arena slots), not overwritten
+    if (dgamma) dgamma[c] = (float)sdx + (accum ? dgamma[c] : 0.f);
+    if (dbeta) dbeta[c] = (float)sd + (accum ? dbeta[c] : 0.f);
+    const double g = gamma ? gamma[c] : 1.0;
+    const double rs = rstd[c], mu = mean[c];
+    const double k1 = g * rs;
+    const double a = sd / (double)M, b = sdx / (double)M;
+    coef[c] = (float)k1;                                    // A
+    coef[C + c] = (float)(-k1 * b * rs);                    // B
+    coef[2 * C + c] = (float)(-k1 * a + k1 * b * rs * mu);  // D
+  }
+};
+
+// Group reduction AND finalize in one launch (one dispatch per BatchNorm instead of two):
+// the blocks of chunk_group_reduce_kernel each write their group's sums, then count
+// themselves on a per-column-block ticket (agent-scope release); the block that arrives
+// last for its 64 channels (acquire) sums the G group rows in a FIXED order -- the same
+// result whichever block finishes last -- runs the finalize and re-arms the ticket.  No
+// block ever waits for another, so there is nothing to hang on.
+template <class FIN>
+__global__ void __launch_bounds__(256) group_finalize_kernel(const float* __restrict__ ws, int nchunks, long stride_k,
+                                                             long off_q, int C, float* __restrict__ gws,
+                                                             unsigned* __restrict__ tickets, const FIN F) {
+  __shared__ float ra[4][64], rb[4][64];
+  __shared__ double da[4][64], db[4][64];
+  __shared__ int last;
+  const int tid = threadIdx.x, cl = tid & 63, pl = tid >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int G = gridDim.y, g = blockIdx.y;
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int k = g * 4 + pl; k < nchunks; k += G * 4) {
+      a += ws[(long)k * stride_k + c];
+      b += ws[(long)k * stride_k + off_q + c];
+    }
+  }
+  ra[pl][cl] = a;
+  rb[pl][cl] = b;
+  __syncthreads();
+  if (pl == 0 && c < C) {  // wave 0 alone stores the group row, so its own release covers it
+    gws[(long)g * 2 * C + c] = (ra[0][cl] + ra[1][cl]) + (ra[2][cl] + ra[3][cl]);
+    gws[(long)g * 2 * C + C + c] = (rb[0][cl] + rb[1][cl]) + (rb[2][cl] + rb[3][cl]);
+  }
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(tickets + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (unsigned)(G - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __hip_atomic_store(tickets + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  double sa = 0.0, sb = 0.0;
+  if (c < C) {
+    for (int k = pl; k < G; k += 4) {
+      sa += gws[(long)k * 2 * C + c];
+      sb += gws[(long)k * 2 * C + C + c];
+    }
+  }
+  da[pl][cl] = sa;
+  db[pl][cl] = sb;
+  __syncthreads();
+  if (pl == 0 && c < C) F(c, (da[0][cl] + da[1][cl]) + (da[2][cl] + da[3][cl]), (db[0][cl] + db[1][cl]) + (db[2][cl] + db[3][cl]));
 }
 
 template <bool RELU, bool DRES>
@@ -465,6 +526,75 @@ __global__ void __launch_bounds__(BLK) bn_bwd_apply_kernel(const bf16_t* __restr
 
 }  // namespace
 
+namespace {
+
+// Per-stream ticket words of group_finalize_kernel (one per 64-channel column block;
+// every launch leaves them at zero).  Streams get their own so concurrent BatchNorms on
+// different streams never share a counter.
+constexpr int MAX_TICKETS = 64;
+unsigned* bn_tickets(hipStream_t s) {
+  static std::mutex mu;
+  static hipStream_t keys[16];
+  static unsigned* slots[16];
+  static int used = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  for (int k = 0; k < used; ++k)
+    if (keys[k] == s) return slots[k];
+  if (used == 16) return nullptr;
+  unsigned* t = nullptr;
+  if (hipMalloc(&t, MAX_TICKETS * sizeof(unsigned)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(t, 0, MAX_TICKETS * sizeof(unsigned), s) != hipSuccess) return nullptr;
+  keys[used] = s;
+  slots[used++] = t;
+  return t;
+}
+
+bool merged_finalize() {  // CLOUD_AMD_BN_FIN_MERGED=0: separate group-reduce and finalize launches (A/B)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_BN_FIN_MERGED");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
+}
+
+// Reduce [nchunks] partial rows (row k: a at ws[k*stride_k + c], b at +off_q) and run the
+// per-channel finalize F: directly when the rows are few, else group-reduce into gws
+// ([512][2][C]) and finalize -- one launch when the ticket path is available, two otherwise.
+template <class FIN, class FinKernel>
+int reduce_finalize(const float* ws, int nchunks, long stride_k, long off_q, int C, float* gws, const FIN& F,
+                    FinKernel fin_kernel, hipStream_t s) {
+  if (nchunks > 64 && gws) {
+    const int G = group_count(nchunks);
+    const dim3 grid(ca_cdiv(C, 64), G);
+    unsigned* tk = (merged_finalize() && (int)grid.x <= MAX_TICKETS) ? bn_tickets(s) : nullptr;
+    if (tk) {
+      group_finalize_kernel<FIN><<<grid, 256, 0, s>>>(ws, nchunks, stride_k, off_q, C, gws, tk, F);
+      CA_LAUNCH_CHECK();
+      return 0;
+    }
+    chunk_group_reduce_kernel<<<grid, 256, 0, s>>>(ws, nchunks, stride_k, off_q, C, gws);
+    CA_LAUNCH_CHECK();
+    fin_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(gws, G, 2L * C, (long)C, C, F);
+  } else {
+    fin_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(ws, nchunks, stride_k, off_q, C, F);
+  }
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ void bn_bwd_finalize_c_kernel(const float* __restrict__ ws, int nchunks, long stride_k, long off_q, int,
+                                         const BwdFin F) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= F.C) return;
+  double sd, sdx;
+  wave_chunk_sum(ws, nchunks, stride_k, off_q, c, sd, sdx);
+  if ((threadIdx.x & 63) != 0) return;
+  F(c, sd, sdx);
+}
+
+}  // namespace
+
 extern "C" {
 
 // Workspace floats needed by the stats / bwd-reduce kernels: 2 * nchunks * C.
@@ -484,11 +614,8 @@ int ca_bn_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, int C,
   const dim3 agrid(ta.ncol, ta.nchunks);
   bn_stats_kernel<<<grid, BLK, 0, s>>>(x, M, C, ws);
   CA_LAUNCH_CHECK();
-  bn_fwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(ws, t.nchunks, (long)C, (long)t.nchunks * C, M, C, gamma,
-                                                         beta, eps, momentum,
-                                                         run_mean, run_var, save_mean, save_rstd,
-                                                         scale_shift, scale_shift + C);
-  CA_LAUNCH_CHECK();
+  const FwdFin F{M, gamma, beta, eps, momentum, run_mean, run_var, save_mean, save_rstd, scale_shift, scale_shift + C};
+  reduce_finalize(ws, t.nchunks, (long)C, (long)t.nchunks * C, C, nullptr, F, bn_fwd_finalize_kernel, s);
   if (relu && res) bn_apply_kernel<true, true><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
   else if (relu) bn_apply_kernel<true, false><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
   else if (res) bn_apply_kernel<false, true><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
@@ -509,19 +636,8 @@ int ca_bn_fwd_partials(const bf16_t* x, const bf16_t* res, bf16_t* y, long M, in
   dim3 grid(t.ncol, t.nchunks);
   const Tiling ta = apply_tiling(M, C);
   const dim3 agrid(ta.ncol, ta.nchunks);
-  const float* fin = partials;
-  int nfin = nparts;
-  if (nparts > 64 && gws) {
-    const int G = group_count(nparts);
-    chunk_group_reduce_kernel<<<dim3(ca_cdiv(C, 64), G), 256, 0, s>>>(partials, nparts, 2L * C, (long)C, C, gws);
-    CA_LAUNCH_CHECK();
-    fin = gws;
-    nfin = G;
-  }
-  bn_fwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(fin, nfin, 2L * C, (long)C, M, C, gamma, beta, eps,
-                                                         momentum, run_mean, run_var, save_mean, save_rstd,
-                                                         scale_shift, scale_shift + C);
-  CA_LAUNCH_CHECK();
+  const FwdFin F{M, gamma, beta, eps, momentum, run_mean, run_var, save_mean, save_rstd, scale_shift, scale_shift + C};
+  reduce_finalize(partials, nparts, 2L * C, (long)C, C, gws, F, bn_fwd_finalize_kernel, s);
   if (relu && res) bn_apply_kernel<true, true><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
   else if (relu) bn_apply_kernel<true, false><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
   else if (res) bn_apply_kernel<false, true><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, y, mask, M, C, ta);
@@ -546,19 +662,8 @@ int ca_bn_fwd_partials_ex(const bf16_t* x, const bf16_t* res, const float* res_s
   dim3 grid(t.ncol, t.nchunks);
   const Tiling ta = apply_tiling(M, C);
   const dim3 agrid(ta.ncol, ta.nchunks);
-  const float* fin = partials;
-  int nfin = nparts;
-  if (nparts > 64 && gws) {
-    const int G = group_count(nparts);
-    chunk_group_reduce_kernel<<<dim3(ca_cdiv(C, 64), G), 256, 0, s>>>(partials, nparts, 2L * C, (long)C, C, gws);
-    CA_LAUNCH_CHECK();
-    fin = gws;
-    nfin = G;
-  }
-  bn_fwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(fin, nfin, 2L * C, (long)C, M, C, gamma, beta, eps,
-                                                         momentum, run_mean, run_var, save_mean, save_rstd,
-                                                         scale_shift, scale_shift + C);
-  CA_LAUNCH_CHECK();
+  const FwdFin F{M, gamma, beta, eps, momentum, run_mean, run_var, save_mean, save_rstd, scale_shift, scale_shift + C};
+  reduce_finalize(partials, nparts, 2L * C, (long)C, C, gws, F, bn_fwd_finalize_kernel, s);
   if (!y) return 0;
   if (relu)
     bn_apply_resbn_kernel<true><<<agrid, BLK, 0, s>>>(x, res, scale_shift, scale_shift + C, res_ss, res_ss + C, y,
@@ -604,13 +709,11 @@ int ca_bn_bwd(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, const bf16
   CA_LAUNCH_CHECK();
   // ws = [nchunks][C] (a) ++ [nchunks][C] (b); group-reduce into the tail of ws
   float* gws = ws + 2L * t.nchunks * C;
-  const int G = group_count(t.nchunks);
-  chunk_group_reduce_kernel<<<dim3(ca_cdiv(C, 64), G), 256, 0, s>>>(ws, t.nchunks, (long)C, (long)t.nchunks * C, C,
-                                                                     gws);
-  CA_LAUNCH_CHECK();
-  bn_bwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(gws, G, 2L * C, (long)C, M, C, gamma, save_mean, save_rstd,
-                                                         dgamma, dbeta, coef, accum, 0);
-  CA_LAUNCH_CHECK();
+  const BwdFin F{M, C, gamma, save_mean, save_rstd, dgamma, dbeta, coef, accum, 0};
+  if (t.nchunks > 64)
+    reduce_finalize(ws, t.nchunks, (long)C, (long)t.nchunks * C, C, gws, F, bn_bwd_finalize_c_kernel, s);
+  else
+    reduce_finalize(ws, t.nchunks, (long)C, (long)t.nchunks * C, C, nullptr, F, bn_bwd_finalize_c_kernel, s);
   if (relu && dres) bn_bwd_apply_kernel<true, true><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
   else if (relu) bn_bwd_apply_kernel<true, false><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
   else if (dres) bn_bwd_apply_kernel<false, true><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
@@ -634,18 +737,8 @@ int ca_bn_bwd_partials(const bf16_t* dy, const bf16_t* y, const uint8_t* mask, c
   dim3 grid(t.ncol, t.nchunks);
   const Tiling ta = apply_tiling(M, C);
   const dim3 agrid(ta.ncol, ta.nchunks);
-  const float* fin = partials;
-  int nfin = nparts;
-  if (nparts > 64) {
-    const int G = group_count(nparts);
-    chunk_group_reduce_kernel<<<dim3(ca_cdiv(C, 64), G), 256, 0, s>>>(partials, nparts, 2L * C, (long)C, C, gws);
-    CA_LAUNCH_CHECK();
-    fin = gws;
-    nfin = G;
-  }
-  bn_bwd_finalize_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(fin, nfin, 2L * C, (long)C, M, C, gamma, save_mean, save_rstd,
-                                                         dgamma, dbeta, coef, accum, 1);
-  CA_LAUNCH_CHECK();
+  const BwdFin F{M, C, gamma, save_mean, save_rstd, dgamma, dbeta, coef, accum, 1};
+  reduce_finalize(partials, nparts, 2L * C, (long)C, C, gws, F, bn_bwd_finalize_c_kernel, s);
   if (!dx) return 0;  // finalize only: the apply runs in the consuming GEMM's operand fetch (ca_gemm_xa)
   if (relu && dres) bn_bwd_apply_kernel<true, true><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);
   else if (relu) bn_bwd_apply_kernel<true, false><<<agrid, BLK, 0, s>>>(dy, y, mask, x, coef, dx, dres, M, C, ta);

@@ -136,17 +136,9 @@ static void launch256x128(const CoreParams& p, int layout, dim3 g, hipStream_t s
   else k256x128<GDenseNC, GDenseNC><<<g, 512, 0, s>>>(p);
 }
 
-template <template <int, int, int> class GA, template <int, int, int> class GB>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k128x192(CoreParams P) {
-  mfma_gemm_glds<128, 192, 2, 2, GA, GB, EPI_BF16>(P);
-}
-
-// 128 x 192 tiles (forward NT only: the N-contiguous loaders need R / 8 to divide the
-// thread count): BERT's N = 2304 / 3072 at M = 8192 -> 768 / 1024 tiles, whole rounds of
-// 3 / 4 blocks per CU
-static void launch128x192(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
-  if (layout == 0) k128x192<GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
-}
+// (a 128 x 192 variant of the glds core was measured in round 5, profiles/r5_s6/r5s6_gb.log:
+// 15-40 % slower than 128 x 128 on every BERT shape and wrong -- the core's epilogue layout
+// assumes a power-of-two BN -- and was removed)
 
 static void launch128(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
   if (layout == 0) k128<GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
@@ -202,8 +194,7 @@ int main(int argc, char** argv) {
                     {"p8h2", 256, 256, launchp8<2>},
                     {"p8sk", 256, 256, launchp8sk},
                     {"w256x128", 256, 128, launch256x128},
-                    {"glds128", 128, 128, launch128},
-                    {"g128x192", 128, 192, launch128x192}};
+                    {"glds128", 128, 128, launch128}};
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
   hipEvent_t e0, e1;
@@ -230,7 +221,6 @@ int main(int argc, char** argv) {
     CHECK(hipStreamSynchronize(s));
     for (const Variant& v : vars) {
       if (only && !strstr(only, v.name)) continue;
-      if (v.launch == launch128x192 && L != 0) continue;
       CoreParams p{};
       p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.C = C; p.ldc = N;
       p.M = M; p.N = N; p.K = K; p.k_per_split = K; p.split_xcd = 1;
