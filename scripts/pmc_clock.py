@@ -59,9 +59,10 @@ def main(d):
             nm = c["SQ_VALU_MFMA_BUSY_CYCLES"]
             print("   mfma_busy_cycles=%.3g gui_active/8=%.3g" % (nm, c["GRBM_GUI_ACTIVE"] / 8))
             print("%-90s n=%3d dur=%8.1fus clk=%.2fGHz mfma_busy=%.3f wait_any=%.2f wait_inst=%.2f active=%.2f "
-                  "lds_conf/inst=%.2f" % (name, n, dur / 1e3, clk, mfma, c["SQ_WAIT_ANY"] / wc,
+                  "lds_conf/inst=%.2f lds_conf/idx_active=%.3f" % (name, n, dur / 1e3, clk, mfma, c["SQ_WAIT_ANY"] / wc,
                                           c["SQ_WAIT_INST_ANY"] / wc, c["SQ_ACTIVE_INST_ANY"] / wc,
-                                          c["SQ_LDS_BANK_CONFLICT"] / max(c["SQ_INSTS_LDS"], 1)))
+                                          c["SQ_LDS_BANK_CONFLICT"] / max(c["SQ_INSTS_LDS"], 1),
+                                          c["SQ_LDS_BANK_CONFLICT"] / max(c["SQ_LDS_IDX_ACTIVE"], 1)))
 
 
 if __name__ == "__main__":
