@@ -24,9 +24,16 @@
 // epilogue of conv.hip (sum g, sum g * z, g = dX gated by the ReLU bitmask of the BN that
 // produced the conv's input).
 //
-// LDS images are [row][64 channels] (128 B per row); 16-B chunk c of row q is stored at chunk
-// c ^ ((q >> 1) & 7), so the 16 lanes of a ds_read_b128 lane group, which read 16 consecutive
-// rows at one chunk, hit 16 distinct 16-B bank slots (two rows share a 256-B bank row).
+// LDS layouts.  Filter image: [row][64 channels] (128 B per row), 16-B chunk c of row q at chunk
+// c ^ ((q >> 1) & 7).  Patch image: CHUNK-MAJOR, [8 chunks][patch pixel q] (16 B per pixel,
+// planes HALO_PLANE bytes apart, a multiple of 256 B): the A-fragment reads of a ds_read_b128
+// lane group ({0-3,12-15,20-27}-style: 16 pixels, two adjacent chunks) then hit 16 distinct
+// 16-B bank slots whenever the fragment's 16 pixels are consecutive patch pixels -- a fragment
+// crossing an image row skips the two pad columns and may double one slot.  Simulated over
+// every (wave, fragment, tap): 4.57 LDS cycles per A read against 6.86 for the XOR-swizzled
+// row-major image (4 = conflict-free).  The patch is written by 8-lane groups of one chunk
+// over 8 consecutive pixels (distinct slots), loaded from global memory as whole 128-B rows
+// per 8 lanes.
 #pragma once
 #include "ca_mfma_core.h"
 
@@ -44,6 +51,16 @@ struct HaloParams {
 };
 
 constexpr int HALO_C = 64, HALO_TR = 8, HALO_WAVES = 7, HALO_NT = HALO_WAVES * 64;
+constexpr int HALO_PLANE = 37 * 256;  // bytes per chunk plane: >= 10 x 58 pixels x 16 B, multiple of 256
+
+// sum over the 16 lanes of a DPP row (row_ror 8, row_ror 4, quad swaps): every lane gets the total
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4e, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false));
+  return v;
+}
 
 __device__ __forceinline__ int halo_swz(int q, int chunk) { return q * 64 + ((chunk ^ ((q >> 1) & 7)) << 3); }
 
@@ -52,7 +69,8 @@ template <bool STATS>
 __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
   constexpr int C = HALO_C, TR = HALO_TR, NT = HALO_NT, W = 56, PW = W + 2, PR = TR + 2;
   constexpr int WIMG = 9 * C * C;      // shorts
-  constexpr int PIMG = PR * PW * C;    // shorts
+  constexpr int PIMG = 8 * HALO_PLANE / 2;  // shorts
+  static_assert(PR * PW * 16 <= HALO_PLANE, "patch plane");
   constexpr int PCH = PR * W * 8;      // 16-B chunks of a patch's interior = 4480 = 10 per thread
   static_assert(PCH % NT == 0, "patch chunks must divide the threads");
   constexpr int PPT = PCH / NT;
@@ -83,28 +101,27 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
   // the patch's left / right zero columns never change
   for (int e = tid; e < PR * 2 * 8; e += NT) {
     const int r = e / 16, side = (e / 8) & 1, ch = e % 8;
-    *reinterpret_cast<s8v*>(pimg + halo_swz(r * PW + (side ? PW - 1 : 0), ch)) = zero8();
+    *reinterpret_cast<s8v*>(pimg + ch * (HALO_PLANE / 2) + (r * PW + (side ? PW - 1 : 0)) * 8) = zero8();
   }
 
-  // this thread's patch chunks: interior chunk e = (r, c, ch), r in [0, PR), c in [0, W)
+  // this thread's patch chunks: chunk i is patch row i, image column c = 8 * wave + (lane & 7),
+  // channel chunk (lane >> 3) & 7 -- each 8-lane group covers one chunk of 8 consecutive pixels
+  // (distinct LDS bank slots on the store), each wave 8 whole 128-B pixel rows per load
+  const int pc = wave * 8 + (lane & 7), pch = (lane >> 3) & 7;
+  static_assert(PPT == PR && HALO_WAVES * 8 == W, "one patch row per chunk, 8 columns per wave");
   auto load_patch = [&](int t, s8v (&v)[PPT]) {
     const int n = t / rgroups, r0 = (t % rgroups) * TR - 1;  // patch row 0 = image row r0
+    const bf16_t* src = P.x + (((long)n * H + r0) * W + pc) * C + pch * 8;
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-      const int e = tid + i * NT;
-      const int r = e / (W * 8), c = (e / 8) % W, ch = e % 8;
-      const int ir = r0 + r;
-      v[i] = (ir >= 0 && ir < H) ? *reinterpret_cast<const s8v*>(P.x + (((long)n * H + ir) * W + c) * C + ch * 8)
-                                 : zero8();
+      const bool ok = (i > 0 || r0 >= 0) && (i < PPT - 1 || r0 + i < H);  // only rows 0 and PR-1 can be pads
+      v[i] = ok ? *reinterpret_cast<const s8v*>(src + (long)i * W * C) : zero8();
     }
   };
+  short* pdst = pimg + pch * (HALO_PLANE / 2) + (pc + 1) * 8;
   auto store_patch = [&](const s8v (&v)[PPT]) {
 #pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const int e = tid + i * NT;
-      const int r = e / (W * 8), c = (e / 8) % W, ch = e % 8;
-      *reinterpret_cast<s8v*>(pimg + halo_swz(r * PW + c + 1, ch)) = v[i];
-    }
+    for (int i = 0; i < PPT; ++i) *reinterpret_cast<s8v*>(pdst + i * PW * 8) = v[i];
   };
 
   // per lane: patch row q0 (tap (0,0)) of the pixel of each of its 4 M fragments
@@ -148,7 +165,8 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
                                                   wimg + halo_swz(tap * C + nf * 16 + (lane & 15), chunk)));
 #pragma unroll
         for (int mf = 0; mf < 4; ++mf)
-          af[mf] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s8v*>(pimg + halo_swz(q0[mf] + dq, chunk)));
+          af[mf] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s8v*>(pimg + chunk * (HALO_PLANE / 2) +
+                                                                           (q0[mf] + dq) * 8));
 #pragma unroll
         for (int mf = 0; mf < 4; ++mf)
 #pragma unroll
@@ -164,29 +182,29 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) ssum[j] = ssq[j] = 0.f;
     const int n = t / rgroups, r0 = (t % rgroups) * TR;
+    const long tile_pix = ((long)n * H + r0) * W;  // first pixel of the tile (rows are whole)
 #pragma unroll
     for (int mf = 0; mf < 4; ++mf) {
       const int p = wave * 64 + mf * 16 + (lane & 15);
-      const long pix = ((long)n * H + r0 + p / W) * W + (p % W);
+      const long pix = tile_pix + p;
+      bf16_t* yp = P.y + pix * C + 4 * kq;
       uint32_t mk = 0xffffffffu;
       if (STATS && P.dgrad) {
         // the 16 channels of this lane (4 groups of 4 at nf * 16 + 4 * kq) span bytes nf*2 + kq/2
-        mk = 0;
+        mk = 0xffffu;
         if (P.bnmask) {
+          const uint8_t* mp = P.bnmask + pix * 8 + (kq >> 1);
+          mk = 0;
 #pragma unroll
-          for (int nf = 0; nf < 4; ++nf)
-            mk |= (((uint32_t)P.bnmask[pix * 8 + nf * 2 + (kq >> 1)] >> ((kq & 1) * 4)) & 0xfu) << (nf * 4);
-        } else {
-          mk = 0xffffu;
+          for (int nf = 0; nf < 4; ++nf) mk |= (((uint32_t)mp[nf * 2] >> ((kq & 1) * 4)) & 0xfu) << (nf * 4);
         }
       }
 #pragma unroll
       for (int nf = 0; nf < 4; ++nf) {
-        const int co = nf * 16 + 4 * kq;
         us4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[mf][nf][r]);
-        *reinterpret_cast<us4*>(P.y + pix * C + co) = o;
+        *reinterpret_cast<us4*>(yp + nf * 16) = o;
         if constexpr (STATS) {
           if (!P.dgrad) {
 #pragma unroll
@@ -196,7 +214,7 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
               ssq[nf * 4 + r] += a * a;
             }
           } else {
-            const us4 z = *reinterpret_cast<const us4*>(P.bnz + pix * C + co);
+            const us4 z = *reinterpret_cast<const us4*>(P.bnz + (yp - P.y) + nf * 16);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float g = ((mk >> (nf * 4 + r)) & 1u) ? bf2f(o[r]) : 0.f;
@@ -208,13 +226,12 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
       }
     }
     if constexpr (STATS) {
+      // sums over the 16 pixel lanes of each 16-lane row: DPP rotates within the row (VALU,
+      // no LDS permutes), every lane ends with the row total
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          ssum[j] += __shfl_xor(ssum[j], o, 64);
-          ssq[j] += __shfl_xor(ssq[j], o, 64);
-        }
+        ssum[j] = row16_sum(ssum[j]);
+        ssq[j] = row16_sum(ssq[j]);
       }
       if ((lane & 15) == 0) {  // this wave's row only: no other wave writes it
 #pragma unroll

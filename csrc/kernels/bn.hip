@@ -431,25 +431,31 @@ struct BwdFin {
 };
 
 // Group reduction AND finalize in one launch (one dispatch per BatchNorm instead of two):
-// the blocks of chunk_group_reduce_kernel each write their group's sums, then count
-// themselves on a per-column-block ticket (agent-scope release); the block that arrives
-// last for its 64 channels (acquire) sums the G group rows in a FIXED order -- the same
-// result whichever block finishes last -- runs the finalize and re-arms the ticket.  No
-// block ever waits for another, so there is nothing to hang on.
+// block = 64 channels x 16 part-lanes (1024 threads); block (x, g) sums partial rows
+// [g * FIN_RPG, (g + 1) * FIN_RPG) of its 64 channels into group row g, then counts itself on a
+// per-column-block ticket (agent-scope release); the block that arrives last for its 64 channels
+// (acquire) sums the G group rows in a FIXED order -- the same result whichever block finishes
+// last -- runs the finalize and re-arms the ticket.  No block ever waits for another.  Groups
+// are 512 rows so the last block's pass is a single round of loads (G <= 49 at 25,088 rows).
+constexpr int FIN_PL = 16, FIN_RPG = 512;
+
 template <class FIN>
-__global__ void __launch_bounds__(256) group_finalize_kernel(const float* __restrict__ ws, int nchunks, long stride_k,
-                                                             long off_q, int C, float* __restrict__ gws,
-                                                             unsigned* __restrict__ tickets, const FIN F) {
-  __shared__ float ra[4][64], rb[4][64];
-  __shared__ double da[4][64], db[4][64];
+__global__ void __launch_bounds__(64 * FIN_PL) group_finalize_kernel(const float* __restrict__ ws, int nchunks,
+                                                                     long stride_k, long off_q, int C,
+                                                                     float* __restrict__ gws,
+                                                                     unsigned* __restrict__ tickets, const FIN F) {
+  __shared__ float ra[FIN_PL][64], rb[FIN_PL][64];
+  __shared__ double da[FIN_PL][64], db[FIN_PL][64];
   __shared__ int last;
   const int tid = threadIdx.x, cl = tid & 63, pl = tid >> 6;
   const int c = blockIdx.x * 64 + cl;
   const int G = gridDim.y, g = blockIdx.y;
   float a = 0.f, b = 0.f;
   if (c < C) {
-#pragma unroll 4
-    for (int k = g * 4 + pl; k < nchunks; k += G * 4) {
+    int k1 = (g + 1) * FIN_RPG;
+    if (k1 > nchunks) k1 = nchunks;
+#pragma unroll 8
+    for (int k = g * FIN_RPG + pl; k < k1; k += FIN_PL) {
       a += ws[(long)k * stride_k + c];
       b += ws[(long)k * stride_k + off_q + c];
     }
@@ -458,8 +464,14 @@ __global__ void __launch_bounds__(256) group_finalize_kernel(const float* __rest
   rb[pl][cl] = b;
   __syncthreads();
   if (pl == 0 && c < C) {  // wave 0 alone stores the group row, so its own release covers it
-    gws[(long)g * 2 * C + c] = (ra[0][cl] + ra[1][cl]) + (ra[2][cl] + ra[3][cl]);
-    gws[(long)g * 2 * C + C + c] = (rb[0][cl] + rb[1][cl]) + (rb[2][cl] + rb[3][cl]);
+    float ta = 0.f, tb = 0.f;
+#pragma unroll
+    for (int i = 0; i < FIN_PL; ++i) {
+      ta += ra[i][cl];
+      tb += rb[i][cl];
+    }
+    gws[(long)g * 2 * C + c] = ta;
+    gws[(long)g * 2 * C + C + c] = tb;
   }
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -476,7 +488,7 @@ __global__ void __launch_bounds__(256) group_finalize_kernel(const float* __rest
   __syncthreads();
   double sa = 0.0, sb = 0.0;
   if (c < C) {
-    for (int k = pl; k < G; k += 4) {
+    for (int k = pl; k < G; k += FIN_PL) {
       sa += gws[(long)k * 2 * C + c];
       sb += gws[(long)k * 2 * C + C + c];
     }
@@ -484,7 +496,15 @@ __global__ void __launch_bounds__(256) group_finalize_kernel(const float* __rest
   da[pl][cl] = sa;
   db[pl][cl] = sb;
   __syncthreads();
-  if (pl == 0 && c < C) F(c, (da[0][cl] + da[1][cl]) + (da[2][cl] + da[3][cl]), (db[0][cl] + db[1][cl]) + (db[2][cl] + db[3][cl]));
+  if (pl == 0 && c < C) {
+    double ta = 0.0, tb = 0.0;
+#pragma unroll
+    for (int i = 0; i < FIN_PL; ++i) {
+      ta += da[i][cl];
+      tb += db[i][cl];
+    }
+    F(c, ta, tb);
+  }
 }
 
 template <bool RELU, bool DRES>
@@ -565,14 +585,15 @@ template <class FIN, class FinKernel>
 int reduce_finalize(const float* ws, int nchunks, long stride_k, long off_q, int C, float* gws, const FIN& F,
                     FinKernel fin_kernel, hipStream_t s) {
   if (nchunks > 64 && gws) {
-    const int G = group_count(nchunks);
-    const dim3 grid(ca_cdiv(C, 64), G);
-    unsigned* tk = (merged_finalize() && (int)grid.x <= MAX_TICKETS) ? bn_tickets(s) : nullptr;
+    unsigned* tk = (merged_finalize() && ca_cdiv(C, 64) <= MAX_TICKETS) ? bn_tickets(s) : nullptr;
     if (tk) {
-      group_finalize_kernel<FIN><<<grid, 256, 0, s>>>(ws, nchunks, stride_k, off_q, C, gws, tk, F);
+      const dim3 g1(ca_cdiv(C, 64), ca_cdiv(nchunks, FIN_RPG));
+      group_finalize_kernel<FIN><<<g1, 64 * FIN_PL, 0, s>>>(ws, nchunks, stride_k, off_q, C, gws, tk, F);
       CA_LAUNCH_CHECK();
       return 0;
     }
+    const int G = group_count(nchunks);
+    const dim3 grid(ca_cdiv(C, 64), G);
     chunk_group_reduce_kernel<<<grid, 256, 0, s>>>(ws, nchunks, stride_k, off_q, C, gws);
     CA_LAUNCH_CHECK();
     fin_kernel<<<ca_cdiv(C, 4), 256, 0, s>>>(gws, G, 2L * C, (long)C, C, F);
