@@ -83,6 +83,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   mfma_gemm_glds<128, 128, 2, 2, GA, GB, EPI_BF16>(P);
 }
 
+// 96-column tiles for BERT's N = 768 shapes at M = 8192 (forward NT only: the N-contiguous
+// loaders need R / 8 to divide the thread count): 128 x 96 -> 512 tiles = 2 per CU exactly,
+// 256 x 96 -> 256 tiles = 1 per CU (the 128 x 128 core's 384 tiles leave half the CUs a second
+// round)
+template <template <int, int, int> class GA, template <int, int, int> class GB>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k128x96(CoreParams P) {
+  mfma_gemm_glds<128, 96, 2, 2, GA, GB, EPI_BF16>(P);
+}
+template <template <int, int, int> class GA, template <int, int, int> class GB>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k256x96(CoreParams P) {
+  mfma_gemm_glds<256, 96, 2, 2, GA, GB, EPI_BF16>(P);
+}
+static void launch128x96(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) k128x96<GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
+}
+static void launch256x96(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) k256x96<GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
+}
+
 struct Variant {
   const char* name;
   int bm, bn;
@@ -194,7 +213,9 @@ int main(int argc, char** argv) {
                     {"p8h2", 256, 256, launchp8<2>},
                     {"p8sk", 256, 256, launchp8sk},
                     {"w256x128", 256, 128, launch256x128},
-                    {"glds128", 128, 128, launch128}};
+                    {"glds128", 128, 128, launch128},
+                    {"g128x96", 128, 96, launch128x96},
+                    {"g256x96", 256, 96, launch256x96}};
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
   hipEvent_t e0, e1;
@@ -221,6 +242,7 @@ int main(int argc, char** argv) {
     CHECK(hipStreamSynchronize(s));
     for (const Variant& v : vars) {
       if (only && !strstr(only, v.name)) continue;
+      if ((v.launch == launch128x96 || v.launch == launch256x96) && L != 0) continue;
       CoreParams p{};
       p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.C = C; p.ldc = N;
       p.M = M; p.N = N; p.K = K; p.k_per_split = K; p.split_xcd = 1;

@@ -71,7 +71,9 @@ def test_backward_finalize_matches_fp64(C, tiles):
     torch.testing.assert_close(dg.double(), 1 + sdx, rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(db.double(), 1 + sd, rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(coefs[0][:C].double(), k1, rtol=1e-6, atol=1e-7)
-    torch.testing.assert_close(coefs[0][C:2 * C].double(), -k1 * (sdx / M) * rstd.double(), rtol=1e-4, atol=1e-9)
+    # B and D are differences of sums of +-10 partials (fp32 group sums): judged against their scale
+    B = -k1 * (sdx / M) * rstd.double()
+    torch.testing.assert_close(coefs[0][C:2 * C].double(), B, rtol=1e-4, atol=1e-4 * float(B.abs().max()))
     D = -k1 * (sd / M) + k1 * (sdx / M) * rstd.double() * mean.double()
-    torch.testing.assert_close(coefs[0][2 * C:].double(), D, rtol=1e-4, atol=1e-9)
+    torch.testing.assert_close(coefs[0][2 * C:].double(), D, rtol=1e-4, atol=1e-4 * float(D.abs().max()))
     assert all(torch.equal(c, coefs[0]) for c in coefs[1:])
