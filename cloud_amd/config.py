@@ -109,9 +109,10 @@ _VARS = [
     Var("CLOUD_AMD_BN_FIN_MERGED", bool, True, "BatchNorm statistics from many partial rows: group reduction and "
         "per-channel finalize in ONE launch (last block per 64 channels finalizes, agent-scope ticket); 0 = two "
         "launches (A/B runs)", "ops"),
-    Var("CLOUD_AMD_CONV_HALO", bool, True, "3x3 / stride-1 / 64-channel convolutions at width 56 (ResNet-50 "
+    Var("CLOUD_AMD_CONV_HALO", int, 1, "3x3 / stride-1 / 64-channel convolutions at width 56 (ResNet-50 "
         "stage 1) forward and input gradient on the LDS-resident kernel (ca_conv_halo.h: input patch and all 9 taps "
-        "in LDS, persistent grid); 0 = implicit-GEMM tiles (A/B runs)", "ops"),
+        "in LDS, persistent grid); 0 = implicit-GEMM tiles, 2 = halo kernel without the software-pipelined "
+        "fragment reads (A/B runs)", "ops"),
     Var("CLOUD_AMD_CONV_EPI_PF", bool, True, "implicit-GEMM forward convolutions with the BN-statistics epilogue: "
         "read 2 staged output rows from LDS before storing", "ops"),
     Var("CLOUD_AMD_SHAPE_LOG", str, None, "profiling: append one JSON line per GEMM/convolution launch (kind, M, N, "

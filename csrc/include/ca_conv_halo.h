@@ -65,7 +65,7 @@ __device__ __forceinline__ float row16_sum(float v) {
 __device__ __forceinline__ int halo_swz(int q, int chunk) { return q * 64 + ((chunk ^ ((q >> 1) & 7)) << 3); }
 
 // W = 56 only (8 x 56 = 448 = 7 x 64 pixels per tile); H % 8 == 0 (host-checked).
-template <bool STATS>
+template <bool STATS, bool PIPE = true>
 __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
   constexpr int C = HALO_C, TR = HALO_TR, NT = HALO_NT, W = 56, PW = W + 2, PR = TR + 2;
   constexpr int WIMG = 9 * C * C;      // shorts
@@ -152,26 +152,47 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
+    // 18 K steps (9 taps x 2 channel halves).  PIPE: the fragments of step s + 1 are read from
+    // LDS while the 16 MFMAs of step s run (two register sets, fully unrolled), so a wave does
+    // not wait out the LDS latency before every step.
+    auto frag_load = [&](int st, bf16x8 (&af)[4], bf16x8 (&bfr)[4]) {
+      const int tap = st >> 1, chunk = (st & 1) * 4 + kq;
       const int dq = (tap / 3) * PW + (tap % 3);
 #pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        const int chunk = kh * 4 + kq;
-        bf16x8 af[4], bfr[4];
+      for (int nf = 0; nf < 4; ++nf)
+        bfr[nf] = __builtin_bit_cast(
+            bf16x8, *reinterpret_cast<const s8v*>(wimg + halo_swz(tap * C + nf * 16 + (lane & 15), chunk)));
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf)
+        af[mf] = __builtin_bit_cast(
+            bf16x8, *reinterpret_cast<const s8v*>(pimg + chunk * (HALO_PLANE / 2) + (q0[mf] + dq) * 8));
+    };
+    auto mfma16 = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[4]) {
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf)
 #pragma unroll
         for (int nf = 0; nf < 4; ++nf)
-          bfr[nf] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s8v*>(
-                                                  wimg + halo_swz(tap * C + nf * 16 + (lane & 15), chunk)));
+          acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nf], af[mf], acc[mf][nf], 0, 0, 0);
+    };
+    if constexpr (PIPE) {
+      bf16x8 fa[2][4], fb[2][4];
+      frag_load(0, fa[0], fb[0]);
 #pragma unroll
-        for (int mf = 0; mf < 4; ++mf)
-          af[mf] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s8v*>(pimg + chunk * (HALO_PLANE / 2) +
-                                                                           (q0[mf] + dq) * 8));
+      for (int st = 0; st < 18; ++st) {
+        if (st + 1 < 18) frag_load(st + 1, fa[(st + 1) & 1], fb[(st + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);  // keep the next step's reads ahead of this step's MFMAs
+        mfma16(fa[st & 1], fb[st & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll 1
+      for (int tap = 0; tap < 9; ++tap) {
 #pragma unroll
-        for (int mf = 0; mf < 4; ++mf)
-#pragma unroll
-          for (int nf = 0; nf < 4; ++nf)
-            acc[mf][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nf], af[mf], acc[mf][nf], 0, 0, 0);
+        for (int kh = 0; kh < 2; ++kh) {
+          bf16x8 af[4], bfr[4];
+          frag_load(tap * 2 + kh, af, bfr);
+          mfma16(af, bfr);
+        }
       }
     }
 

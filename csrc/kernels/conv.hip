@@ -878,18 +878,24 @@ int launch_n64(const CoreParams& p0, hipStream_t s) {
 
 // 3x3 / s1 / p1 / 64-channel convolutions at width 56 (ResNet-50 stage-1 conv2, forward and
 // input gradient) on the LDS-resident patch + filter kernel (csrc/include/ca_conv_halo.h);
-// CLOUD_AMD_CONV_HALO=0 keeps them on the implicit-GEMM kernels (A/B runs).
-template <bool STATS>
+// CLOUD_AMD_CONV_HALO=0 keeps them on the implicit-GEMM kernels, =2 runs the halo kernel
+// without the software-pipelined fragment reads (A/B runs).
+template <bool STATS, bool PIPE>
 __global__ void __launch_bounds__(HALO_NT) conv3x3_halo_kernel(HaloParams P) {
-  conv3x3_halo<STATS>(P);
+  conv3x3_halo<STATS, PIPE>(P);
 }
 
-bool halo_shape(int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw) {
+int halo_mode() {
   static int en = -1;
   if (en < 0) {
     const char* e = getenv("CLOUD_AMD_CONV_HALO");
-    en = (e && e[0] == '0') ? 0 : 1;
+    en = !e ? 1 : (e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1));
   }
+  return en;
+}
+
+bool halo_shape(int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw) {
+  const int en = halo_mode();
   return en && KH == 3 && KW == 3 && sh == 1 && sw == 1 && ph == 1 && pw == 1 && Cin == HALO_C && Cout == HALO_C &&
          W == 56 && H % HALO_TR == 0 && use_glds();
 }
@@ -913,8 +919,11 @@ int halo_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   hp.x = x; hp.w = w; hp.y = y; hp.stats = stats; hp.bnz = bnz; hp.bnmask = bnmask;
   hp.N = Nb; hp.H = H; hp.W = W; hp.dgrad = dgrad;
   const int g = halo_grid(Nb, H);
-  if (stats) conv3x3_halo_kernel<true><<<g, HALO_NT, 0, s>>>(hp);
-  else conv3x3_halo_kernel<false><<<g, HALO_NT, 0, s>>>(hp);
+  const bool pipe = halo_mode() != 2;
+  if (stats && pipe) conv3x3_halo_kernel<true, true><<<g, HALO_NT, 0, s>>>(hp);
+  else if (stats) conv3x3_halo_kernel<true, false><<<g, HALO_NT, 0, s>>>(hp);
+  else if (pipe) conv3x3_halo_kernel<false, true><<<g, HALO_NT, 0, s>>>(hp);
+  else conv3x3_halo_kernel<false, false><<<g, HALO_NT, 0, s>>>(hp);
   CA_LAUNCH_CHECK();
   return 0;
 }

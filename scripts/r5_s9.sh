@@ -25,4 +25,11 @@ for f in gpurun_out/${tag}_rn_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f
 CLOUD_AMD_WGRAD_STREAM=0 $S 300 ${tag}_rprof.log rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_rprof -o run --output-format csv -- python bench.py --via-run 0 --steps 5 --warmup 3 || exit 1
 python3 scripts/step_kernels.py gpurun_out/${tag}_rprof sgd_kernel > gpurun_out/${tag}_rn_step_kernels.txt 2>&1 || true
 head -45 gpurun_out/${tag}_rn_step_kernels.txt
+GB_VARIANTS=glds128,g128x96,g256x96,p8h2 $S 200 ${tag}_gb.log bin/gemm_bench 20 8192,768,3072,0 8192,768,768,0 8192,2304,768,0 8192,3072,768,0 || exit 1
+grep -h '"variant"' gpurun_out/${tag}_gb.log | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); print('%-9s %5d %5d %5d L%d %8.1f us %7.1f TF bad=%d rel=%.2e' % (d['variant'],d['M'],d['N'],d['K'],d['layout'],d['us'],d['TF'],d['bad'],d['rel_l2']))"
+CLOUD_AMD_CONV_HALO=2 $S 120 ${tag}_cs2.log python bench/conv_shapes.py l1_c2 1024 || exit 1
+grep tag gpurun_out/${tag}_cs2.log
 echo SESSION_DONE
