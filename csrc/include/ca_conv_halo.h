@@ -65,7 +65,8 @@ __device__ __forceinline__ float row16_sum(float v) {
 __device__ __forceinline__ int halo_swz(int q, int chunk) { return q * 64 + ((chunk ^ ((q >> 1) & 7)) << 3); }
 
 // W = 56 only (8 x 56 = 448 = 7 x 64 pixels per tile); H % 8 == 0 (host-checked).
-template <bool STATS, bool PIPE = true>
+// STATS: 0 none, 1 forward statistics (sum, sum of squares), 2 input-gradient BN-backward statistics
+template <int STATS, bool PIPE = true>
 __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
   constexpr int C = HALO_C, TR = HALO_TR, NT = HALO_NT, W = 56, PW = W + 2, PR = TR + 2;
   constexpr int WIMG = 9 * C * C;      // shorts
@@ -74,7 +75,7 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
   constexpr int PCH = PR * W * 8;      // 16-B chunks of a patch's interior = 4480 = 10 per thread
   static_assert(PCH % NT == 0, "patch chunks must divide the threads");
   constexpr int PPT = PCH / NT;
-  constexpr int SRED = STATS ? HALO_WAVES * 2 * C * 2 : 0;  // shorts: per-wave [2][64] fp32 statistics
+  constexpr int SRED = STATS != 0 ? HALO_WAVES * 2 * C * 2 : 0;  // shorts: per-wave [2][64] fp32 statistics
   __shared__ __attribute__((aligned(16))) short smem[WIMG + PIMG + SRED];
   short* wimg = smem;
   short* pimg = smem + WIMG;
@@ -88,15 +89,17 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
   // filter image [tap][n][k]: fwd n = co, k = ci (W[co][tap][ci]); dgrad n = ci, k = co
   // (W[co][8 - tap][ci]).  Written once.
   for (int e = tid; e < 9 * C * 8; e += NT) {
-    const int tap = e / (C * 8), n = (e / 8) % C, ch = e % 8;
-    s8v v;
-    if (!P.dgrad) {
-      v = *reinterpret_cast<const s8v*>(P.w + ((long)n * 9 + tap) * C + ch * 8);
-    } else {
+    if (!P.dgrad) {  // e = (tap, co, ci chunk): one 16-B row piece per iteration
+      const int tap = e / (C * 8), n = (e / 8) % C, ch = e % 8;
+      *reinterpret_cast<s8v*>(wimg + halo_swz(tap * C + n, ch)) =
+          *reinterpret_cast<const s8v*>(P.w + ((long)n * 9 + tap) * C + ch * 8);
+    } else {  // e = (source tap, co, ci chunk): 8 consecutive ci of one co scatter to 8 image rows
+      const int tp = e / (C * 8), co = (e / 8) % C, cc = e % 8;
+      const s8v v = *reinterpret_cast<const s8v*>(P.w + ((long)co * 9 + tp) * C + cc * 8);
+      const int tap = 8 - tp;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (short)P.w[((long)(ch * 8 + j) * 9 + (8 - tap)) * C + n];
+      for (int j = 0; j < 8; ++j) wimg[halo_swz(tap * C + cc * 8 + j, co >> 3) + (co & 7)] = v[j];
     }
-    *reinterpret_cast<s8v*>(wimg + halo_swz(tap * C + n, ch)) = v;
   }
   // the patch's left / right zero columns never change
   for (int e = tid; e < PR * 2 * 8; e += NT) {
@@ -204,44 +207,51 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
     for (int j = 0; j < 16; ++j) ssum[j] = ssq[j] = 0.f;
     const int n = t / rgroups, r0 = (t % rgroups) * TR;
     const long tile_pix = ((long)n * H + r0) * W;  // first pixel of the tile (rows are whole)
+    const long pix0 = tile_pix + wave * 64 + (lane & 15);  // pixel of fragment 0; fragment mf: + 16 mf
+    // dgrad statistics: every z / mask load of the tile is issued before the first use (one
+    // memory latency per tile; the fragment registers are dead here)
+    us4 zv[4][4];
+    uint32_t mv[4][2];
+    if constexpr (STATS == 2) {
+#pragma unroll
+      for (int mf = 0; mf < 4; ++mf) {
+        const long pix = pix0 + mf * 16;
+        if (P.bnmask) {
+          const uint2 m = *reinterpret_cast<const uint2*>(P.bnmask + pix * 8);
+          mv[mf][0] = m.x;
+          mv[mf][1] = m.y;
+        } else {
+          mv[mf][0] = mv[mf][1] = 0xffffffffu;
+        }
+#pragma unroll
+        for (int nf = 0; nf < 4; ++nf) zv[mf][nf] = *reinterpret_cast<const us4*>(P.bnz + pix * C + 4 * kq + nf * 16);
+      }
+    }
 #pragma unroll
     for (int mf = 0; mf < 4; ++mf) {
-      const int p = wave * 64 + mf * 16 + (lane & 15);
-      const long pix = tile_pix + p;
-      bf16_t* yp = P.y + pix * C + 4 * kq;
-      uint32_t mk = 0xffffffffu;
-      if (STATS && P.dgrad) {
-        // the 16 channels of this lane (4 groups of 4 at nf * 16 + 4 * kq) span bytes nf*2 + kq/2
-        mk = 0xffffu;
-        if (P.bnmask) {
-          const uint8_t* mp = P.bnmask + pix * 8 + (kq >> 1);
-          mk = 0;
-#pragma unroll
-          for (int nf = 0; nf < 4; ++nf) mk |= (((uint32_t)mp[nf * 2] >> ((kq & 1) * 4)) & 0xfu) << (nf * 4);
-        }
-      }
+      bf16_t* yp = P.y + (pix0 + mf * 16) * C + 4 * kq;
 #pragma unroll
       for (int nf = 0; nf < 4; ++nf) {
         us4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = f2bf(acc[mf][nf][r]);
         *reinterpret_cast<us4*>(yp + nf * 16) = o;
-        if constexpr (STATS) {
-          if (!P.dgrad) {
+        if constexpr (STATS == 1) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float a = bf2f(o[r]);
-              ssum[nf * 4 + r] += a;
-              ssq[nf * 4 + r] += a * a;
-            }
-          } else {
-            const us4 z = *reinterpret_cast<const us4*>(P.bnz + (yp - P.y) + nf * 16);
+          for (int r = 0; r < 4; ++r) {
+            const float a = bf2f(o[r]);
+            ssum[nf * 4 + r] += a;
+            ssq[nf * 4 + r] += a * a;
+          }
+        } else if constexpr (STATS == 2) {
+          // channels nf*16 + 4*kq + r: mask byte nf*2 + kq/2, nibble kq&1
+          const uint32_t byte = (mv[mf][nf >> 1] >> (((nf & 1) * 2 + (kq >> 1)) * 8)) & 0xffu;
+          const uint32_t nib = (byte >> ((kq & 1) * 4)) & 0xfu;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float g = ((mk >> (nf * 4 + r)) & 1u) ? bf2f(o[r]) : 0.f;
-              ssum[nf * 4 + r] += g;
-              ssq[nf * 4 + r] += g * bf2f(z[r]);
-            }
+          for (int r = 0; r < 4; ++r) {
+            const float g = ((nib >> r) & 1u) ? bf2f(o[r]) : 0.f;
+            ssum[nf * 4 + r] += g;
+            ssq[nf * 4 + r] += g * bf2f(zv[mf][nf][r]);
           }
         }
       }

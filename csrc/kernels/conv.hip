@@ -880,7 +880,7 @@ int launch_n64(const CoreParams& p0, hipStream_t s) {
 // input gradient) on the LDS-resident patch + filter kernel (csrc/include/ca_conv_halo.h);
 // CLOUD_AMD_CONV_HALO=0 keeps them on the implicit-GEMM kernels, =2 runs the halo kernel
 // without the software-pipelined fragment reads (A/B runs).
-template <bool STATS, bool PIPE>
+template <int STATS, bool PIPE>
 __global__ void __launch_bounds__(HALO_NT) conv3x3_halo_kernel(HaloParams P) {
   conv3x3_halo<STATS, PIPE>(P);
 }
@@ -920,10 +920,16 @@ int halo_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   hp.N = Nb; hp.H = H; hp.W = W; hp.dgrad = dgrad;
   const int g = halo_grid(Nb, H);
   const bool pipe = halo_mode() != 2;
-  if (stats && pipe) conv3x3_halo_kernel<true, true><<<g, HALO_NT, 0, s>>>(hp);
-  else if (stats) conv3x3_halo_kernel<true, false><<<g, HALO_NT, 0, s>>>(hp);
-  else if (pipe) conv3x3_halo_kernel<false, true><<<g, HALO_NT, 0, s>>>(hp);
-  else conv3x3_halo_kernel<false, false><<<g, HALO_NT, 0, s>>>(hp);
+  const int mode = stats ? (dgrad ? 2 : 1) : 0;
+  if (pipe) {
+    if (mode == 2) conv3x3_halo_kernel<2, true><<<g, HALO_NT, 0, s>>>(hp);
+    else if (mode == 1) conv3x3_halo_kernel<1, true><<<g, HALO_NT, 0, s>>>(hp);
+    else conv3x3_halo_kernel<0, true><<<g, HALO_NT, 0, s>>>(hp);
+  } else {
+    if (mode == 2) conv3x3_halo_kernel<2, false><<<g, HALO_NT, 0, s>>>(hp);
+    else if (mode == 1) conv3x3_halo_kernel<1, false><<<g, HALO_NT, 0, s>>>(hp);
+    else conv3x3_halo_kernel<0, false><<<g, HALO_NT, 0, s>>>(hp);
+  }
   CA_LAUNCH_CHECK();
   return 0;
 }
