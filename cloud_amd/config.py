@@ -102,6 +102,8 @@ _VARS = [
         "forward 1x1 convs, BERT bias/GELU/GELU'/beta dense layers): 4 staged output rows in flight per trip", "ops"),
     Var("CLOUD_AMD_ATTN_FUSED_BWD", bool, True, "attention at S = 64 / 128: one workgroup per (batch, head) for "
         "the forward and a single fused backward kernel; 0 keeps the 64-query-block kernels", "ops"),
+    Var("CLOUD_AMD_GEMM_256X96", bool, True, "forward GEMMs whose 256 x 96 grid fills whole rounds while the 128 x "
+        "128 grid leaves a partial one (BERT QKV, M = 8192, N = 2304) run on 256 x 96 tiles; 0 = off (A/B)", "ops"),
     Var("CLOUD_AMD_GEMM_STREAMK", int, 0, "two-phase 256 x 256 GEMM: 0 off (default; measured slower than the "
         "128 x 128 core on BERT's M = 8192 shapes), 1 stream-K on under-filled grids, 2 wherever allowed (tests)", "ops"),
     Var("CLOUD_AMD_LN_BWD8", bool, False, "retired round-5 A/B knob (8-wave LayerNorm backward, measured 1.5 % slower "

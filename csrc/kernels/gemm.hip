@@ -46,6 +46,14 @@ bool epi_pf() {
   return v != 0;
 }
 
+// 256 x 96 tiles for forward GEMMs whose 128 x 128 grid ends in a partial round while the
+// 256 x 96 grid fills whole rounds (BERT's QKV projection, M = 8192, N = 2304: 1,152 tiles =
+// 4.5 rounds vs 768 = 3; 41.9 -> 36.8 us, profiles/r5_s9/r5s9_gb.log)
+template <int EPI>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) dense_gemm_256x96_kernel(CoreParams P) {
+  mfma_gemm_glds<256, 96, 2, 2, GDenseKC, GDenseKC, EPI>(P);
+}
+
 // 8 waves (2 x 4, wave tile 64 x BN/4) with a double-buffered LDS-DMA pipeline:
 // same 16 waves/CU occupancy as the 4-wave single-stage kernel, but the next K
 // tile's DMA overlaps this tile's MFMAs (CLOUD_AMD_GEMM_CORE=glds8).
@@ -286,6 +294,21 @@ static double tile_balance(long tiles) {
   return (double)tiles / (double)(rounds * cus);
 }
 
+// 256 x 96 instead of 128 x 128 (forward, both operands K-contiguous, no split): only when the
+// 96-wide grid is >= 2 whole rounds and the 128 grid leaves a partial one.  Measured on the
+// BERT shapes: QKV (N = 2304) wins; N = 768 (one round of 256 x 96) and N = 3072 (whole
+// 128 rounds) lose (profiles/r5_s9/r5s9_gb.log).  CLOUD_AMD_GEMM_256X96=0 turns it off.
+static bool use_256x96(const CoreParams& p, int splits) {
+  static int en = -1;
+  if (en < 0) {
+    const char* e = getenv("CLOUD_AMD_GEMM_256X96");
+    en = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!en || splits != 1 || p.N % 96 || p.M < 4096) return false;
+  const long t96 = ((p.M + 255) / 256) * (p.N / 96), t128 = ((p.M + 127) / 128) * ((p.N + 127) / 128);
+  return t96 >= 512 && tile_balance(t96) >= 0.999 && tile_balance(t128) < 0.95;
+}
+
 // The 256 core pays when its grid fills the chip in (nearly) whole rounds and every block
 // has enough K tiles to amortise its 3-tile prologue and its 128-KB epilogue: >= 2 rounds
 // at >= 85 % slot use, or exactly whole rounds, and >= 16 K tiles of 32 per block.  (BERT's
@@ -441,6 +464,14 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
         return -2;
       CA_LAUNCH_CHECK();
       return 0;
+    }
+    if constexpr (EPI == EPI_BF16 && GA<BM, 1, 256>::KC && GB<BN, 1, 256>::KC) {
+      if (use_glds() && use_256x96(p, splits)) {
+        const int t = ((p.M + 255) / 256) * (p.N / 96);
+        dense_gemm_256x96_kernel<EPI><<<dim3(t, 1, 1), 256, 0, s>>>(p);
+        CA_LAUNCH_CHECK();
+        return 0;
+      }
     }
     if (use_256x128(p, splits)) {
       const int t = ((p.M + 255) / 256) * ((p.N + 127) / 128);

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 S=scripts/gpu_step.sh
 tag=${1:-r5s10}
 PT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
-$S 300 ${tag}_t.log $PT tests/test_conv_halo_gpu.py tests/test_bn_finalize_gpu.py tests/test_bn_fold_gpu.py || exit 1
+$S 300 ${tag}_t.log $PT tests/test_conv_halo_gpu.py tests/test_bn_finalize_gpu.py tests/test_bn_fold_gpu.py tests/test_gemm_256x96_gpu.py tests/test_gemm_streamk_gpu.py || exit 1
 grep -q "FAILED\|Error" gpurun_out/${tag}_t.log && { echo T_FAILED; tail -30 gpurun_out/${tag}_t.log; exit 1; }
 grep -E "passed|failed" gpurun_out/${tag}_t.log
 $S 120 ${tag}_cs.log python bench/conv_shapes.py l1_c2 1024 || exit 1
@@ -21,4 +21,9 @@ CLOUD_AMD_WGRAD_STREAM=0 $S 300 ${tag}_rprof.log rocprofv3 --kernel-trace --stat
 python3 scripts/step_kernels.py gpurun_out/${tag}_rprof sgd_kernel > gpurun_out/${tag}_rn_step_kernels.txt 2>&1 || true
 head -16 gpurun_out/${tag}_rn_step_kernels.txt
 grep halo gpurun_out/${tag}_rn_step_kernels.txt | head -8
+for r in 1 2; do
+$S 200 ${tag}_bert_q1_$r.log python bench/bert_base_synth.py --steps 20 --warmup 5 || exit 1
+CLOUD_AMD_GEMM_256X96=0 $S 200 ${tag}_bert_q0_$r.log python bench/bert_base_synth.py --steps 20 --warmup 5 || exit 1
+done
+for f in gpurun_out/${tag}_bert_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f | tail -1)"; done
 echo SESSION_DONE
