@@ -423,8 +423,12 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
     // the calling core's LDS (SMEM_SHORTS bf16 slots) must hold the three statistics rows
     static_assert(!Z2 || 3 * (NT / (BN / 8)) * BN * 4 <= 2 * SMEM_SHORTS, "three statistics rows must fit the LDS");
     constexpr int PF = BNS ? (IT < 2 ? IT : 2) : (IT < EPF ? IT : EPF);
-    const int col = (tid % (BN / 8)) * 8;
-    const int gn = n0 + col;
+    // FIXCOL: NT is a multiple of BN / 8, so a thread keeps one 8-column group for every row it
+    // walks (the statistics epilogues need that); otherwise (BN = 96 on 256 threads, plain
+    // epilogues only) the column group follows the chunk index
+    constexpr bool FIXCOL = NT % (BN / 8) == 0;
+    static_assert(FIXCOL || (!RSTAT && EPI == EPI_BF16), "column groups must divide the threads");
+    const int col0 = (tid % (BN / 8)) * 8;
     const bool has_beta = P.beta != 0.f;
 #pragma unroll 1
     for (int it0 = 0; it0 < IT; it0 += PF) {
@@ -435,6 +439,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
 #pragma unroll
       for (int u = 0; u < PF; ++u) {
         const int gm = m0 + (tid + (it0 + u) * NT) / (BN / 8);
+        const int gn = n0 + (FIXCOL ? col0 : ((tid + (it0 + u) * NT) % (BN / 8)) * 8);
         okr[u] = gm < P.M && gn < P.N;
         orow[u] = okr[u] ? out_row(P, gm) : 0;
         const bf16_t* bsrc = (RES && P.res_src) ? P.res_src : Cg;
@@ -457,6 +462,8 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
       for (int u = 0; u < PF; ++u) {
         if (!okr[u]) continue;
         const int row = (tid + (it0 + u) * NT) / (BN / 8);
+        const int col = FIXCOL ? col0 : ((tid + (it0 + u) * NT) % (BN / 8)) * 8;
+        const int gn = n0 + col;
         const int gm = m0 + row;
         s8v v = *reinterpret_cast<const s8v*>(Cs + EL::idx(row, col));
         bf16_t* dst = Cg + orow[u] * P.ldc + gn;
@@ -543,7 +550,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
           }
         }
       }
-    } else if (P.stats) {
+    } else if (FIXCOL && NT % BN == 0 && P.stats) {  // (host: never set for other tiles)
       // per-column sum / sum of squares of the stored bf16 values of this tile
       constexpr int TPC = NT / BN;
       const int col = tid % BN, part = tid / BN;

@@ -304,7 +304,7 @@ static bool use_256x96(const CoreParams& p, int splits) {
     const char* e = getenv("CLOUD_AMD_GEMM_256X96");
     en = (e && e[0] == '0') ? 0 : 1;
   }
-  if (!en || splits != 1 || p.N % 96 || p.M < 4096) return false;
+  if (!en || splits != 1 || p.N % 96 || p.M < 4096 || p.stats) return false;
   const long t96 = ((p.M + 255) / 256) * (p.N / 96), t128 = ((p.M + 127) / 128) * ((p.N + 127) / 128);
   return t96 >= 512 && tile_balance(t96) >= 0.999 && tile_balance(t128) < 0.95;
 }

@@ -42,13 +42,15 @@ __global__ void init_uniform(bf16_t* p, long n, uint32_t seed) {
   }
 }
 
-// reference: C[m][n] = sum_k A(m,k) B(k,n) in fp32, rows m = r * row_step only
+// reference: C[m][n] = sum_k A(m,k) B(k,n) in fp32, rows m = r * row_step + r % row_step only
+// (every residue of the row index within a 16-row MFMA fragment is sampled)
 __global__ void ref_gemm(const bf16_t* A, long lda, const bf16_t* B, long ldb, int layout, float* C, int M, int N, int K,
                          int row_step, int rows) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   const int r = blockIdx.y;
   if (n >= N || r >= rows) return;
-  const int m = r * row_step;
+  int m = r * row_step + r % row_step;
+  if (m >= M) m = M - 1;
   float s = 0.f;
   for (int k = 0; k < K; ++k) {
     const float a = layout == 2 ? bf2f(A[(long)k * lda + m]) : bf2f(A[(long)m * lda + k]);
@@ -254,7 +256,7 @@ int main(int argc, char** argv) {
       CHECK(hipStreamSynchronize(s));
       std::vector<bf16_t> out((long)rows * N);
       for (int r = 0; r < rows; ++r)
-        CHECK(hipMemcpy(out.data() + (long)r * N, C + (long)r * row_step * N, (long)N * 2, hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(out.data() + (long)r * N, C + std::min((long)r * row_step + r % row_step, (long)M - 1) * N, (long)N * 2, hipMemcpyDeviceToHost));
       double num = 0, den = 0, maxe = 0;
       long bad = 0;
       for (long i = 0; i < (long)rows * N; ++i) {

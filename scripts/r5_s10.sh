@@ -10,6 +10,8 @@ PT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
 $S 300 ${tag}_t.log $PT tests/test_conv_halo_gpu.py tests/test_bn_finalize_gpu.py tests/test_bn_fold_gpu.py tests/test_gemm_256x96_gpu.py tests/test_gemm_streamk_gpu.py || exit 1
 grep -q "FAILED\|Error" gpurun_out/${tag}_t.log && { echo T_FAILED; tail -30 gpurun_out/${tag}_t.log; exit 1; }
 grep -E "passed|failed" gpurun_out/${tag}_t.log
+GB_VARIANTS=glds128,g128x96,g256x96 $S 120 ${tag}_gb.log bin/gemm_bench 10 8192,2304,768,0 8192,768,3072,0 || exit 1
+grep -h '"variant"' gpurun_out/${tag}_gb.log | cut -c1-160
 $S 120 ${tag}_cs.log python bench/conv_shapes.py l1_c2 1024 || exit 1
 grep tag gpurun_out/${tag}_cs.log
 for r in 1 2; do
