@@ -192,6 +192,8 @@ def conv_wgrad(dy, x, w_shape, stride, padding, out, beta=1.0, blocks=None):
     # slabs stay small next to the pixel operands, and more splits fill the CUs
     target = blocks or (_WGRAD_BLOCKS_SMALLM if Cout <= 128 else _WGRAD_BLOCKS)
     splits = ext.gemm_splitk_effective(kred, wgrad_splits(Cout, ncols, kred, target_blocks=target))
+    if not (KH == 1 and KW == 1):  # the kernel that will run decides (one slab per workgroup on the halo kernel)
+        splits = ext.conv_wgrad_splits(N, H, W, Cin, Cout, KH, KW, stride, stride, padding, padding, splits)
     ws = torch.empty(splits * Cout * ncols, dtype=torch.float32, device=x.device)
     obf = int(out.dtype == torch.bfloat16)
     if KH == 1 and KW == 1 and stride == 1 and padding == 0:

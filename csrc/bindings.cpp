@@ -36,6 +36,7 @@ int ca_gemm_bf16_bnstats(int, const bf16_t*, long, const bf16_t*, long, bf16_t*,
 long ca_conv_dgrad_stat_tiles(int, int, int, int, int);
 long ca_conv_dgrad_stat_rows(int, int, int, int, int, int, int, int, int, int, int, float);
 long ca_conv_stat_rows(int, int, int, int, int, int, int, int, int, int, int);
+int ca_conv_wgrad_splits(int, int, int, int, int, int, int, int, int, int, int, int);
 int ca_bn_fwd_partials_ex(const bf16_t*, const bf16_t*, const float*, bf16_t*, long, int, const float*, int,
                           const float*, const float*, float, float, float*, float*, float*, float*, float*, int,
                           uint8_t*, float*, hipStream_t);
@@ -250,6 +251,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("conv_stat_rows", [](int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph,
                              int pw) { return ca_conv_stat_rows(Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw); });
+  m.def("conv_wgrad_splits", [](int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph,
+                                int pw, int fallback) {
+    return ca_conv_wgrad_splits(Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw, fallback);
+  });
   m.def("conv_dgrad_bnstats", [](u64 dy, u64 w, u64 dx, int Nb, int H, int W, int Cin, int Cout, int KH, int KW,
                                  int sh, int sw, int ph, int pw, float beta, u64 z, u64 mask, u64 stats, u64 s) {
     check(ca_conv_dgrad_bnstats(P(const bf16_t*, dy), P(const bf16_t*, w), P(bf16_t*, dx), Nb, H, W, Cin, Cout, KH, KW,

@@ -155,6 +155,31 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+    const int n = t / rgroups, r0 = (t % rgroups) * TR;
+    const long tile_pix = ((long)n * H + r0) * W;  // first pixel of the tile (rows are whole)
+    const long pix0 = tile_pix + wave * 64 + (lane & 15);  // pixel of fragment 0; fragment mf: + 16 mf
+    // dgrad statistics: the tile's z / mask loads are issued halfway through its MFMAs (PIPE)
+    // or at the start of the epilogue, all before the first use
+    us4 zv[4][4];
+    uint32_t mv[4][2];
+    auto load_bn = [&]() {
+      if constexpr (STATS == 2) {
+#pragma unroll
+        for (int mf = 0; mf < 4; ++mf) {
+          const long pix = pix0 + mf * 16;
+          if (P.bnmask) {
+            const uint2 m = *reinterpret_cast<const uint2*>(P.bnmask + pix * 8);
+            mv[mf][0] = m.x;
+            mv[mf][1] = m.y;
+          } else {
+            mv[mf][0] = mv[mf][1] = 0xffffffffu;
+          }
+#pragma unroll
+          for (int nf = 0; nf < 4; ++nf)
+            zv[mf][nf] = *reinterpret_cast<const us4*>(P.bnz + pix * C + 4 * kq + nf * 16);
+        }
+      }
+    };
     // 18 K steps (9 taps x 2 channel halves).  PIPE: the fragments of step s + 1 are read from
     // LDS while the 16 MFMAs of step s run (two register sets, fully unrolled), so a wave does
     // not wait out the LDS latency before every step.
@@ -183,6 +208,7 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
 #pragma unroll
       for (int st = 0; st < 18; ++st) {
         if (st + 1 < 18) frag_load(st + 1, fa[(st + 1) & 1], fb[(st + 1) & 1]);
+        if (st == 8) load_bn();
         __builtin_amdgcn_sched_barrier(0);  // keep the next step's reads ahead of this step's MFMAs
         mfma16(fa[st & 1], fb[st & 1]);
         __builtin_amdgcn_sched_barrier(0);
@@ -197,6 +223,7 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
           mfma16(af, bfr);
         }
       }
+      load_bn();
     }
 
     // epilogue: lane holds pixel (mf*16 + lane&15), channels nf*16 + 4*kq + r.  The tile's
@@ -205,28 +232,6 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
     float ssum[16], ssq[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) ssum[j] = ssq[j] = 0.f;
-    const int n = t / rgroups, r0 = (t % rgroups) * TR;
-    const long tile_pix = ((long)n * H + r0) * W;  // first pixel of the tile (rows are whole)
-    const long pix0 = tile_pix + wave * 64 + (lane & 15);  // pixel of fragment 0; fragment mf: + 16 mf
-    // dgrad statistics: every z / mask load of the tile is issued before the first use (one
-    // memory latency per tile; the fragment registers are dead here)
-    us4 zv[4][4];
-    uint32_t mv[4][2];
-    if constexpr (STATS == 2) {
-#pragma unroll
-      for (int mf = 0; mf < 4; ++mf) {
-        const long pix = pix0 + mf * 16;
-        if (P.bnmask) {
-          const uint2 m = *reinterpret_cast<const uint2*>(P.bnmask + pix * 8);
-          mv[mf][0] = m.x;
-          mv[mf][1] = m.y;
-        } else {
-          mv[mf][0] = mv[mf][1] = 0xffffffffu;
-        }
-#pragma unroll
-        for (int nf = 0; nf < 4; ++nf) zv[mf][nf] = *reinterpret_cast<const us4*>(P.bnz + pix * C + 4 * kq + nf * 16);
-      }
-    }
 #pragma unroll
     for (int mf = 0; mf < 4; ++mf) {
       bf16_t* yp = P.y + (pix0 + mf * 16) * C + 4 * kq;
@@ -285,6 +290,144 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
       P.stats[((long)blockIdx.x * 2 + k) * C + c] = a;
     }
   }
+}
+
+}  // namespace ca
+
+namespace ca {
+
+// ------------------------------------------------------------------ weight gradient --
+// dW[co][tap][ci] = sum over pixels p of dY[p][co] * X[p + tap][ci] for the same convolutions
+// (3x3 / s1 / p1, 64 -> 64 channels, W = 56).  The implicit-GEMM weight gradient gathers the
+// shifted input nine times per pixel tile and runs 64-row tiles of a 64 x 576 output split
+// thousands of ways (ResNet-50 stage 1, batch 1024: 406 TF/s).  Here a persistent workgroup
+// (8 waves, one per CU) keeps the WHOLE 64 x 576 partial sum in registers across all its
+// tiles (wave w: output rows 32 (w & 1) .. + 32, columns 144 (w >> 1) .. + 144 = 2 x 9
+// fragments) and per tile of 8 image rows stages
+//   * the output gradient tile, [448 pixels][64 channels], and
+//   * the input patch, [10 x 58 positions][64 channels] with zero borders,
+// once in LDS; K = pixels.  Both operands are read with the transposing LDS read
+// (ds_read_b64_tr_b16, the GDenseNC layout of ca_mfma_core.h) -- a B fragment of tap (dr, dc)
+// is the patch read at the pixel rows shifted by dr * 58 + dc: every group of 8 pixels a lane
+// reads lies in one image row (56 = 7 x 8), so its 8 patch rows are consecutive.  Each
+// workgroup writes ONE fp32 [64][576] partial; the split-K reduce sums them.
+struct HaloWgParams {
+  const bf16_t* x;   // input [N][H][W][64]
+  const bf16_t* dy;  // output gradient [N][H][W][64]
+  float* ws;         // [gridDim.x][64][576] fp32 partials
+  int N, H, W;
+};
+
+constexpr int HWG_WAVES = 8, HWG_NT = HWG_WAVES * 64;
+
+// NC-layout fragment (ca_mfma_core.h read_frag_sw<R, false>) whose K rows are given per lane:
+// krow = the LDS row holding k = 8 * (lane >> 4), the lane's group of 8 consecutive K rows
+__device__ __forceinline__ bf16x8 read_frag_nc_rows(const short* lds, int r0, int krow, int lane) {
+  constexpr int R = 64;
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  const int k = krow + q;
+  const int lc = (r0 >> 3) + (p >> 1);
+  const int sub = 4 * (p & 1);
+  const short* b0 = lds + k * R + ((lc ^ nc_swz<R>(k)) << 3) + sub;
+  const short* b1 = lds + (k + 4) * R + ((lc ^ nc_swz<R>(k + 4)) << 3) + sub;
+  s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b0));
+  s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(b1));
+  s8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ void conv3x3_halo_wgrad(const HaloWgParams& P) {
+  constexpr int C = HALO_C, TR = HALO_TR, NT = HWG_NT, W = 56, PW = W + 2, PR = TR + 2;
+  constexpr int TP = TR * W;              // 448 pixels per tile
+  constexpr int DCH = TP * 8 / NT;        // 7 output-gradient chunks per thread
+  constexpr int PCH = PR * W * 8;         // 4480 patch interior chunks
+  constexpr int PPT = (PCH + NT - 1) / NT;  // 9 (the last one partial)
+  static_assert(TP * 8 % NT == 0, "tile chunks");
+  __shared__ __attribute__((aligned(16))) short smem[TP * C + PR * PW * C];
+  short* dimg = smem;
+  short* pimg = smem + TP * C;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = P.H, rgroups = H / TR, ntiles = P.N * rgroups;
+  const int cfb = (wave & 1) * 2, nfb = (wave >> 1) * 9;
+
+  for (int e = tid; e < PR * 2 * 8; e += NT) {  // zero pad columns, once
+    const int r = e / 16, side = (e / 8) & 1, ch = e % 8;
+    const int q = r * PW + (side ? PW - 1 : 0);
+    *reinterpret_cast<s8v*>(pimg + q * C + ((ch ^ nc_swz<64>(q)) << 3)) = zero8();
+  }
+
+  s8v dv[DCH], pv[PPT];
+  auto load = [&](int t) {
+    const int n = t / rgroups, r0 = (t % rgroups) * TR;
+    const bf16_t* dsrc = P.dy + ((long)n * H + r0) * W * C;
+#pragma unroll
+    for (int i = 0; i < DCH; ++i) dv[i] = *reinterpret_cast<const s8v*>(dsrc + (long)(tid + i * NT) * 8);
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int e = tid + i * NT;
+      const int pr = e / (W * 8), pc = (e / 8) % W, ch = e % 8;
+      const int ir = r0 - 1 + pr;
+      pv[i] = (e < PCH && ir >= 0 && ir < H)
+                  ? *reinterpret_cast<const s8v*>(P.x + (((long)n * H + ir) * W + pc) * C + ch * 8)
+                  : zero8();
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < DCH; ++i) {
+      const int e = tid + i * NT, px = e >> 3, ch = e & 7;
+      *reinterpret_cast<s8v*>(dimg + px * C + ((ch ^ nc_swz<64>(px)) << 3)) = dv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int e = tid + i * NT;
+      if (e < PCH) {
+        const int pr = e / (W * 8), pc = (e / 8) % W, ch = e % 8;
+        const int q = pr * PW + pc + 1;
+        *reinterpret_cast<s8v*>(pimg + q * C + ((ch ^ nc_swz<64>(q)) << 3)) = pv[i];
+      }
+    }
+  };
+
+  f4v acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  int t = blockIdx.x;
+  if (t < ntiles) load(t);
+  for (; t < ntiles; t += gridDim.x) {
+    __syncthreads();  // previous tile's reads retired
+    store();
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) load(t + gridDim.x);  // in flight during the MFMAs
+#pragma unroll 1
+    for (int ks = 0; ks < TP / 32; ++ks) {
+      const int p0 = ks * 32;
+      const int pg = p0 + 8 * (lane >> 4);  // this lane's group of 8 pixels (one image row)
+      const int prow = pg / W, pcol = pg % W;
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = read_frag_sw<64, false>(dimg, (cfb + i) * 16, p0, lane);
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const int nf = nfb + j, tap = nf >> 2, cif = nf & 3;
+        const int krow = (prow + tap / 3) * PW + pcol + tap % 3;
+        const bf16x8 bf = read_frag_nc_rows(pimg, cif * 16, krow, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf, af[i], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  // lane holds dW[co = (cfb + i) * 16 + (lane & 15)][n = (nfb + j) * 16 + 4 * (lane >> 4) + r]
+  float* dst = P.ws + (long)blockIdx.x * C * 576;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+      *reinterpret_cast<f4v*>(dst + ((cfb + i) * 16 + (lane & 15)) * 576 + (nfb + j) * 16 + 4 * (lane >> 4)) = acc[i][j];
 }
 
 }  // namespace ca

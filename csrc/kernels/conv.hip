@@ -913,6 +913,18 @@ int halo_grid(int Nb, int H) {
   return (int)(tiles < cus ? tiles : cus);
 }
 
+__global__ void __launch_bounds__(HWG_NT) conv3x3_halo_wgrad_kernel(HaloWgParams P) { conv3x3_halo_wgrad(P); }
+
+// weight gradient on the halo kernel: CLOUD_AMD_CONV_HALO_WGRAD=0 keeps the implicit GEMM
+bool halo_wgrad_on() {
+  static int en = -1;
+  if (en < 0) {
+    const char* e = getenv("CLOUD_AMD_CONV_HALO_WGRAD");
+    en = (e && e[0] == '0') ? 0 : 1;
+  }
+  return en != 0;
+}
+
 int halo_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int W, float* stats, const bf16_t* bnz,
                 const uint8_t* bnmask, int dgrad, hipStream_t s) {
   HaloParams hp{};
@@ -1134,6 +1146,13 @@ int ca_conv_dgrad_bnstats(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb,
 int ca_conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, float beta, int Nb, int H, int W,
                   int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw, int splits, float* ws,
                   hipStream_t s) {
+  if (halo_shape(H, W, Cin, Cout, KH, KW, sh, sw, ph, pw) && halo_wgrad_on() && splits == halo_grid(Nb, H)) {
+    // one fp32 [64][576] partial per persistent workgroup (ca_conv_wgrad_splits sized ws)
+    HaloWgParams hp{x, dy, ws, Nb, H, W};
+    conv3x3_halo_wgrad_kernel<<<splits, HWG_NT, 0, s>>>(hp);
+    CA_LAUNCH_CHECK();
+    return ca_splitk_reduce(ws, splits, (long)Cout * KH * KW * Cin, dw, dw_bf16, beta, s);
+  }
   CoreParams p = conv_params(Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw);
   if (!geom_ok(Cin, Cout, (long)Nb * H * W)) return -1;
   p.A = dy; p.lda = Cout; p.B = x;
@@ -1172,6 +1191,14 @@ int ca_conv_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, int dw_bf16, floa
                      : launch<128, 128, DenseNC, ConvWgradB, GDenseNC, GConvWgradB, EPI_F32_PARTIAL>(p, splits, s);
   if (rc) return rc;
   return ca_splitk_reduce(ws, splits, (long)p.M * p.N, dw, dw_bf16, beta, s);
+}
+
+// Split count (fp32 partial slabs) ca_conv_wgrad will use for this shape: the halo kernel's
+// persistent grid where it applies, else `fallback` (the caller's split-K choice).
+int ca_conv_wgrad_splits(int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw,
+                         int fallback) {
+  if (halo_shape(H, W, Cin, Cout, KH, KW, sh, sw, ph, pw) && halo_wgrad_on()) return halo_grid(Nb, H);
+  return fallback;
 }
 
 int ca_conv_out_hw(int H, int KH, int sh, int ph) { return (H + 2 * ph - KH) / sh + 1; }

@@ -64,3 +64,22 @@ def test_halo_plain_input_gradient_and_forward_without_statistics():
     dx = raw.conv_dgrad(y, w, x.shape, 1, 1)
     ref = F.conv_transpose2d(_nchw(y), _nchw(w).contiguous(), padding=1).permute(0, 2, 3, 1)
     assert _rel(dx, ref) < 5e-3
+
+
+@pytest.mark.parametrize("N", [4, 64])
+def test_halo_weight_gradient(N):
+    """conv3x3_halo_wgrad: one fp32 [64][576] partial per persistent workgroup, split-K reduce
+    into the bf16 gradient with beta accumulation (the flat-arena contract)."""
+    from cloud_amd.ops import raw
+
+    torch.manual_seed(200 + N)
+    x = torch.randn(N, 56, 56, 64, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(N, 56, 56, 64, device="cuda").to(torch.bfloat16)
+    prev = (torch.randn(64, 3, 3, 64, device="cuda") * 10).to(torch.bfloat16)
+    out = prev.clone()
+    raw.conv_wgrad(dy, x, (64, 3, 3, 64), 1, 1, out=out, beta=1.0)
+    ref = torch.nn.grad.conv2d_weight(_nchw(x), (64, 64, 3, 3), _nchw(dy), padding=1).permute(0, 2, 3, 1)
+    assert _rel(out.float() - prev.float(), ref) < 2e-2  # bf16 output rounding on top of the sum
+    out32 = torch.zeros(64, 3, 3, 64, device="cuda")
+    raw.conv_wgrad(dy, x, (64, 3, 3, 64), 1, 1, out=out32, beta=0.0)
+    assert _rel(out32, ref) < 2e-3
