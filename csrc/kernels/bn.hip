@@ -561,6 +561,9 @@ unsigned* bn_tickets(hipStream_t s) {
   for (int k = 0; k < used; ++k)
     if (keys[k] == s) return slots[k];
   if (used == 16) return nullptr;
+  // no allocation inside a hipGraph capture: the two-launch path is captured instead
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
   unsigned* t = nullptr;
   if (hipMalloc(&t, MAX_TICKETS * sizeof(unsigned)) != hipSuccess) return nullptr;
   if (hipMemsetAsync(t, 0, MAX_TICKETS * sizeof(unsigned), s) != hipSuccess) return nullptr;
