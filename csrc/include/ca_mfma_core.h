@@ -145,6 +145,49 @@ __device__ __forceinline__ float gelu_cdf(float x) {
   return x >= 0.f ? 1.f - h : h;
 }
 
+// Two elements at a time on packed-FP32 math (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two
+// lanes' worth of FMAs per instruction; rcp / exp stay per element).  Same formula as gelu_cdf.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v gelu_cdf2(f2v x) {
+  const f2v z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+  const f2v d = __builtin_elementwise_fma(f2v{0.5f, 0.5f}, z, f2v{1.f, 1.f});
+  const f2v t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f2v q = __builtin_elementwise_fma(t, f2v{2.465172979e-01f, 2.465172979e-01f}, f2v{-1.186114945e+00f, -1.186114945e+00f});
+  q = __builtin_elementwise_fma(t, q, f2v{2.147474464e+00f, 2.147474464e+00f});
+  q = __builtin_elementwise_fma(t, q, f2v{-1.637753152e+00f, -1.637753152e+00f});
+  q = __builtin_elementwise_fma(t, q, f2v{4.023215817e-01f, 4.023215817e-01f});
+  q = __builtin_elementwise_fma(t, q, f2v{-2.687568603e-01f, -2.687568603e-01f});
+  q = __builtin_elementwise_fma(t, q, f2v{1.396300565e-01f, 1.396300565e-01f});
+  q = __builtin_elementwise_fma(t, q, f2v{5.397006155e-01f, 5.397006155e-01f});
+  q = __builtin_elementwise_fma(t, q, f2v{1.442729204e+00f, 1.442729204e+00f});
+  q = __builtin_elementwise_fma(t, q, f2v{-1.825748218e+00f, -1.825748218e+00f});
+  const f2v e = __builtin_elementwise_fma(x, x * -0.72134752044448170f, q);
+  const f2v h = 0.5f * t * f2v{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+  return f2v{x.x >= 0.f ? 1.f - h.x : h.x, x.y >= 0.f ? 1.f - h.y : h.y};
+}
+
+// GELU(x) / v * GELU'(x) on an 8-column bf16 chunk, two elements per packed step
+__device__ __forceinline__ void gelu8(s8v& v) {
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const f2v x = {bf2f((bf16_t)v[j]), bf2f((bf16_t)v[j + 1])};
+    const f2v y = x * gelu_cdf2(x);
+    v[j] = (short)f2bf(y.x);
+    v[j + 1] = (short)f2bf(y.y);
+  }
+}
+__device__ __forceinline__ void gelu_grad_mul8(s8v& v, const s8v& src) {
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const f2v x = {bf2f((bf16_t)src[j]), bf2f((bf16_t)src[j + 1])};
+    const f2v e = x * x * -0.72134752044448170f;
+    const f2v d = __builtin_elementwise_fma(x * 0.3989422804014327f,
+                                            f2v{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)}, gelu_cdf2(x));
+    v[j] = (short)f2bf(bf2f((bf16_t)v[j]) * d.x);
+    v[j + 1] = (short)f2bf(bf2f((bf16_t)v[j + 1]) * d.y);
+  }
+}
+
 __device__ __forceinline__ float act_fwd(int act, float x) {
   switch (act) {
     case ACT_GELU: return x * gelu_cdf(x);
@@ -471,9 +514,15 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
           if (P.preact) *reinterpret_cast<s8v*>(P.preact + (long)gm * P.ld_aux + gn) = v;
           if (P.dact_src) {
             const s8v src = RSTAT ? *reinterpret_cast<const s8v*>(P.dact_src + (long)gm * P.ld_aux + gn) : dsrc[RSTAT ? 0 : u];
+            if (P.act == ACT_GELU) {
+              gelu_grad_mul8(v, src);
+            } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-              v[j] = (short)f2bf(bf2f((bf16_t)v[j]) * act_grad(P.act, bf2f((bf16_t)src[j])));
+              for (int j = 0; j < 8; ++j)
+                v[j] = (short)f2bf(bf2f((bf16_t)v[j]) * act_grad(P.act, bf2f((bf16_t)src[j])));
+            }
+          } else if (P.act == ACT_GELU) {
+            gelu8(v);
           } else if (P.act != ACT_NONE) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] = (short)f2bf(act_fwd(P.act, bf2f((bf16_t)v[j])));
