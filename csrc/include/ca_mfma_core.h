@@ -391,7 +391,7 @@ __device__ __forceinline__ void mfma_acc(f4v (&acc)[FM][FN], const bf16x8 (&af)[
 // storing any (batched LDS latency; dense GEMMs only -- the conv loaders' registers leave
 // no room, see docs/performance.md)
 template <int BM, int BN, int WM, int WN, int EPI, int SMEM_SHORTS, int EPF = 1, int FM = BM / WM / 16,
-          int FN = BN / WN / 16, bool QUAD = false>
+          int FN = BN / WN / 16, bool QUAD = false, bool BIAS_IN_ACC = false>
 __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM][FN], short* smem, int m0, int n0,
                                               int tm, int tid) {
   constexpr int NT = WM * WN * 64;
@@ -422,7 +422,7 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
     return;
   } else {
     short* Cs = smem;
-    if (P.bias) {
+    if (!BIAS_IN_ACC && P.bias) {  // (BIAS_IN_ACC: the core started its accumulators at the bias)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
 #pragma unroll
@@ -950,11 +950,29 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
   LA la(P, true, m0, tid);
   LB lb(P, false, n0, tid);
 
+  // dense-layer bias: the accumulators START at the bias (loaded before the K loop, its latency
+  // under the first DMA; no registers beyond the accumulators) and the epilogue skips its own
+  // bias add -- which waited one memory round trip per tile (BERT FFN1 forward: +11 us per call)
   f4v acc[FM][FN];
+  constexpr bool BIAS0 = EPI == EPI_BF16;
+  if (BIAS0 && P.bias) {
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+    for (int j = 0; j < FN; ++j) {
+      f4v b;
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < 4; ++r) {
+        const int gn = n0 + wn * (BN / WN) + 4 * (lane >> 4) + j * 16 + r;
+        b[r] = gn < P.N ? P.bias[gn] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) acc[i][j] = b;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  }
 
   const auto ra = loader_rsrc(la);
   const auto rb = loader_rsrc(lb);
@@ -1003,7 +1021,7 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
       __builtin_amdgcn_s_barrier();
     }
   }
-  gemm_epilogue<BM, BN, WM, WN, EPI, SMEM, EPF>(P, acc, smem, m0, n0, tm, tid);
+  gemm_epilogue<BM, BN, WM, WN, EPI, SMEM, EPF, FM, FN, false, BIAS0>(P, acc, smem, m0, n0, tm, tid);
 }
 
 }  // namespace ca
