@@ -955,24 +955,29 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
   // bias add -- which waited one memory round trip per tile (BERT FFN1 forward: +11 us per call)
   f4v acc[FM][FN];
   constexpr bool BIAS0 = EPI == EPI_BF16;
-  if (BIAS0 && P.bias) {
+  // (called right after the first K tile's DMA is issued: the bias loads then share its wait;
+  // addresses are clamped instead of branched so the 16 loads go out back to back)
+  auto init_acc = [&]() {
+    if (BIAS0 && P.bias) {
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      f4v b;
+      for (int j = 0; j < FN; ++j) {
+        f4v b;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gn = n0 + wn * (BN / WN) + 4 * (lane >> 4) + j * 16 + r;
-        b[r] = gn < P.N ? P.bias[gn] : 0.f;
+        for (int r = 0; r < 4; ++r) {
+          const int gn = n0 + wn * (BN / WN) + 4 * (lane >> 4) + j * 16 + r;
+          const float v = P.bias[gn < P.N ? gn : P.N - 1];
+          b[r] = gn < P.N ? v : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) acc[i][j] = b;
       }
+    } else {
 #pragma unroll
-      for (int i = 0; i < FM; ++i) acc[i][j] = b;
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
     }
-  } else {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
-  }
+  };
 
   const auto ra = loader_rsrc(la);
   const auto rb = loader_rsrc(lb);
@@ -999,7 +1004,23 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
   };
 
   if constexpr (NSTAGE == 1) {
-    for (int t = 0; t < nk; ++t) {
+    int t0 = 0;
+    if constexpr (BIAS0) {
+      if (nk > 0) {  // first K tile peeled: the bias loads of the accumulator init ride behind its DMA
+        issue(0, smem);
+        init_acc();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        compute(smem);
+        __syncthreads();
+        t0 = 1;
+      } else {
+        init_acc();
+      }
+    } else {
+      init_acc();
+    }
+    for (int t = t0; t < nk; ++t) {
       issue(t, smem);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -1007,7 +1028,11 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
       __syncthreads();
     }
   } else {
-    if (nk > 0) issue(0, smem);
+    if (nk == 0) init_acc();
+    if (nk > 0) {
+      issue(0, smem);
+      init_acc();
+    }
     for (int t = 0; t < nk; ++t) {
       if (t + 1 < nk) {
         issue(t + 1, smem + ((t + 1) & 1) * STAGE);

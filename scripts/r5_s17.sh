@@ -15,5 +15,8 @@ grep case gpurun_out/${tag}_epi.log
 for r in 1 2; do
 $S 200 ${tag}_bert_$r.log python bench/bert_base_synth.py --steps 20 --warmup 5 || exit 1
 done
-for f in gpurun_out/${tag}_bert_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f | tail -1)"; done
+for r in 1 2; do
+$S 200 ${tag}_rn_$r.log python bench.py --steps 20 --warmup 5 || exit 1
+done
+for f in gpurun_out/${tag}_bert_*.log gpurun_out/${tag}_rn_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f | tail -1)"; done
 echo SESSION_DONE
