@@ -955,8 +955,8 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
   // bias add -- which waited one memory round trip per tile (BERT FFN1 forward: +11 us per call)
   f4v acc[FM][FN];
   constexpr bool BIAS0 = EPI == EPI_BF16;
-  // (called right after the first K tile's DMA is issued: the bias loads then share its wait;
-  // addresses are clamped instead of branched so the 16 loads go out back to back)
+  // (addresses clamped instead of branched so the 16 loads go out back to back.  Issuing them
+  // behind the first K tile's DMA instead -- first tile peeled -- measured no better)
   auto init_acc = [&]() {
     if (BIAS0 && P.bias) {
 #pragma unroll
@@ -1003,24 +1003,9 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
     }
   };
 
+  init_acc();
   if constexpr (NSTAGE == 1) {
-    int t0 = 0;
-    if constexpr (BIAS0) {
-      if (nk > 0) {  // first K tile peeled: the bias loads of the accumulator init ride behind its DMA
-        issue(0, smem);
-        init_acc();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        compute(smem);
-        __syncthreads();
-        t0 = 1;
-      } else {
-        init_acc();
-      }
-    } else {
-      init_acc();
-    }
-    for (int t = t0; t < nk; ++t) {
+    for (int t = 0; t < nk; ++t) {
       issue(t, smem);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -1028,11 +1013,7 @@ __device__ __forceinline__ void mfma_gemm_glds(const CoreParams& P) {
       __syncthreads();
     }
   } else {
-    if (nk == 0) init_acc();
-    if (nk > 0) {
-      issue(0, smem);
-      init_acc();
-    }
+    if (nk > 0) issue(0, smem);
     for (int t = 0; t < nk; ++t) {
       if (t + 1 < nk) {
         issue(t + 1, smem + ((t + 1) & 1) * STAGE);
