@@ -53,16 +53,30 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+// Wave-wide sum / max, every lane gets the result.  DPP within each 16-lane row (row_ror 8 / 4,
+// quad swaps: VALU ops, no LDS permutes), then the four row totals read as scalars in a fixed
+// order -- against six ds_bpermute round trips of the __shfl_xor butterfly.
+#define CA_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), (ctrl), 0xf, 0xf, false))
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += CA_DPP(v, 0x128);  // row_ror:8
+  v += CA_DPP(v, 0x124);  // row_ror:4
+  v += CA_DPP(v, 0x4e);   // quad_perm [2,3,0,1]
+  v += CA_DPP(v, 0xb1);   // quad_perm [1,0,3,2]
+  return (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))) +
+         (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
+          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48)));
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, CA_DPP(v, 0x128));
+  v = fmaxf(v, CA_DPP(v, 0x124));
+  v = fmaxf(v, CA_DPP(v, 0x4e));
+  v = fmaxf(v, CA_DPP(v, 0xb1));
+  return fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))),
+               fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48))));
 }
 
 static inline int ca_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
