@@ -222,6 +222,131 @@ __global__ void __launch_bounds__(LN_BLK) ln_bwd_kernel(const bf16_t* __restrict
   }
 }
 
+// 16-wave form: the same per-row math with one row per wave (8,192 waves at BERT's M = 8192
+// instead of 2,048 walking four rows each: the row's loads, two wave reductions and stores are
+// one latency chain, so more waves in flight is the lever), and the block's 16 partial rows
+// summed in LDS by a fixed pairing tree (8+8, 4+4, 2+2, 1+1: deterministic) into the same ONE
+// [3][C] partial row per block as ln_bwd_kernel -- the finalisation is unchanged.
+template <int NV>
+__global__ void __launch_bounds__(1024) ln_bwd16_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
+                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                        const float* __restrict__ gamma, bf16_t* __restrict__ dh,
+                                                        bf16_t* __restrict__ dx, float* __restrict__ part, long M,
+                                                        int C, DropCfg din, DropCfg dout) {
+  extern __shared__ float red[];  // [8 waves][3][C] partial rows, then gamma [C]
+  float* sg = red + 24 * C;       // (gamma from LDS per row: 12 fewer registers per lane)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int C4 = C >> 2;
+  for (int c = threadIdx.x; c < C; c += 1024) sg[c] = gamma[c];
+  __syncthreads();
+  float ag[NV][4], ab[NV][4], ax[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ag[i][j] = ab[i][j] = ax[i][j] = 0.f;
+  const float invC = 1.f / (float)C;
+  for (long row = (long)blockIdx.x * 16 + wave; row < M; row += (long)gridDim.x * 16) {
+    const long base = row * C;
+    const float mu = mean[row], rs = rstd[row];
+    float d[NV][4], xh[NV][4];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < C4) {
+        load4(dy + base + 4 * c4, d[i]);
+        load4(h + base + 4 * c4, xh[i]);
+      }
+    }
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < C4) {
+        const f4 gv = *reinterpret_cast<const f4*>(sg + 4 * c4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (dout.on) d[i][j] *= drop_mul(dout, base + 4 * c4 + j);
+          xh[i][j] = (xh[i][j] - mu) * rs;
+          ag[i][j] += d[i][j] * xh[i][j];
+          ab[i][j] += d[i][j];
+          const float gd = gv[j] * d[i][j];
+          sa += gd;
+          sb += gd * xh[i][j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[i][j] = xh[i][j] = 0.f;
+      }
+    }
+    const float a = wave_sum(sa) * invC, b = wave_sum(sb) * invC;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 >= C4) continue;
+      const f4 gv = *reinterpret_cast<const f4*>(sg + 4 * c4);
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = rs * (gv[j] * d[i][j] - a - xh[i][j] * b);
+      store4(dh + base + 4 * c4, o);
+      if (dx) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] *= din.on ? drop_mul(din, base + 4 * c4 + j) : 1.f;
+        store4(dx + base + 4 * c4, o);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ax[i][j] += o[j];
+    }
+  }
+  // fixed pairing tree over the 16 waves' partials
+#pragma unroll
+  for (int sp = 8; sp >= 1; sp >>= 1) {
+    if (wave >= sp && wave < 2 * sp) {
+      float* r = red + (long)(wave - sp) * 3 * C;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c4 = lane + 64 * i;
+        if (c4 < C4) {
+          *reinterpret_cast<f4*>(r + 4 * c4) = f4{ag[i][0], ag[i][1], ag[i][2], ag[i][3]};
+          *reinterpret_cast<f4*>(r + C + 4 * c4) = f4{ab[i][0], ab[i][1], ab[i][2], ab[i][3]};
+          *reinterpret_cast<f4*>(r + 2 * C + 4 * c4) = f4{ax[i][0], ax[i][1], ax[i][2], ax[i][3]};
+        }
+      }
+    }
+    __syncthreads();
+    if (wave < sp) {
+      const float* r = red + (long)wave * 3 * C;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c4 = lane + 64 * i;
+        if (c4 < C4) {
+          const f4 p0 = *reinterpret_cast<const f4*>(r + 4 * c4);
+          const f4 p1 = *reinterpret_cast<const f4*>(r + C + 4 * c4);
+          const f4 p2 = *reinterpret_cast<const f4*>(r + 2 * C + 4 * c4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            ag[i][j] += p0[j];
+            ab[i][j] += p1[j];
+            ax[i][j] += p2[j];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+    float* dst = part + (long)blockIdx.x * 3 * C;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < C4) {
+        *reinterpret_cast<f4*>(dst + 4 * c4) = f4{ag[i][0], ag[i][1], ag[i][2], ag[i][3]};
+        *reinterpret_cast<f4*>(dst + C + 4 * c4) = f4{ab[i][0], ab[i][1], ab[i][2], ab[i][3]};
+        *reinterpret_cast<f4*>(dst + 2 * C + 4 * c4) = f4{ax[i][0], ax[i][1], ax[i][2], ax[i][3]};
+      }
+    }
+  }
+}
+
 // out[c] (+)= sum_p part[p*stride + c], for c < N; out2 / out3 (optional) get columns
 // N..2N-1 / 2N..3N-1.  Block = 16 columns x 16 part-lanes (enough waves in flight to
 // hide the partial-slab reads; deterministic fixed-order tree).
@@ -523,9 +648,22 @@ int ln_fwd_launch(const bf16_t* x, const bf16_t* res, const float* g, const floa
   return 0;
 }
 
+bool ln_bwd16() {  // CLOUD_AMD_LN_BWD16=0: the 4-wave kernel walking four rows per wave (A/B)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_LN_BWD16");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
+}
+
 template <int NV>
 int ln_bwd_launch(const bf16_t* dy, const bf16_t* h, const float* mu, const float* rs, const float* g, bf16_t* dh,
                   bf16_t* dx, float* part, int nblk, long M, int C, DropCfg din, DropCfg dout, hipStream_t s) {
+  if (ln_bwd16() && C <= 1344) {
+    ln_bwd16_kernel<NV><<<nblk, 1024, 25 * C * sizeof(float), s>>>(dy, h, mu, rs, g, dh, dx, part, M, C, din, dout);
+    return 0;
+  }
   ln_bwd_kernel<NV><<<nblk, LN_BLK, 12 * C * sizeof(float), s>>>(dy, h, mu, rs, g, dh, dx, part, M, C, din, dout);
   return 0;
 }

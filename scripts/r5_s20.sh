@@ -15,6 +15,7 @@ for b in 640 256 384 1024; do
 CLOUD_AMD_DENSE_WGRAD_BLOCKS=$b $S 200 ${tag}_b${b}_$r.log python bench/bert_base_synth.py --steps 20 --warmup 5 || exit 1
 done
 CLOUD_AMD_EPI_PF=0 $S 200 ${tag}_pf0_$r.log python bench/bert_base_synth.py --steps 20 --warmup 5 || exit 1
+CLOUD_AMD_LN_BWD16=0 $S 200 ${tag}_ln4_$r.log python bench/bert_base_synth.py --steps 20 --warmup 5 || exit 1
 done
 for f in gpurun_out/${tag}_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f | tail -1)"; done
 rm -rf gpurun_out/${tag}_bprof
