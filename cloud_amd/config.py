@@ -105,8 +105,9 @@ _VARS = [
     Var("CLOUD_AMD_CONV_HALO_WGRAD", bool, True, "the weight gradient of the same 3x3 / 64-channel / width-56 "
         "convolutions on the LDS-resident kernel (ca_conv_halo.h conv3x3_halo_wgrad: 64 x 576 partial in registers, "
         "one fp32 slab per workgroup); 0 = implicit GEMM (A/B)", "ops"),
-    Var("CLOUD_AMD_LN_BWD16", bool, True, "LayerNorm backward on 16-wave blocks, one row per wave, the block's "
-        "partials summed by a fixed LDS tree; 0 = 4-wave blocks walking four rows per wave (A/B)", "ops"),
+    Var("CLOUD_AMD_LN_BWD16", bool, False, "LayerNorm backward on 16-wave blocks, one row per wave, the block's "
+        "partials summed by a fixed LDS tree (measured 2.8 % slower on BERT beside the weight-gradient side stream; "
+        "default: 4-wave blocks walking four rows per wave)", "ops"),
     Var("CLOUD_AMD_GEMM_256X96", bool, True, "forward GEMMs whose 256 x 96 grid fills whole rounds while the 128 x "
         "128 grid leaves a partial one (BERT QKV, M = 8192, N = 2304) run on 256 x 96 tiles; 0 = off (A/B)", "ops"),
     Var("CLOUD_AMD_GEMM_STREAMK", int, 0, "two-phase 256 x 256 GEMM: 0 off (default; measured slower than the "

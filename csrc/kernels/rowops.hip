@@ -648,11 +648,15 @@ int ln_fwd_launch(const bf16_t* x, const bf16_t* res, const float* g, const floa
   return 0;
 }
 
-bool ln_bwd16() {  // CLOUD_AMD_LN_BWD16=0: the 4-wave kernel walking four rows per wave (A/B)
+// CLOUD_AMD_LN_BWD16=1 selects the 16-wave form.  Off by default: same kernel time in a
+// serialized profile (0.587 vs 0.585 ms per BERT step) but BERT 2.8 % SLOWER with the weight-
+// gradient side stream running beside it (7,061 / 7,079 vs 6,879 / 6,881 seq/s with it on,
+// profiles/r5_s20/) -- its 1024-thread, 77-KB blocks crowd the side stream's GEMMs off the CUs.
+bool ln_bwd16() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("CLOUD_AMD_LN_BWD16");
-    v = (e && e[0] == '0') ? 0 : 1;
+    v = (e && e[0] == '1') ? 1 : 0;
   }
   return v != 0;
 }
