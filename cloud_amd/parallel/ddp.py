@@ -236,7 +236,7 @@ class GradAllReducer:
                 b.index = i
         for b in self.buckets:
             for s in b.slots:
-                self._param_bucket[id(s.param)] = b
+                self._param_bucket[id(s.param)] = (s.param, b)
 
     def _install_hooks(self):
         for b in self.buckets:
@@ -252,7 +252,10 @@ class GradAllReducer:
         if not self._sync_enabled or id(p) in self._seen:
             return
         self._seen.add(id(p))
-        b = self._param_bucket.get(id(p))
+        pb = self._param_bucket.get(id(p))
+        # (identity checked: a dead reducer's id(param) keys can be reused by another model's
+        # parameters while the dead one still sits in _ACTIVE awaiting cycle collection)
+        b = pb[1] if pb is not None and pb[0] is p else None
         if b is None or b.launched:
             return
         b.pending -= 1
@@ -261,7 +264,8 @@ class GradAllReducer:
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record(torch.cuda.current_stream(b.tensor.device))
                 b.ready_ev = ev
-            if self.world > 1 or not self._probe:  # world 1: hooks exist for the readiness probe only
+            # world 1: hooks exist for the readiness probe and / or the per-slice optimizer
+            if self.world > 1 or self.optimizer is not None or not self._probe:
                 self._launch_ready()
 
     def _wire(self, b):
@@ -276,6 +280,12 @@ class GradAllReducer:
 
     def _launch(self, b):
         trace.mark("bucket%d" % b.index)
+        if self.world <= 1:
+            # nothing to reduce: the bucket's gradients are final, so its slice of the fused
+            # update can start now, on the optimizer stream, beside the rest of backward
+            self._update_slice(b, torch.cuda.current_stream(b.tensor.device))
+            b.launched = True
+            return
         if self.comm is not None:
             # native communicator: the copy to the wire dtype, the collective and the copy
             # back all run on the communicator's stream, after the gradients' producers
@@ -351,6 +361,11 @@ class GradAllReducer:
         if self._probe:
             self._log_ready()
         if self.world <= 1:
+            if self.optimizer is not None:
+                while self._next < len(self.buckets):
+                    self._launch(self.buckets[self._next])
+                    self._next += 1
+                self._join_sliced()
             self.reset()
             return
         dev_timed = self.timing and self._device_timed
@@ -517,7 +532,9 @@ class GradAllReducer:
     # -- per-slice optimizer ---------------------------------------------------------
     def attach_optimizer(self, optimizer):
         """Run ``optimizer``'s fused update per bucket, as each bucket's collective completes
-        (RCCL transports): bucket k's update runs on a dedicated stream while bucket k+1 is
+        (RCCL transports; at world 1 as soon as the bucket's gradients are final -- only for
+        loops that do not touch gradients between backward and ``step()``: ``fit``, the
+        benches): bucket k's update runs on a dedicated stream while bucket k+1 is
         still on the wire and backward is still running, so after the last collective only the
         last bucket's update remains -- for BERT that is the word-embedding tail instead of the
         whole-arena AdamW.  The elementwise update is the same per element, so the weights are
@@ -527,11 +544,19 @@ class GradAllReducer:
         first), or with ``CLOUD_AMD_SLICED_OPT=0``.  Returns True when enabled."""
         from .. import config
 
-        ok = (self.world > 1 and self._device_timed and getattr(optimizer, "clipnorm", None) is None
+        cuda = bool(self.arenas) and self.arenas[0].grad.is_cuda
+        # world 1: no collective, so each bucket's update starts as soon as backward has
+        # produced its last gradient -- the optimizer pass overlaps the rest of backward
+        # (BERT: the 0.65-ms AdamW pass was fully exposed after backward)
+        wire_ok = (self.world > 1 and self._device_timed) or (self.world == 1 and cuda)
+        ok = (wire_ok and getattr(optimizer, "clipnorm", None) is None
               and config.get("CLOUD_AMD_SLICED_OPT") and hasattr(optimizer, "sliced_begin"))
         self.optimizer = optimizer if ok else None
         if ok and self._opt_stream is None:
             self._opt_stream = torch.cuda.Stream(self.arenas[0].grad.device)
+        if ok and self.world == 1 and not self._hooks:
+            self._install_hooks()
+            _ACTIVE.add(self)
         return bool(ok)
 
     def _update_slice(self, b, after_stream):

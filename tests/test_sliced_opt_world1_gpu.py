@@ -1,0 +1,80 @@
+"""Per-bucket optimizer at world 1 (cloud_amd/parallel/ddp.py attach_optimizer): with no
+collective, each gradient bucket's slice of the fused AdamW / SGD update starts on the optimizer
+stream as soon as backward has produced the bucket's last gradient, beside the rest of backward.
+The update is elementwise, so after several steps the weights must be BITWISE those of the
+whole-arena ``step()`` -- BERT (bf16 + fp32 arenas, AdamW with and without weight decay) and
+ResNet-50 (SGD + momentum, the fused bottleneck backward writing gradients in place)."""
+import gc
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _bert_run(sliced, steps=4):
+    from cloud_amd.models.bert import BertConfig, BertForSequenceClassification
+    from cloud_amd.ops import softmax_cross_entropy
+    from cloud_amd.optim import AdamW
+    from cloud_amd.parallel.ddp import GradAllReducer
+
+    torch.manual_seed(0)
+    cfg = BertConfig.base(num_hidden_layers=2, num_labels=2)
+    m = BertForSequenceClassification(cfg, device="cuda")
+    opt = AdamW(m, learning_rate=1e-3, weight_decay=0.01)
+    red = GradAllReducer(opt.arenas, world=1, bucket_mb=4.0)
+    if sliced:
+        assert red.attach_optimizer(opt) is True
+    g = torch.Generator(device="cuda").manual_seed(7)
+    ids = torch.randint(1000, 30522, (16, 128), device="cuda", generator=g)
+    tts = torch.zeros_like(ids)
+    am = torch.ones_like(ids)
+    labels = torch.randint(0, 2, (16,), device="cuda", generator=g)
+    for _ in range(steps):
+        opt.zero_grad()
+        loss, _ = softmax_cross_entropy(m(ids, tts, am), labels, denom=16)
+        loss.backward()
+        red.finish()
+        opt.step()
+    torch.cuda.synchronize()
+    return [p.detach().clone() for p in m.parameters()], float(loss)
+
+
+def test_bert_adamw_sliced_world1_is_bitwise_whole_step():
+    a, la = _bert_run(True)
+    gc.collect()
+    b, lb = _bert_run(False)
+    assert la == lb
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
+
+
+def _resnet_run(sliced, steps=3):
+    from cloud_amd.models import resnet50
+    from cloud_amd.ops import softmax_cross_entropy
+    from cloud_amd.optim import SGD
+    from cloud_amd.parallel.ddp import GradAllReducer
+
+    torch.manual_seed(0)
+    m = resnet50(num_classes=1000, dtype=torch.bfloat16, device="cuda")
+    opt = SGD(m, learning_rate=0.1, momentum=0.9)
+    red = GradAllReducer(opt.arenas, world=1, bucket_mb=16.0)
+    if sliced:
+        assert red.attach_optimizer(opt) is True
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(32, 224, 224, 3, device="cuda", generator=g).to(torch.bfloat16)
+    y = torch.randint(0, 1000, (32,), device="cuda", generator=g)
+    for _ in range(steps):
+        opt.zero_grad()
+        loss, _ = softmax_cross_entropy(m(x), y)
+        loss.backward()
+        red.finish()
+        opt.step()
+    torch.cuda.synchronize()
+    return [p.detach().clone() for p in m.parameters()]
+
+
+def test_resnet_sgd_sliced_world1_is_bitwise_whole_step():
+    a = _resnet_run(True)
+    gc.collect()
+    b = _resnet_run(False)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))
