@@ -241,7 +241,17 @@ class GradAllReducer:
     def _install_hooks(self):
         for b in self.buckets:
             for s in b.slots:
-                self._hooks.append(s.param.register_post_accumulate_grad_hook(self._on_grad))
+                self._hooks.append(s.param.register_post_accumulate_grad_hook(self._on_hook))
+
+    def _on_hook(self, p):
+        # autograd's post-accumulate hook fires when the Function that took ``p`` returns --
+        # also when it returned no gradient for it.  A parameter whose gradient is finished
+        # LATER by deferred side-stream work (runtime/side_stream.defer marks it) must be
+        # counted only by that work's explicit notify_grad_ready, or its bucket would launch
+        # (all-reduce / optimizer slice) before the weight-gradient GEMM has written it.
+        if getattr(p, "_ca_explicit_notify", False):
+            return
+        self._on_grad(p)
 
     def _on_grad(self, p):
         # A parameter can be reported twice per step: explicitly by an op that wrote its

@@ -100,7 +100,11 @@ def begin_pass():
 
 def defer(event, params, notify):
     """Queue params whose gradients the side stream finishes at ``event``; ``notify(p)``
-    runs for each once the main stream has been ordered after it."""
+    runs for each once the main stream has been ordered after it.  The params are marked
+    ``_ca_explicit_notify``: the DP engine then ignores autograd's post-accumulate hook for
+    them (it fires when the layer's backward returns, before the side stream is done)."""
+    for p in params:
+        p._ca_explicit_notify = True
     if event is None:
         for p in params:
             notify(p)
