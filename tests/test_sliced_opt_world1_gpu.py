@@ -2,8 +2,9 @@
 collective, each gradient bucket's slice of the fused AdamW / SGD update starts on the optimizer
 stream as soon as backward has produced the bucket's last gradient, beside the rest of backward.
 The update is elementwise, so after several steps the weights must be BITWISE those of the
-whole-arena ``step()`` -- BERT (bf16 + fp32 arenas, AdamW with and without weight decay) and
-ResNet-50 (SGD + momentum, the fused bottleneck backward writing gradients in place)."""
+whole-arena ``step()`` -- BERT (bf16 + fp32 arenas, AdamW with and without weight decay; no
+dropout, whose seeds advance a process-global counter, and unique token ids) and ResNet-50 (SGD +
+momentum, the fused bottleneck backward writing gradients in place)."""
 import gc
 
 import pytest
@@ -19,14 +20,16 @@ def _bert_run(sliced, steps=4):
     from cloud_amd.parallel.ddp import GradAllReducer
 
     torch.manual_seed(0)
-    cfg = BertConfig.base(num_hidden_layers=2, num_labels=2)
+    cfg = BertConfig.base(num_hidden_layers=2, num_labels=2, hidden_dropout_prob=0.0,
+                          attention_probs_dropout_prob=0.0)  # (dropout seeds advance a global counter)
     m = BertForSequenceClassification(cfg, device="cuda")
     opt = AdamW(m, learning_rate=1e-3, weight_decay=0.01)
     red = GradAllReducer(opt.arenas, world=1, bucket_mb=4.0)
     if sliced:
         assert red.attach_optimizer(opt) is True
     g = torch.Generator(device="cuda").manual_seed(7)
-    ids = torch.randint(1000, 30522, (16, 128), device="cuda", generator=g)
+    # unique token ids: the word-embedding gradient rows then take one (atomic) contribution each
+    ids = (torch.randperm(29000, device="cuda", generator=g)[:16 * 128] + 1000).view(16, 128)
     tts = torch.zeros_like(ids)
     am = torch.ones_like(ids)
     labels = torch.randint(0, 2, (16,), device="cuda", generator=g)
@@ -37,7 +40,7 @@ def _bert_run(sliced, steps=4):
         red.finish()
         opt.step()
     torch.cuda.synchronize()
-    return [p.detach().clone() for p in m.parameters()], float(loss)
+    return {n: p.detach().clone() for n, p in m.named_parameters()}, float(loss.detach())
 
 
 def test_bert_adamw_sliced_world1_is_bitwise_whole_step():
@@ -45,7 +48,13 @@ def test_bert_adamw_sliced_world1_is_bitwise_whole_step():
     gc.collect()
     b, lb = _bert_run(False)
     assert la == lb
-    assert all(torch.equal(x, y) for x, y in zip(a, b))
+    for n in a:
+        if n == "embeddings.token_type":
+            # its one row takes all 2,048 tokens' fp32 atomic adds: not bitwise run to run
+            # even without slicing (profiles/r5_s23/)
+            torch.testing.assert_close(a[n], b[n], rtol=0, atol=1e-6)
+        else:
+            assert torch.equal(a[n], b[n]), n
 
 
 def _resnet_run(sliced, steps=3):
