@@ -176,3 +176,60 @@ def test_gloo_comm_accounting_consistent():
         assert math.isfinite(t["allreduce_ms"]) and math.isfinite(t["exposed_comm_ms"])
         assert t["allreduce_ms"] > 0, t
         assert t["exposed_comm_ms"] <= step_ms, (t, step_ms)
+
+
+class _DeferredWeightFn(torch.autograd.Function):
+    """y = x @ w^T whose weight gradient is NOT returned to autograd: it is written into the
+    arena later (as BERT's deferred side-stream weight-gradient GEMMs do) -- autograd's
+    post-accumulate hook for ``w`` still fires when this backward returns."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        _LATE.append((w, g.t() @ x))  # the "late" weight gradient
+        return g @ w, None
+
+
+_LATE = []
+
+
+@pytest.mark.parametrize("explicit", [True, False])
+def test_deferred_gradient_counted_only_by_explicit_notify(explicit):
+    """A parameter handed to runtime/side_stream.defer is marked ``_ca_explicit_notify``: the
+    DP engine must ignore autograd's hook for it and launch its bucket only after the explicit
+    ``notify_grad_ready`` (unmarked, the hook launches the bucket before the gradient exists --
+    the race the mark removes)."""
+    from cloud_amd.parallel import ddp
+
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(16, 16, bias=False)
+    opt = SGD(lin, learning_rate=0.0)
+    ref = [None]
+    fake = FakeComm(ref)
+    red = GradAllReducer(opt.arenas, bucket_mb=64.0, transport=fake, world=2)
+    ref[0] = red
+    w = lin.weight
+    if explicit:
+        w._ca_explicit_notify = True
+    _LATE.clear()
+    x = torch.randn(4, 16, requires_grad=True)
+    opt.zero_grad()
+    _DeferredWeightFn.apply(x, w).square().sum().backward()
+    launched = [e for e in fake.log if e[0] == "launch"]
+    if not explicit:
+        assert launched, "unmarked: the hook alone launched the bucket (gradient not written yet)"
+        red.finish()
+        return
+    assert not launched  # the hook did not count w
+    (wp, gw), = _LATE
+    w.grad.copy_(gw)  # the deferred work lands ...
+    ddp.notify_grad_ready(w)  # ... and announces it
+    launched = [e for e in fake.log if e[0] == "launch"]
+    assert launched and all(e[2] for e in launched)
+    red.finish()
+    torch.testing.assert_close(w.grad, 2.0 * gw)
