@@ -5,7 +5,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, __file__.rsplit("/tests/", 1)[0])
+sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
 
 
 def run(sliced, steps):
