@@ -194,6 +194,9 @@ _VARS = [
     Var("CLOUD_AMD_SLICED_OPT", bool, True, "multi-GPU: run the fused optimizer update per gradient bucket as "
         "each bucket's all-reduce completes (overlapping the next bucket's), instead of once after the last one",
         "distributed"),
+    Var("CLOUD_AMD_SLICED_OPT_WORLD1", bool, False, "one GPU: start each gradient bucket's optimizer slice as soon "
+        "as its gradients are final, beside the rest of backward (measured slower on MI355X: off by default)",
+        "distributed"),
     Var("CLOUD_AMD_GRAD_REDUCE_DTYPE", str, "auto", "wire dtype of the gradient all-reduce: 'bf16' (every "
         "bucket, fp32 arenas through a bf16 copy: half the bytes), 'fp32' (every bucket through fp32), 'native' "
         "(each arena in its own dtype), 'auto' (= native: fp32 master-weight gradients keep fp32 sums; 'bf16' is "

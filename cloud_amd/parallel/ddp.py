@@ -542,9 +542,9 @@ class GradAllReducer:
     # -- per-slice optimizer ---------------------------------------------------------
     def attach_optimizer(self, optimizer):
         """Run ``optimizer``'s fused update per bucket, as each bucket's collective completes
-        (RCCL transports; at world 1 as soon as the bucket's gradients are final -- only for
-        loops that do not touch gradients between backward and ``step()``: ``fit``, the
-        benches): bucket k's update runs on a dedicated stream while bucket k+1 is
+        (RCCL transports; opt-in at world 1, as soon as the bucket's gradients are final --
+        only for loops that do not touch gradients between backward and ``step()``): bucket
+        k's update runs on a dedicated stream while bucket k+1 is
         still on the wire and backward is still running, so after the last collective only the
         last bucket's update remains -- for BERT that is the word-embedding tail instead of the
         whole-arena AdamW.  The elementwise update is the same per element, so the weights are
@@ -555,10 +555,13 @@ class GradAllReducer:
         from .. import config
 
         cuda = bool(self.arenas) and self.arenas[0].grad.is_cuda
-        # world 1: no collective, so each bucket's update starts as soon as backward has
-        # produced its last gradient -- the optimizer pass overlaps the rest of backward
-        # (BERT: the 0.65-ms AdamW pass was fully exposed after backward)
-        wire_ok = (self.world > 1 and self._device_timed) or (self.world == 1 and cuda)
+        # world 1 (opt-in, CLOUD_AMD_SLICED_OPT_WORLD1): no collective, so each bucket's update
+        # starts as soon as backward has produced its last gradient, beside the rest of
+        # backward.  Measured SLOWER on one MI355X -- BERT 6,927 vs 6,969 seq/s, ResNet-50
+        # 15,231 vs 15,278 img/s (profiles/r5_s22/): the bandwidth-bound update competes with
+        # backward's own memory traffic and adds a launch per bucket
+        wire_ok = ((self.world > 1 and self._device_timed)
+                   or (self.world == 1 and cuda and config.get("CLOUD_AMD_SLICED_OPT_WORLD1")))
         ok = (wire_ok and getattr(optimizer, "clipnorm", None) is None
               and config.get("CLOUD_AMD_SLICED_OPT") and hasattr(optimizer, "sliced_begin"))
         self.optimizer = optimizer if ok else None

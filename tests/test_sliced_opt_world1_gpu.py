@@ -13,6 +13,11 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _world1_slicing(monkeypatch):
+    monkeypatch.setenv("CLOUD_AMD_SLICED_OPT_WORLD1", "1")  # opt-in (measured slower on one GPU)
+
+
 def _bert_run(sliced, steps=1):
     from cloud_amd.models.bert import BertConfig, BertForSequenceClassification
     from cloud_amd.ops import softmax_cross_entropy
