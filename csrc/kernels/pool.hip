@@ -309,76 +309,117 @@ __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_kernel(const bf16_t* __r
 // the network, 64 ch at 112x112) is never written or re-read.  Each window element is
 // rounded to bf16 before the max, exactly as the separate BN-apply + max-pool would see
 // it; the 1-byte argmax per output channel feeds the backward.  ss = [scale C | shift C].
+//
+// The kernel is VALU-bound if written per tap (a float compare-and-select chain: ~2,000
+// VALU per thread, profiles/r5_s21 0.64 ms at b1024), so the max runs on integer keys:
+// after the ReLU the bf16 bit pattern orders like an unsigned integer, and
+//   key = bits << 16 | (63 - (3 kh + kx))
+// (kx = column in the thread's 3x5 patch) makes max(key) the window maximum AND its first
+// row-major tap -- the strict '>' scan's tie rule -- in one v_max3_u32 per three taps.
+// 3 kh + kx orders both windows' taps row-major (kx <= 2 for the first, 2 <= kx <= 4 for
+// the second) and decodes to the tap with one subtraction.  BN + ReLU + rounding run on
+// packed pairs (v_pk_fma_f32, v_cvt_pk_bf16_f32, v_pk_max_i16 against 0 on the bf16 bits).
+// Border taps load the clamped (duplicate) pixel and take the duplicate's key, so they
+// change neither the max nor the argmax and need no mask.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+typedef short ps2 __attribute__((ext_vector_type(2)));
+typedef __bf16 pb2 __attribute__((ext_vector_type(2)));
+typedef unsigned short pu2 __attribute__((ext_vector_type(2)));
+
+// two packed bf16 z -> two packed bf16 relu(z * s + h), rounded as f2bf would
+__device__ __forceinline__ uint32_t bn_relu_pk(uint32_t p, pf2 s, pf2 h) {
+  const pf2 x = {__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+  const pf2 f = __builtin_elementwise_fma(x, s, h);
+  const ps2 q = __builtin_bit_cast(ps2, __builtin_convertvector(f, pb2));
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(q, (ps2){0, 0}));
+}
+
+__device__ __forceinline__ uint32_t max3u(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_elementwise_max(__builtin_elementwise_max(a, b), c);
+}
+
 __global__ void __launch_bounds__(256) bn_relu_maxpool_s2k3_kernel(const bf16_t* __restrict__ z,
                                                                   const float* __restrict__ ss,
                                                                   bf16_t* __restrict__ y, uint8_t* __restrict__ idx,
                                                                   int N, int H, int W, int C, int OH, int OW) {
   // one thread: two horizontally adjacent outputs (ow, ow + 1), 8 channels -- their windows
-  // share a column, so 15 loads instead of 18, all issued before any is used (clamped
-  // addresses, border taps masked after)
+  // share a column, so 15 loads instead of 18, all issued before any is used
   const int CT = C / 8;
   const int OW2 = (OW + 1) / 2;
   const long total = (long)N * OH * OW2 * CT;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int vc = (int)(t % CT);
-    long r = t / CT;
-    const int ow0 = 2 * (int)(r % OW2); r /= OW2;
-    const int oh = (int)(r % OH);
-    const int n = (int)(r / OH);
-    float sc[8], sh[8];
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < (uint32_t)total; t += gridDim.x * blockDim.x) {
+    const int vc = (int)(t % (uint32_t)CT);
+    uint32_t r = t / (uint32_t)CT;
+    const int ow0 = 2 * (int)(r % (uint32_t)OW2); r /= (uint32_t)OW2;
+    const int oh = (int)(r % (uint32_t)OH);
+    const int n = (int)(r / (uint32_t)OH);
+    const float4 s0 = *reinterpret_cast<const float4*>(ss + vc * 8);
+    const float4 s1 = *reinterpret_cast<const float4*>(ss + vc * 8 + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(ss + C + vc * 8);
+    const float4 h1 = *reinterpret_cast<const float4*>(ss + C + vc * 8 + 4);
+    const pf2 sc[4] = {{s0.x, s0.y}, {s0.z, s0.w}, {s1.x, s1.y}, {s1.z, s1.w}};
+    const pf2 sh[4] = {{h0.x, h0.y}, {h0.z, h0.w}, {h1.x, h1.y}, {h1.z, h1.w}};
+    uint4 v[3][5];
+    uint32_t lo[3][5];  // 63 - (3 kh + kx) of the pixel actually loaded (clamped)
+    int wo[5], kxc[5];  // clamped columns: element offset in the row, patch column
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      sc[j] = ss[vc * 8 + j];
-      sh[j] = ss[C + vc * 8 + j];
+    for (int kx = 0; kx < 5; ++kx) {
+      const int w = ow0 * 2 - 1 + kx;
+      const int wc = w < 0 ? 0 : (w >= W ? W - 1 : w);
+      wo[kx] = wc * C + vc * 8;
+      kxc[kx] = wc - ow0 * 2 + 1;
     }
-    us8 v[3][5];
-    bool ok[3][5];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
       const int h = oh * 2 - 1 + kh;
       const int hc = h < 0 ? 0 : (h >= H ? H - 1 : h);
+      const bf16_t* zr = z + (long)((n * H + hc) * W) * C;
 #pragma unroll
       for (int kx = 0; kx < 5; ++kx) {
-        const int w = ow0 * 2 - 1 + kx;
-        const int wc = w < 0 ? 0 : (w >= W ? W - 1 : w);
-        ok[kh][kx] = h >= 0 && h < H && w >= 0 && w < W;
-        v[kh][kx] = *reinterpret_cast<const us8*>(z + (((long)n * H + hc) * W + wc) * C + vc * 8);
+        lo[kh][kx] = (uint32_t)(63 - 3 * (hc - oh * 2 + 1) - kxc[kx]);
+        v[kh][kx] = *reinterpret_cast<const uint4*>(zr + wo[kx]);
       }
+    }
+    uint32_t best[2][8];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      uint32_t key[5][8];
+#pragma unroll
+      for (int kx = 0; kx < 5; ++kx) {
+        const uint32_t u[4] = {v[kh][kx].x, v[kh][kx].y, v[kh][kx].z, v[kh][kx].w};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const uint32_t b = bn_relu_pk(u[p], sc[p], sh[p]);
+          key[kx][2 * p] = (b << 16) | lo[kh][kx];
+          key[kx][2 * p + 1] = (b & 0xffff0000u) | lo[kh][kx];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t m = max3u(key[2 * q][j], key[2 * q + 1][j], key[2 * q + 2][j]);
+          best[q][j] = kh == 0 ? m : __builtin_elementwise_max(best[q][j], m);
+        }
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int ow = ow0 + q;
       if (ow >= OW) continue;
-      float best[8];
-      uint8_t bi[8];
+      uint4 o;
+      uint32_t ob[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        best[j] = -INFINITY;
-        bi[j] = 0;
-      }
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-#pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const int kx = 2 * q + kw;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float f = fmaxf(bf2f(v[kh][kx][j]) * sc[j] + sh[j], 0.f);
-            f = bf2f(f2bf(f));
-            if (ok[kh][kx] && f > best[j]) { best[j] = f; bi[j] = (uint8_t)(kh * 3 + kw); }
-          }
-        }
-      }
-      us8 o;
-      uint64_t packed = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        o[j] = f2bf(best[j]);
-        packed |= (uint64_t)bi[j] << (8 * j);
-      }
+      for (int j = 0; j < 8; ++j) ob[j] = (uint32_t)(63 - 2 * q) - (best[q][j] & 63u);  // tap index
+      o.x = (best[q][1] & 0xffff0000u) | (best[q][0] >> 16);
+      o.y = (best[q][3] & 0xffff0000u) | (best[q][2] >> 16);
+      o.z = (best[q][5] & 0xffff0000u) | (best[q][4] >> 16);
+      o.w = (best[q][7] & 0xffff0000u) | (best[q][6] >> 16);
+      uint2 pk;
+      pk.x = ob[0] | (ob[1] << 8) | (ob[2] << 16) | (ob[3] << 24);
+      pk.y = ob[4] | (ob[5] << 8) | (ob[6] << 16) | (ob[7] << 24);
       const long oo = (((long)n * OH + oh) * OW + ow) * C + vc * 8;
-      *reinterpret_cast<us8*>(y + oo) = o;
-      *reinterpret_cast<uint64_t*>(idx + oo) = packed;
+      *reinterpret_cast<uint4*>(y + oo) = o;
+      *reinterpret_cast<uint2*>(idx + oo) = pk;
     }
   }
 }
@@ -396,55 +437,57 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_s2k3_kernel(const bf16_t*
 // and read back at b1024) and applies the BN backward to it -- g never reaches memory.
 
 // g of the 2x2 stem-pixel block (bi, bj) of image n, channels 8 vc .. 8 vc + 7, rounded to
-// bf16 as the stored tensor was
+// bf16 as the stored tensor was.  Branch-free (the per-tap 'if' chain compiled to ~150 exec-mask
+// branches and ~1,100 VALU per thread: profiles/r5_s21 0.65 + 0.88 ms): a window's gradient is
+// gated on the packed bf16 bits -- pooled output > 0 and window inside the image, v_pk_min_u16
+// to a 0/1 multiplier and v_pk_mul_lo_u16 -- then each of the block's 9 (window, pixel) pairs
+// is one argmax-byte compare and select; a pixel's terms add in window order (wy, wx) as before.
 __device__ __forceinline__ void stem_block_grad(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ ypool,
                                                 const uint8_t* __restrict__ idx, int n, int bi, int bj, int vc,
                                                 int C, int OH, int OW, float (&acc)[2][2][8]) {
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[a][b][j] = 0.f;
-  // the four windows' loads first (clamped, masked after): none behind a branch
-  us8 gvs[2][2], yvs[2][2];
-  uint64_t ids[2][2];
+  // the four windows' loads first (clamped; a clamped window's gate is zero)
+  uint4 gvs[2][2], yvs[2][2];
+  uint2 ids[2][2];
+  const int owc[2] = {bj * C + vc * 8, (bj + 1 < OW ? bj + 1 : OW - 1) * C + vc * 8};
 #pragma unroll
   for (int wy = 0; wy < 2; ++wy)
 #pragma unroll
     for (int wx = 0; wx < 2; ++wx) {
-      const int oh = bi + wy < OH ? bi + wy : OH - 1, ow = bj + wx < OW ? bj + wx : OW - 1;
-      const long oo = (((long)n * OH + oh) * OW + ow) * C + vc * 8;
-      gvs[wy][wx] = *reinterpret_cast<const us8*>(dy + oo);
-      yvs[wy][wx] = *reinterpret_cast<const us8*>(ypool + oo);
-      ids[wy][wx] = *reinterpret_cast<const uint64_t*>(idx + oo);
+      const int oh = bi + wy < OH ? bi + wy : OH - 1;
+      const long oo = (long)((n * OH + oh) * OW) * C + owc[wx];
+      gvs[wy][wx] = *reinterpret_cast<const uint4*>(dy + oo);
+      yvs[wy][wx] = *reinterpret_cast<const uint4*>(ypool + oo);
+      ids[wy][wx] = *reinterpret_cast<const uint2*>(idx + oo);
     }
+  float gw[2][2][8];  // gated window gradients
+  uint32_t tw[2][2][8];  // argmax taps
 #pragma unroll
-  for (int wy = 0; wy < 2; ++wy) {
-    const int oh = bi + wy;
-    if (oh >= OH) continue;
+  for (int wy = 0; wy < 2; ++wy)
 #pragma unroll
     for (int wx = 0; wx < 2; ++wx) {
-      const int ow = bj + wx;
-      if (ow >= OW) continue;
-      const us8 gv = gvs[wy][wx];
-      const us8 yv = yvs[wy][wx];
-      const uint64_t id = ids[wy][wx];
+      const bool inside = bi + wy < OH && bj + wx < OW;
+      const pu2 lim = inside ? (pu2){1, 1} : (pu2){0, 0};
+      const uint32_t gu[4] = {gvs[wy][wx].x, gvs[wy][wx].y, gvs[wy][wx].z, gvs[wy][wx].w};
+      const uint32_t yu[4] = {yvs[wy][wx].x, yvs[wy][wx].y, yvs[wy][wx].z, yvs[wy][wx].w};
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        const int kh = a + 1 - 2 * wy;
-        if (kh < 0 || kh > 2) continue;
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int kw = b + 1 - 2 * wx;
-          if (kw < 0 || kw > 2) continue;
-          const uint32_t want = (uint32_t)(kh * 3 + kw);
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (((id >> (8 * j)) & 0xff) == want && bf2f(yv[j]) > 0.f) acc[a][b][j] += bf2f(gv[j]);
-        }
+      for (int p = 0; p < 4; ++p) {
+        // y >= 0 (a ReLU output): bits > 0 <=> y > 0; min(bits, 1) is the 0/1 multiplier
+        const pu2 mul = __builtin_elementwise_min(__builtin_bit_cast(pu2, yu[p]), lim);
+        const uint32_t gg = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pu2, gu[p]) * mul);
+        gw[wy][wx][2 * p] = __uint_as_float(gg << 16);
+        gw[wy][wx][2 * p + 1] = __uint_as_float(gg & 0xffff0000u);
       }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tw[wy][wx][j] = ((j < 4 ? ids[wy][wx].x : ids[wy][wx].y) >> (8 * (j & 3))) & 0xffu;
     }
+  // pixel (a, b) is tap (a + 1 - 2 wy) * 3 + (b + 1 - 2 wx) of window (wy, wx) when both are in [0, 2]
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    acc[0][0][j] = tw[0][0][j] == 4 ? gw[0][0][j] : 0.f;
+    acc[0][1][j] = (tw[0][0][j] == 5 ? gw[0][0][j] : 0.f) + (tw[0][1][j] == 3 ? gw[0][1][j] : 0.f);
+    acc[1][0][j] = (tw[0][0][j] == 7 ? gw[0][0][j] : 0.f) + (tw[1][0][j] == 1 ? gw[1][0][j] : 0.f);
+    acc[1][1][j] = (tw[0][0][j] == 8 ? gw[0][0][j] : 0.f) + (tw[0][1][j] == 6 ? gw[0][1][j] : 0.f) +
+                   (tw[1][0][j] == 2 ? gw[1][0][j] : 0.f) + (tw[1][1][j] == 0 ? gw[1][1][j] : 0.f);
   }
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -466,20 +509,20 @@ __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnstats_kernel(
   float s1[8], s2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
-  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  for (long t = t0; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int vc = (int)(t % CT);
-    long r = t / CT;
-    const int bj = (int)(r % Wb); r /= Wb;
-    const int bi = (int)(r % Hb);
-    const int n = (int)(r / Hb);
+  const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint32_t t = t0; t < (uint32_t)total; t += gridDim.x * blockDim.x) {
+    const int vc = (int)(t % (uint32_t)CT);
+    uint32_t r = t / (uint32_t)CT;
+    const int bj = (int)(r % (uint32_t)Wb); r /= (uint32_t)Wb;
+    const int bi = (int)(r % (uint32_t)Hb);
+    const int n = (int)(r / (uint32_t)Hb);
     us8 zvs[2][2];  // z of the block, loaded up front (clamped) with the windows' operands
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int h = 2 * bi + a < H ? 2 * bi + a : H - 1, w = 2 * bj + b < W ? 2 * bj + b : W - 1;
-        zvs[a][b] = *reinterpret_cast<const us8*>(z + (((long)n * H + h) * W + w) * C + vc * 8);
+        zvs[a][b] = *reinterpret_cast<const us8*>(z + (long)((n * H + h) * W) * C + (w * C + vc * 8));
       }
     float acc[2][2][8];
     stem_block_grad(dy, ypool, idx, n, bi, bj, vc, C, OH, OW, acc);
@@ -491,7 +534,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnstats_kernel(
       for (int b = 0; b < 2; ++b) {
         const int w = 2 * bj + b;
         if (w >= W) continue;
-        const long off = (((long)n * H + h) * W + w) * C + vc * 8;
+        const long off = (long)((n * H + h) * W) * C + (w * C + vc * 8);
         const us8 zv = zvs[a][b];
         us8 o;
 #pragma unroll
@@ -528,13 +571,13 @@ __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnapply_kernel(
   const int CT = C / 8;
   const int Hb = (H + 1) / 2, Wb = (W + 1) / 2;
   const long total = (long)N * Hb * Wb * CT;
-  const long t0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  for (long t = t0; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int vc = (int)(t % CT);
-    long r = t / CT;
-    const int bj = (int)(r % Wb); r /= Wb;
-    const int bi = (int)(r % Hb);
-    const int n = (int)(r / Hb);
+  const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint32_t t = t0; t < (uint32_t)total; t += gridDim.x * blockDim.x) {
+    const int vc = (int)(t % (uint32_t)CT);
+    uint32_t r = t / (uint32_t)CT;
+    const int bj = (int)(r % (uint32_t)Wb); r /= (uint32_t)Wb;
+    const int bi = (int)(r % (uint32_t)Hb);
+    const int n = (int)(r / (uint32_t)Hb);
     float A[8], B[8], D[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -552,7 +595,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnapply_kernel(
       for (int b = 0; b < 2; ++b) {
         const int w = 2 * bj + b;
         if (w >= W) continue;
-        const long off = (((long)n * H + h) * W + w) * C + vc * 8;
+        const long off = (long)((n * H + h) * W) * C + (w * C + vc * 8);
         const us8 zv = *reinterpret_cast<const us8*>(z + off);
         us8 o;
 #pragma unroll
@@ -569,6 +612,7 @@ int ca_bn_relu_maxpool_s2k3(const bf16_t* z, const float* ss, bf16_t* y, uint8_t
                             int OH, int OW, hipStream_t st) {
   if (C % 8 != 0 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
   const long total = (long)N * OH * ((OW + 1) / 2) * (C / 8);
+  if (total >= (1L << 31) || (long)N * H * W >= (1L << 31)) return -1;  // 32-bit thread / pixel indices
   const int grid = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
   bn_relu_maxpool_s2k3_kernel<<<grid, 256, 0, st>>>(z, ss, y, idx, N, H, W, C, OH, OW);
   CA_LAUNCH_CHECK();
@@ -585,6 +629,8 @@ int ca_maxpool_bnstats_parts(int N, int H, int W, int C) {
 int ca_maxpool_bwd_s2k3_bnstats(const bf16_t* dy, const bf16_t* ypool, const uint8_t* idx, const bf16_t* z, bf16_t* g,
                                 float* part, int N, int H, int W, int C, int OH, int OW, hipStream_t st) {
   if (C % 8 != 0 || 256 % (C / 8) != 0 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
+  if ((long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8) >= (1L << 31) || (long)N * H * W >= (1L << 31))
+    return -1;  // 32-bit thread / pixel indices
   const int grid = ca_maxpool_bnstats_parts(N, H, W, C);
   if (g) maxpool_bwd_s2k3_bnstats_kernel<true><<<grid, 256, 0, st>>>(dy, ypool, idx, z, g, part, N, H, W, C, OH, OW);
   else maxpool_bwd_s2k3_bnstats_kernel<false><<<grid, 256, 0, st>>>(dy, ypool, idx, z, g, part, N, H, W, C, OH, OW);
@@ -599,6 +645,7 @@ int ca_maxpool_bwd_s2k3_bnapply(const bf16_t* dy, const bf16_t* ypool, const uin
                                 hipStream_t st) {
   if (C % 8 != 0 || OH != (H - 1) / 2 + 1 || OW != (W - 1) / 2 + 1) return -1;
   const long total = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+  if (total >= (1L << 31) || (long)N * H * W >= (1L << 31)) return -1;  // 32-bit thread / pixel indices
   maxpool_bwd_s2k3_bnapply_kernel<<<ca_stream_grid(total, 256), 256, 0, st>>>(dy, ypool, idx, z, coef, dz, N, H, W,
                                                                               C, OH, OW);
   CA_LAUNCH_CHECK();
