@@ -515,11 +515,13 @@ __global__ void __launch_bounds__(SQ * 4) __attribute__((amdgpu_waves_per_eu(4))
       const int qi = t * 16 + (lane & 15);
       const float ls = lse_s[qi], dvq = dv_s[qi];
       s4v pk;
+      float dm[4] = {1.f, 1.f, 1.f, 1.f};  // the row's four consecutive keys: two hashes
+      if (a.drop.on) drop_mul4(a.drop, bhss + (uint32_t)(qi * SQ + kr), dm);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kr + r;
         const float pr = key < klen ? exp2f(p[t][r] * c2 - ls) : 0.f;
-        const float mul = a.drop.on ? drop_mul(a.drop, bhss + (uint32_t)(qi * SQ + key)) : 1.f;
+        const float mul = dm[r];
         pk[r] = (short)f2bf(pr * mul);
         dsr[t][r] = (short)f2bf(pr * (dp[t][r] * mul - dvq));
       }
@@ -670,15 +672,23 @@ __global__ void __launch_bounds__(SQ * 4) attn_fwd_short_kernel(AttnArgs a) {
   for (int half = 0; half < SQ / 64; ++half) {
     if (half) __builtin_amdgcn_wave_barrier();  // the previous half's P reads precede these writes
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt)
+    for (int tt = 0; tt < 4; ++tt) {
+      const int t = half * 4 + tt;
+      // keys across lanes: a lane pair shares each row's hash (drop_mul_lanepair; SQ is even)
+      float dm[4] = {1.f, 1.f, 1.f, 1.f};
+      if (a.drop.on) {
+        static_assert(SQ % 2 == 0, "lane-pair dropout hashing needs an even row length");
+        const int keyev = t * 16 + (lane & 14);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int t = half * 4 + tt;
-        const int q = q0 + (lane >> 4) * 4 + r;
-        const int key = t * 16 + (lane & 15);
-        const float mul = a.drop.on ? drop_mul(a.drop, bhss + (uint32_t)(q * SQ + key)) : 1.f;
-        slab[((lane >> 4) * 4 + r) * LDT + tt * 16 + (lane & 15)] = (short)f2bf(s[t][r] * mul);
+        for (int rr = 0; rr < 4; rr += 2) {
+          const int qh = q0 + (lane >> 4) * 4 + rr + (lane & 1);
+          drop_mul_lanepair(a.drop, (bhss + (uint32_t)(qh * SQ + keyev)) >> 1, lane, dm[rr], dm[rr + 1]);
+        }
       }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        slab[((lane >> 4) * 4 + r) * LDT + tt * 16 + (lane & 15)] = (short)f2bf(s[t][r] * dm[r]);
+    }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {

@@ -58,8 +58,10 @@ __global__ void __launch_bounds__(LN_BLK) ln_fwd_kernel(const bf16_t* __restrict
         for (int j = 0; j < 4; ++j) v[i][j] += xb[j];
       }
       if (din.on) {
+        float m[4];
+        drop_mul4(din, base + 4 * c4, m);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[i][j] *= drop_mul(din, base + 4 * c4 + j);
+        for (int j = 0; j < 4; ++j) v[i][j] *= m[j];
       }
       if (res) {
         float r[4];
@@ -93,11 +95,13 @@ __global__ void __launch_bounds__(LN_BLK) ln_fwd_kernel(const bf16_t* __restrict
     if (h_out) store4(h_out + base + 4 * c4, v[i]);
     const f4 g = *reinterpret_cast<const f4*>(gamma + 4 * c4);
     const f4 b = *reinterpret_cast<const f4*>(beta + 4 * c4);
-    float o[4];
+    float o[4], m[4] = {1.f, 1.f, 1.f, 1.f};
+    if (dout.on) drop_mul4(dout, base + 4 * c4, m);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      o[j] = (v[i][j] - mean) * rstd * g[j] + b[j];
-      if (dout.on) o[j] *= drop_mul(dout, base + 4 * c4 + j);
+    for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + b[j];
+    if (dout.on) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] *= m[j];
     }
     store4(y + base + 4 * c4, o);
   }
@@ -167,9 +171,14 @@ __global__ void __launch_bounds__(LN_BLK) ln_bwd_kernel(const bf16_t* __restrict
     for (int i = 0; i < NV; ++i) {
       const int c4 = lane + 64 * i;
       if (c4 < C4) {
+        if (dout.on) {
+          float m[4];
+          drop_mul4(dout, base + 4 * c4, m);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) d[i][j] *= m[j];
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if (dout.on) d[i][j] *= drop_mul(dout, base + 4 * c4 + j);
           xh[i][j] = (xh[i][j] - mu) * rs;
           ag[i][j] += d[i][j] * xh[i][j];
           ab[i][j] += d[i][j];
@@ -192,8 +201,12 @@ __global__ void __launch_bounds__(LN_BLK) ln_bwd_kernel(const bf16_t* __restrict
       for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] * d[i][j] - a - xh[i][j] * b);
       store4(dh + base + 4 * c4, o);
       if (dx) {
+        if (din.on) {
+          float m[4];
+          drop_mul4(din, base + 4 * c4, m);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] *= din.on ? drop_mul(din, base + 4 * c4 + j) : 1.f;
+          for (int j = 0; j < 4; ++j) o[j] *= m[j];
+        }
         store4(dx + base + 4 * c4, o);
       }
 #pragma unroll
@@ -263,9 +276,14 @@ __global__ void __launch_bounds__(1024) ln_bwd16_kernel(const bf16_t* __restrict
       const int c4 = lane + 64 * i;
       if (c4 < C4) {
         const f4 gv = *reinterpret_cast<const f4*>(sg + 4 * c4);
+        if (dout.on) {
+          float m[4];
+          drop_mul4(dout, base + 4 * c4, m);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) d[i][j] *= m[j];
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if (dout.on) d[i][j] *= drop_mul(dout, base + 4 * c4 + j);
           xh[i][j] = (xh[i][j] - mu) * rs;
           ag[i][j] += d[i][j] * xh[i][j];
           ab[i][j] += d[i][j];
@@ -289,8 +307,12 @@ __global__ void __launch_bounds__(1024) ln_bwd16_kernel(const bf16_t* __restrict
       for (int j = 0; j < 4; ++j) o[j] = rs * (gv[j] * d[i][j] - a - xh[i][j] * b);
       store4(dh + base + 4 * c4, o);
       if (dx) {
+        if (din.on) {
+          float m[4];
+          drop_mul4(din, base + 4 * c4, m);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] *= din.on ? drop_mul(din, base + 4 * c4 + j) : 1.f;
+          for (int j = 0; j < 4; ++j) o[j] *= m[j];
+        }
         store4(dx + base + 4 * c4, o);
       }
 #pragma unroll
@@ -630,8 +652,11 @@ __global__ void __launch_bounds__(256) dropout_kernel(const bf16_t* __restrict__
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
     us8 u = *reinterpret_cast<const us8*>(x + 8 * i);
     us8 o;
+    float m[8];
+    drop_mul4(d, 8 * i, *reinterpret_cast<float(*)[4]>(m));
+    drop_mul4(d, 8 * i + 4, *reinterpret_cast<float(*)[4]>(m + 4));
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(u[j]) * drop_mul(d, 8 * i + j));
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(u[j]) * m[j]);
     *reinterpret_cast<us8*>(y + 8 * i) = o;
   }
 }

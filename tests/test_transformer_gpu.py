@@ -208,8 +208,9 @@ def test_embedding_sum_and_scatter():
 
 
 def test_dropout_hash_statistics():
-    """The per-element dropout hash (ca_rng.h): keep rate at BERT's p, bit-identical
-    regeneration from (seed, index), no correlation between neighbours or between seeds."""
+    """The dropout hash (ca_rng.h; one 32-bit hash per element pair, a 16-bit half each): keep
+    rate at BERT's p, bit-identical regeneration from (seed, index), no correlation between
+    neighbours (lag 1 = the two halves of one hash) or between seeds."""
     from cloud_amd.ops import raw
 
     n = 64 * 12 * 128 * 128  # one BERT-base attention-probability tensor
@@ -219,7 +220,7 @@ def test_dropout_hash_statistics():
     m1 = raw.dropout_mask(n, 0.1, 1234)
     assert torch.equal(m1, raw.dropout_mask(n, 0.1, 1234))  # regeneration
     a = m1.float() - m1.float().mean()
-    for lag in (1, 64, 128, 128 * 128):
+    for lag in (1, 2, 3, 64, 128, 128 * 128):
         c = (a[:-lag] * a[lag:]).mean().item() / a.var().item()
         assert abs(c) < 5e-3, (lag, c)
     b = raw.dropout_mask(n, 0.1, 1235).float()
