@@ -97,6 +97,16 @@ template <template <int, int, int> class GA, template <int, int, int> class GB>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k256x96(CoreParams P) {
   mfma_gemm_glds<256, 96, 2, 2, GA, GB, EPI_BF16>(P);
 }
+// the 128 x 64 tile the dispatcher runs for BERT's N = 768 forwards (768 tiles = 3 rounds)
+template <template <int, int, int> class GA, template <int, int, int> class GB>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k128x64(CoreParams P) {
+  mfma_gemm_glds<128, 64, 2, 2, GA, GB, EPI_BF16>(P);
+}
+static void launch128x64(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) k128x64<GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
+  else if (layout == 1) k128x64<GDenseKC, GDenseNC><<<g, 256, 0, s>>>(p);
+  else k128x64<GDenseNC, GDenseNC><<<g, 256, 0, s>>>(p);
+}
 static void launch128x96(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
   if (layout == 0) k128x96<GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
 }
@@ -216,6 +226,7 @@ int main(int argc, char** argv) {
                     {"p8sk", 256, 256, launchp8sk},
                     {"w256x128", 256, 128, launch256x128},
                     {"glds128", 128, 128, launch128},
+                    {"g128x64", 128, 64, launch128x64},
                     {"g128x96", 128, 96, launch128x96},
                     {"g256x96", 256, 96, launch256x96}};
   hipStream_t s;
