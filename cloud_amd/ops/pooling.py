@@ -174,6 +174,7 @@ class _StemTailFn(torch.autograd.Function):
 def stem_tail_ok(z, bn, pool, partials):
     return (bn.training and bn.relu and partials is not None and z.is_cuda and z.dtype == torch.bfloat16
             and z.is_contiguous() and z.shape[-1] % 8 == 0 and 256 % (z.shape[-1] // 8) == 0
+            and z.shape[0] * z.shape[1] * z.shape[2] < 2 ** 31  # the kernels' 32-bit pixel indices
             and (pool.k, pool.stride, pool.padding) == (3, 2, 1) and _ext.use_native(z))
 
 
