@@ -114,6 +114,7 @@ _VARS = [
         "128 x 128 core on BERT's M = 8192 shapes), 1 stream-K on under-filled grids, 2 wherever allowed (tests)", "ops"),
     Var("CLOUD_AMD_LN_BWD8", bool, False, "retired round-5 A/B knob (8-wave LayerNorm backward, measured 1.5 % slower "
         "and removed); ignored", "ops"),
+    Var("CLOUD_AMD_BN_FIN_RPG", int, 512, "BatchNorm statistics finalize: partial rows per group block (64-512)", "ops"),
     Var("CLOUD_AMD_BN_FIN_MERGED", bool, True, "BatchNorm statistics from many partial rows: group reduction and "
         "per-channel finalize in ONE launch (last block per 64 channels finalizes, agent-scope ticket); 0 = two "
         "launches (A/B runs)", "ops"),

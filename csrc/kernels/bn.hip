@@ -436,12 +436,25 @@ struct BwdFin {
 // per-column-block ticket (agent-scope release); the block that arrives last for its 64 channels
 // (acquire) sums the G group rows in a FIXED order -- the same result whichever block finishes
 // last -- runs the finalize and re-arms the ticket.  No block ever waits for another.  Groups
-// are 512 rows so the last block's pass is a single round of loads (G <= 49 at 25,088 rows).
-constexpr int FIN_PL = 16, FIN_RPG = 512;
+// are 512 rows by default so the last block's pass is a single round of loads (G <= 49 at
+// 25,088 rows).
+constexpr int FIN_PL = 16;
+
+// partial rows per group (CLOUD_AMD_BN_FIN_RPG, 64..512, default 512): fewer rows per group =
+// more blocks reading the partials at once, and more group rows for the last block to sum
+int fin_rpg() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_BN_FIN_RPG");
+    const int r = e ? atoi(e) : 512;
+    v = (r >= 64 && r <= 512 && r % FIN_PL == 0) ? r : 512;
+  }
+  return v;
+}
 
 template <class FIN>
 __global__ void __launch_bounds__(64 * FIN_PL) group_finalize_kernel(const float* __restrict__ ws, int nchunks,
-                                                                     long stride_k, long off_q, int C,
+                                                                     long stride_k, long off_q, int C, int rpg,
                                                                      float* __restrict__ gws,
                                                                      unsigned* __restrict__ tickets, const FIN F) {
   __shared__ float ra[FIN_PL][64], rb[FIN_PL][64];
@@ -452,10 +465,10 @@ __global__ void __launch_bounds__(64 * FIN_PL) group_finalize_kernel(const float
   const int G = gridDim.y, g = blockIdx.y;
   float a = 0.f, b = 0.f;
   if (c < C) {
-    int k1 = (g + 1) * FIN_RPG;
+    int k1 = (g + 1) * rpg;
     if (k1 > nchunks) k1 = nchunks;
 #pragma unroll 8
-    for (int k = g * FIN_RPG + pl; k < k1; k += FIN_PL) {
+    for (int k = g * rpg + pl; k < k1; k += FIN_PL) {
       a += ws[(long)k * stride_k + c];
       b += ws[(long)k * stride_k + off_q + c];
     }
@@ -589,9 +602,10 @@ int reduce_finalize(const float* ws, int nchunks, long stride_k, long off_q, int
                     FinKernel fin_kernel, hipStream_t s) {
   if (nchunks > 64 && gws) {
     unsigned* tk = (merged_finalize() && ca_cdiv(C, 64) <= MAX_TICKETS) ? bn_tickets(s) : nullptr;
-    if (tk) {
-      const dim3 g1(ca_cdiv(C, 64), ca_cdiv(nchunks, FIN_RPG));
-      group_finalize_kernel<FIN><<<g1, 64 * FIN_PL, 0, s>>>(ws, nchunks, stride_k, off_q, C, gws, tk, F);
+    const int rpg = fin_rpg();
+    if (tk && ca_cdiv(nchunks, rpg) <= 512) {  // (gws holds 512 group rows)
+      const dim3 g1(ca_cdiv(C, 64), ca_cdiv(nchunks, rpg));
+      group_finalize_kernel<FIN><<<g1, 64 * FIN_PL, 0, s>>>(ws, nchunks, stride_k, off_q, C, rpg, gws, tk, F);
       CA_LAUNCH_CHECK();
       return 0;
     }
