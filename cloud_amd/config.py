@@ -105,10 +105,6 @@ _VARS = [
     Var("CLOUD_AMD_CONV_HALO_WGRAD", bool, True, "the weight gradient of the same 3x3 / 64-channel / width-56 "
         "convolutions on the LDS-resident kernel (ca_conv_halo.h conv3x3_halo_wgrad: 64 x 576 partial in registers, "
         "one fp32 slab per workgroup); 0 = implicit GEMM (A/B)", "ops"),
-    Var("CLOUD_AMD_LN_FWD_PF", bool, False, "LayerNorm forward: software-pipelined grid-stride kernel (next row's "
-        "loads in flight while the current row is reduced and stored)", "ops"),
-    Var("CLOUD_AMD_LN_FWD_BLOCKS", int, 512, "LayerNorm forward with CLOUD_AMD_LN_FWD_PF: 4-wave blocks in the grid",
-        "ops"),
     Var("CLOUD_AMD_LN_BWD16", bool, False, "LayerNorm backward on 16-wave blocks, one row per wave, the block's "
         "partials summed by a fixed LDS tree (measured 2.8 % slower on BERT beside the weight-gradient side stream; "
         "default: 4-wave blocks walking four rows per wave)", "ops"),

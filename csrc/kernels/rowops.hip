@@ -111,118 +111,6 @@ __global__ void __launch_bounds__(LN_BLK) ln_fwd_kernel(const bf16_t* __restrict
   }
 }
 
-// Software-pipelined form of ln_fwd_kernel (CLOUD_AMD_LN_FWD_PF): a fixed grid of 4-wave
-// blocks, each wave walking rows at a grid stride with the NEXT row's x / residual loads in
-// flight while the current row is reduced and stored -- one row per wave with every wave
-// resident issues all reads, then all writes, so HBM sees the two phases one after the other.
-// gamma / beta / the GEMM bias are held in registers across rows.  Same per-row arithmetic
-// (and order) as ln_fwd_kernel: bitwise-equal outputs.
-template <int NV>
-__global__ void __launch_bounds__(LN_BLK) ln_fwd_pf_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
-                                                           const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta, bf16_t* __restrict__ y,
-                                                           bf16_t* __restrict__ h_out, float* __restrict__ mean_out,
-                                                           float* __restrict__ rstd_out, long M, int C, float eps,
-                                                           DropCfg din, DropCfg dout, const float* __restrict__ xbias) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int C4 = C >> 2;
-  float gg[NV][4], bb[NV][4], xbv[NV][4];
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c4 = lane + 64 * i;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      gg[i][j] = c4 < C4 ? gamma[4 * c4 + j] : 0.f;
-      bb[i][j] = c4 < C4 ? beta[4 * c4 + j] : 0.f;
-      xbv[i][j] = (c4 < C4 && xbias) ? xbias[4 * c4 + j] : 0.f;
-    }
-  }
-  const long stride = (long)gridDim.x * (LN_BLK / 64);
-  long row = (long)blockIdx.x * (LN_BLK / 64) + wave;
-  float nx[NV][4], nr[NV][4];
-  auto fetch = [&](long r) {
-    if (r >= M) return;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c4 = lane + 64 * i;
-      if (c4 < C4) {
-        load4(x + r * C + 4 * c4, nx[i]);
-        if (res) load4(res + r * C + 4 * c4, nr[i]);
-      }
-    }
-  };
-  fetch(row);
-  for (; row < M; row += stride) {
-    const long base = row * C;
-    float v[NV][4], rr[NV][4];
-#pragma unroll
-    for (int i = 0; i < NV; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[i][j] = nx[i][j];
-        rr[i][j] = nr[i][j];
-      }
-    fetch(row + stride);
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c4 = lane + 64 * i;
-      if (c4 < C4) {
-        if (xbias) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[i][j] += xbv[i][j];
-        }
-        if (din.on) {
-          float m[4];
-          drop_mul4(din, base + 4 * c4, m);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[i][j] *= m[j];
-        }
-        if (res) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[i][j] += rr[i][j];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s += v[i][j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[i][j] = 0.f;
-      }
-    }
-    const float mean = wave_sum(s) / (float)C;
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < NV; ++i)
-      if (lane + 64 * i < C4) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float d = v[i][j] - mean;
-          q += d * d;
-        }
-      }
-    const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int c4 = lane + 64 * i;
-      if (c4 >= C4) continue;
-      if (h_out) store4(h_out + base + 4 * c4, v[i]);
-      float o[4], m[4] = {1.f, 1.f, 1.f, 1.f};
-      if (dout.on) drop_mul4(dout, base + 4 * c4, m);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * gg[i][j] + bb[i][j];
-      if (dout.on) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] *= m[j];
-      }
-      store4(y + base + 4 * c4, o);
-    }
-    if (lane == 0) {
-      mean_out[row] = mean;
-      rstd_out[row] = rstd;
-    }
-  }
-}
-
 // grid-stride over rows; per-block [2][C] partials (dgamma, dbeta) in `part`.
 template <int NV>
 __global__ void __launch_bounds__(LN_BLK) ln_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ h,
@@ -778,34 +666,9 @@ __global__ void dropout_mask_kernel(uint8_t* __restrict__ m, long n, long base, 
     m[i] = drop_mul(d, base + i) != 0.f;
 }
 
-// CLOUD_AMD_LN_FWD_PF: the software-pipelined LayerNorm forward on CLOUD_AMD_LN_FWD_BLOCKS blocks
-bool ln_fwd_pf() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CLOUD_AMD_LN_FWD_PF");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v != 0;
-}
-int ln_fwd_blocks() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CLOUD_AMD_LN_FWD_BLOCKS");
-    const int b = e ? atoi(e) : 512;
-    v = b >= 64 ? b : 512;
-  }
-  return v;
-}
-
 template <int NV>
 int ln_fwd_launch(const bf16_t* x, const bf16_t* res, const float* g, const float* b, bf16_t* y, bf16_t* h, float* mu,
                   float* rs, long M, int C, float eps, DropCfg din, DropCfg dout, const float* xb, hipStream_t s) {
-  if (ln_fwd_pf()) {
-    const long blocks = ca_cdiv(M, 4);
-    const int grid = (int)(blocks < ln_fwd_blocks() ? blocks : ln_fwd_blocks());
-    ln_fwd_pf_kernel<NV><<<grid, LN_BLK, 0, s>>>(x, res, g, b, y, h, mu, rs, M, C, eps, din, dout, xb);
-    return 0;
-  }
   ln_fwd_kernel<NV><<<ca_cdiv(M, 4), LN_BLK, 0, s>>>(x, res, g, b, y, h, mu, rs, M, C, eps, din, dout, xb);
   return 0;
 }
