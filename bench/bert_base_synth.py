@@ -182,12 +182,23 @@ def main():
     if reducer is not None:
         reducer.timing_start()
         reducer.probe_readiness()  # per-bucket gradient-ready events -> overlap budget
+    # per-step host time, and the part of it spent blocked in the fused optimizer's run-ahead
+    # bound: host_ms - paced = the host's own launch cost (host-bound if it nears ms_per_step)
+    pacer = getattr(opt, "pacer", None) if not args.stock else None
+    host_ms, paced_ms = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        th = time.perf_counter()
+        w0 = pacer.wait_ms if pacer is not None else 0.0
         loss = train_step()
+        host_ms.append((time.perf_counter() - th) * 1e3)
+        paced_ms.append((pacer.wait_ms if pacer is not None else 0.0) - w0)
     torch.cuda.synchronize()
     dist_env.barrier()
     dt = time.perf_counter() - t0
+    unpaced = sorted(h - w for h, w in zip(host_ms, paced_ms))
+    host_launch = {"unpaced_median_ms": round(unpaced[len(unpaced) // 2], 3),
+                   "unpaced_max_ms": round(unpaced[-1], 3)} if unpaced else None
     per_rank = [v / args.steps * 1000.0 for v in dist_env.all_gather_floats(dt, device)]
     elapsed = dist_env.all_reduce_max(dt, device)
     busbw = dist_env.allreduce_busbw(device) if world > 1 else None
@@ -215,7 +226,7 @@ def main():
                        "optimizer": "adamw"},
             "impl": impl, "gc_frozen_objects": gc_frozen, "first_step_latency_s": round(first, 3),
             "run_to_first_step_s": round(run_to_first, 3) if run_to_first is not None else None,
-            "startup_phases_rank0": phases,
+            "startup_phases_rank0": phases, "host_launch_rank0": host_launch,
             "launched_via": benchlaunch.launched_via(), "comm": comm,
             "backend": dist.get_backend() if world > 1 else None,
             "shared_gpu": bool(config.get("CLOUD_AMD_SHARED_GPU")),
