@@ -15,6 +15,8 @@
 #include "ca_mfma_core.h"
 #include "ca_rng.h"
 
+#include <mutex>
+
 namespace {
 
 typedef unsigned short us4v __attribute__((ext_vector_type(4)));
@@ -455,9 +457,14 @@ __global__ void __launch_bounds__(256) embed_sum_kernel(const int32_t* __restric
 // their loads before adding (one memory round trip per column group, not one per row:
 // 111 -> a few us at 8192 x 768).
 constexpr int EB_RW = 16;
+//
+// tws / ticket (token types, T <= 2): DETERMINISTIC form -- each block writes its pre-reduced
+// [2][C] row into tws[blockIdx.x] instead of adding it atomically, and the block that arrives
+// last (agent-scope ticket, as bn.hip group_finalize_kernel) adds the rows in block order.
 __global__ void __launch_bounds__(256) embed_bwd_kernel(const bf16_t* __restrict__ dh, const int32_t* __restrict__ ids,
                                                         const int32_t* __restrict__ tts, float* __restrict__ dword,
-                                                        float* __restrict__ dtype, long M, int C, int T, int pad_id) {
+                                                        float* __restrict__ dtype, long M, int C, int T, int pad_id,
+                                                        float* __restrict__ tws, unsigned* __restrict__ ticket) {
   const int lane = threadIdx.x & 63;
   const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const long nw = (long)gridDim.x * 4;
@@ -516,8 +523,32 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const bf16_t* __restrict
         const int t = k >> 8, e = k & 255;  // e = lane * 4 + j
         if (t >= T || cb + (e >> 2) >= C / 4) continue;
         const float v = tred[0][t][e] + tred[1][t][e] + tred[2][t][e] + tred[3][t][e];
-        atomicAdd(dtype + (long)t * C + 4 * (cb + (e >> 2)) + (e & 3), v);
+        const long col = 4 * (cb + (e >> 2)) + (e & 3);
+        if (tws) tws[((long)blockIdx.x * 2 + t) * C + col] = v;
+        else atomicAdd(dtype + (long)t * C + col, v);
       }
+    }
+  }
+  if (tws && dtype && T <= 2) {
+    __shared__ int last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    for (long k = threadIdx.x; k < (long)T * C; k += 256) {
+      const int t = (int)(k / C);
+      const long col = k - (long)t * C;
+      float v = 0.f;
+      for (unsigned b = 0; b < gridDim.x; ++b) v += tws[((long)b * 2 + t) * C + col];
+      dtype[k] += v;
     }
   }
 }
@@ -948,6 +979,48 @@ int ca_embed_sum(const int32_t* ids, const int32_t* tts, const float* word, cons
   return 0;
 }
 
+// Workspace of the deterministic token-type gradient: [64 blocks][2][C] fp32 + a ticket, one per
+// stream (a ticket must never be shared by kernels running concurrently), allocated on first use
+// outside any graph capture (a capture falls back to the atomic form).
+static void embed_type_ws(int C, hipStream_t s, float** ws, unsigned** tk) {
+  static std::mutex mu;
+  static hipStream_t keys[8];
+  static float* bufs[8];
+  static unsigned* tks[8];
+  static int caps[8];
+  static int used = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  int k = 0;
+  while (k < used && keys[k] != s) ++k;
+  if (k < used && caps[k] >= C) {
+    *ws = bufs[k];
+    *tk = tks[k];
+    return;
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+  if (k == used && used == 8) return;
+  if (k < used) {  // wider C than before: the stream's old buffer is retired after its work
+    if (hipStreamSynchronize(s) != hipSuccess) return;
+    (void)hipFree(bufs[k]);
+    (void)hipFree(tks[k]);
+  }
+  float* b = nullptr;
+  unsigned* t = nullptr;
+  if (hipMalloc(&b, (size_t)64 * 2 * C * sizeof(float)) != hipSuccess) return;
+  if (hipMalloc(&t, sizeof(unsigned)) != hipSuccess || hipMemset(t, 0, sizeof(unsigned)) != hipSuccess) {
+    (void)hipFree(b);
+    return;
+  }
+  keys[k] = s;
+  bufs[k] = b;
+  tks[k] = t;
+  caps[k] = C;
+  if (k == used) ++used;
+  *ws = b;
+  *tk = t;
+}
+
 int ca_embed_bwd(const bf16_t* dh, const int32_t* ids, const int32_t* tts, float* dword, float* dpos, float* dtype,
                  long M, int S, int C, int T, int pos_offset, int pad_id, int V, hipStream_t s) {
   if (C % 4 != 0) return -1;
@@ -964,7 +1037,10 @@ int ca_embed_bwd(const bf16_t* dh, const int32_t* ids, const int32_t* tts, float
     int grid = ca_cdiv(M, 4 * EB_RW);
     if (!(dword && !owner) && grid > 64) grid = 64;
     if (grid < 1) grid = 1;
-    embed_bwd_kernel<<<grid, 256, 0, s>>>(dh, ids, tts, owner ? nullptr : dword, dtype, M, C, T, pad_id);
+    float* tws = nullptr;
+    unsigned* tk = nullptr;
+    if (dtype && T <= 2 && !(dword && !owner)) embed_type_ws(C, s, &tws, &tk);  // null: atomics
+    embed_bwd_kernel<<<grid, 256, 0, s>>>(dh, ids, tts, owner ? nullptr : dword, dtype, M, C, T, pad_id, tws, tk);
     CA_LAUNCH_CHECK();
   }
   if (dpos) {
