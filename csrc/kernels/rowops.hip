@@ -543,11 +543,21 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const bf16_t* __restrict
       __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    // the <= 64 block rows of a column loaded at once (clamped rows read, then zeroed), then
+    // summed in block order: one memory round trip per column instead of 64
+    const int G = (int)gridDim.x;
     for (long k = threadIdx.x; k < (long)T * C; k += 256) {
       const int t = (int)(k / C);
       const long col = k - (long)t * C;
+      float r[64];
+#pragma unroll
+      for (int b = 0; b < 64; ++b) {
+        const float x = tws[((long)(b < G ? b : G - 1) * 2 + t) * C + col];
+        r[b] = b < G ? x : 0.f;
+      }
       float v = 0.f;
-      for (unsigned b = 0; b < gridDim.x; ++b) v += tws[((long)b * 2 + t) * C + col];
+#pragma unroll
+      for (int b = 0; b < 64; ++b) v += r[b];
       dtype[k] += v;
     }
   }
