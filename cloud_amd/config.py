@@ -24,6 +24,8 @@ class Var:
 _VARS = [
     # launcher / run()
     Var("CLOUD_AMD_JOBS_DIR", str, "./jobs", "where run() stages job directories", "launcher"),
+    Var("CLOUD_AMD_HOME", str, "~/.cloud_amd", "per-user state: the job-id index (jobs/<id> -> job directory) that "
+        "python -m cloud_amd.jobs uses to find a job from any directory", "launcher"),
     Var("CLOUD_AMD_STAGE_COPY", bool, False, "stage code files by copying too (default: code "
         "hard-linked, every other file copied; a running job then never sees in-place edits of its sources)", "launcher"),
     Var("CLOUD_AMD_CPU_AFFINITY", bool, True, "launcher pins each GPU rank to the cores of its GPU's NUMA node "
@@ -50,6 +52,9 @@ _VARS = [
     Var("CLOUD_AMD_PG_TIMEOUT_S", float, 600.0, "torch.distributed process-group timeout", "launcher"),
     # kernels / ops
     Var("CLOUD_AMD_OPS", str, "native", "'native' HIP kernels or 'torch' stock ops", "ops"),
+    Var("CLOUD_AMD_DETERMINISTIC", bool, False, "raise instead of taking an order-dependent float-atomic kernel "
+        "path (embedding gradient with more than two token types or rows wider than the owner kernel holds)",
+        "ops"),
     Var("CLOUD_AMD_GEMM", str, "native", "dense GEMMs: 'native' or 'torch'", "ops"),
     Var("CLOUD_AMD_CONV", str, "native", "convolutions: 'native' or 'torch'", "ops"),
     Var("CLOUD_AMD_GEMM_CORE", str, "auto", "GEMM core: 'auto' (128x128 LDS-DMA core plus the 256x256 two-phase "
@@ -192,8 +197,15 @@ _VARS = [
         "projection that fed it (no separate column-sum pass)", "ops"),
     Var("CLOUD_AMD_TAIL_BUCKET_MB", float, 1.0, "cap on the last gradient bucket (the first layers' gradients, "
         "ready only when backward ends: its all-reduce is exposed)", "distributed"),
-    Var("CLOUD_AMD_SLICED_OPT", bool, True, "multi-GPU: run the fused optimizer update per gradient bucket as "
-        "each bucket's all-reduce completes (overlapping the next bucket's), instead of once after the last one",
+    Var("CLOUD_AMD_SLICED_OPT", bool, False, "multi-GPU: run the fused optimizer update per gradient bucket as "
+        "each bucket's all-reduce completes (overlapping the next bucket's), instead of once after the last one "
+        "(opt-in until a multi-GPU run has shown it bitwise equal to the whole step and faster: the bench's N > 1 "
+        "A/B cells measure both)",
+        "distributed"),
+    Var("CLOUD_AMD_TAPE_REDUCE", str, "overlap", "custom loops under a multi-replica strategy: 'overlap' -- "
+        "tf.GradientTape.gradient returns the cross-replica SUM, all-reduced bucket by bucket during backward "
+        "(Horovod DistributedGradientTape semantics); 'replica' -- per-replica gradients, summed in "
+        "apply_gradients (TF MirroredStrategy semantics: a clip between the two sees one replica's gradient)",
         "distributed"),
     Var("CLOUD_AMD_SLICED_OPT_WORLD1", bool, False, "one GPU: start each gradient bucket's optimizer slice as soon "
         "as its gradients are final, beside the rest of backward (measured slower on MI355X: off by default)",

@@ -12,8 +12,11 @@ but the "cluster" is the local node:
   ``worker`` roles (``use_chief_in_tf_config`` semantics of reference
   ``deploy.py:159-161``), the remote markers, and per-rank log files
   ``logs/<role>-<index>[-gpu<k>].log``;
-* a watchdog: if any rank exits non-zero the rest of the group is terminated,
-  exit codes go to ``job.json`` and the job is marked FAILED;
+* a detached supervisor process (:mod:`.supervisor`) owns the ranks: if any rank exits
+  non-zero the rest of the group is terminated, exit codes go to ``job.json`` and the
+  job is marked FAILED -- also after the submitting process has exited (fire-and-forget
+  ``run()``); ``python -m cloud_amd.jobs describe|stream-logs|cancel <id>`` attaches to
+  it by id;
 * ``stream_logs=True`` tails every rank's log to stdout until the job ends (reference
   ``deploy.py:187-211`` streams the whole job); with more than one rank each line is
   prefixed ``[chief-0]`` / ``[worker-1]`` / ``[chief-0-gpu3]`` (the log file's stem);
@@ -35,13 +38,13 @@ import signal
 import socket
 import subprocess
 import sys
-import threading
 import time
 import uuid
 
 from .. import config
-from . import topology
+from . import supervisor, topology
 
+SUPERVISOR_PID = "supervisor.pid"
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
@@ -115,63 +118,110 @@ def _print_logs_info(job_id, job_dir):
     print("Your job ID is: ", job_id)
     print("Please access your job logs at the following URL:")
     print("file://{}".format(os.path.join(job_dir, "logs")))
+    # the reference's gcloud hints (cloud_fit/client.py:277-286), for the local job service
+    print("To describe the job:  python -m cloud_amd.jobs describe {}".format(job_id))
+    print("To stream its logs:   python -m cloud_amd.jobs stream-logs {}".format(job_id))
+    print("To cancel it:         python -m cloud_amd.jobs cancel {}".format(job_id))
 
 
 class Job:
-    """A running local job (all rank processes + watchdog)."""
+    """Client handle of a job run by its detached supervisor (:mod:`.supervisor`).
 
-    def __init__(self, job_id, job_dir, procs, ranks, meta):
-        self.job_id, self.job_dir, self.procs, self.ranks, self.meta = job_id, job_dir, procs, ranks, meta
-        self._done = threading.Event()
-        self.returncode = None
-        self._watch = threading.Thread(target=self._watchdog, daemon=True)
-        self._watch.start()
+    The supervisor owns the ranks; this object only reads ``job.json`` (written
+    atomically by the supervisor) and signals the supervisor.  It can be dropped at any
+    time -- the job keeps running, fails as a group and records its final state -- and
+    re-created from the job id with :meth:`attach` (``python -m cloud_amd.jobs``)."""
 
-    def _write_meta(self):
-        with open(os.path.join(self.job_dir, "job.json"), "w") as f:
-            json.dump(self.meta, f, indent=2)
+    def __init__(self, job_id, job_dir, ranks, meta, supervisor=None):
+        self.job_id, self.job_dir, self.ranks = job_id, job_dir, ranks
+        self._meta = meta
+        self._sup = supervisor  # Popen of the supervisor when this process started it
 
-    def _watchdog(self):
-        failed_at = None
-        first_failure = None
-        while True:
-            codes = [p.poll() for p in self.procs]
-            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
-            if bad and failed_at is None:
-                failed_at = time.time()
-                # the rank that failed, before the watchdog kills the rest
-                self.meta["failed_rank"], first_failure = bad[0]
-                for p in self.procs:
-                    if p.poll() is None:
-                        try:
-                            os.killpg(p.pid, signal.SIGTERM)
-                        except (ProcessLookupError, PermissionError):
-                            pass
-            if failed_at is not None and time.time() - failed_at > 15:
-                for p in self.procs:
-                    if p.poll() is None:
-                        try:
-                            os.killpg(p.pid, signal.SIGKILL)
-                        except (ProcessLookupError, PermissionError):
-                            pass
-            if all(c is not None for c in codes):
-                break
-            time.sleep(0.2)
-        codes = [p.returncode for p in self.procs]
-        self.meta["exit_codes"] = codes
-        self.meta["end_time"] = time.time()
-        self.returncode = first_failure if first_failure is not None else next((c for c in codes if c != 0), 0)
-        self.meta["state"] = "SUCCEEDED" if self.returncode == 0 else "FAILED"
-        self._write_meta()
-        self._done.set()
+    @classmethod
+    def attach(cls, job_id, jobs_dir=None):
+        """The job with this id (or job directory path)."""
+        job_dir = find_job_dir(job_id, jobs_dir)
+        meta = supervisor.read_json(os.path.join(job_dir, supervisor.JOB_META))
+        return cls(meta["job_id"], job_dir, meta["ranks"], meta)
 
-    def wait(self, timeout=None):
-        self._done.wait(timeout)
-        return self.returncode
+    # -- state ------------------------------------------------------------------------
+    def refresh(self):
+        try:
+            self._meta = supervisor.read_json(os.path.join(self.job_dir, supervisor.JOB_META))
+        except (OSError, ValueError):  # between the supervisor's write and rename: keep the last
+            pass
+        return self._meta
+
+    @property
+    def meta(self):
+        return self.refresh()
+
+    @property
+    def state(self):
+        return self.refresh().get("state")
+
+    @property
+    def returncode(self):
+        m = self.refresh()
+        return m.get("returncode") if m.get("state") in supervisor.TERMINAL_STATES else None
+
+    def supervisor_pid(self):
+        pid = self._meta.get("supervisor_pid")
+        if pid is None and self._sup is not None:
+            pid = self._sup.pid
+        if pid is None:  # the launcher records it beside job.json right after the spawn
+            try:
+                with open(os.path.join(self.job_dir, SUPERVISOR_PID)) as f:
+                    pid = int(f.read().strip())
+            except (OSError, ValueError):
+                pid = None
+        return pid
+
+    def supervisor_alive(self):
+        if self._sup is not None:
+            return self._sup.poll() is None
+        pid = self.supervisor_pid()
+        if pid is None:  # submitted this instant: the pid file is not written yet
+            return time.time() - float(self._meta.get("start_time") or 0) < 60
+        return _pid_alive(pid)
 
     def done(self):
-        return self._done.is_set()
+        m = self.refresh()
+        if m.get("state") in supervisor.TERMINAL_STATES:
+            return True
+        if m.get("state") in ("SUBMITTED", "RUNNING") and not self.supervisor_alive():
+            # the supervisor is gone without a final word (killed): re-read once, then say so
+            m = self.refresh()
+            if m.get("state") not in supervisor.TERMINAL_STATES:
+                m = dict(m, state="LOST", returncode=1, error="supervisor exited without recording a final state")
+                supervisor.write_json_atomic(os.path.join(self.job_dir, supervisor.JOB_META), m)
+                self._meta = m
+            return True
+        return False
 
+    def wait(self, timeout=None):
+        t_end = None if timeout is None else time.time() + timeout
+        while not self.done():
+            if t_end is not None and time.time() >= t_end:
+                return None
+            time.sleep(0.05)
+        return self.returncode if self.state != "LOST" else 1
+
+    def cancel(self, wait=True, timeout=60):
+        """Ask the supervisor to stop the job (SIGTERM to every rank, SIGKILL after the
+        grace period); returns the final state when ``wait``."""
+        self.refresh()
+        pid = self.supervisor_pid()
+        if pid and not self.done():
+            try:
+                os.kill(pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        if wait:
+            self.wait(timeout)
+        return self.state
+
+    # -- logs -------------------------------------------------------------------------
     def log_path(self, rank=0):
         return os.path.join(self.job_dir, "logs", log_name(self.ranks[rank]))
 
@@ -251,8 +301,9 @@ class Job:
 
 
 def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, entry_point_args=None,
-           job_labels=None, extra_env=None, profile=False, python=None):
-    """Spawn all ranks of a staged job; returns a :class:`Job`."""
+           job_labels=None, extra_env=None, profile=False, python=None, kill_grace_s=15.0):
+    """Hand a staged job to its supervisor, which spawns and watches every rank; returns
+    the client :class:`Job` at once."""
     ranks = plan_ranks(chief_config, worker_count, worker_config)
     world = len(ranks)
     port = free_port()
@@ -282,7 +333,7 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
             cpu_sets = [None] * len(ranks)
     for info, cpus in zip(ranks, cpu_sets):
         info["cpus"] = topology.format_cpulist(cpus) if cpus else None
-    procs = []
+    spec = []
     for info, cpus in zip(ranks, cpu_sets):
         env = dict(os.environ)
         for k, v in comm_env.items():
@@ -311,14 +362,20 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
             prof_dir = os.path.join(job_dir, "profile")
             cmd = ["rocprofv3", "--kernel-trace", "--stats", "-d", prof_dir, "-o", "rank0",
                    "--output-format", "csv", "--"] + cmd
-        logf = open(os.path.join(job_dir, "logs", log_name(info)), "w")
-        p = subprocess.Popen(cmd, cwd=app_dir, env=env, stdout=logf, stderr=subprocess.STDOUT,
-                             start_new_session=True)
-        _pin(p.pid, cpus)
-        logf.close()
-        procs.append(p)
-    job = Job(job_id, job_dir, procs, ranks, meta)
-    job._write_meta()
+        # only what differs from this process's environment goes to disk: the supervisor
+        # inherits the rest
+        delta = {k: v for k, v in env.items() if os.environ.get(k) != v}
+        spec.append({"rank": info["rank"], "cmd": cmd, "cwd": app_dir, "env": delta,
+                     "log": os.path.join(job_dir, "logs", log_name(info)), "cpus": sorted(cpus) if cpus else None})
+    meta["state"] = "SUBMITTED"
+    supervisor.write_json_atomic(os.path.join(job_dir, supervisor.LAUNCH_SPEC),
+                                 {"ranks": spec, "kill_grace_s": kill_grace_s})
+    supervisor.write_json_atomic(os.path.join(job_dir, supervisor.JOB_META), meta)
+    _register(job_id, job_dir)
+    sup = supervisor.start(job_dir, python=python, pkg_root=PKG_ROOT)
+    with open(os.path.join(job_dir, SUPERVISOR_PID), "w") as f:
+        f.write("%d\n" % sup.pid)
+    job = Job(job_id, job_dir, ranks, meta, supervisor=sup)
     try:
         from .. import monitoring
 
@@ -328,17 +385,81 @@ def launch(job_id, job_dir, target, chief_config, worker_count, worker_config, e
     return job
 
 
-def _pin(pid, cpus):
-    """Pin a freshly spawned rank to its CPU set from the parent (``sched_setaffinity(pid)``):
-    no ``preexec_fn``, which Python documents as unsafe when the launching process has
-    threads.  Popen returns after the child's exec, and the interpreter creates its worker
-    threads (OpenMP, HIP) only later, at ``import torch``, so they inherit this mask."""
-    if not cpus:
-        return
+def _pid_alive(pid):
+    """True while ``pid`` runs (a zombie counts as exited)."""
+    if not pid:
+        return False
     try:
-        os.sched_setaffinity(pid, list(cpus))
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    try:
+        with open("/proc/%d/stat" % pid) as f:
+            return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+    except OSError:
+        return True
+
+
+def index_dir():
+    """Where job ids are mapped to job directories, so ``python -m cloud_amd.jobs`` finds a
+    job from any working directory (``$CLOUD_AMD_HOME/jobs``, default ``~/.cloud_amd/jobs``)."""
+    home = os.environ.get("CLOUD_AMD_HOME") or os.path.join(os.path.expanduser("~"), ".cloud_amd")
+    return os.path.join(home, "jobs")
+
+
+def _register(job_id, job_dir):
+    try:
+        d = index_dir()
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, job_id), "w") as f:
+            f.write(os.path.abspath(job_dir) + "\n")
+    except OSError:  # the index is a convenience; the job directory is the record
+        pass
+
+
+def find_job_dir(job_id, jobs_dir=None):
+    """Directory of job ``job_id``: a path to a job directory, ``<jobs_dir>/<id>``,
+    ``$CLOUD_AMD_JOBS_DIR/<id>``, ``./jobs/<id>``, then the id index."""
+    from . import stage
+
+    if os.path.isfile(os.path.join(job_id, supervisor.JOB_META)):
+        return os.path.abspath(job_id)
+    cands = [os.path.join(jobs_dir, job_id)] if jobs_dir else []
+    cands.append(os.path.join(stage.jobs_root(), job_id))
+    try:
+        with open(os.path.join(index_dir(), job_id)) as f:
+            cands.append(f.read().strip())
     except OSError:
         pass
+    for c in cands:
+        if c and os.path.isfile(os.path.join(c, supervisor.JOB_META)):
+            return os.path.abspath(c)
+    raise FileNotFoundError("no job %r (looked in %s)" % (job_id, ", ".join(c for c in cands if c)))
+
+
+def list_jobs(jobs_dir=None):
+    """Job directories known here: ``jobs_dir`` / ``$CLOUD_AMD_JOBS_DIR`` / ``./jobs`` and the index."""
+    from . import stage
+
+    seen = {}
+    for root in [jobs_dir, stage.jobs_root()]:
+        if root and os.path.isdir(root):
+            for name in os.listdir(root):
+                d = os.path.join(root, name)
+                if os.path.isfile(os.path.join(d, supervisor.JOB_META)):
+                    seen.setdefault(name, os.path.abspath(d))
+    if os.path.isdir(index_dir()):
+        for name in os.listdir(index_dir()):
+            try:
+                with open(os.path.join(index_dir(), name)) as f:
+                    d = f.read().strip()
+            except OSError:
+                continue
+            if os.path.isfile(os.path.join(d, supervisor.JOB_META)):
+                seen.setdefault(name, d)
+    return seen
 
 
 def deploy_job(job_id, job_dir, target, chief_config, worker_count, worker_config, entry_point_args,

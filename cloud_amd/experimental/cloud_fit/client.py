@@ -10,7 +10,8 @@ reference's layout::
 
 and launches ``python -m cloud_amd.experimental.cloud_fit.remote --remote_dir
 <dir> --distribution_strategy <name>`` as a local multi-process job (one rank
-per MI355X, or CPU ranks on a GPU-less node).  Returns the job id.
+per MI355X, or CPU ranks on a GPU-less node).  Returns the job id as soon as the job
+is submitted (its supervisor runs it to completion on its own).
 """
 from __future__ import annotations
 
@@ -29,8 +30,14 @@ ASSET_FILES = ("fit_kwargs.pkl", "x.pkl", "validation_data.pkl", "callbacks.pkl"
 
 
 def cloud_fit(model, remote_dir, region=None, project_id=None, image_uri=None,
-              distribution_strategy=DEFAULT_DISTRIBUTION_STRATEGY, job_spec=None, job_id=None, wait=True,
+              distribution_strategy=DEFAULT_DISTRIBUTION_STRATEGY, job_spec=None, job_id=None, wait=False,
               **fit_kwargs):
+    """Serialise ``model`` and the ``fit`` arguments into ``remote_dir`` and submit the
+    training job; returns the job id right after submission, as the reference does
+    (``client.py:227-286``).  The job runs under its detached supervisor:
+    ``python -m cloud_amd.jobs describe|stream-logs|cancel <job_id>`` follows it, and
+    ``cloud_amd.core.launcher.Job.attach(job_id).wait()`` blocks on it.  ``wait=True``
+    blocks here and raises ``RuntimeError`` if the job fails."""
     if distribution_strategy not in utils.SUPPORTED_DISTRIBUTION_STRATEGIES:
         raise ValueError("{} is not supported. Supported Strategies are {}".format(
             distribution_strategy, list(utils.SUPPORTED_DISTRIBUTION_STRATEGIES.keys())))
@@ -106,7 +113,7 @@ def _default_job_spec(region=None, image_uri=None, entry_point_args=None,
                               "region": region or topology.get_region(), "args": entry_point_args or []}}
 
 
-def _submit_job(job_spec, wait=True):
+def _submit_job(job_spec, wait=False):
     ti = job_spec["trainingInput"]
     job_id = job_spec["jobId"]
     tmp = tempfile.mkdtemp(prefix="cloud_fit_")

@@ -109,6 +109,24 @@ class Optimizer:
         impl = self._impl
         red = getattr(self, "_reducer", None)
         reduced = red is not None and red.tape_reduced
+        if not getattr(impl, "_ca_tape_fresh", False):
+            # the arena was not written by a tape this step: slots of variables missing from
+            # this call would keep last step's gradient where the update kernel does not zero
+            # it (CPU path, fuse_zero_grad=False) -- clear them; a gradient that IS its slot
+            # is saved first
+            pairs = [(g.clone() if g is not None and v.grad is not None and g.data_ptr() == v.grad.data_ptr()
+                      else g, v) for g, v in pairs]
+            impl.zero_grad()
+        impl._ca_tape_fresh = False
+        n_slots = sum(len(a.slots) for a in impl.arenas)
+        if len(pairs) < n_slots:
+            # a variable left out of this call keeps its weights, as in TF: no gradient
+            # (neither a stale one nor the tape's) reaches its slot
+            given = {id(v) for _, v in pairs}
+            for a in impl.arenas:
+                for sl in a.slots:
+                    if id(sl.param) not in given and sl.param.grad is not None:
+                        sl.param.grad.zero_()
         for g, v in pairs:
             slot = v.grad
             if g is None:

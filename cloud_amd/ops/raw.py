@@ -776,14 +776,48 @@ def embed_sum(ids, tts, word, pos, type_, seq_len, pos_offset=0):
     return h
 
 
+# embed_bwd's deterministic token-type workspace: per (device, stream) -- a ticket must
+# never be shared by kernels that can run concurrently -- taken from the caching allocator
+# and kept; the kernel's last block resets the ticket to 0 for the next launch.
+_EMBED_WS = {}
+# how many embed_bwd calls took the order-dependent float-atomic path (tests assert 0 where
+# the step must be bitwise reproducible; CLOUD_AMD_DETERMINISTIC=1 makes it an error)
+EMBED_NONDETERMINISTIC_CALLS = 0
+
+
+def _embed_ws(C, device):
+    stream = torch.cuda.current_stream(device)
+    key = (device.index, stream.cuda_stream)
+    ws = _EMBED_WS.get(key)
+    if ws is None or ws[0].numel() < 64 * 2 * C:
+        # a tensor owned by this stream: the caching allocator ties its reuse to the stream
+        ws = (torch.empty(64 * 2 * C, dtype=torch.float32, device=device),
+              torch.zeros(1, dtype=torch.int32, device=device))
+        _EMBED_WS[key] = ws
+    return ws
+
+
 def embed_bwd(dh, ids, tts, dword, dpos, dtype_, seq_len, n_types, pos_offset=0, pad_id=-1):
     """Scatter-add into dword (deterministic owner-row kernel; ids outside [0, vocab) and
-    ``pad_id`` get nothing), dpos / dtype_ reduced."""
+    ``pad_id`` get nothing), dpos / dtype_ reduced -- the token-type rows by a fixed-order
+    reduction over a workspace from the caching allocator.  A gradient that must take the
+    float-atomic path (more than two token types, rows wider than the owner kernel holds) is
+    counted in ``EMBED_NONDETERMINISTIC_CALLS`` and raises under ``CLOUD_AMD_DETERMINISTIC=1``."""
+    global EMBED_NONDETERMINISTIC_CALLS
     ext = _ext.load(required=True)
     M, C = dh.shape
     V = dword.shape[0] if dword is not None else 0
-    ext.embed_bwd(dh.data_ptr(), ids.data_ptr(), _ext.ptr(tts), _ext.ptr(dword), _ext.ptr(dpos), _ext.ptr(dtype_), M,
-                  seq_len, C, n_types, pos_offset, int(pad_id), int(V), _st(dh.device))
+    tws = tk = None
+    if dtype_ is not None and n_types <= 2:
+        tws, tk = _embed_ws(C, dh.device)
+    nondet = ext.embed_bwd(dh.data_ptr(), ids.data_ptr(), _ext.ptr(tts), _ext.ptr(dword), _ext.ptr(dpos),
+                           _ext.ptr(dtype_), M, seq_len, C, n_types, pos_offset, int(pad_id), int(V), _ext.ptr(tws),
+                           _ext.ptr(tk), _st(dh.device))
+    if nondet:
+        EMBED_NONDETERMINISTIC_CALLS += 1
+        if os.environ.get("CLOUD_AMD_DETERMINISTIC") == "1":
+            raise RuntimeError("embed_bwd: C=%d, %d token types has no deterministic kernel "
+                               "(CLOUD_AMD_DETERMINISTIC=1)" % (C, n_types))
 
 
 def attn_fwd(qkv, B, S, H, key_len=None, p_drop=0.0, seed=0, scale=None):

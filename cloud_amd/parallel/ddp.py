@@ -551,7 +551,8 @@ class GradAllReducer:
         bitwise those of the whole-arena ``step()`` (tests/test_rccl_dataplane_gpu.py).
         ``optimizer.step()`` after ``finish()`` then only closes the step.  Off when the
         transport is not stream-ordered (gloo / CPU), with ``clipnorm`` (needs the global norm
-        first), or with ``CLOUD_AMD_SLICED_OPT=0``.  Returns True when enabled."""
+        first), and unless opted in: ``CLOUD_AMD_SLICED_OPT=1`` (world > 1) /
+        ``CLOUD_AMD_SLICED_OPT_WORLD1=1`` (world 1).  Returns True when enabled."""
         from .. import config
 
         cuda = bool(self.arenas) and self.arenas[0].grad.is_cuda
@@ -563,7 +564,7 @@ class GradAllReducer:
         wire_ok = ((self.world > 1 and self._device_timed)
                    or (self.world == 1 and cuda and config.get("CLOUD_AMD_SLICED_OPT_WORLD1")))
         ok = (wire_ok and getattr(optimizer, "clipnorm", None) is None
-              and config.get("CLOUD_AMD_SLICED_OPT") and hasattr(optimizer, "sliced_begin"))
+              and (self.world == 1 or config.get("CLOUD_AMD_SLICED_OPT")) and hasattr(optimizer, "sliced_begin"))
         self.optimizer = optimizer if ok else None
         if ok and self._opt_stream is None:
             self._opt_stream = torch.cuda.Stream(self.arenas[0].grad.device)

@@ -22,6 +22,7 @@ import types
 
 import torch
 
+from . import config as _ca_config
 from . import keras  # noqa: F401
 from .keras.data import AUTOTUNE as _AUTOTUNE
 from .keras.data import Dataset as _Dataset
@@ -40,15 +41,20 @@ class GradientTape:
       arena (``ops/dense.py``), so ``gradient()`` first zeroes the owning optimizer's
       gradient arena and then runs ``backward(inputs=sources)``, which accumulates every
       other gradient into the same arena slices;
-    * under a multi-replica strategy the optimizer's bucketed all-reduce
+    * under a multi-replica strategy, ``CLOUD_AMD_TAPE_REDUCE`` picks the semantics:
+      ``overlap`` (default) -- the optimizer's bucketed all-reduce
       (:class:`cloud_amd.parallel.ddp.GradAllReducer`) launches each bucket from the backward
       hooks as its gradients complete (overlapped with the rest of backward) and is joined
-      before ``gradient()`` returns -- the returned gradients are the cross-replica SUM, as
+      before ``gradient()`` returns: the returned gradients are the cross-replica SUM, as
       Horovod's ``DistributedGradientTape`` returns them, and ``apply_gradients`` does not
-      reduce them again;
+      reduce them again.  A non-linear transform between ``gradient()`` and
+      ``apply_gradients`` (``clip_by_global_norm``) then sees the global sum.  ``replica`` --
+      TF ``MirroredStrategy`` semantics: per-replica gradients, summed in
+      ``apply_gradients`` (no overlap with backward);
     * the returned tensors are views of the arena (``v.grad``): no copy, and
       ``apply_gradients`` recognises them.  They are valid until the next ``gradient()``
-      over the same variables; ``tf.identity``-style copies (``g.clone()``) keep them.
+      over the same variables; ``tf.identity``-style copies (``g.clone()``) keep them.  A
+      ``persistent=True`` tape returns copies (a second ``gradient()`` overwrites the arena).
 
     Other sources (plain tensors, variables before the optimizer's first step) get
     ``torch.autograd.grad`` results (zeros for unconnected sources).  Reference pattern:
@@ -84,33 +90,56 @@ class GradientTape:
         owners = self._owners(srcs)
         for opt in owners:
             opt.zero_grad()  # the arena slots are accumulated into in place
+        for opt in owners:
+            opt._ca_tape_fresh = True  # apply_gradients: these slots were written this step
         reducers = [o.reducer for o in owners if getattr(o, "reducer", None) is not None and o.reducer.world > 1]
+        overlap = _ca_config.get("CLOUD_AMD_TAPE_REDUCE") == "overlap"
         if owners and all(getattr(s, "_ca_arena", False) and s.grad is not None for s in srcs):
-            target.backward(gradient=output_gradients, inputs=srcs, retain_graph=self.persistent)
-            for r in reducers:
-                r.finish()  # buckets launched during backward; the compute stream joins them
-                r.tape_reduced = True
+            if overlap:
+                target.backward(gradient=output_gradients, inputs=srcs, retain_graph=self.persistent)
+                for r in reducers:
+                    r.finish()  # buckets launched during backward; the compute stream joins them
+                    r.tape_reduced = True
+            else:  # per-replica gradients (TF semantics): apply_gradients reduces them
+                self._backward_unreduced(reducers, lambda: target.backward(
+                    gradient=output_gradients, inputs=srcs, retain_graph=self.persistent))
             out = [s.grad for s in srcs]
+            if self.persistent:
+                # a persistent tape may be asked again: the next gradient() re-zeroes and
+                # overwrites the arena, so the caller keeps copies, not views
+                out = [g.clone() for g in out]
             return out[0] if single else out
         # mixed / non-arena sources: no bucket may launch while autograd.grad runs (the copies
         # apply_gradients makes would race a reduction already in flight); the optimizer
         # reduces the whole arena in apply_gradients instead
-        prev = [(r, r._sync_enabled) for r in reducers]
-        for r, _ in prev:
-            r._sync_enabled = False
-        try:
-            grads = torch.autograd.grad(target, srcs, grad_outputs=output_gradients, allow_unused=True,
-                                        retain_graph=self.persistent)
-        finally:
-            for r, was in prev:
-                r._sync_enabled = was
-                r.reset()
+        box = []
+        self._backward_unreduced(reducers, lambda: box.append(torch.autograd.grad(
+            target, srcs, grad_outputs=output_gradients, allow_unused=True, retain_graph=self.persistent)))
+        grads = box[0]
         out = []
         for g, s in zip(grads, srcs):
             if g is None and getattr(s, "_ca_arena", False) and s.grad is not None:
                 g = s.grad  # written in place by a native backward (autograd saw no gradient)
             out.append(g if g is not None else torch.zeros_like(s))
         return out[0] if single else out
+
+
+def _backward_unreduced_impl(reducers, fn):
+    """Run ``fn`` (a backward) with the reducers' bucket launches off; they are reset after,
+    so ``apply_gradients`` all-reduces the whole arena."""
+    prev = [(r, r._sync_enabled) for r in reducers]
+    for r, _ in prev:
+        r._sync_enabled = False
+    try:
+        fn()
+    finally:
+        for r, was in prev:
+            r._sync_enabled = was
+            r.reset()
+            r.tape_reduced = False
+
+
+GradientTape._backward_unreduced = staticmethod(_backward_unreduced_impl)
 
 
 def function(fn=None, **_kw):

@@ -109,7 +109,7 @@ int ca_splitk_bias_act(const float*, int, long, int, const float*, int, bf16_t*,
 int ca_embed_sum(const int32_t*, const int32_t*, const float*, const float*, const float*, bf16_t*, long, int, int, int,
                  hipStream_t);
 int ca_embed_bwd(const bf16_t*, const int32_t*, const int32_t*, float*, float*, float*, long, int, int, int, int, int,
-                 int, hipStream_t);
+                 int, float*, unsigned*, hipStream_t);
 int ca_dropout(const bf16_t*, bf16_t*, long, float, uint64_t, hipStream_t);
 int ca_dropout_mask(uint8_t*, long, long, float, uint64_t, hipStream_t);
 int ca_attn_fwd(const bf16_t*, bf16_t*, float*, const int*, int, int, int, float, float, uint64_t, hipStream_t);
@@ -425,10 +425,14 @@ PYBIND11_MODULE(_C, m) {
     check(ca_embed_sum(P(const int32_t*, ids), P(const int32_t*, tts), P(const float*, word), P(const float*, pos),
                        P(const float*, type), P(bf16_t*, h), M, S_, C, po, S(s)), "embed_sum");
   });
+  // returns 1 when a gradient took the order-dependent float-atomic path
   m.def("embed_bwd", [](u64 dh, u64 ids, u64 tts, u64 dw, u64 dp, u64 dt, long M, int S_, int C, int T, int po,
-                        int pad_id, int V, u64 s) {
-    check(ca_embed_bwd(P(const bf16_t*, dh), P(const int32_t*, ids), P(const int32_t*, tts), P(float*, dw),
-                       P(float*, dp), P(float*, dt), M, S_, C, T, po, pad_id, V, S(s)), "embed_bwd");
+                        int pad_id, int V, u64 tws, u64 tk, u64 s) {
+    const int r = ca_embed_bwd(P(const bf16_t*, dh), P(const int32_t*, ids), P(const int32_t*, tts), P(float*, dw),
+                               P(float*, dp), P(float*, dt), M, S_, C, T, po, pad_id, V, P(float*, tws),
+                               P(unsigned*, tk), S(s));
+    if (r < 0) check(r, "embed_bwd");
+    return r;
   });
   m.def("dropout", [](u64 x, u64 y, long n, float p, u64 seed, u64 s) {
     check(ca_dropout(P(const bf16_t*, x), P(bf16_t*, y), n, p, seed, S(s)), "dropout");

@@ -14,12 +14,23 @@
 // raises TimeoutError -- a peer that hangs before joining (rather than exiting) no longer
 // stalls every rank until the launcher's job timeout.  In non-blocking mode any call may
 // return ncclInProgress; settle() polls it to completion with the GIL released.
+//
+// Lifetime: every use of comm_ happens under mu_, taken only with the GIL released (so a
+// thread waiting for mu_ never holds the GIL another thread needs to finish).  abort()
+// (the Python watchdog's thread) first raises abort_req_: a settle() or finalize loop in
+// flight sees it, aborts the communicator itself and raises, and only then does abort()
+// get mu_ -- comm_ is never freed under a poller.  settle() and the finalize loop also
+// have a deadline (timeout_s): a peer that keeps a call ncclInProgress forever ends in
+// ncclCommAbort + an exception instead of a spin.  async_error() only try-locks: while a
+// call is in flight it answers "healthy" (that call polls the same state itself).
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <rccl/rccl.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <chrono>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -65,10 +76,14 @@ struct InitTimeout : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
+double since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 class Comm {
  public:
   Comm(int nranks, int rank, py::bytes uid, int device, double timeout_s)
-      : nranks_(nranks), rank_(rank), device_(device) {
+      : timeout_s_(timeout_s), nranks_(nranks), rank_(rank), device_(device) {
     std::string u = uid;
     if (u.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("unique id must be 128 bytes");
     ncclUniqueId id;
@@ -88,7 +103,7 @@ class Comm {
       ncclResult_t r = ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg);
       if (r != ncclSuccess && r != ncclInProgress) {
         comm_ = nullptr;
-        destroy();
+        destroy_locked();
         nccl_check(r, "ncclCommInitRankConfig");
       }
       state = r;
@@ -106,89 +121,102 @@ class Comm {
     }
     init_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (!comm_) {
-      destroy();
+      destroy_locked();
       throw InitTimeout("ncclCommInitRankConfig: rank " + std::to_string(rank) + " of " + std::to_string(nranks) +
                         " not joined by all peers within " + std::to_string(timeout_s) + " s (aborted)");
     }
     if (state != ncclSuccess) {
       ncclCommAbort(comm_);
       comm_ = nullptr;
-      destroy();
+      destroy_locked();
       nccl_check(state, "ncclCommInitRankConfig (async)");
     }
   }
 
-  ~Comm() { destroy(); }
-
-  void destroy() {
-    if (comm_) {
-      hipStreamSynchronize(stream_);
-      // non-blocking communicator: finalize (flush) and let it settle before the destroy
-      ncclResult_t st = ncclCommFinalize(comm_);
-      while (st == ncclInProgress) {
-        std::this_thread::yield();
-        if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) break;
-      }
-      ncclCommDestroy(comm_);
-      comm_ = nullptr;
-    }
-    if (stream_) {
-      hipEventDestroy(ready_);
-      hipEventDestroy(done_);
-      hipStreamDestroy(stream_);
-      stream_ = nullptr;
+  ~Comm() {
+    try {
+      destroy();
+    } catch (...) {
     }
   }
 
+  void destroy() {
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> g(mu_);
+    destroy_locked();
+  }
+
   void abort() {
+    abort_req_.store(true);
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> g(mu_);  // a poller in flight aborts and releases first
     if (comm_) {
       ncclCommAbort(comm_);
       comm_ = nullptr;
     }
   }
 
-  // comm stream waits for the work already queued on the compute stream
-  void after(uint64_t compute) {
-    live();
-    hip_check(hipEventRecord(ready_, S(compute)), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(stream_, ready_, 0), "hipStreamWaitEvent");
-  }
-
   void all_reduce(uint64_t buf, size_t count, int dtype, int op, uint64_t compute) {
-    after(compute);
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> g(mu_);
+    after_locked(compute);
     settle(ncclAllReduce(P(buf), P(buf), count, dtype_of(dtype), op_of(op), comm_, stream_), "ncclAllReduce");
   }
 
   void broadcast(uint64_t buf, size_t count, int dtype, int root, uint64_t compute) {
-    after(compute);
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> g(mu_);
+    after_locked(compute);
     settle(ncclBroadcast(P(buf), P(buf), count, dtype_of(dtype), root, comm_, stream_), "ncclBroadcast");
   }
 
   void reduce_scatter(uint64_t send, uint64_t recv, size_t recvcount, int dtype, int op, uint64_t compute) {
-    after(compute);
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> g(mu_);
+    after_locked(compute);
     settle(ncclReduceScatter(P(send), P(recv), recvcount, dtype_of(dtype), op_of(op), comm_, stream_),
            "ncclReduceScatter");
   }
 
   void all_gather(uint64_t send, uint64_t recv, size_t sendcount, int dtype, uint64_t compute) {
-    after(compute);
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> g(mu_);
+    after_locked(compute);
     settle(ncclAllGather(P(send), P(recv), sendcount, dtype_of(dtype), comm_, stream_), "ncclAllGather");
   }
 
   // compute stream waits for every collective issued so far
   void join(uint64_t compute) {
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> g(mu_);
     live();
     hip_check(hipEventRecord(done_, stream_), "hipEventRecord");
     hip_check(hipStreamWaitEvent(S(compute), done_, 0), "hipStreamWaitEvent");
   }
 
+  // polls instead of blocking in hipStreamSynchronize, so an abort ends the wait
   void synchronize() {
     py::gil_scoped_release nogil;
-    hip_check(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    hipStream_t s;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      live();
+      s = stream_;
+    }
+    for (;;) {
+      hipError_t e = hipStreamQuery(s);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) hip_check(e, "hipStreamQuery");
+      if (abort_req_.load()) throw std::runtime_error("synchronize: communicator aborted");
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
   }
 
-  // 0 = healthy; otherwise the ncclResult_t of an asynchronous failure (watchdog)
+  // 0 = healthy (or a call in flight); otherwise the ncclResult_t of an asynchronous failure
   int async_error() {
+    py::gil_scoped_release nogil;
+    std::unique_lock<std::mutex> g(mu_, std::try_to_lock);
+    if (!g.owns_lock()) return 0;
     if (!comm_) return -1;
     ncclResult_t r = ncclSuccess;
     nccl_check(ncclCommGetAsyncError(comm_, &r), "ncclCommGetAsyncError");
@@ -205,18 +233,76 @@ class Comm {
   void live() const {
     if (!comm_) throw std::runtime_error("communicator destroyed or aborted");
   }
+
+  // comm stream waits for the work already queued on the compute stream (mu_ held)
+  void after_locked(uint64_t compute) {
+    live();
+    hip_check(hipEventRecord(ready_, S(compute)), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(stream_, ready_, 0), "hipStreamWaitEvent");
+  }
+
+  void abort_locked() {
+    if (comm_) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+  }
+
   // a non-blocking communicator may answer ncclInProgress: the call is enqueued once its
-  // state settles (the watchdog aborts a communicator whose peer failed, which ends this)
+  // state settles.  Ends on success, an error, abort() or the deadline (mu_ held).
   void settle(ncclResult_t r, const char* what) {
-    if (r == ncclInProgress) {
-      py::gil_scoped_release nogil;
-      do {
-        std::this_thread::yield();
-        if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) break;
-      } while (r == ncclInProgress);
+    auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress) {
+      if (abort_req_.load()) {
+        abort_locked();
+        throw std::runtime_error(std::string(what) + ": communicator aborted");
+      }
+      if (timeout_s_ > 0 && since(t0) > timeout_s_) {
+        abort_locked();
+        throw std::runtime_error(std::string(what) + ": still in progress after " + std::to_string(timeout_s_) +
+                                 " s (communicator aborted)");
+      }
+      std::this_thread::yield();
+      if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) break;
     }
     nccl_check(r, what);
   }
+
+  // finalize (flush) and destroy; abort instead when an abort was asked for or the
+  // finalize does not settle within the deadline (mu_ held, or not shared yet)
+  void destroy_locked() {
+    if (comm_) {
+      if (abort_req_.load()) {
+        abort_locked();
+      } else {
+        hipStreamSynchronize(stream_);
+        ncclResult_t st = ncclCommFinalize(comm_);
+        auto t0 = std::chrono::steady_clock::now();
+        while (st == ncclInProgress) {
+          if (abort_req_.load() || (timeout_s_ > 0 && since(t0) > timeout_s_)) {
+            abort_locked();
+            break;
+          }
+          std::this_thread::yield();
+          if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) break;
+        }
+        if (comm_) {
+          ncclCommDestroy(comm_);
+          comm_ = nullptr;
+        }
+      }
+    }
+    if (stream_) {
+      hipEventDestroy(ready_);
+      hipEventDestroy(done_);
+      hipStreamDestroy(stream_);
+      stream_ = nullptr;
+    }
+  }
+
+  std::mutex mu_;
+  std::atomic<bool> abort_req_{false};
+  double timeout_s_;
   double init_s_ = 0.0;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;

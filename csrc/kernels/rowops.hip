@@ -15,7 +15,6 @@
 #include "ca_mfma_core.h"
 #include "ca_rng.h"
 
-#include <mutex>
 
 namespace {
 
@@ -531,9 +530,13 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const bf16_t* __restrict
   }
   if (tws && dtype && T <= 2) {
     __shared__ int last;
+    // all 4 waves stored rows of tws: each drains its own stores into L2 before the
+    // barrier, so lane 0's agent release (L2 write-back) covers every wave's rows
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the fence's own wait can be dropped
       last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     }
     __syncthreads();
@@ -989,51 +992,16 @@ int ca_embed_sum(const int32_t* ids, const int32_t* tts, const float* word, cons
   return 0;
 }
 
-// Workspace of the deterministic token-type gradient: [64 blocks][2][C] fp32 + a ticket, one per
-// stream (a ticket must never be shared by kernels running concurrently), allocated on first use
-// outside any graph capture (a capture falls back to the atomic form).
-static void embed_type_ws(int C, hipStream_t s, float** ws, unsigned** tk) {
-  static std::mutex mu;
-  static hipStream_t keys[8];
-  static float* bufs[8];
-  static unsigned* tks[8];
-  static int caps[8];
-  static int used = 0;
-  std::lock_guard<std::mutex> lk(mu);
-  int k = 0;
-  while (k < used && keys[k] != s) ++k;
-  if (k < used && caps[k] >= C) {
-    *ws = bufs[k];
-    *tk = tks[k];
-    return;
-  }
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
-  if (k == used && used == 8) return;
-  if (k < used) {  // wider C than before: the stream's old buffer is retired after its work
-    if (hipStreamSynchronize(s) != hipSuccess) return;
-    (void)hipFree(bufs[k]);
-    (void)hipFree(tks[k]);
-  }
-  float* b = nullptr;
-  unsigned* t = nullptr;
-  if (hipMalloc(&b, (size_t)64 * 2 * C * sizeof(float)) != hipSuccess) return;
-  if (hipMalloc(&t, sizeof(unsigned)) != hipSuccess || hipMemset(t, 0, sizeof(unsigned)) != hipSuccess) {
-    (void)hipFree(b);
-    return;
-  }
-  keys[k] = s;
-  bufs[k] = b;
-  tks[k] = t;
-  caps[k] = C;
-  if (k == used) ++used;
-  *ws = b;
-  *tk = t;
-}
-
+// tws / tk: the deterministic token-type reduction's workspace ([64 blocks][2][C] fp32) and
+// its ticket (zero at launch; the kernel's last block resets it), owned by the caller --
+// one per stream, from the caching allocator (cloud_amd/ops/raw.py embed_bwd).
+// Returns 0, or 1 when a gradient took the order-dependent float-atomic path (more than
+// two token types, rows wider than the owner kernel holds, or no workspace given).
 int ca_embed_bwd(const bf16_t* dh, const int32_t* ids, const int32_t* tts, float* dword, float* dpos, float* dtype,
-                 long M, int S, int C, int T, int pos_offset, int pad_id, int V, hipStream_t s) {
+                 long M, int S, int C, int T, int pos_offset, int pad_id, int V, float* tws, unsigned* tk,
+                 hipStream_t s) {
   if (C % 4 != 0) return -1;
+  int nondet = 0;
   // word rows: the owner kernel (deterministic) when its LDS rows hold C; token types (and
   // wide rows) on the segment-pre-reduced atomic scatter
   const bool owner = dword && C <= EW_CMAX && V > 0 && M < (1L << 31);
@@ -1047,17 +1015,17 @@ int ca_embed_bwd(const bf16_t* dh, const int32_t* ids, const int32_t* tts, float
     int grid = ca_cdiv(M, 4 * EB_RW);
     if (!(dword && !owner) && grid > 64) grid = 64;
     if (grid < 1) grid = 1;
-    float* tws = nullptr;
-    unsigned* tk = nullptr;
-    if (dtype && T <= 2 && !(dword && !owner)) embed_type_ws(C, s, &tws, &tk);  // null: atomics
-    embed_bwd_kernel<<<grid, 256, 0, s>>>(dh, ids, tts, owner ? nullptr : dword, dtype, M, C, T, pad_id, tws, tk);
+    const bool det_type = dtype && T <= 2 && !(dword && !owner) && tws && tk;
+    if ((dword && !owner) || (dtype && !det_type)) nondet = 1;
+    embed_bwd_kernel<<<grid, 256, 0, s>>>(dh, ids, tts, owner ? nullptr : dword, dtype, M, C, T, pad_id,
+                                          det_type ? tws : nullptr, det_type ? tk : nullptr);
     CA_LAUNCH_CHECK();
   }
   if (dpos) {
     embed_pos_bwd_kernel<<<ca_cdiv((long)S * (C / 4), 256), 256, 0, s>>>(dh, dpos, M, S, C, pos_offset);
     CA_LAUNCH_CHECK();
   }
-  return 0;
+  return nondet;
 }
 
 int ca_dropout(const bf16_t* x, bf16_t* y, long n, float p, uint64_t seed, hipStream_t s) {

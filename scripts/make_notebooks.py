@@ -201,6 +201,12 @@ SIMPLE_REMOTE_DIR = os.path.join(REMOTE_DIR, str(uuid.uuid4()))
 job_id = client.cloud_fit(model=simple_model, remote_dir=SIMPLE_REMOTE_DIR, x=x, y=y,
                           epochs=5 if SMALL else 100, batch_size=len(x), verbose=2)
 """),
+    ("md", "`cloud_fit` returns as soon as the job is submitted; the job runs under its own supervisor "
+           "(`python -m cloud_amd.jobs describe|stream-logs <job_id>` from any shell). Wait for it here:"),
+    ("code", """
+from cloud_amd.core.launcher import Job
+assert Job.attach(job_id).wait() == 0
+"""),
     ("code", """
 trained = tf.keras.models.load_model(os.path.join(SIMPLE_REMOTE_DIR, "output"))
 print("RESULT cloud_fit_nb job={} loss={:.4f}".format(job_id, trained.evaluate(x, y)))

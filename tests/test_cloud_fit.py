@@ -85,6 +85,10 @@ def test_cloud_fit_two_process_job(tmp_path, monkeypatch):
     job_id = client.cloud_fit(_model(), rd, x=x, y=y, epochs=2, batch_size=32,
                               callbacks=[CountingCallback(str(tmp_path))], job_id="cloud_fit_test")
     assert job_id == "cloud_fit_test"
+    # returns at submission (reference client.py:227-286); the detached job finishes on its own
+    from cloud_amd.core import launcher
+
+    assert launcher.Job.attach(job_id).wait(300) == 0
     meta = json.load(open(tmp_path / "jobs" / job_id / "job.json"))
     assert meta["state"] == "SUCCEEDED" and meta["world_size"] == 2
     assert os.path.exists(os.path.join(rd, "output", "weights.pt"))

@@ -65,7 +65,8 @@ def _count_syncs(fn):
 
 def _worker(rank, port, out_path, transport, wire, sliced=False):
     os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                      CLOUD_AMD_COMM=transport, CLOUD_AMD_GRAD_REDUCE_DTYPE=wire)
+                      CLOUD_AMD_COMM=transport, CLOUD_AMD_GRAD_REDUCE_DTYPE=wire,
+                      CLOUD_AMD_SLICED_OPT="1" if sliced else "0")  # opt-in since round 6
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
 
@@ -146,7 +147,7 @@ def _worker(rank, port, out_path, transport, wire, sliced=False):
 @pytest.mark.parametrize("wire,sliced", [("bf16", True), ("fp32", True), ("fp32", False)])
 def test_rccl_data_plane_world1_forced_multirank(tmp_path, transport, wire, sliced):
     """``sliced``: the fused SGD runs per bucket on its own stream as each bucket's collective
-    completes (``attach_optimizer``, the multi-GPU default); the weights must still be BITWISE
+    completes (``attach_optimizer``, opt-in ``CLOUD_AMD_SLICED_OPT=1``); the weights must still be BITWISE
     those of the whole-arena step without DP."""
     out = str(tmp_path / "r.pt")
     mp.spawn(_worker, args=(_free_port(), out, transport, wire, sliced), nprocs=1, join=True)

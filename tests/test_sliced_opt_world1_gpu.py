@@ -49,6 +49,9 @@ def _bert_run(sliced, steps=1):
 
 
 def test_bert_adamw_sliced_world1_is_bitwise_whole_step():
+    from cloud_amd.ops import raw
+
+    n0 = raw.EMBED_NONDETERMINISTIC_CALLS
     a, la = _bert_run(True, steps=3)
     gc.collect()
     b, lb = _bert_run(False, steps=3)
@@ -58,6 +61,9 @@ def test_bert_adamw_sliced_world1_is_bitwise_whole_step():
     # profiles/r5_s23/)
     for n in a:
         assert torch.equal(a[n], b[n]), n
+    # ... and no embedding gradient took the order-dependent atomic path (a silent fallback
+    # would make this comparison pass or fail by luck)
+    assert raw.EMBED_NONDETERMINISTIC_CALLS == n0
 
 
 def _resnet_run(sliced, steps=3):
