@@ -68,6 +68,10 @@ def parse(argv=None):
     ap.add_argument("--grad-reduce-dtype", choices=("auto", "bf16", "fp32", "native"), default=None,
                     help="wire dtype of the gradient all-reduce (default auto: bf16 for every bucket of a bf16 model)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--ab", type=int, default=1,
+                    help="N > 1: after the timed region, a <= 5-step A/B per DP-engine cell (per-bucket optimizer "
+                         "on/off x buckets 16/32/64 MB x torch/native RCCL; CLOUD_AMD_BENCH_AB selects cells)")
+    ap.add_argument("--ab-steps", type=int, default=5)
     ap.add_argument("--via-run", type=int, default=int(os.environ.get("CLOUD_AMD_BENCH_VIA_RUN", "1")),
                     help="1 (default): launch the ranks through cloud_amd.run(); 0: train in this process")
     return ap.parse_args(argv)
@@ -160,11 +164,13 @@ def main():
             loss.backward()
         return loss.detach()  # never keep the autograd graph alive across steps
 
+    holder = {"red": reducer}  # the DP A/B cells after the timed region swap reducers
+
     def train_step():
         opt.zero_grad()
         loss = fwd_bwd()
         with trace.range("allreduce_join"):
-            reducer.finish()
+            holder["red"].finish()
         with trace.range("optimizer"):
             opt.step()
         return loss
@@ -228,7 +234,7 @@ def main():
         [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)] if evs else None, host_ms,
         host0, benchlaunch.host_state(), probe=step_probe.close(), paced_ms=paced_ms)
     comm = reducer.timing_summary()
-    budget = reducer.overlap_budget()
+    budget = reducer.overlap_budget(optimizer=opt)
     per_rank_ms = [v / args.steps * 1000.0 for v in dist_env.all_gather_floats(t1 - t0, device)]
     elapsed = dist_env.all_reduce_max(t1 - t0, device)
     ms = elapsed / args.steps * 1000.0
@@ -250,6 +256,7 @@ def main():
         monitoring.observe(monitoring.STEP_TIME, ms)
     except Exception:
         pass
+    out = None
     if rank == 0:
         launched = benchlaunch.launched_via()
         backend = "none"
@@ -295,11 +302,36 @@ def main():
             "final_loss": round(final_loss, 4),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2**30, 2) if on_gpu else None,
         }
+
+    def emit(ab=None):
+        if out is None:
+            return
+        if ab is not None:
+            out["dp_ab"] = {"cells": ab, "best": dp_ab.best(ab), "steps_per_cell": args.ab_steps,
+                            "note": "after the timed region; value above is the default configuration"}
         line = json.dumps(_finite(out), allow_nan=False)
         print(line, flush=True)
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+
+    # N > 1: a bounded step-level A/B of the DP knobs no one-GPU box can settle (per-bucket
+    # optimizer, bucket size, transport) -- cloud_amd/utils/dp_ab.py
+    from cloud_amd.utils import dp_ab
+
+    cells = dp_ab.cells_from_env() if (world > 1 and args.ab) else []
+    if cells:
+        dp_ab.teardown(reducer)
+        ab = []
+
+        def build(bucket_mb):
+            return strategy.gradient_reducer(opt.arenas, bucket_mb=bucket_mb, reduce_dtype=args.grad_reduce_dtype)
+
+        dp_ab.run_cells(build, lambda r: holder.__setitem__("red", r), train_step, opt, device, cells,
+                        steps=args.ab_steps, on_timeout=lambda res: emit(list(res)), results=ab)
+        emit(ab)
+    else:
+        emit()
     if world > 1:
         import torch.distributed as dist
 

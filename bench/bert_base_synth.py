@@ -40,6 +40,11 @@ def parse():
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--grad-reduce-dtype", choices=("auto", "bf16", "fp32", "native"), default=None)
+    ap.add_argument("--ab", type=int, default=1, help="N > 1: DP-engine A/B cells after the timed region")
+    ap.add_argument("--ab-steps", type=int, default=5)
+    ap.add_argument("--embed-wire", choices=("bf16", "native"), default="bf16",
+                    help="wire dtype of the word-embedding table's gradient all-reduce (split into pipelined "
+                         "sub-buckets; bf16 halves its bytes -- error bound: tests/test_grad_reduce_precision.py)")
     ap.add_argument("--via-run", type=int, default=int(os.environ.get("CLOUD_AMD_BENCH_VIA_RUN", "1")))
     return ap.parse_args()
 
@@ -138,18 +143,23 @@ def main():
 
         cfg = BertConfig.base(num_hidden_layers=args.layers, num_labels=2)
         model = BertForSequenceClassification(cfg, device=device)
+        if args.embed_wire == "bf16":
+            # the table's gradient is the last one backward produces: its collective is exposed
+            model.embeddings.word._ca_wire_dtype = torch.bfloat16
         opt = AdamW(model, learning_rate=args.lr, weight_decay=0.01, grad_scale=1.0 / world)
         reducer = strategy.gradient_reducer(opt.arenas, bucket_mb=args.bucket_mb,
                                             reduce_dtype=args.grad_reduce_dtype)
         reducer.broadcast_parameters()
         reducer.attach_optimizer(opt)  # world > 1: AdamW per bucket as each all-reduce completes
 
+        holder = {"red": reducer}  # the DP A/B cells after the timed region swap reducers
+
         def train_step():
             opt.zero_grad()
             logits = model(ids, tts, am)
             loss, _ = softmax_cross_entropy(logits, labels, denom=B)
             loss.backward()
-            reducer.finish()
+            holder["red"].finish()
             opt.step()
             return loss
         impl = "cloud_amd: fused layer fwd/bwd, MFMA GEMM epilogues, fused attention/LN, AdamW arena"
@@ -213,9 +223,10 @@ def main():
         comm = dict(reducer.describe(), allreduce_ms=dist_env.all_reduce_max(t["allreduce_ms"], device),
                     exposed_comm_ms=dist_env.all_reduce_max(t["exposed_comm_ms"], device), timing=t.get("timing"),
                     busbw_gbs=busbw, comm_probe=probe, sliced_optimizer=reducer.optimizer is not None,
-                    overlap_budget=reducer.overlap_budget())
+                    overlap_budget=reducer.overlap_budget(optimizer=opt), embed_wire=args.embed_wire)
+    out = None
     if rank == 0:
-        print(json.dumps(_finite({
+        out = ({
             "metric": "sequences/sec BERT-base fine-tune synthetic GLUE (seq %d)" % S,
             "value": round(sps, 2), "unit": "sequences/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1000, 3), "higher_is_better": True,
@@ -233,8 +244,32 @@ def main():
             "tokens_per_sec": round(sps * S, 1), "final_loss": round(float(loss.detach().float()), 4),
             "strategy": strategy.name, "replicas_consistent": replicas_consistent,
             "rank_ms_per_step": {"min": round(min(per_rank), 3), "max": round(max(per_rank), 3)},
-            "plain_gemm_engine": _plain_gemm_summary()}),
-            allow_nan=False), flush=True)
+            "plain_gemm_engine": _plain_gemm_summary()})
+
+    def emit(ab=None):
+        if out is None:
+            return
+        if ab is not None:
+            out["dp_ab"] = {"cells": ab, "best": dp_ab.best(ab), "steps_per_cell": args.ab_steps,
+                            "note": "after the timed region; value above is the default configuration"}
+        print(json.dumps(_finite(out), allow_nan=False), flush=True)
+
+    # N > 1: bounded step-level A/B of the DP knobs (cloud_amd/utils/dp_ab.py)
+    from cloud_amd.utils import dp_ab
+
+    cells = dp_ab.cells_from_env() if (world > 1 and args.ab and reducer is not None) else []
+    if cells:
+        dp_ab.teardown(reducer)
+        ab = []
+
+        def build(bucket_mb):
+            return strategy.gradient_reducer(opt.arenas, bucket_mb=bucket_mb, reduce_dtype=args.grad_reduce_dtype)
+
+        dp_ab.run_cells(build, lambda r: holder.__setitem__("red", r), train_step, opt, device, cells,
+                        steps=args.ab_steps, on_timeout=lambda res: emit(list(res)), results=ab)
+        emit(ab)
+    else:
+        emit()
     if world > 1:
         import torch.distributed as dist
 

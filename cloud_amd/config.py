@@ -207,6 +207,12 @@ _VARS = [
         "(Horovod DistributedGradientTape semantics); 'replica' -- per-replica gradients, summed in "
         "apply_gradients (TF MirroredStrategy semantics: a clip between the two sees one replica's gradient)",
         "distributed"),
+    Var("CLOUD_AMD_SPLIT_PARAM_MB", float, 0.0, "a parameter larger than this is all-reduced as >= "
+        "CLOUD_AMD_SPLIT_PARAM_MIN sub-buckets of about one bucket each, pipelined with the per-bucket optimizer "
+        "(0 / unset: twice the bucket size)", "distributed"),
+    Var("CLOUD_AMD_SPLIT_PARAM_MIN", int, 4, "minimum chunks of a split parameter", "distributed"),
+    Var("CLOUD_AMD_BENCH_AB", str, "1", "benches at N > 1: DP-engine A/B cells after the timed region ('0' off, "
+        "'1' the 12 default cells, or 'transport:bucket_mb:sliced,...')", "bench"),
     Var("CLOUD_AMD_SLICED_OPT_WORLD1", bool, False, "one GPU: start each gradient bucket's optimizer slice as soon "
         "as its gradients are final, beside the rest of backward (measured slower on MI355X: off by default)",
         "distributed"),

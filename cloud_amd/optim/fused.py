@@ -166,6 +166,18 @@ class FusedOptimizer:
                 hv = self._slice_hv[wd] = [float(v) for v in self._hp_values(wd)]
             self._update(ai, arena, a, b, None, hv)
 
+    def update_bytes_per_elem(self, arena):
+        """HBM bytes one element of ``arena`` moves through the fused update (master read +
+        write, optimizer state read + write, gradient read + in-kernel zero, model-copy
+        write): the DP engine's overlap budget prices an update slice with it."""
+        ai = self.arenas.index(arena)
+        st = self.state[ai]
+        b = 2 * arena.master.element_size() + 2 * arena.grad.element_size()
+        b += sum(2 * t.element_size() for t in st.values() if t.numel() == arena.n)
+        if arena.model is not None:
+            b += arena.model.element_size()
+        return b
+
     def sliced_end_pending(self):
         """Every slice of this step has been issued: the next ``step()`` only closes it."""
         self._sliced_done = True

@@ -96,10 +96,12 @@ class _TorchTransport:
 
 class Bucket:
     __slots__ = ("arena", "lo", "hi", "slots", "pending", "work", "launched", "index", "wire", "wire_buf", "ev",
-                 "span", "ready_ev")
+                 "span", "ready_ev", "wire_dtype", "part")
 
-    def __init__(self, arena, lo, hi, slots, index):
+    def __init__(self, arena, lo, hi, slots, index, wire_dtype=None, part=None):
         self.arena, self.lo, self.hi, self.slots, self.index = arena, lo, hi, slots, index
+        self.wire_dtype = wire_dtype  # per-bucket wire dtype (None: the reducer's)
+        self.part = part  # (k, n): chunk k of n of one split parameter, else None
         self.pending = len(slots)
         self.work = None
         self.launched = False
@@ -116,8 +118,10 @@ class Bucket:
 
 class GradAllReducer:
     def __init__(self, arenas, process_group=None, bucket_mb=None, overlap=True, reduce_dtype=None,
-                 transport=None, world=None):
+                 transport=None, world=None, wire_dtypes=None):
         self.arenas = arenas
+        # per-parameter wire dtype overrides {param: dtype} (see _param_wire)
+        self._wire_overrides = {id(p): dt for p, dt in (wire_dtypes or {}).items()}
         self.pg = process_group
         if world is None:
             world = dist.get_world_size(process_group) if dist.is_initialized() else 1
@@ -200,17 +204,47 @@ class GradAllReducer:
             self._install_hooks()
             _ACTIVE.add(self)
 
+    def _param_wire(self, p):
+        """Wire dtype override of one parameter: ``wire_dtypes[p]`` given to the reducer, or
+        the parameter's ``_ca_wire_dtype`` attribute (e.g. BERT's word-embedding table)."""
+        dt = self._wire_overrides.get(id(p)) if self._wire_overrides else None
+        return dt if dt is not None else getattr(p, "_ca_wire_dtype", None)
+
     def _build(self):
         # An arena is in reverse forward order, so its LAST bucket holds the first layers,
         # whose gradients exist only when backward ends: that all-reduce is never hidden
         # behind compute.  Each arena's final bucket is capped at CLOUD_AMD_TAIL_BUCKET_MB
         # (split off the end of the arena) so the exposed collectives are small ones.
+        #
+        # A parameter larger than CLOUD_AMD_SPLIT_PARAM_MB (default 2 buckets) is cut into
+        # sub-buckets of about one bucket each (at least CLOUD_AMD_SPLIT_PARAM_MIN chunks): all
+        # become ready together (one gradient), then go on the wire one after another, so with
+        # the per-bucket optimizer chunk k's update runs while chunk k+1 is in flight -- BERT's
+        # 91 MB word-embedding gradient, produced last in backward, is otherwise one
+        # collective followed by one serial AdamW over the whole table.
         tail = int(float(os.environ.get("CLOUD_AMD_TAIL_BUCKET_MB", 1.0)) * (1 << 20))
+        split_mb = float(os.environ.get("CLOUD_AMD_SPLIT_PARAM_MB") or 0) or 2 * self.bucket_mb
+        split_bytes = int(split_mb * (1 << 20))
+        min_chunks = max(int(os.environ.get("CLOUD_AMD_SPLIT_PARAM_MIN", 4)), 1)
         for a in self.arenas:
             es = a.grad.element_size()
             cur, lo = [], 0
             for s in a.slots:
                 end = s.offset + ((s.numel + 63) // 64) * 64
+                nbytes = (end - s.offset) * es
+                if split_bytes > 0 and nbytes > split_bytes:
+                    # close the open bucket at this slot, then the slot's own chunks
+                    if cur:
+                        self.buckets.append(Bucket(a, lo, s.offset, cur, len(self.buckets)))
+                    n = max(-(-nbytes // self.bucket_bytes), min_chunks)
+                    step = -(-((end - s.offset) // 64) // n) * 64
+                    cuts = list(range(s.offset, end, step)) + [end]
+                    wd = self._param_wire(s.param)
+                    for k in range(len(cuts) - 1):
+                        self.buckets.append(Bucket(a, cuts[k], cuts[k + 1], [s], len(self.buckets), wire_dtype=wd,
+                                                   part=(k, len(cuts) - 1)))
+                    cur, lo = [], end
+                    continue
                 cur.append(s)
                 if (end - lo) * es >= self.bucket_bytes:
                     self.buckets.append(Bucket(a, lo, end, cur, len(self.buckets)))
@@ -224,19 +258,26 @@ class GradAllReducer:
                     self.buckets.append(Bucket(a, lo, cut, cur[:k], len(self.buckets)))
                     cur, lo = cur[k:], cut
                 self.buckets.append(Bucket(a, lo, a.n, cur, len(self.buckets)))
+        # buckets of whole slots take a per-parameter wire dtype only when every slot agrees
+        for b in self.buckets:
+            if b.part is None:
+                dts = {self._param_wire(s.param) for s in b.slots}
+                if len(dts) == 1:
+                    b.wire_dtype = dts.pop()
         # Launch order = the order buckets COMPLETE in backward (their last slot in reverse
         # registration order), across arenas -- not arena by arena: BERT's fp32 arena starts
         # with the word-embedding table, whose gradient is the very last one backward produces,
         # and a strictly ordered launch would hold every bf16 bucket behind it (nothing
         # overlapped; overlap_budget showed ~1.5 ms exposed at 300 GB/s).  Every rank builds the
-        # same order from the same model.
+        # same order from the same model.  (Chunks of one parameter keep their order.)
         if os.environ.get("CLOUD_AMD_BUCKET_ORDER", "ready") == "ready":
             self.buckets.sort(key=lambda b: (max(s.seq for s in b.slots), b.index))
             for i, b in enumerate(self.buckets):
                 b.index = i
         for b in self.buckets:
             for s in b.slots:
-                self._param_bucket[id(s.param)] = (s.param, b)
+                ent = self._param_bucket.setdefault(id(s.param), (s.param, []))
+                ent[1].append(b)
 
     def _install_hooks(self):
         for b in self.buckets:
@@ -265,25 +306,32 @@ class GradAllReducer:
         pb = self._param_bucket.get(id(p))
         # (identity checked: a dead reducer's id(param) keys can be reused by another model's
         # parameters while the dead one still sits in _ACTIVE awaiting cycle collection)
-        b = pb[1] if pb is not None and pb[0] is p else None
-        if b is None or b.launched:
-            return
-        b.pending -= 1
-        if b.pending <= 0:
-            if self._probe:
-                ev = torch.cuda.Event(enable_timing=True)
-                ev.record(torch.cuda.current_stream(b.tensor.device))
-                b.ready_ev = ev
-            # world 1: hooks exist for the readiness probe and / or the per-slice optimizer
-            if self.world > 1 or self.optimizer is not None or not self._probe:
-                self._launch_ready()
+        bs = pb[1] if pb is not None and pb[0] is p else ()
+        ready = False
+        for b in bs:  # one bucket, or every chunk of a split parameter
+            if b.launched:
+                continue
+            b.pending -= 1
+            if b.pending <= 0:
+                ready = True
+                if self._probe:
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record(torch.cuda.current_stream(b.tensor.device))
+                    b.ready_ev = ev
+        # world 1: hooks exist for the readiness probe and / or the per-slice optimizer
+        if ready and (self.world > 1 or self.optimizer is not None or not self._probe):
+            self._launch_ready()
+
+    def _wire_dtype(self, b):
+        return b.wire_dtype if b.wire_dtype is not None else (self.reduce_dtype or b.tensor.dtype)
 
     def _wire(self, b):
         """The tensor this bucket's collective reduces; runs on the comm stream."""
-        if self.reduce_dtype is None or self.reduce_dtype == b.tensor.dtype:
+        dt = self._wire_dtype(b)
+        if dt == b.tensor.dtype:
             return b.tensor
         if b.wire_buf is None:
-            b.wire_buf = torch.empty(b.hi - b.lo, dtype=self.reduce_dtype, device=b.tensor.device)
+            b.wire_buf = torch.empty(b.hi - b.lo, dtype=dt, device=b.tensor.device)
         b.wire_buf.copy_(b.tensor)
         b.wire = b.wire_buf
         return b.wire
@@ -532,11 +580,13 @@ class GradAllReducer:
         def name(dt):
             return str(dt).replace("torch.", "")
 
-        wire = sorted({name(self.reduce_dtype or a.grad.dtype) for a in self.arenas})
-        wire_mb = sum((b.hi - b.lo) * (self.reduce_dtype or b.tensor.dtype).itemsize for b in self.buckets) / 2 ** 20
+        wire = sorted({name(self._wire_dtype(b)) for b in self.buckets})
+        wire_mb = sum((b.hi - b.lo) * self._wire_dtype(b).itemsize for b in self.buckets) / 2 ** 20
+        split = sorted({(b.part[1], name(self._wire_dtype(b))) for b in self.buckets if b.part is not None})
         return {"buckets": len(self.buckets), "bucket_mb": self.bucket_mb,
                 "reduce_dtype": wire[0] if len(wire) == 1 else "mixed(%s)" % ",".join(wire),
                 "grad_dtypes": sorted({name(a.grad.dtype) for a in self.arenas}),
+                "split_params": [{"chunks": n, "wire": w} for n, w in split],
                 "wire_mb_per_step": round(wire_mb, 2), "transport": transport, "world": self.world}
 
     # -- per-slice optimizer ---------------------------------------------------------
@@ -609,12 +659,19 @@ class GradAllReducer:
         self._ready_log.append((end, [b.ready_ev for b in self.buckets]))
         self._ready_log = self._ready_log[-64:]
 
-    def overlap_budget(self, busbw_gbs=(150.0, 300.0), world=None):
+    def overlap_budget(self, busbw_gbs=(150.0, 300.0), world=None, optimizer=None, hbm_gbs=5000.0):
         """Per bucket: wire MB and how many ms before the end of backward its gradients were
         ready (mean over the probed steps; 0 for buckets completed only by ``finish``), and the
         exposed communication PREDICTED for a serial comm path at each bus bandwidth (nccl-tests
         convention: a bucket of B bytes takes B * 2(n-1)/n / busbw) with n = ``world`` (default:
-        this job's world, 8 at world 1).  Call after a device synchronize."""
+        this job's world, 8 at world 1).
+
+        With an ``optimizer`` (default: the attached per-bucket one) the prediction also prices
+        the update slices at ``hbm_gbs``: ``predicted_exposed_step_ms`` is the time from the end
+        of backward until the last slice has run when each bucket's slice follows its collective
+        on one optimizer stream (the per-bucket optimizer), and ``predicted_exposed_whole_ms``
+        the same with the whole-arena update after the last collective -- both beyond the
+        backward; the difference is what slicing buys.  Call after a device synchronize."""
         if not self._ready_log:
             return None
         n = world or (self.world if self.world > 1 else 8)
@@ -625,18 +682,34 @@ class GradAllReducer:
                 if ev is not None:
                     before[i] += max(ev.elapsed_time(end), 0.0)
         before = [v / len(self._ready_log) for v in before]
-        mb = [(b.hi - b.lo) * (self.reduce_dtype or b.tensor.dtype).itemsize / 2 ** 20 for b in self.buckets]
-        pred = {}
+        mb = [(b.hi - b.lo) * self._wire_dtype(b).itemsize / 2 ** 20 for b in self.buckets]
+        opt = optimizer if optimizer is not None else self.optimizer
+        upd = None
+        if opt is not None and hasattr(opt, "update_bytes_per_elem"):
+            upd = [(b.hi - b.lo) * opt.update_bytes_per_elem(b.arena) / (hbm_gbs * 1e9) * 1e3 for b in self.buckets]
+        pred, pred_step, pred_whole = {}, {}, {}
         for bw in busbw_gbs:
             t_end = None
+            t_opt = None  # end of the last update slice issued (one optimizer stream)
             for i in range(nb):  # launch order = bucket order
                 dur = mb[i] * 2 ** 20 * 2.0 * (n - 1) / n / (bw * 1e9) * 1e3
                 start = -before[i] if t_end is None else max(-before[i], t_end)
                 t_end = start + dur
+                if upd is not None:
+                    t_opt = max(t_end, t_opt if t_opt is not None else t_end) + upd[i]
             pred["%g" % bw] = round(max(t_end or 0.0, 0.0), 3)
-        return {"world_predicted": n, "steps": len(self._ready_log),
-                "buckets": [{"mb": round(m, 2), "ready_before_bwd_end_ms": round(v, 3)} for m, v in zip(mb, before)],
-                "predicted_exposed_comm_ms": pred}
+            if upd is not None:
+                pred_step["%g" % bw] = round(max(t_opt or 0.0, 0.0), 3)
+                pred_whole["%g" % bw] = round(max(t_end or 0.0, 0.0) + sum(upd), 3)
+        out = {"world_predicted": n, "steps": len(self._ready_log),
+               "buckets": [{"mb": round(m, 2), "ready_before_bwd_end_ms": round(v, 3),
+                            "wire": str(self._wire_dtype(b)).replace("torch.", "")}
+                           for m, v, b in zip(mb, before, self.buckets)],
+               "predicted_exposed_comm_ms": pred}
+        if upd is not None:
+            out.update({"hbm_gbs": hbm_gbs, "update_ms_total": round(sum(upd), 3),
+                        "predicted_exposed_step_ms": pred_step, "predicted_exposed_whole_ms": pred_whole})
+        return out
 
     def broadcast_parameters(self, src=0):
         """C2: make every rank start from rank ``src``'s weights (one call per arena)."""

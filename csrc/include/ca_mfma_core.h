@@ -365,7 +365,7 @@ struct DenseNC {
 // keep the padded layout (row stride 36 banks: conflict-free for the same pattern).
 template <int BN>
 struct EpiLayout {
-  static constexpr bool SWZ = (BN >= 128);
+  static constexpr bool SWZ = (BN >= 128) && (BN & (BN - 1)) == 0;  // XOR stays inside a power-of-two row
   static constexpr int LD = SWZ ? BN : BN + PAD;
   __device__ static __forceinline__ int idx(int row, int col) {
     return SWZ ? row * LD + (col ^ ((row & 15) << 3)) : row * LD + col;

@@ -16,6 +16,7 @@
 
 #include "ca_gemm256.h"
 #include "ca_gemm256p8.h"
+#include "ca_gemm_w4.h"
 
 using namespace ca;
 
@@ -112,6 +113,17 @@ static void launch128x96(const CoreParams& p, int layout, dim3 g, hipStream_t s)
 }
 static void launch256x96(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
   if (layout == 0) k256x96<GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
+}
+
+// four waves, one workgroup per CU, accumulators in AGPRs (ca_gemm_w4.h)
+template <int BN, template <int, int, int> class GA, template <int, int, int> class GB>
+__global__ void __launch_bounds__(256, 1) kw4(CoreParams P) {
+  mfma_gemm_w4<BN, GA, GB, EPI_BF16>(P);
+}
+template <int BN>
+static void launchw4(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) kw4<BN, GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
+  else if (layout == 1) kw4<BN, GDenseKC, GDenseNC><<<g, 256, 0, s>>>(p);
 }
 
 struct Variant {
@@ -228,7 +240,11 @@ int main(int argc, char** argv) {
                     {"glds128", 128, 128, launch128},
                     {"g128x64", 128, 64, launch128x64},
                     {"g128x96", 128, 96, launch128x96},
-                    {"g256x96", 256, 96, launch256x96}};
+                    {"g256x96", 256, 96, launch256x96},
+                    {"w4n256", 256, 256, launchw4<256>},
+                    {"w4n192", 256, 192, launchw4<192>},
+                    {"w4n160", 256, 160, launchw4<160>},
+                    {"w4n128", 256, 128, launchw4<128>}};
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
   hipEvent_t e0, e1;
@@ -256,6 +272,7 @@ int main(int argc, char** argv) {
     for (const Variant& v : vars) {
       if (only && !strstr(only, v.name)) continue;
       if ((v.launch == launch128x96 || v.launch == launch256x96) && L != 0) continue;
+      if (strncmp(v.name, "w4", 2) == 0 && (L == 2 || (L == 1 && v.bn != 256 && v.bn != 128))) continue;
       CoreParams p{};
       p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.C = C; p.ldc = N;
       p.M = M; p.N = N; p.K = K; p.k_per_split = K; p.split_xcd = 1;

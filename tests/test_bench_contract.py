@@ -52,6 +52,19 @@ def test_bench_two_ranks_via_run_cpu(tmp_path):
     assert len(ss["probe_steps"]) == 2 and len(ss["host_launch_ms_steps"]) == 2
     assert {"gc_ms", "gc_gen", "minflt", "majflt", "dev_alloc"} <= set(ss["probe_steps"][0])
     assert j["gc_frozen_objects"] > 0  # runtime.gc_control.freeze() ran after warmup
+    # N > 1: the DP-engine A/B after the timed region: 12 cells of <= 5
+    # timed steps -- per-bucket optimizer x bucket size x transport -- each with ms/step and
+    # the exposed communication; the headline value is the default configuration's
+    ab = j["dp_ab"]
+    cells = ab["cells"]
+    assert len(cells) == 12 and ab["steps_per_cell"] == 5
+    assert {(c["transport"], c["bucket_mb"], c["sliced"]) for c in cells} == {
+        (t, b, sl) for t in ("torch", "rccl") for b in (16.0, 32.0, 64.0) for sl in (False, True)}
+    for c in cells:
+        assert "error" not in c, c
+        assert c["ms_per_step"] > 0 and c["exposed_comm_ms"] >= 0 and c["steps"] == 5 and c["buckets"] >= 1
+        assert c["sliced_active"] is False  # gloo is not stream-ordered: the cell reports it ran whole-arena
+    assert ab["best"] in cells
     job = os.listdir(tmp_path / "jobs")
     assert len(job) == 1
     meta = json.load(open(tmp_path / "jobs" / job[0] / "job.json"))

@@ -233,3 +233,41 @@ def test_deferred_gradient_counted_only_by_explicit_notify(explicit):
     assert launched and all(e[2] for e in launched)
     red.finish()
     torch.testing.assert_close(w.grad, 2.0 * gw)
+
+
+def test_large_parameter_split_into_pipelined_sub_buckets():
+    """A parameter larger than CLOUD_AMD_SPLIT_PARAM_MB is reduced as >= 4 chunks of about one
+    bucket each (BERT's 91 MB word-embedding gradient): the chunks cover
+    it exactly, launch back to back in chunk order once its gradient exists, carry the
+    parameter's own wire dtype, and the reduced gradient equals the unsplit one."""
+    torch.manual_seed(0)
+    emb = torch.nn.Embedding(4096, 64)   # 1 MB fp32: split at 0.25 MB
+    head = torch.nn.Linear(64, 8)
+    model = torch.nn.Sequential(emb, head)
+    emb.weight._ca_wire_dtype = torch.bfloat16
+    opt = SGD(model, learning_rate=0.1)
+    ref = [None]
+    fake = FakeComm(ref)
+    os.environ["CLOUD_AMD_SPLIT_PARAM_MB"] = "0.25"
+    try:
+        red = GradAllReducer(opt.arenas, bucket_mb=0.125, transport=fake, world=2)
+    finally:
+        del os.environ["CLOUD_AMD_SPLIT_PARAM_MB"]
+    ref[0] = red
+    parts = [b for b in red.buckets if b.part is not None]
+    assert len(parts) >= 4 and all(b.part[1] == len(parts) for b in parts)
+    assert [b.part[0] for b in parts] == list(range(len(parts)))  # launch order = chunk order
+    assert sum(b.hi - b.lo for b in parts) >= emb.weight.numel()
+    assert all(b.wire_dtype == torch.bfloat16 for b in parts)
+    assert all(b.wire_dtype is None for b in red.buckets if b.part is None)
+    d = red.describe()
+    assert d["split_params"] == [{"chunks": len(parts), "wire": "bfloat16"}]
+    ids = torch.randint(0, 4096, (32,))
+    opt.zero_grad()
+    head(emb(ids)).square().sum().backward()
+    expect = emb.weight.grad.detach().clone()
+    red.finish()
+    launches = [e for e in fake.log if e[0] == "launch"]
+    assert all(ok for _, _, ok in launches)
+    # FakeWork doubles the wire tensor (2 replicas); the bf16 wire rounds each chunk once
+    torch.testing.assert_close(emb.weight.grad, (2 * expect).bfloat16().float(), rtol=0, atol=0)

@@ -68,6 +68,19 @@ def _worker(rank, port, out_dir):
         red.finish()
         bert[wire] = {"emb": emb.grad.flatten().tolist(), "ln": ln.grad.tolist(),
                       "describe": red.describe()}
+    # per-parameter wire (round 6): the embedding table alone on a bf16 wire, split into >= 4
+    # pipelined chunks; the LayerNorm vectors keep fp32 sums
+    os.environ["CLOUD_AMD_SPLIT_PARAM_MB"] = "0.5"
+    emb = torch.nn.Parameter(torch.zeros(EMB_ROWS, 768))
+    emb._ca_wire_dtype = torch.bfloat16
+    ln = torch.nn.Parameter(torch.zeros(LN))
+    opt = SGD([emb, ln], learning_rate=0.0)
+    red = GradAllReducer(opt.arenas, bucket_mb=1.0)
+    ge, gl = _bert_grads(rank)
+    emb.grad.copy_(ge)
+    ln.grad.copy_(gl)
+    red.finish()
+    bert["split"] = {"emb": emb.grad.flatten().tolist(), "ln": ln.grad.tolist(), "describe": red.describe()}
     if rank == 0:
         with open(os.path.join(out_dir, "sums.json"), "w") as f:
             json.dump(res, f)
@@ -122,4 +135,12 @@ def test_bf16_vs_fp32_wire_error_at_8_ranks(tmp_path):
     assert d_bf["reduce_dtype"] == "bfloat16" and d_fp["reduce_dtype"] == "float32"
     assert d_bf["grad_dtypes"] == ["float32"]
     assert abs(d_bf["wire_mb_per_step"] * 2 - d_fp["wire_mb_per_step"]) < 0.05  # half the bytes
+    for k, ex in (("emb", emb_exact), ("ln", ln_exact)):
+        got = torch.tensor(bert["split"][k], dtype=torch.float64)
+        berr["split_" + k] = float((got - ex).norm() / ex.norm())
+    assert berr["split_emb"] < 3.0 * ulp and berr["split_ln"] < 1e-6, berr
+    d_sp = bert["split"]["describe"]
+    assert d_sp["split_params"] and d_sp["split_params"][0]["chunks"] >= 4
+    assert d_sp["split_params"][0]["wire"] == "bfloat16"
+    assert d_bf["wire_mb_per_step"] - 0.05 < d_sp["wire_mb_per_step"] < d_fp["wire_mb_per_step"]
     print("BERT fp32-arena 8-rank sums, relative L2 error:", json.dumps(berr))
