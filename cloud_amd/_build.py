@@ -99,9 +99,16 @@ def kernel_sources():
     return sorted((CSRC / "kernels").glob("*.hip"))
 
 
+def experimental_flags():
+    """CLOUD_AMD_BUILD_EXPERIMENTAL=1 compiles the experiment-only GEMM cores (glds8, the
+    256 x 256 ring core, stream-K, 256 x 128) into _C for A/B runs; the default build leaves
+    them out."""
+    return ["-DCA_EXPERIMENTAL=1"] if os.environ.get("CLOUD_AMD_BUILD_EXPERIMENTAL") == "1" else []
+
+
 def build_kernels(verbose=False, jobs=None) -> Path:
     hipcc = _hipcc()
-    inc = [f"-I{CSRC / 'include'}"]
+    inc = [f"-I{CSRC / 'include'}"] + experimental_flags()
     srcs = kernel_sources()
     bind = CSRC / "bindings.cpp"
     jobs = jobs or min(8, os.cpu_count() or 4)

@@ -60,7 +60,9 @@ _VARS = [
     Var("CLOUD_AMD_GEMM_CORE", str, "auto", "GEMM core: 'auto' (128x128 LDS-DMA core plus the 256x256 two-phase "
         "core of ca_gemm256p8.h for large GEMMs), 'glds_ring' (128 core plus the 256x256 ring core), 'glds' (128 "
         "core only), 'vp8' / 'v256' (the two-phase / ring 256 core whenever M, N >= 256), 'glds8', 'reg' "
-        "(register staging)", "ops"),
+        "(register staging); 'glds_ring' / 'v256' / 'glds8' need CLOUD_AMD_BUILD_EXPERIMENTAL=1", "ops"),
+    Var("CLOUD_AMD_BUILD_EXPERIMENTAL", bool, False, "build: also compile the experiment-only GEMM cores (glds8, "
+        "256x256 ring, stream-K, 256x128) into _C for A/B runs", "ops"),
     Var("CLOUD_AMD_WGRAD_BLOCKS", int, 512, "convolution weight gradients: split-K so that about this many "
         "workgroups run (tiles x splits); fewer splits = less fp32 slab traffic, more = fuller CUs", "ops"),
     Var("CLOUD_AMD_WGRAD_BLOCKS_SMALLM", int, 512, "convolution weight gradients with <= 128 output channels "

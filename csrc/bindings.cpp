@@ -67,6 +67,7 @@ int ca_gemm_bf16(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, i
                  hipStream_t);
 int ca_gemm_set_core(int);
 int ca_gemm_set_streamk(int);
+int ca_gemm_experimental_built();
 int ca_gemm_stat_rows(int, int, int, long, long, long);
 int ca_bn_relu_maxpool_s2k3(const bf16_t*, const float*, bf16_t*, uint8_t*, int, int, int, int, int, int, hipStream_t);
 int ca_maxpool_bnstats_parts(int, int, int, int);
@@ -310,6 +311,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gemm_set_core", [](int kind) { return ca_gemm_set_core(kind); });
   m.def("gemm_set_streamk", [](int mode) { return ca_gemm_set_streamk(mode); });
+  m.def("experimental_built", []() { return ca_gemm_experimental_built() != 0; });
   m.def("maxpool_bnstats_parts", [](int N, int H, int W, int C) { return ca_maxpool_bnstats_parts(N, H, W, C); });
   m.def("maxpool_bwd_s2k3_bnstats", [](u64 dy, u64 yp, u64 idx, u64 z, u64 g, u64 part, int N, int H, int W, int C,
                                        int OH, int OW, u64 s) {

@@ -37,7 +37,9 @@ __device__ __forceinline__ void mfma_agpr(f4v& acc, const bf16x8& b, const bf16x
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
 }
 
-template <int BN, template <int, int, int> class LAT, template <int, int, int> class LBT, int EPI>
+// DIAG (bench builds only): 1 = no DMA after the prologue (MFMA + LDS-read ceiling, wrong
+// results); 2 = no MFMAs (load-path floor, wrong results)
+template <int BN, template <int, int, int> class LAT, template <int, int, int> class LBT, int EPI, int DIAG = 0>
 __device__ __forceinline__ void mfma_gemm_w4(const CoreParams& P) {
   constexpr int BM = 256, NT = 256, WM = 2, WN = 2;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
@@ -123,12 +125,17 @@ __device__ __forceinline__ void mfma_gemm_w4(const CoreParams& P) {
       bf16x8 anxt = acur;
       if (st + 1 < NS) anxt = read_frag_sw<BM, A_KC>(As, wm * (BM / WM) + ((st + 1) % FM) * 16, ((st + 1) / FM) * 32, lane);
       if (kk == 0 && i < FN) b1[i] = read_frag_sw<BN, B_KC>(Bs, wn * (BN / WN) + i * 16, 32, lane);
-      if (pf) {
+      if (pf && DIAG != 1) {
 #pragma unroll
         for (int q = (st * NPC) / NS; q < ((st + 1) * NPC) / NS; ++q) dma_piece(q, k1, nb);
       }
+      if constexpr (DIAG != 2) {
 #pragma unroll
-      for (int j = 0; j < FN; ++j) mfma_agpr(acc[i][j], kk == 0 ? b0[j] : b1[j], acur);
+        for (int j = 0; j < FN; ++j) mfma_agpr(acc[i][j], kk == 0 ? b0[j] : b1[j], acur);
+      } else {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(b0[j]), "v"(b1[j]), "v"(acur));
+      }
       acur = anxt;
     }
     if constexpr (loader_stateful<LA>::value) la.advance();

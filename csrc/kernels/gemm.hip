@@ -14,6 +14,13 @@
 #include "ca_gemm256p8.h"
 #include "ca_gemm_xa.h"
 
+// Experiment-only cores -- the 8-wave glds8 variant, the 256 x 256 ring core, stream-K and the
+// 256 x 128 variant -- each measured slower than the default dispatch (docs/performance.md) and
+// kept for A/B runs: compiled only with CLOUD_AMD_BUILD_EXPERIMENTAL=1 (-DCA_EXPERIMENTAL=1).
+#ifndef CA_EXPERIMENTAL
+#define CA_EXPERIMENTAL 0
+#endif
+
 namespace {
 using namespace ca;
 
@@ -54,6 +61,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) d
   mfma_gemm_glds<256, 96, 2, 2, GDenseKC, GDenseKC, EPI>(P);
 }
 
+#if CA_EXPERIMENTAL
 // 8 waves (2 x 4, wave tile 64 x BN/4) with a double-buffered LDS-DMA pipeline:
 // same 16 waves/CU occupancy as the 4-wave single-stage kernel, but the next K
 // tile's DMA overlaps this tile's MFMAs (CLOUD_AMD_GEMM_CORE=glds8).
@@ -61,7 +69,9 @@ template <int BM, int BN, template <int, int, int> class LA, template <int, int,
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) dense_gemm_glds8_kernel(CoreParams P) {
   mfma_gemm_glds<BM, BN, 2, 4, LA, LB, EPI, 2>(P);
 }
+#endif  // CA_EXPERIMENTAL
 
+#if CA_EXPERIMENTAL
 // The 256 x 256 ring core (csrc/include/ca_gemm256.h) for large GEMMs: one 512-thread
 // workgroup per CU.  K-contiguous operands use the 32-deep KC32 loader, N-contiguous ones
 // the same GDenseNC loader as the 128 cores.
@@ -69,6 +79,7 @@ template <template <int, int, int> class LA, template <int, int, int> class LB, 
 __global__ void __launch_bounds__(512) dense_gemm_256_kernel(CoreParams P) {
   mfma_gemm_256<LA, LB, EPI>(P);
 }
+#endif  // CA_EXPERIMENTAL
 
 // The 256 x 256 x 64 core with two staggered wave groups and two phases per K tile
 // (csrc/include/ca_gemm256p8.h).
@@ -77,6 +88,7 @@ __global__ void __launch_bounds__(512) dense_gemm_256p8_kernel(CoreParams P) {
   mfma_gemm_256p8<LA, LB, EPI, 2>(P);
 }
 
+#if CA_EXPERIMENTAL
 // Stream-K form of the same core (ca_gemm256p8.h mfma_gemm_256p8_sk): one workgroup per CU,
 // each an equal range of the (tile, K iteration) space.
 template <template <int, int, int> class LA, template <int, int, int> class LB, int EPI>
@@ -89,6 +101,7 @@ template <template <int, int, int> class LA, template <int, int, int> class LB, 
 __global__ void __launch_bounds__(512) dense_gemm_256x128_kernel(CoreParams P) {
   mfma_gemm_256x128<LA, LB, EPI>(P);
 }
+#endif  // CA_EXPERIMENTAL
 
 // CLOUD_AMD_GEMM_CORE selects the core (A/B comparisons; ca_gemm_set_core overrides it):
 // 0 "reg" = register-staged, 1 "glds" = glds single stage (4 waves) only, 2 "glds8" = glds
@@ -110,6 +123,9 @@ int core_kind() {
                         : strcmp(e, "vp8") == 0       ? 6
                                                       : 5);
   }
+#if !CA_EXPERIMENTAL
+  if (g_core_kind >= 2 && g_core_kind <= 4) g_core_kind = 5;  // not built: the default dispatch
+#endif
   return g_core_kind;
 }
 bool core_p8() { return core_kind() == 5 || core_kind() == 6; }
@@ -325,6 +341,7 @@ static bool use_256(const CoreParams& p, int splits) {
   return t >= 256 && (tile_balance(t) >= 0.999 || (t >= 512 && tile_balance(t) >= 0.85));
 }
 
+#if CA_EXPERIMENTAL
 // 256 x 128 tiles where 256 x 256 tiles do not fill whole rounds but 256 x 128 tiles do
 // (BERT-base FFN1 forward / FFN2 input gradient at M = 8192: N = 3072 -> 768 tiles = 3 rounds;
 // 256 x 256 gives 384 = 1.5).  Opt-in (CLOUD_AMD_GEMM_256X128=1): measured 669 vs 830 TF/s for
@@ -405,6 +422,8 @@ static int streamk_workspace(hipStream_t s, int tiles, SkParams& S) {
   return 0;
 }
 
+#endif  // CA_EXPERIMENTAL
+
 template <int BM, int BN, template <int, int, int> class LA, template <int, int, int> class LB,
           template <int, int, int> class GA, template <int, int, int> class GB, int EPI>
 int launch(const CoreParams& p0, int splits, hipStream_t s) {
@@ -415,6 +434,7 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
   // (ca_mfma_core.h BUF_CAP): rows of a tile (KC) or one split's K range (NC)
   const long span = (long)(p.k_per_split + BK > 256 ? p.k_per_split + BK : 256) * (p.lda > p.ldb ? p.lda : p.ldb) * 2;
   if (use_glds() && span >= (long)BUF_CAP) return -3;
+#if CA_EXPERIMENTAL
   if constexpr (BM == 128 && BN == 128 && EPI == EPI_BF16) {
     if (use_streamk(p, splits)) {
       SkParams S{};
@@ -438,6 +458,7 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
       return 0;
     }
   }
+#endif  // CA_EXPERIMENTAL
   if constexpr (BM == 128 && BN == 128 && (EPI == EPI_BF16 || EPI == EPI_F32_PARTIAL || EPI == EPI_BF16_ST)) {
     if (use_256(p, splits)) {
       const int t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
@@ -454,6 +475,7 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
         CA_LAUNCH_CHECK();
         return 0;
       }
+#if CA_EXPERIMENTAL
       if constexpr (AK && BKC)
         dense_gemm_256_kernel<GDenseKC32, GDenseKC32, EPI><<<dim3(t256, 1, splits), 512, 0, s>>>(p);
       else if constexpr (AK && !BKC)
@@ -464,6 +486,9 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
         return -2;
       CA_LAUNCH_CHECK();
       return 0;
+#else
+      return -2;  // unreachable: without the experimental build core_p8() holds whenever use_256 does
+#endif
     }
     if constexpr (EPI == EPI_BF16 && GA<BM, 1, 256>::KC && GB<BN, 1, 256>::KC) {
       if (use_glds() && use_256x96(p, splits)) {
@@ -473,6 +498,7 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
         return 0;
       }
     }
+#if CA_EXPERIMENTAL
     if (use_256x128(p, splits)) {
       const int t = ((p.M + 255) / 256) * ((p.N + 127) / 128);
       constexpr bool AK = GA<BM, 1, 256>::KC, BKC = GB<BN, 1, 256>::KC;
@@ -485,12 +511,15 @@ int launch(const CoreParams& p0, int splits, hipStream_t s) {
       CA_LAUNCH_CHECK();
       return 0;
     }
+#endif  // CA_EXPERIMENTAL
   }
+#if CA_EXPERIMENTAL
   if (BN == 128 && core_kind() == 2) {
     dense_gemm_glds8_kernel<BM, BN, GA, GB, EPI><<<dim3(tiles, 1, splits), 512, 0, s>>>(p);
     CA_LAUNCH_CHECK();
     return 0;
   }
+#endif
   // K-contiguous operands only (forward GEMMs): the N-contiguous loaders' extra registers
   // make the batched epilogue spill (448-480 B/lane of scratch)
   // Dense-layer epilogues that read memory (act' source, old C for beta) or run the
@@ -655,7 +684,11 @@ int xa_launch(const CoreParams& p0, const XaParams& x, hipStream_t s) {
 template <int EPI>
 int dispatch(int layout, const CoreParams& p, int splits, hipStream_t s) {
   // stream-K runs on 256 x 256 tiles whatever the 128-tile grid's balance (launch<128, 128>)
+#if CA_EXPERIMENTAL
   const bool small_n = !(EPI == EPI_BF16 && use_streamk(p, splits)) && want_small_n(p, splits);
+#else
+  const bool small_n = want_small_n(p, splits);
+#endif
   switch (layout) {
     case 0:
       return small_n ? launch<128, 64, DenseKC, DenseKC, GDenseKC, GDenseKC, EPI>(p, splits, s)
@@ -693,14 +726,24 @@ int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long l
 // Select the GEMM core for this process (values as CLOUD_AMD_GEMM_CORE above); returns
 // the previous one.
 // Stream-K mode (CLOUD_AMD_GEMM_STREAMK: 0 off, 1 auto, 2 wherever allowed); returns the previous.
+// -1: stream-K is not in this build (CLOUD_AMD_BUILD_EXPERIMENTAL=1 builds it)
 int ca_gemm_set_streamk(int mode) {
+#if CA_EXPERIMENTAL
   const int prev = streamk_mode();
   if (mode >= 0 && mode <= 2) g_streamk = mode;
   return prev;
+#else
+  (void)mode;
+  return -1;
+#endif
 }
 
+int ca_gemm_experimental_built() { return CA_EXPERIMENTAL; }
+
+// -1: the requested core is not in this build (kinds 2-4 need CLOUD_AMD_BUILD_EXPERIMENTAL=1)
 int ca_gemm_set_core(int kind) {
   const int prev = core_kind();
+  if (!CA_EXPERIMENTAL && kind >= 2 && kind <= 4) return -1;
   if (kind >= 0 && kind <= 6) g_core_kind = kind;
   return prev;
 }

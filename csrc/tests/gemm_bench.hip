@@ -116,14 +116,14 @@ static void launch256x96(const CoreParams& p, int layout, dim3 g, hipStream_t s)
 }
 
 // four waves, one workgroup per CU, accumulators in AGPRs (ca_gemm_w4.h)
-template <int BN, template <int, int, int> class GA, template <int, int, int> class GB>
+template <int BN, template <int, int, int> class GA, template <int, int, int> class GB, int DIAG = 0>
 __global__ void __launch_bounds__(256, 1) kw4(CoreParams P) {
-  mfma_gemm_w4<BN, GA, GB, EPI_BF16>(P);
+  mfma_gemm_w4<BN, GA, GB, EPI_BF16, DIAG>(P);
 }
-template <int BN>
+template <int BN, int DIAG = 0>
 static void launchw4(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
-  if (layout == 0) kw4<BN, GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
-  else if (layout == 1) kw4<BN, GDenseKC, GDenseNC><<<g, 256, 0, s>>>(p);
+  if (layout == 0) kw4<BN, GDenseKC, GDenseKC, DIAG><<<g, 256, 0, s>>>(p);
+  else if (layout == 1 && DIAG == 0) kw4<BN, GDenseKC, GDenseNC><<<g, 256, 0, s>>>(p);
 }
 
 struct Variant {
@@ -244,7 +244,9 @@ int main(int argc, char** argv) {
                     {"w4n256", 256, 256, launchw4<256>},
                     {"w4n192", 256, 192, launchw4<192>},
                     {"w4n160", 256, 160, launchw4<160>},
-                    {"w4n128", 256, 128, launchw4<128>}};
+                    {"w4n128", 256, 128, launchw4<128>},
+                    {"w4d1n256", 256, 256, launchw4<256, 1>},
+                    {"w4d2n256", 256, 256, launchw4<256, 2>}};
   hipStream_t s;
   CHECK(hipStreamCreate(&s));
   hipEvent_t e0, e1;

@@ -17,6 +17,8 @@ def streamk():
     from cloud_amd.ops import _ext
 
     ext = _ext.load(required=True)
+    if not ext.experimental_built():
+        pytest.skip("stream-K: experiment-only, built with CLOUD_AMD_BUILD_EXPERIMENTAL=1")
     prev = ext.gemm_set_streamk(2)  # wherever the operands allow
     yield ext
     ext.gemm_set_streamk(prev)
