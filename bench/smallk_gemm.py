@@ -4,7 +4,8 @@ CLOUD_AMD_SMALLK_BATCH (default 1024): cloud_amd MFMA kernels (with and without 
 BN-statistics epilogue -- the ResNet forward form, on the persistent resident-weight core
 where it applies: compare runs with CLOUD_AMD_GEMM_PRW=0/1) vs hipBLASLt (torch.mm) vs a
 plain copy of the output size.  Reports us and effective HBM TB/s (A read + C write).
-One JSON line per case."""
+One JSON line per case.  CLOUD_AMD_SMALLK_SET=conv3: the conv3 expansions of stages 2-4
+(N = 512 / 1024 / 2048) -- compare CLOUD_AMD_GEMM_PRWN=0/1 (column-chunked persistent core)."""
 import json
 import os
 import sys
@@ -21,8 +22,11 @@ def main():
     dev = torch.device("cuda", 0)
     st = _ext.stream_handle(dev)
     B = int(os.environ.get("CLOUD_AMD_SMALLK_BATCH", "1024"))
-    for (M, K, N) in [(B * 56 * 56, 64, 256), (B * 56 * 56, 256, 64), (B * 56 * 56, 64, 64),
-                      (B * 56 * 56, 256, 128), (B * 28 * 28, 128, 512), (B * 28 * 28, 512, 128)]:
+    shapes = [(B * 56 * 56, 64, 256), (B * 56 * 56, 256, 64), (B * 56 * 56, 64, 64),
+              (B * 56 * 56, 256, 128), (B * 28 * 28, 128, 512), (B * 28 * 28, 512, 128)]
+    if os.environ.get("CLOUD_AMD_SMALLK_SET") == "conv3":
+        shapes = [(B * 28 * 28, 128, 512), (B * 14 * 14, 256, 1024), (B * 7 * 7, 512, 2048)]
+    for (M, K, N) in shapes:
         a = torch.randn(M, K, device=dev).to(torch.bfloat16)
         w = torch.randn(N, K, device=dev).to(torch.bfloat16)
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
@@ -49,7 +53,8 @@ def main():
         def readsum():
             torch.sum(src, dtype=torch.float32)
 
-        r = {"M": M, "K": K, "N": N, "stat_rows": stats.shape[0], "prw": os.environ.get("CLOUD_AMD_GEMM_PRW", "1")}
+        r = {"M": M, "K": K, "N": N, "stat_rows": stats.shape[0], "prw": os.environ.get("CLOUD_AMD_GEMM_PRW", "1"),
+             "prwn": os.environ.get("CLOUD_AMD_GEMM_PRWN", "1")}
         for name, fn, b in [("ours", ours, byts), ("ours_stats", ours_st, byts), ("hipblaslt", blas, byts),
                             ("copy_C", copy, 2 * M * N * 2),
                             ("fill_C", fill, M * N * 2), ("read_C", readsum, M * N * 2)]:

@@ -89,6 +89,8 @@ _VARS = [
         "the workgroups (one contiguous sweep); 0 = one contiguous row chunk per workgroup", "ops"),
     Var("CLOUD_AMD_CONV_TALL", bool, True, "<= 64-channel 3x3 convolutions (fwd, stride-1 dgrad): 256 x 64 tiles "
         "with 4 x 1 waves; 0 = 128 x 64 with 2 x 2 waves", "ops"),
+    Var("CLOUD_AMD_STEM_LDS", bool, True, "space-to-depth stem convolution forward on the LDS-resident patch + filter "
+        "kernel (csrc/include/ca_conv_stem.h); 0 = the implicit-GEMM row-segment loader", "ops"),
     Var("CLOUD_AMD_STEM_TALL", bool, True, "space-to-depth stem convolution on the tall 256 x 64 tiles too (0.88 -> "
         "0.72 ms per call at b1024); 0 = 128 x 64 tiles (A/B runs)", "ops"),
     Var("CLOUD_AMD_STEM_BWD_RECOMPUTE", bool, True, "ResNet stem tail backward: a statistics-only max-pool "
@@ -105,6 +107,11 @@ _VARS = [
     Var("CLOUD_AMD_GEMM_PRW", bool, True, "forward 1x1 convolutions with N = 256, K = 64 (ResNet layer-1 conv3 "
         "and shortcut): persistent resident-weight core (csrc/include/ca_gemm_prw.h); 0 = the tiled 128 core",
         "ops"),
+    Var("CLOUD_AMD_GEMM_PRWN", bool, True, "forward 1x1 convolutions N = 512 / K = 128 and N = 1024 / K = 256 with "
+        "BN statistics (ResNet stage-2 / stage-3 conv3): the persistent core with the weight resident in column "
+        "chunks (ca_gemm_prw.h); 0 = the tiled 128 core", "ops"),
+    Var("CLOUD_AMD_SMALLK_SET", str, "", "bench/smallk_gemm.py shape set ('conv3': the conv3 expansions of "
+        "stages 2-4)", "bench"),
     Var("CLOUD_AMD_EPI_PF", bool, True, "GEMM epilogues that read memory or run an activation (BN-statistics "
         "forward 1x1 convs, BERT bias/GELU/GELU'/beta dense layers): 4 staged output rows in flight per trip", "ops"),
     Var("CLOUD_AMD_ATTN_FUSED_BWD", bool, True, "attention at S = 64 / 128: one workgroup per (batch, head) for "

@@ -181,7 +181,12 @@ def stem_conv_s2d(x, w, stats=False):
     N, H, W, _ = x.shape
     Cout = w.shape[0]
     OH, OW = _out(H, 7, 2, 3), _out(W, 7, 2, 3)
-    part = stats_buffer(N * OH * OW, Cout, x.device) if stats else None
+    part = None
+    if stats:
+        # the kernel that will run decides the partial rows (one per workgroup on the
+        # LDS-resident stem kernel, one per 128 output pixels on the implicit GEMM)
+        rows = _ext.load(required=True).conv_stat_rows(N, OH + 3, OW + 3, 16, Cout, 4, 4, 1, 1, 0, 0)
+        part = torch.empty((rows, 2, Cout), dtype=torch.float32, device=x.device)
     param = w if (w.is_leaf and w.requires_grad) else None
     y = _StemS2DFn.apply(x, w.detach() if param is not None else w, param, part)
     return (y, part) if stats else y

@@ -64,6 +64,17 @@ __device__ __forceinline__ float row16_sum(float v) {
 
 __device__ __forceinline__ int halo_swz(int q, int chunk) { return q * 64 + ((chunk ^ ((q >> 1) & 7)) << 3); }
 
+// raw barrier (no fence: __syncthreads()'s fence would drain the vector-memory counter) and the
+// counted waits of the persistent tile loops here and in ca_conv_stem.h
+__device__ __forceinline__ void halo_bar() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void halo_vm_wait16() { asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); }
+__device__ __forceinline__ void halo_vm_wait28() { asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); }
+__device__ __forceinline__ void halo_vm_wait0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void lgkm_wait0_h() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // W = 56 only (8 x 56 = 448 = 7 x 64 pixels per tile); H % 8 == 0 (host-checked).
 // STATS: 0 none, 1 forward statistics (sum, sum of squares), 2 input-gradient BN-backward statistics
 template <int STATS, bool PIPE = true>
@@ -112,13 +123,17 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
   // (distinct LDS bank slots on the store), each wave 8 whole 128-B pixel rows per load
   const int pc = wave * 8 + (lane & 7), pch = (lane >> 3) & 7;
   static_assert(PPT == PR && HALO_WAVES * 8 == W, "one patch row per chunk, 8 columns per wave");
+  // Branch-free: a pad row loads its clamped in-image neighbour and is zeroed after the load (a
+  // load under a branch makes hipcc wait vmcnt(0) where the branches join).
   auto load_patch = [&](int t, s8v (&v)[PPT]) {
     const int n = t / rgroups, r0 = (t % rgroups) * TR - 1;  // patch row 0 = image row r0
     const bf16_t* src = P.x + (((long)n * H + r0) * W + pc) * C + pch * 8;
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       const bool ok = (i > 0 || r0 >= 0) && (i < PPT - 1 || r0 + i < H);  // only rows 0 and PR-1 can be pads
-      v[i] = ok ? *reinterpret_cast<const s8v*>(src + (long)i * W * C) : zero8();
+      const int ii = i == 0 ? (ok ? 0 : 1) : (i == PPT - 1 ? (ok ? i : i - 1) : i);
+      const s8v ld = *reinterpret_cast<const s8v*>(src + (long)ii * W * C);
+      v[i] = ok ? ld : zero8();
     }
   };
   short* pdst = pimg + pch * (HALO_PLANE / 2) + (pc + 1) * 8;
@@ -140,15 +155,22 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
     for (int e = tid; e < HALO_WAVES * 2 * C; e += NT) sred[e] = 0.f;
   }
 
+  // Tile loop: the next tile's patch loads are issued at the top of a tile, BEFORE its epilogue
+  // stores, and written to LDS at the bottom behind a counted vmcnt(16), so a tile's 16 output
+  // stores per lane stay in flight across the next tile's MFMAs.  (With a __syncthreads() at the
+  // loop top hipcc drained vmcnt to 0 there: every tile waited out its own store latency.)
+  // Inside the loop only LDS is shared between the waves: raw s_barriers with lgkmcnt(0).
   int t = blockIdx.x;
   s8v nxt[PPT];
-  if (t < ntiles) load_patch(t, nxt);
-  for (; t < ntiles; t += gridDim.x) {
-    __syncthreads();  // previous tile's LDS reads retired (and, first trip, the filter image written)
+  if (t < ntiles) {
+    load_patch(t, nxt);
+    halo_vm_wait0();
     store_patch(nxt);
-    __syncthreads();
+  }
+  __syncthreads();  // the filter image, the pad columns and the first patch written
+  for (; t < ntiles; t += gridDim.x) {
     const int tn = t + gridDim.x;
-    if (tn < ntiles) load_patch(tn, nxt);  // in flight during the MFMAs below
+    load_patch(tn < ntiles ? tn : t, nxt);  // in flight during the MFMAs and stores below
 
     f4v acc[4][4];
 #pragma unroll
@@ -279,6 +301,12 @@ __device__ __forceinline__ void conv3x3_halo(const HaloParams& P) {
           }
       }
     }
+    lgkm_wait0_h();
+    halo_bar();      // every wave's patch reads of this tile retired
+    halo_vm_wait16();  // this thread's next-patch loads landed; its 16 output stores may still fly
+    store_patch(nxt);
+    lgkm_wait0_h();
+    halo_bar();      // the next patch is in LDS
   }
   if constexpr (STATS) {
     __syncthreads();

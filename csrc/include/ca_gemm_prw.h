@@ -19,6 +19,17 @@
 //   * accumulates the BN-forward statistics [sum | sum of squares] of the stored bf16
 //     values in registers across ALL its tiles and writes ONE partial row per workgroup
 //     (gridDim.x rows instead of M / 128: 256 instead of 25,088 at ResNet-50 stage 1, b1024).
+//
+// Column chunks (P.prw_chunks = NCH > 1): a weight too large for LDS (ResNet's conv3
+// expansions, N = 512..2048 at K = 128..512) is split into NCH chunks of BN columns; NCH
+// workgroups share one row range, each with its chunk of B resident, and stream the SAME A
+// tiles.  The NCH workgroups of a range are dealt to one XCD (block b runs on XCD b % 8), start
+// together and run the same step sequence, so an A tile is fetched from HBM once and read by the
+// other NCH - 1 from that XCD's L2 or the MALL (measured: spreading the chunks over the XCDs
+// costs ~1 %, so the re-reads are not the bound).  The data-parallel 128 x 128 core ran these
+// write-heavy shapes at 2.4-3.1 TB/s; this runs ResNet-50's stage-2 conv3 ~15 % faster (3.7
+// TB/s), stage 3 ~4 % (gemm.hip prw_kind).  Partials: one row per range, each chunk writing its
+// BN columns.
 // Barriers are bare s_barrier (a __syncthreads fence would wait for vmcnt(0) and drain the
 // prefetch); LDS writes are ordered by lgkmcnt(0) before them.
 #pragma once
@@ -75,8 +86,21 @@ __device__ __forceinline__ void prw_gemm_body(const CoreParams& P) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int T = (P.M + BM - 1) / BM;
-  const int t0 = (int)((long)blockIdx.x * T / gridDim.x), t1 = (int)((long)(blockIdx.x + 1) * T / gridDim.x);
+  // (row range, column chunk) of this workgroup; with chunks the host makes gridDim.x a
+  // multiple of 8 * NCH, and the chunks of a range share the XCD b % 8
+  const int NCH = P.prw_chunks > 1 ? P.prw_chunks : 1;
+  int range = blockIdx.x, chunk = 0, R = gridDim.x;
+  if (NCH > 1) {
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int rpx = (gridDim.x >> 3) / NCH;  // ranges per XCD
+    range = xcd * rpx + j / NCH;
+    chunk = j % NCH;
+    R = gridDim.x / NCH;
+  }
+  const int t0 = (int)((long)range * T / R), t1 = (int)((long)(range + 1) * T / R);
   const int nsteps = (t1 - t0) * NK;
+  const long col0 = (long)chunk * BN;  // first output column (and B row) of this chunk
+  const long ntot = (long)NCH * BN;    // == P.N
 
   // A chunk i of this thread: tile row (tid >> 3) + 64 i, swizzled 16-B slot (tid & 7) ^ (row & 7)
   const int arow = tid >> 3;
@@ -91,8 +115,8 @@ __device__ __forceinline__ void prw_gemm_body(const CoreParams& P) {
 
   // resident B: NK slices [BN][64], same swizzle as the A stages
   {
-    const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(P.B), (short)0,
-                                                      (int)buf_span((long)P.N * P.ldb * 2), 0x00020000);
+    const auto rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(P.B + col0 * P.ldb), (short)0,
+                                                      (int)buf_span((long)BN * P.ldb * 2), 0x00020000);
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk)
 #pragma unroll
@@ -168,8 +192,8 @@ __device__ __forceinline__ void prw_gemm_body(const CoreParams& P) {
       }
     lgkm_wait0();
     bar256();
-    const auto rc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<bf16_t*>(P.C) + m0 * P.ldc, (short)0,
-                                                      (int)buf_span((P.M - m0) * P.ldc * 2), 0x00020000);
+    const auto rc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<bf16_t*>(P.C) + m0 * P.ldc + col0, (short)0,
+                                                      (int)buf_span((P.M - m0) * P.ldc * 2 - col0 * 2), 0x00020000);
     s8v v[IT];
 #pragma unroll
     for (int it = 0; it < IT; ++it) v[it] = *reinterpret_cast<const s8v*>(Cs + EL::idx(epart + it * RP, ecol));
@@ -208,9 +232,9 @@ __device__ __forceinline__ void prw_gemm_body(const CoreParams& P) {
         ts += sred[pp * BN + c];
         tq += sred[(RP + pp) * BN + c];
       }
-      float* st = P.stats + (long)blockIdx.x * 2 * P.N;
+      float* st = P.stats + (long)range * 2 * ntot + col0;
       st[c] = ts;
-      st[P.N + c] = tq;
+      st[ntot + c] = tq;
     }
   }
 }

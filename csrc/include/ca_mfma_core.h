@@ -107,6 +107,7 @@ struct CoreParams {
   int dg_py, dg_px, dg_kh0, dg_kw0, dg_nh, dg_nw, dg_dy0, dg_dx0, Hq, Wq;
   FastDiv div_wq, div_hq, div_nw;
   int split_xcd;  // split-K grids: deal (split, tile) ranges to XCDs split-major (blk_pos)
+  int prw_chunks; // persistent resident-weight core: column chunks of BN (0 / 1 = the whole N resident)
   unsigned long long* stamps;  // diagnostic builds only (in-kernel s_memtime stamps)
 };
 

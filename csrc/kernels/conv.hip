@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include "ca_conv_halo.h"
+#include "ca_conv_stem.h"
 #include "ca_mfma_core.h"
 
 namespace {
@@ -901,7 +902,7 @@ bool halo_shape(int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw,
 }
 
 // persistent grid: one workgroup per CU (the 148-KB LDS image), at most one per tile
-int halo_grid(int Nb, int H) {
+int conv_cus() {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -909,6 +910,11 @@ int halo_grid(int Nb, int H) {
     cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
            prop.multiProcessorCount > 0) ? prop.multiProcessorCount : 256;
   }
+  return cus;
+}
+
+int halo_grid(int Nb, int H) {
+  const int cus = conv_cus();
   const long tiles = (long)Nb * (H / HALO_TR);
   return (int)(tiles < cus ? tiles : cus);
 }
@@ -946,6 +952,46 @@ int halo_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   return 0;
 }
 
+// Space-to-depth stem (4x4 / s1 / p0, 16 -> 64 channels, output width 112) on the LDS-resident
+// patch + filter kernel (csrc/include/ca_conv_stem.h); CLOUD_AMD_STEM_LDS=0 keeps it on the
+// implicit-GEMM row-segment loader (A/B runs).
+template <bool STATS>
+__global__ void __launch_bounds__(STEM_NT) conv_stem_s2d_kernel(StemParams P) {
+  conv_stem_s2d<STATS>(P);
+}
+
+bool stem_lds_on() {
+  static int en = -1;
+  if (en < 0) {
+    const char* e = getenv("CLOUD_AMD_STEM_LDS");
+    en = (e && e[0] == '0') ? 0 : 1;
+  }
+  return en != 0;
+}
+
+bool stem_shape(int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw) {
+  return stem_lds_on() && KH == 4 && KW == 4 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && Cin == STEM_CI &&
+         Cout == STEM_C && W == STEM_PW && H > 3 && (H - 3) % STEM_TR == 0;
+}
+
+// persistent grid: one workgroup per CU (196 VGPRs per lane: a second 7-wave workgroup does
+// not fit the register file), at most one per tile
+int stem_grid(int Nb, int H) {
+  const long tiles = (long)Nb * ((H - 3) / STEM_TR);
+  const long g = conv_cus();
+  return (int)(tiles < g ? tiles : g);
+}
+
+int stem_launch(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, float* stats, hipStream_t s) {
+  StemParams sp{};
+  sp.x = x; sp.w = w; sp.y = y; sp.stats = stats; sp.N = Nb; sp.OH = H - 3;
+  const int g = stem_grid(Nb, H);
+  if (stats) conv_stem_s2d_kernel<true><<<g, STEM_NT, 0, s>>>(sp);
+  else conv_stem_s2d_kernel<false><<<g, STEM_NT, 0, s>>>(sp);
+  CA_LAUNCH_CHECK();
+  return 0;
+}
+
 CoreParams conv_params(int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw) {
   CoreParams p{};
   p.Nb = Nb; p.H = H; p.W = W; p.Cin = Cin; p.Cout = Cout; p.KH = KH; p.KW = KW;
@@ -977,6 +1023,7 @@ int ca_conv_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, int 
   if (!geom_ok(Cin, Cout, (long)Nb * H * W)) return -1;
   if (halo_shape(H, W, Cin, Cout, KH, KW, sh, sw, ph, pw))
     return halo_launch(x, w, y, Nb, H, W, stats, nullptr, nullptr, 0, s);
+  if (stem_shape(H, W, Cin, Cout, KH, KW, sh, sw, ph, pw) && use_glds()) return stem_launch(x, w, y, Nb, H, stats, s);
   p.A = x; p.B = w; p.lda = Cin; p.ldb = (long)KH * KW * Cin; p.C = y; p.ldc = Cout;
   p.M = Nb * p.OH * p.OW; p.N = Cout; p.K = KH * KW * Cin; p.k_per_split = p.K;
   p.stats = stats;
@@ -1027,9 +1074,10 @@ int ca_conv_fwd_ex(const bf16_t* x, const bf16_t* w, bf16_t* y, int Nb, int H, i
 long ca_conv_dgrad_stat_tiles(int Nb, int H, int W, int sh, int sw);
 
 // Rows of the BN-forward statistics partials ca_conv_fwd(stats != null) writes: one per
-// 128 output pixels on the implicit-GEMM kernels, one per workgroup on the halo kernel.
+// 128 output pixels on the implicit-GEMM kernels, one per workgroup on the halo and stem kernels.
 long ca_conv_stat_rows(int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh, int sw, int ph, int pw) {
   if (halo_shape(H, W, Cin, Cout, KH, KW, sh, sw, ph, pw)) return halo_grid(Nb, H);
+  if (stem_shape(H, W, Cin, Cout, KH, KW, sh, sw, ph, pw) && use_glds()) return stem_grid(Nb, H);
   const long oh = (H + 2 * ph - KH) / sh + 1, ow = (W + 2 * pw - KW) / sw + 1;
   return ((long)Nb * oh * ow + 127) / 128;
 }

@@ -172,36 +172,98 @@ int cu_count() {
 //   N 128, K 256: 468-492 vs 468 us
 // so the other shapes stay on the tiled core, whose 4 co-resident blocks per CU already keep
 // enough loads in flight for their read-heavy tiles.
-int prw_kind(int M, int N, int K, long lda, long ldb, long ldc) {
+// Column-chunked kinds (ca_gemm_prw.h "Column chunks"): ResNet's conv3 expansions, forward
+// with statistics only -- N = 512 / K = 128 (stage 2, 4 chunks of 128) and N = 1024 / K = 256
+// (stage 3, 8 of 128).  Measured at b1024 with statistics (bench/smallk_gemm.py, profiles/r6_s7,
+// r6_s8): stage 2 334.6 -> 274-290 us, stage 3 218.6 -> 209-211 us; not taken: stage 4
+// (N = 2048 / K = 512, 32 chunks of 64: 143.5 -> 270.6 us), ring depth 5 at stage 2 (no change),
+// 16 chunks of 64 at stage 3 (296 us), and the chunks of a range spread over the XCDs instead
+// of sharing one (211.8 vs 209.1 us: the A re-reads are not the bound -- the per-tile epilogue
+// turnaround of one 8-wave workgroup per CU is).  CLOUD_AMD_GEMM_PRWN=0 keeps them on the tiled
+// cores (A/B runs).
+bool prwn_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("CLOUD_AMD_GEMM_PRWN");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v != 0;
+}
+
+int prw_kind(int M, int N, int K, long lda, long ldb, long ldc, bool stats) {
   if (!prw_enabled() || lda != K || ldb != K || ldc != N || M < 128) return 0;
   if ((long)M * K * 2 >= (long)BUF_CAP || (long)M * N * 2 >= (long)BUF_CAP) return 0;
   if (N == 256 && K == 64) return 2;
+  if (!stats || !prwn_enabled() || cu_count() % 256 != 0) return 0;
+  if (N == 512 && K == 128) return 3;
+  if (N == 1024 && K == 256) return 4;
   return 0;
 }
 
+// (BN, KT, NS, column chunks) of each kind
+struct PrwCfg {
+  int bn, kt, ns, chunks;
+};
+PrwCfg prw_cfg(int kind) {
+  switch (kind) {
+    case 2: return {256, 64, 3, 1};
+    case 3: return {128, 128, 3, 4};
+    case 4: return {128, 256, 3, 8};
+    default: return {0, 0, 0, 0};
+  }
+}
+
 template <int BN, int KT, int NS>
-int prw_grid_for(int M) {
+int prw_grid_for(int M, int chunks) {
   constexpr int bytes = PrwGeom<BN, KT, NS>::BYTES;
   static_assert(bytes <= 160 * 1024, "LDS");
   int per_cu = (160 * 1024) / bytes;
   if (per_cu > 4) per_cu = 4;
   const int tiles = (M + 127) / 128;
+  if (chunks > 1) {
+    // a multiple of 8 * chunks (the chunks of a range on one XCD), at most one range per tile
+    const int unit = 8 * chunks;
+    int ranges = (cu_count() * per_cu / unit) * 8;
+    if (ranges > tiles) ranges = tiles / 8 * 8;
+    return ranges < 8 ? 0 : ranges * chunks;
+  }
   const int g = cu_count() * per_cu;
   return g < tiles ? g : tiles;
 }
 
-int prw_grid(int kind, int M) { return kind == 2 ? prw_grid_for<256, 64, 3>(M) : 0; }
+int prw_grid(int kind, int M) {
+  switch (kind) {
+    case 2: return prw_grid_for<256, 64, 3>(M, 1);
+    case 3: return prw_grid_for<128, 128, 3>(M, 4);
+    case 4: return prw_grid_for<128, 256, 3>(M, 8);
+    default: return 0;
+  }
+}
 
-int prw_launch(int kind, const CoreParams& p, hipStream_t s) {
-  const int g = prw_grid(kind, p.M);
+// rows of the statistics partials: one per workgroup, or one per range with column chunks
+int prw_stat_rows(int kind, int M) {
+  const int g = prw_grid(kind, M);
+  const int ch = prw_cfg(kind).chunks;
+  return ch > 1 ? g / ch : g;
+}
+
+int prw_launch(int kind, const CoreParams& p0, hipStream_t s) {
+  const int g = prw_grid(kind, p0.M);
+  if (g <= 0) return -2;
+  CoreParams p = p0;
+  p.prw_chunks = prw_cfg(kind).chunks;
   const bool st = p.stats != nullptr;
 #define CA_PRW(BN_, KT_, NS_)                                                             \
   do {                                                                                    \
     if (st) prw_gemm_kernel<BN_, KT_, NS_, true><<<g, 512, 0, s>>>(p);                    \
     else prw_gemm_kernel<BN_, KT_, NS_, false><<<g, 512, 0, s>>>(p);                      \
   } while (0)
-  if (kind != 2) return -2;
-  CA_PRW(256, 64, 3);
+  switch (kind) {
+    case 2: CA_PRW(256, 64, 3); break;
+    case 3: CA_PRW(128, 128, 3); break;
+    case 4: CA_PRW(128, 256, 3); break;
+    default: return -2;
+  }
 #undef CA_PRW
   CA_LAUNCH_CHECK();
   return 0;
@@ -782,10 +844,10 @@ int ca_gemm_bf16(int layout, const bf16_t* A, long lda, const bf16_t* B, long ld
   CoreParams p = base_params(A, lda, B, ldb, C, ldc, M, N, K);
   p.stats = stats;
   p.beta = beta;
-  if (!stats && layout == 0 && prw_kind(M, N, K, lda, ldb, ldc) == 2) return prw_launch(2, p, s);
+  if (!stats && layout == 0 && prw_kind(M, N, K, lda, ldb, ldc, false) == 2) return prw_launch(2, p, s);
   if (stats && layout == 0) {  // forward 1x1 conv feeding a BatchNorm: register-accumulated statistics
-    const int kind = prw_kind(M, N, K, lda, ldb, ldc);
-    if (kind) return prw_launch(kind, p, s);  // one partial row per workgroup (ca_gemm_stat_rows)
+    const int kind = prw_kind(M, N, K, lda, ldb, ldc, true);
+    if (kind && prw_grid(kind, M) > 0) return prw_launch(kind, p, s);  // one partial row per workgroup / range
     return want_small_n(p, 1) ? launch<128, 64, DenseKC, DenseKC, GDenseKC, GDenseKC, EPI_BF16_ST>(p, 1, s)
                               : launch<128, 128, DenseKC, DenseKC, GDenseKC, GDenseKC, EPI_BF16_ST>(p, 1, s);
   }
@@ -795,8 +857,8 @@ int ca_gemm_bf16(int layout, const bf16_t* A, long lda, const bf16_t* B, long ld
 // Rows of the [rows][2][N] statistics partials ca_gemm_bf16(layout 0, stats != null) writes:
 // one per workgroup on the persistent core, one per 128 GEMM rows otherwise.
 int ca_gemm_stat_rows(int M, int N, int K, long lda, long ldb, long ldc) {
-  const int kind = prw_kind(M, N, K, lda, ldb, ldc);
-  return kind ? prw_grid(kind, M) : (M + 127) / 128;
+  const int kind = prw_kind(M, N, K, lda, ldb, ldc, true);
+  return (kind && prw_grid(kind, M) > 0) ? prw_stat_rows(kind, M) : (M + 127) / 128;
 }
 
 // Input-gradient GEMM (NN: dX = dY W) whose output feeds a BatchNorm(+ReLU) backward:

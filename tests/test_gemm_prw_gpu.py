@@ -1,7 +1,8 @@
 """Persistent resident-weight GEMM core (csrc/include/ca_gemm_prw.h) for the small-K forward
 1x1 convolutions with the BN-statistics epilogue, against a plain PyTorch fp32 GEMM of the
 same bf16 operands: every covered (N, K), a ragged last tile, grids with fewer tiles than
-workgroups and many tiles per workgroup; the [rows][2][N] partials (one row per workgroup)
+workgroups and many tiles per workgroup; the [rows][2][N] partials (one row per workgroup,
+or per row range for the column-chunked kinds -- ResNet's conv3 expansions, N = 512..2048)
 must sum to the column sums / sums of squares of the stored bf16 output.  Also checks that
 the fused ResNet block's forward statistics agree with and without the core."""
 import pytest
@@ -14,11 +15,16 @@ def _rel(a, b):
     return float((a.float() - b).norm() / b.norm().clamp_min(1e-12))
 
 
-@pytest.mark.parametrize("N,K", [(256, 64), (64, 64), (64, 256), (128, 256)])
-@pytest.mark.parametrize("M", [128 * 3 + 17, 200_000 + 77])
+PERSISTENT = {(256, 64), (512, 128), (1024, 256)}
+
+
+@pytest.mark.parametrize("N,K", [(256, 64), (64, 64), (64, 256), (128, 256), (512, 128), (1024, 256),
+                                 (2048, 512)])
+@pytest.mark.parametrize("M", [128 * 3 + 17, 128 * 8 + 5, 200_000 + 77])
 def test_prw_forward_stats(N, K, M):
-    """(256, 64) runs on the persistent core; the other shapes check that the row count the
-    host reports matches what the tiled core writes."""
+    """PERSISTENT shapes run on the persistent core (column-chunked above N = 256, when the grid
+    has at least 8 row ranges); the other shapes check that the row count the host reports
+    matches what the tiled core writes."""
     from cloud_amd.ops import _ext, raw
 
     ext = _ext.load(required=True)
@@ -29,7 +35,7 @@ def test_prw_forward_stats(N, K, M):
     rows = ext.gemm_stat_rows(M, N, K, K, K, N)
     assert st.shape == (rows, 2, N)
     assert rows <= (M + 127) // 128  # persistent: one row per workgroup (<= one per tile)
-    if (N, K) != (256, 64):
+    if (N, K) not in PERSISTENT:
         assert rows == (M + 127) // 128
     st.fill_(float("nan"))  # every row must be written
     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
@@ -53,6 +59,10 @@ def test_prw_rows_fall_back_when_not_covered():
     assert ext.gemm_stat_rows(M, 128, 512, 512, 512, 128) == (M + 127) // 128
     # covered shape: at most (workgroups per CU) x CUs rows
     assert ext.gemm_stat_rows(M, 256, 64, 64, 64, 256) <= 4 * 256
+    # column-chunked kinds: one row per range of row tiles (8 ranges per XCD or fewer)
+    assert ext.gemm_stat_rows(M, 1024, 256, 256, 256, 1024) in (32, (M + 127) // 128)
+    # too few tiles for 8 ranges: tiled core
+    assert ext.gemm_stat_rows(500, 1024, 256, 256, 256, 1024) == 4
 
 
 def test_conv_fwd_1x1_stats_match_tiled_core():
