@@ -86,10 +86,15 @@ def _grad_out(p):
     return torch.zeros_like(p, dtype=torch.float32 if p.dtype == torch.float32 else p.dtype), True
 
 
-def _notify(p):
-    from ..parallel import ddp
+_DDP = []
 
-    ddp.notify_grad_ready(p)
+
+def _notify(p):
+    if not _DDP:
+        from ..parallel import ddp
+
+        _DDP.append(ddp.notify_grad_ready)
+    _DDP[0](p)
 
 
 class BertEmbeddings(nn.Module):

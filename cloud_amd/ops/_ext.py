@@ -22,8 +22,14 @@ _ext = None
 _err = None
 
 
+_OPS_MODE = []
+
+
 def ops_mode() -> str:
-    return os.environ.get("CLOUD_AMD_OPS", "native").lower()
+    """``CLOUD_AMD_OPS`` (read once per process: asked on every op)."""
+    if not _OPS_MODE:
+        _OPS_MODE.append(os.environ.get("CLOUD_AMD_OPS", "native").lower())
+    return _OPS_MODE[0]
 
 
 def load(required: bool = False):
@@ -54,7 +60,21 @@ def use_native(*tensors) -> bool:
     return True
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_handle(device=None) -> int:
+    """The current HIP stream of ``device`` as an integer handle.  Called once per kernel
+    launch: the raw-stream query costs ~0.3 us where ``torch.cuda.current_stream(d).cuda_stream``
+    (a Stream object per call) cost ~4.3 us of host time (BERT step: ~300 launches,
+    profiles/r6_s12)."""
+    if _RAW_STREAM is not None:
+        if isinstance(device, torch.device) and device.index is not None:
+            return _RAW_STREAM(device.index)
+        if isinstance(device, int):
+            return _RAW_STREAM(device)
+        if device is None or (isinstance(device, torch.device) and device.type == "cuda"):
+            return _RAW_STREAM(torch.cuda.current_device())
     return torch.cuda.current_stream(device).cuda_stream
 
 

@@ -32,6 +32,8 @@ def _log(kind, M, N, K, nbytes, **kw):
 
 
 def _nb(*ts):
+    if _SHAPE_LOG is None:  # the byte counts only feed the shape log (evaluated per launch)
+        return 0
     return sum(t.numel() * t.element_size() for t in ts if t is not None)
 
 
@@ -536,9 +538,9 @@ def gemm(a, w, bias=None, act=None, preact=None, out=None, beta=0.0, layout=NT, 
     N = w.shape[0] if layout == NT else w.shape[1]
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
-    if (act in (None, "none", "linear") and preact is None and dact_src is None and stats is None
-            and beta in (0.0, 1.0) and layout in (NT, NN) and a.is_cuda and a.stride(1) == 1 and w.is_contiguous()
-            and out.is_contiguous() and (bias is None or layout == NT) and PLAIN_GEMM._mode() != "never"):
+    if (PLAIN_GEMM._mode() != "never" and act in (None, "none", "linear") and preact is None and dact_src is None
+            and stats is None and beta in (0.0, 1.0) and layout in (NT, NN) and a.is_cuda and a.stride(1) == 1
+            and w.is_contiguous() and out.is_contiguous() and (bias is None or layout == NT)):
         key = (layout, M, N, K, bias is not None, float(beta))
         if key not in PLAIN_GEMM.decisions and PLAIN_GEMM._mode() == "auto":
             scratch = torch.zeros_like(out)
@@ -576,11 +578,12 @@ class GradFinalizeBatch:
         self.groups = {}  # issuing stream -> (stream, jobs, betas, keep)
 
     def _group(self, t):
-        st = torch.cuda.current_stream(t.device) if t.device.type == "cuda" else None
-        key = None if st is None else st.cuda_stream
-        if key not in self.groups:
-            self.groups[key] = (st, [], [], [])
-        return self.groups[key]
+        # keyed by the raw handle of the issuing stream (no Stream object per job)
+        key = _ext.stream_handle(t.device) if t.device.type == "cuda" else None
+        g = self.groups.get(key)
+        if g is None:
+            g = self.groups[key] = (key, [], [], [])
+        return g
 
     def add_splitk(self, ws, splits, n, out, beta):
         _, jobs, betas, keep = self._group(ws)
@@ -599,14 +602,9 @@ class GradFinalizeBatch:
         """One launch per issuing stream, on that stream (a job runs after the kernel that
         produced its partials, and its workspace was allocated from that stream's pool)."""
         ext = _ext.load(required=True)
-        for st, jobs, betas, keep in self.groups.values():
-            if not betas:
-                continue
-            if st is None:
-                ext.grad_finalize_multi(jobs, betas, 0)
-            else:
-                with torch.cuda.stream(st):
-                    ext.grad_finalize_multi(jobs, betas, st.cuda_stream)
+        for handle, jobs, betas, keep in self.groups.values():
+            if betas:
+                ext.grad_finalize_multi(jobs, betas, handle or 0)
         self.groups = {}
 
 

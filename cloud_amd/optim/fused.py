@@ -50,6 +50,9 @@ class FusedOptimizer:
 
     def __init__(self, params, learning_rate=1e-3, weight_decay=0.0, grad_scale=1.0, decay_fn=None,
                  clipnorm=None):
+        from ..runtime import host
+
+        host.configure()
         if isinstance(params, torch.nn.Module):
             named = list(params.named_parameters())
         else:

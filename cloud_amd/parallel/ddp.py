@@ -55,11 +55,27 @@ _ACTIVE = weakref.WeakSet()
 _DDP_ORDER = os.environ.get("CLOUD_AMD_DDP_ORDER", "event")
 
 
+# notify_grad_ready runs for every parameter of every step (~150 times per BERT step): it walks
+# a cached tuple of weak references instead of iterating the WeakSet (~2 us per call).  The
+# cache is rebuilt when a reducer is activated (_activate) or collected (the set shrinks).
+_SNAP = [(), -1]
+
+
+def _activate(r):
+    _ACTIVE.add(r)
+    _SNAP[1] = -1
+
+
 def notify_grad_ready(param):
     """Called by ops that write a parameter's gradient straight into its arena
     slice (bypassing autograd's AccumulateGrad, hence its hooks)."""
-    for r in list(_ACTIVE):
-        r._on_grad(param)
+    n = len(_ACTIVE)
+    if n != _SNAP[1]:
+        _SNAP[0], _SNAP[1] = tuple(weakref.ref(r) for r in _ACTIVE), n
+    for ref in _SNAP[0]:
+        r = ref()
+        if r is not None:
+            r._on_grad(param)
 
 
 def _busy_ms(evs):
@@ -202,7 +218,7 @@ class GradAllReducer:
         self._build()
         if self.world > 1 and overlap:
             self._install_hooks()
-            _ACTIVE.add(self)
+            _activate(self)
 
     def _param_wire(self, p):
         """Wire dtype override of one parameter: ``wire_dtypes[p]`` given to the reducer, or
@@ -620,7 +636,7 @@ class GradAllReducer:
             self._opt_stream = torch.cuda.Stream(self.arenas[0].grad.device)
         if ok and self.world == 1 and not self._hooks:
             self._install_hooks()
-            _ACTIVE.add(self)
+            _activate(self)
         return bool(ok)
 
     def _update_slice(self, b, after_stream):
@@ -651,7 +667,7 @@ class GradAllReducer:
         self._ready_log = []
         if self._probe and not self._hooks:
             self._install_hooks()
-            _ACTIVE.add(self)
+            _activate(self)
 
     def _log_ready(self):
         end = torch.cuda.Event(enable_timing=True)

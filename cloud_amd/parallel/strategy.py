@@ -40,6 +40,9 @@ class Strategy:
     name = "Strategy"
 
     def __init__(self, device=None):
+        from ..runtime import host
+
+        host.configure()
         self._device = torch.device(device) if device is not None else None
         self._prev = None
 

@@ -24,8 +24,38 @@ from __future__ import annotations
 import torch
 
 from .. import config
+from ..ops import _ext
 
 _STREAMS = {}
+_set_stream = getattr(torch._C, "_cuda_setStream", None)
+_get_stream = getattr(torch._C, "_cuda_getCurrentStream", None)
+
+
+class _on_stream:
+    """``with torch.cuda.stream(s)`` on the raw getter / setter (the torch context builds Stream
+    objects and queries the current stream twice per use -- runtime/host.py); restores the
+    stream that was current on entry."""
+
+    __slots__ = ("s", "prev")
+
+    def __init__(self, s):
+        self.s = s
+
+    def __enter__(self):
+        if _set_stream is None or _get_stream is None:  # pragma: no cover - older torch
+            self.prev = torch.cuda.current_stream(self.s.device)
+            torch.cuda.set_stream(self.s)
+            return
+        self.prev = _get_stream(self.s.device_index)
+        _set_stream(stream_id=self.s.stream_id, device_index=self.s.device_index, device_type=self.s.device_type)
+
+    def __exit__(self, *exc):
+        p = self.prev
+        if isinstance(p, torch.cuda.Stream):  # pragma: no cover
+            torch.cuda.set_stream(p)
+        else:
+            _set_stream(stream_id=p[0], device_index=p[1], device_type=p[2])
+        return False
 
 
 def side_stream(device):
@@ -44,13 +74,16 @@ class SideWork:
         self.enabled = bool(enabled) and device.type == "cuda"
         self.main = torch.cuda.current_stream(device) if self.enabled else None
         self.side = side_stream(device) if self.enabled else None
+        if self.enabled:
+            self._ext = _ext.load(required=True)
+            self._mh, self._sh = self.main.cuda_stream, self.side.cuda_stream
         self.used = False
 
     def run(self, fn, *tensors):
         if not self.enabled:
             return fn()
-        self.side.wait_stream(self.main)
-        with torch.cuda.stream(self.side):
+        self._ext.stream_wait(self._sh, self._mh)  # side waits for the main stream's work so far
+        with _on_stream(self.side):
             r = fn()
         for t in tensors:
             if t is not None:
@@ -60,7 +93,7 @@ class SideWork:
 
     def join(self):
         if self.used:
-            self.main.wait_stream(self.side)
+            self._ext.stream_wait(self._mh, self._sh)
             self.used = False
 
     def detach(self):

@@ -2,6 +2,8 @@
 // pointers (uintptr_t from torch.Tensor.data_ptr()) and the HIP stream handle
 // (torch.cuda.current_stream().cuda_stream); shape/dtype validation happens in
 // the Python layer (cloud_amd/ops/*).  A non-zero HIP status raises.
+#include <atomic>
+#include <mutex>
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -134,9 +136,34 @@ static void check(int rc, const char* what) {
 
 typedef unsigned long long u64;
 
+// dst waits for everything queued on src so far: a record / wait pair on a pooled event (no
+// Python Event object per fork -- runtime/side_stream.py SideWork).  A wait binds to the
+// record that precedes it, so an event is reusable as soon as its wait is enqueued; the ring
+// only keeps concurrent callers (autograd threads) off each other's event.
+static int stream_wait(u64 dst, u64 src) {
+  static hipEvent_t ring[16];
+  static std::atomic<int> next{0};
+  static std::once_flag once;
+  static hipError_t init_err = hipSuccess;
+  std::call_once(once, [] {
+    for (auto& e : ring) {
+      const hipError_t rc = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+      if (rc != hipSuccess) init_err = rc;
+    }
+  });
+  if (init_err != hipSuccess) return (int)init_err;
+  hipEvent_t e = ring[next.fetch_add(1) & 15];
+  hipError_t rc = hipEventRecord(e, S(src));
+  if (rc == hipSuccess) rc = hipStreamWaitEvent(S(dst), e, 0);
+  return (int)rc;
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "cloud_amd gfx950 HIP kernels";
   m.attr("ARCH") = "gfx950";
+
+  m.def("stream_wait", [](u64 dst, u64 src) { check(stream_wait(dst, src), "stream_wait"); },
+        "dst waits for the work queued on src so far (pooled event)");
 
   // hp: device hyper-parameter array (0 = use hv, passed by value); zero_g: fused zero_grad
   m.def("sgd_step", [](u64 p, u64 g, int gbf, u64 mom, u64 p16, u64 hp, const std::vector<float>& hv, long n,

@@ -72,12 +72,24 @@ def main():
         step()
     host = (time.perf_counter() - t0) / steps * 1e3
     torch.cuda.synchronize()
-    pr = cProfile.Profile()
-    pr.enable()
-    for _ in range(steps):
-        step()
-    pr.disable()
-    torch.cuda.synchronize()
+    # backward on the calling thread so the profile sees the Functions' Python (autograd
+    # otherwise runs CUDA backward on a device thread)
+    with torch.autograd.set_multithreading_enabled(False):
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        host1 = (time.perf_counter() - t0) / steps * 1e3
+        torch.cuda.synchronize()
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(steps):
+            step()
+        pr.disable()
+        torch.cuda.synchronize()
+    print("host ms/step, backward on the calling thread: %.3f" % host1)
     out = io.StringIO()
     pstats.Stats(pr, stream=out).sort_stats("tottime").print_stats(45)
     print("host ms/step (unprofiled, pacer off): %.3f" % host)
