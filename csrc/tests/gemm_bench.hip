@@ -108,6 +108,26 @@ static void launch128x64(const CoreParams& p, int layout, dim3 g, hipStream_t s)
   else if (layout == 1) k128x64<GDenseKC, GDenseNC><<<g, 256, 0, s>>>(p);
   else k128x64<GDenseNC, GDenseNC><<<g, 256, 0, s>>>(p);
 }
+// the same tile with the DMA of K tile t+1 in flight during tile t (two LDS stages, 48 KB:
+// three blocks per CU still fit -- the shape only has three per CU), 4 or 8 waves
+template <template <int, int, int> class GA, template <int, int, int> class GB>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k128x64s2(CoreParams P) {
+  mfma_gemm_glds<128, 64, 2, 2, GA, GB, EPI_BF16, 2>(P);
+}
+template <template <int, int, int> class GA, template <int, int, int> class GB>
+__global__ void __launch_bounds__(512) k128x64w8(CoreParams P) {
+  mfma_gemm_glds<128, 64, 4, 2, GA, GB, EPI_BF16, 2>(P);
+}
+static void launch128x64s2(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) k128x64s2<GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
+  else if (layout == 1) k128x64s2<GDenseKC, GDenseNC><<<g, 256, 0, s>>>(p);
+  else k128x64s2<GDenseNC, GDenseNC><<<g, 256, 0, s>>>(p);
+}
+static void launch128x64w8(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
+  if (layout == 0) k128x64w8<GDenseKC, GDenseKC><<<g, 512, 0, s>>>(p);
+  else if (layout == 1) k128x64w8<GDenseKC, GDenseNC><<<g, 512, 0, s>>>(p);
+  else k128x64w8<GDenseNC, GDenseNC><<<g, 512, 0, s>>>(p);
+}
 static void launch128x96(const CoreParams& p, int layout, dim3 g, hipStream_t s) {
   if (layout == 0) k128x96<GDenseKC, GDenseKC><<<g, 256, 0, s>>>(p);
 }
@@ -239,6 +259,8 @@ int main(int argc, char** argv) {
                     {"w256x128", 256, 128, launch256x128},
                     {"glds128", 128, 128, launch128},
                     {"g128x64", 128, 64, launch128x64},
+                    {"g128x64s2", 128, 64, launch128x64s2},
+                    {"g128x64w8", 128, 64, launch128x64w8},
                     {"g128x96", 128, 96, launch128x96},
                     {"g256x96", 256, 96, launch256x96},
                     {"w4n256", 256, 256, launchw4<256>},
