@@ -242,7 +242,7 @@ class _BottleneckFn(torch.autograd.Function):
             ddp.notify_grad_ready(bn.bias)
             return r
 
-        def dgrad(conv, dz, shape, bn_src, out=None, beta=0.0, res=None):
+        def dgrad(conv, dz, shape, bn_src, out=None, beta=0.0, res=None, beta_stride=1):
             """Input gradient; with ``bn_src`` = (z, mask[, z2]) of the BN(s) that consume it,
             also their backward statistics from the epilogue.  Returns (dx, partials,
             partials2); z2 is honoured by the residual-gated (``res``) form only."""
@@ -250,7 +250,7 @@ class _BottleneckFn(torch.autograd.Function):
             if bn is not None and res is None:
                 bn = bn[:2]
             r = raw.conv_dgrad(dz, conv.weight, shape, conv.stride, conv.padding, out=out, beta=beta, bn=bn,
-                               res=res)
+                               res=res, beta_stride=beta_stride)
             if bn is None:
                 return r, None, None
             return (r[0], r[1], r[2] if len(r) > 2 else None)
@@ -325,6 +325,7 @@ class _BottleneckFn(torch.autograd.Function):
             dz1, _ = bn_back(blk.bn1, dy1, z1, (s1, m1), partials=p1)
             del dy1
         del p1
+        dx_stride = 1  # > 1: dx holds the strided shortcut's one parity class only (below)
         if ds is not None:
             zd, sd = saved[12], saved[13]
             c = ds["conv"]
@@ -343,7 +344,12 @@ class _BottleneckFn(torch.autograd.Function):
                 else:
                     dzd, _ = bn_back(ds["bn"], dres, zd, (sd, None))
                 del dres
-                dx = raw.conv_dgrad(dzd, c.weight, x.shape, c.stride, c.padding)
+                # strided 1x1 shortcut: only its one non-empty parity class is written; conv1's
+                # input gradient below reads the other pixels as zeros (never stored)
+                sparse = (coef1 is None and c.stride > 1 and c.padding == 0 and c.weight.shape[1:3] == (1, 1)
+                          and config.get("CLOUD_AMD_DS_SPARSE_DGRAD"))
+                dx = raw.conv_dgrad(dzd, c.weight, x.shape, c.stride, c.padding, skip_empty=sparse)
+                dx_stride = c.stride if sparse else 1
                 wgrad(c, dzd, x)
                 del dzd
         elif gate_res:
@@ -366,7 +372,8 @@ class _BottleneckFn(torch.autograd.Function):
             del dy1
             p_prev, p_prev2 = (None, None) if bn_src is None else (r[1], r[2] if len(r) > 2 else None)
         else:
-            _, p_prev, p_prev2 = dgrad(blk.conv1, dz1, x.shape, ctx.prev_src, out=dx, beta=1.0, res=res1)
+            _, p_prev, p_prev2 = dgrad(blk.conv1, dz1, x.shape, ctx.prev_src, out=dx, beta=1.0, res=res1,
+                                       beta_stride=dx_stride)
         del dout
         if p_prev is not None:
             _park(dx, p_prev, p_prev2)

@@ -106,8 +106,16 @@ def conv_fwd(x, w, stride, padding, stats=None):
     return y
 
 
-def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res=None):
+def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res=None, beta_stride=1,
+               skip_empty=False):
     """dx (+= beta * out) for y = conv(x, w).
+
+    ``skip_empty`` (strided convolutions, beta 0): the output-parity classes no filter tap
+    reaches -- for a 1x1 / stride-s / pad-0 projection shortcut, every pixel but those with h
+    and w multiples of s -- are left UNWRITTEN instead of zero-filled.  ``beta_stride`` = s
+    (1x1 convolutions with beta): ``out`` is such a tensor; its unwritten pixels are read as
+    zeros (never loaded), so the pair writes dx once instead of zero-filling (s^2-1)/s^2 of it
+    and reading those zeros back.
 
     ``bn=(z, mask)``: dx is the gradient of a BatchNorm(+ReLU) output whose input was
     ``z`` (``mask``: its ReLU bitmask, or None).  The GEMM epilogue then also writes the
@@ -124,6 +132,9 @@ def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res
     N, H, W, Cin = x_shape
     Cout, KH, KW, _ = w.shape
     dx = out if out is not None else torch.empty(x_shape, dtype=torch.bfloat16, device=dy.device)
+    if beta_stride > 1:
+        assert is_gemm_conv(w, stride, padding) and res is None and out is not None and beta != 0, \
+            "beta_stride: a 1x1 input gradient accumulated into a skip_empty strided one"
     if res is not None:
         src, rmask = res
         assert is_gemm_conv(w, stride, padding) and src.shape == dx.shape and src.is_contiguous()
@@ -151,8 +162,13 @@ def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res
         assert z.shape == dx.shape and z.is_contiguous() and (mask is None or mask.shape == (N * H * W, Cin // 8))
         if is_gemm_conv(w, stride, padding):
             part = torch.empty(((N * H * W + 127) // 128, 2, Cin), dtype=torch.float32, device=dy.device)
-            ext.gemm_bf16_bnstats(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin, Cout,
-                                  float(beta), z.data_ptr(), _ext.ptr(mask), part.data_ptr(), _st(dy.device))
+            if beta_stride > 1:
+                ext.dgrad_gemm(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin, Cout,
+                               float(beta), 0, 0, z.data_ptr(), _ext.ptr(mask), part.data_ptr(), _st(dy.device),
+                               par_s=int(beta_stride), par_h=H, par_w=W)
+            else:
+                ext.gemm_bf16_bnstats(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin,
+                                      Cout, float(beta), z.data_ptr(), _ext.ptr(mask), part.data_ptr(), _st(dy.device))
             _log("dgrad1x1_bn", N * H * W, Cin, Cout, _nb(dy, w, dx, z, mask) + (_nb(dx) if beta else 0))
         else:
             rows = ext.conv_dgrad_stat_rows(N, H, W, Cin, Cout, KH, KW, stride, stride, padding, padding,
@@ -165,12 +181,18 @@ def conv_dgrad(dy, w, x_shape, stride, padding, out=None, beta=0.0, bn=None, res
                  launches=stride * stride)
         return dx, part
     if is_gemm_conv(w, stride, padding):
-        ext.gemm_bf16(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin, Cout, 0,
-                      float(beta), _st(dy.device))
-        _log("dgrad1x1", N * H * W, Cin, Cout, _nb(dy, w, dx) + (_nb(dx) if beta else 0))
+        if beta_stride > 1:
+            ext.dgrad_gemm(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin, Cout,
+                           float(beta), 0, 0, 0, 0, 0, _st(dy.device), par_s=int(beta_stride), par_h=H, par_w=W)
+        else:
+            ext.gemm_bf16(NN, dy.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, N * H * W, Cin, Cout, 0,
+                          float(beta), _st(dy.device))
+        _log("dgrad1x1", N * H * W, Cin, Cout, _nb(dy, w, dx) + (_nb(dx) // beta_stride ** 2 if beta else 0))
         return dx
+    if skip_empty:
+        assert beta == 0 and stride > 1, "skip_empty: strided convolutions, beta 0"
     ext.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), N, H, W, Cin, Cout, KH, KW, stride, stride, padding,
-                   padding, float(beta), _st(dy.device))
+                   padding, float(beta), _st(dy.device), skip_empty=int(bool(skip_empty)))
     _log("dgrad%dx%ds%d" % (KH, KW, stride), N * H * W, Cin, Cout * KH * KW, _nb(dy, w, dx), launches=stride * stride)
     return dx
 

@@ -50,7 +50,8 @@ int ca_gemm_xa_dw(const bf16_t*, const bf16_t*, const uint8_t*, const float*, co
                   const bf16_t*, const uint8_t*, float*, const bf16_t*, float*, const bf16_t*, long, void*, int, float,
                   float*, int, hipStream_t);
 int ca_dgrad_gemm(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float, const bf16_t*,
-                  const uint8_t*, const bf16_t*, const uint8_t*, float*, hipStream_t, const bf16_t*, float*);
+                  const uint8_t*, const bf16_t*, const uint8_t*, float*, hipStream_t, const bf16_t*, float*, int, int,
+                  int);
 int ca_conv_dgrad_bnstats(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int,
                           int, float, const bf16_t*, const uint8_t*, float*, hipStream_t);
 int ca_u8_normalize(const uint8_t*, bf16_t*, long, int, const float*, const float*, hipStream_t);
@@ -82,7 +83,7 @@ int ca_conv_fwd_ex(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, in
 int ca_conv_fwd(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int, float*,
                 hipStream_t);
 int ca_conv_dgrad(const bf16_t*, const bf16_t*, bf16_t*, int, int, int, int, int, int, int, int, int, int, int, float,
-                  hipStream_t);
+                  hipStream_t, int);
 int ca_conv_wgrad(const bf16_t*, const bf16_t*, void*, int, float, int, int, int, int, int, int, int, int, int, int,
                   int, int, float*, hipStream_t);
 int ca_splitk_reduce(const float*, int, long, void*, int, float, hipStream_t);
@@ -229,14 +230,17 @@ PYBIND11_MODULE(_C, m) {
           "gemm_bf16_bnstats");
   });
   m.def("dgrad_gemm", [](int layout, u64 A, long lda, u64 B, long ldb, u64 C, long ldc, int M, int N, int K,
-                         float beta, u64 res, u64 res_mask, u64 z, u64 mask, u64 stats, u64 s, u64 z2, u64 stats2) {
+                         float beta, u64 res, u64 res_mask, u64 z, u64 mask, u64 stats, u64 s, u64 z2, u64 stats2,
+                         int par_s, int par_h, int par_w) {
     check(ca_dgrad_gemm(layout, P(const bf16_t*, A), lda, P(const bf16_t*, B), ldb, P(bf16_t*, C), ldc, M, N, K, beta,
                         P(const bf16_t*, res), P(const uint8_t*, res_mask), P(const bf16_t*, z),
-                        P(const uint8_t*, mask), P(float*, stats), S(s), P(const bf16_t*, z2), P(float*, stats2)),
+                        P(const uint8_t*, mask), P(float*, stats), S(s), P(const bf16_t*, z2), P(float*, stats2), par_s,
+                        par_h, par_w),
           "dgrad_gemm");
   }, py::arg("layout"), py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"),
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("beta"), py::arg("res"), py::arg("res_mask"), py::arg("z"),
-        py::arg("mask"), py::arg("stats"), py::arg("s"), py::arg("z2") = 0, py::arg("stats2") = 0);
+        py::arg("mask"), py::arg("stats"), py::arg("s"), py::arg("z2") = 0, py::arg("stats2") = 0,
+        py::arg("par_s") = 0, py::arg("par_h") = 0, py::arg("par_w") = 0);
   m.def("gemm_xa", [](int layout, int mode, u64 src0, u64 src1, u64 mask_in, u64 c0, u64 c1, u64 c2, u64 c3, u64 side,
                       u64 mask_out, long lda, u64 B, long ldb, u64 C, long ldc, int M, int N, int K, float beta,
                       u64 res, u64 res_mask, u64 z, u64 mask, u64 stats, u64 z2, u64 stats2, u64 s) {
@@ -359,10 +363,12 @@ PYBIND11_MODULE(_C, m) {
                          ph, pw, P(const float*, bias), act, S(s)), "conv_fwd_ex");
   });
   m.def("conv_dgrad", [](u64 dy, u64 w, u64 dx, int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int sh,
-                         int sw, int ph, int pw, float beta, u64 s) {
+                         int sw, int ph, int pw, float beta, u64 s, int skip_empty) {
     check(ca_conv_dgrad(P(const bf16_t*, dy), P(const bf16_t*, w), P(bf16_t*, dx), Nb, H, W, Cin, Cout, KH, KW, sh, sw,
-                        ph, pw, beta, S(s)), "conv_dgrad");
-  });
+                        ph, pw, beta, S(s), skip_empty), "conv_dgrad");
+  }, py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("Cin"),
+        py::arg("Cout"), py::arg("KH"), py::arg("KW"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"),
+        py::arg("beta"), py::arg("s"), py::arg("skip_empty") = 0);
   m.def("conv_wgrad", [](u64 dy, u64 x, u64 dw, int dw_bf16, float beta, int Nb, int H, int W, int Cin, int Cout,
                          int KH, int KW, int sh, int sw, int ph, int pw, int splits, u64 ws, u64 s) {
     check(ca_conv_wgrad(P(const bf16_t*, dy), P(const bf16_t*, x), P(void*, dw), dw_bf16, beta, Nb, H, W, Cin, Cout,

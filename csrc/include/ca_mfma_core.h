@@ -109,7 +109,23 @@ struct CoreParams {
   int split_xcd;  // split-K grids: deal (split, tile) ranges to XCDs split-major (blk_pos)
   int prw_chunks; // persistent resident-weight core: column chunks of BN (0 / 1 = the whole N resident)
   unsigned long long* stamps;  // diagnostic builds only (in-kernel s_memtime stamps)
+  // sparse beta source: with bpar_s > 1 the old C (output rows = NHWC pixels of an
+  // [*, H, W] image, W = div_bpw.d, H = div_bph.d) holds values only at pixels whose h and w
+  // are multiples of bpar_s -- the others are implicit zeros, never read (a strided 1x1
+  // convolution's input gradient, written for its one non-empty parity class only)
+  int bpar_s;
+  FastDiv div_bpw, div_bph;
 };
+
+// whether the beta-accumulate source of output row `orow` is stored (see CoreParams::bpar_s)
+__device__ __forceinline__ bool beta_row_stored(const CoreParams& P, long orow) {
+  if (P.bpar_s <= 1) return true;
+  const uint32_t t = fdiv((uint32_t)orow, P.div_bpw);
+  const int w = (int)((uint32_t)orow - t * P.div_bpw.d);
+  const uint32_t t2 = fdiv(t, P.div_bph);
+  const int h = (int)(t - t2 * P.div_bph.d);
+  return (h % P.bpar_s) == 0 && (w % P.bpar_s) == 0;
+}
 
 // output row of GEMM row gm (identity unless the parity-class row map is on)
 __device__ __forceinline__ long out_row(const CoreParams& P, int gm) {
@@ -487,7 +503,9 @@ __device__ __forceinline__ void gemm_epilogue(const CoreParams& P, f4v (&acc)[FM
         okr[u] = gm < P.M && gn < P.N;
         orow[u] = okr[u] ? out_row(P, gm) : 0;
         const bf16_t* bsrc = (RES && P.res_src) ? P.res_src : Cg;
-        opre[u] = (has_beta && okr[u]) ? *reinterpret_cast<const s8v*>(bsrc + orow[u] * P.ldc + gn) : zero8();
+        opre[u] = (has_beta && okr[u] && beta_row_stored(P, orow[u]))
+                      ? *reinterpret_cast<const s8v*>(bsrc + orow[u] * P.ldc + gn)
+                      : zero8();
         mk[u] = 0xff00u;
         if constexpr (!RSTAT) {
           dsrc[u] = (P.dact_src && okr[u]) ? *reinterpret_cast<const s8v*>(P.dact_src + (long)gm * P.ld_aux + gn)

@@ -1126,7 +1126,7 @@ static int launch_dgrad_s(const CoreParams& q, int Cin, hipStream_t s) {
 
 static int conv_dgrad_impl(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb, int H, int W, int Cin, int Cout,
                            int KH, int KW, int sh, int sw, int ph, int pw, float beta, const bf16_t* bnz,
-                           const uint8_t* bnmask, float* stats, hipStream_t s) {
+                           const uint8_t* bnmask, float* stats, hipStream_t s, int skip_empty = 0) {
   CoreParams p = conv_params(Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw);
   if (!geom_ok(Cin, Cout, (long)Nb * H * W)) return -1;
   if (beta == 0.f && halo_shape(H, W, Cin, Cout, KH, KW, sh, sw, ph, pw))
@@ -1155,6 +1155,9 @@ static int conv_dgrad_impl(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb
         q.Hq = (H - py + sh - 1) / sh;
         q.Wq = (W - px + sw - 1) / sw;
         if (q.Hq <= 0 || q.Wq <= 0) continue;
+        // skip_empty: a class no tap reaches keeps its pixels unwritten (the caller's next
+        // GEMM into dx reads them as zeros: CoreParams::bpar_s)
+        if (skip_empty && q.dg_nh * q.dg_nw == 0) continue;
         q.div_hq = make_fastdiv(q.Hq);
         q.div_wq = make_fastdiv(q.Wq);
         q.div_nw = make_fastdiv(q.dg_nw > 0 ? q.dg_nw : 1);
@@ -1176,9 +1179,15 @@ static int conv_dgrad_impl(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb
 extern "C" {
 
 // dx[Nb,H,W,Cin] = dgrad(dy[Nb,OH,OW,Cout], w) (+ beta * dx).
+// skip_empty (strided, beta 0 only): output-parity classes without taps are left unwritten
+// instead of zero-filled.
 int ca_conv_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, int Nb, int H, int W, int Cin, int Cout, int KH,
-                  int KW, int sh, int sw, int ph, int pw, float beta, hipStream_t s) {
-  return conv_dgrad_impl(dy, w, dx, Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw, beta, nullptr, nullptr, nullptr, s);
+                  int KW, int sh, int sw, int ph, int pw, float beta, hipStream_t s, int skip_empty) {
+  if (skip_empty && (beta != 0.f || (sh == 1 && sw == 1))) return -1;
+  // (the non-LDS-DMA loaders run one implicit GEMM over every pixel: it writes the empty
+  // classes' zeros anyway, which a sparse-beta reader may equally skip)
+  return conv_dgrad_impl(dy, w, dx, Nb, H, W, Cin, Cout, KH, KW, sh, sw, ph, pw, beta, nullptr, nullptr, nullptr, s,
+                         skip_empty);
 }
 
 // Same, plus the BN-backward statistics epilogue (see ca_gemm_bf16_bnstats): `stats`

@@ -783,7 +783,8 @@ extern "C" {
 
 int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N,
                   int K, float beta, const bf16_t* res_src, const uint8_t* res_mask, const bf16_t* bnz,
-                  const uint8_t* bnmask, float* stats, hipStream_t s, const bf16_t* bnz2, float* stats2);
+                  const uint8_t* bnmask, float* stats, hipStream_t s, const bf16_t* bnz2, float* stats2,
+                  int par_s, int par_h, int par_w);
 
 // Select the GEMM core for this process (values as CLOUD_AMD_GEMM_CORE above); returns
 // the previous one.
@@ -869,7 +870,7 @@ int ca_gemm_bf16_bnstats(int layout, const bf16_t* A, long lda, const bf16_t* B,
                          int M, int N, int K, float beta, const bf16_t* bnz, const uint8_t* bnmask, float* stats,
                          hipStream_t s) {
   return ca_dgrad_gemm(layout, A, lda, B, ldb, C, ldc, M, N, K, beta, nullptr, nullptr, bnz, bnmask, stats, s, nullptr,
-                       nullptr);
+                       nullptr, 0, 0, 0);
 }
 
 // Input-gradient GEMM (NN) with the two backward epilogue options of a ResNet block:
@@ -880,13 +881,22 @@ int ca_gemm_bf16_bnstats(int layout, const bf16_t* A, long lda, const bf16_t* B,
 //   bnz2 / stats2 (with res_src): the same for a second BN fed by the same gated gradient.
 int ca_dgrad_gemm(int layout, const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N,
                   int K, float beta, const bf16_t* res_src, const uint8_t* res_mask, const bf16_t* bnz,
-                  const uint8_t* bnmask, float* stats, hipStream_t s, const bf16_t* bnz2, float* stats2) {
+                  const uint8_t* bnmask, float* stats, hipStream_t s, const bf16_t* bnz2, float* stats2,
+                  int par_s, int par_h, int par_w) {
   if (M <= 0 || N < 8 || N % 8 != 0 || K % 8 != 0 || layout != 1 || (bnz && !stats)) return -1;
   if (bnz2 && (!bnz || !stats2 || !res_src)) return -1;
+  // par_s > 1: old C stored only at pixels (h, w) both multiples of par_s of an [*, par_h, par_w]
+  // image (rows are its NHWC pixels, ldc its channels): the other rows' beta term is zero
+  if (par_s > 1 && (par_h <= 0 || par_w <= 0 || M % ((long)par_h * par_w) != 0 || res_src)) return -1;
   CoreParams p = base_params(A, lda, B, ldb, C, ldc, M, N, K);
   p.beta = beta;
   p.res_src = res_src;
   p.res_mask = res_mask;
+  if (par_s > 1 && beta != 0.f) {
+    p.bpar_s = par_s;
+    p.div_bpw = make_fastdiv(par_w);
+    p.div_bph = make_fastdiv(par_h);
+  }
   if (!bnz) return dispatch<EPI_BF16>(layout, p, 1, s);
   p.stats = stats;
   p.bnz = bnz;

@@ -535,3 +535,41 @@ def test_dgrad_gated_residual_epilogue(with_bn):
     else:
         dx = raw.conv_dgrad(dy, w, src.shape, 1, 0, beta=1.0, res=(src, bits))
     torch.testing.assert_close(dx.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("H,with_bn", [(16, True), (15, True), (14, False)])
+def test_sparse_shortcut_dgrad_then_sparse_beta_accumulate(H, with_bn):
+    """Projection-block input gradient without the zero-fill: the strided 1x1 shortcut's
+    dgrad writes only its non-empty parity class (skip_empty; the other pixels hold NaN
+    here) and conv1's 1x1 dgrad accumulates into it reading those pixels as zeros
+    (beta_stride).  Must equal the dense pair bitwise, and the fp32 reference closely."""
+    from cloud_amd.ops import raw
+
+    torch.manual_seed(21)
+    N, Cin, Cd, C1, s = 3, 64, 256, 128, 2
+    OH = (H - 1) // s + 1
+    dzd = torch.randn(N, OH, OH, Cd, device=DEV).to(torch.bfloat16)
+    wd = (torch.randn(Cd, 1, 1, Cin, device=DEV) / Cd ** 0.5).to(torch.bfloat16)
+    dz1 = torch.randn(N, H, H, C1, device=DEV).to(torch.bfloat16)
+    w1 = (torch.randn(C1, 1, 1, Cin, device=DEV) / C1 ** 0.5).to(torch.bfloat16)
+    z = (torch.randn(N, H, H, Cin, device=DEV) + 0.3).to(torch.bfloat16)
+    bits = _relu_bits(torch.rand(N * H * H, Cin, device=DEV) > 0.4)
+    bn = (z, bits) if with_bn else None
+
+    dense = raw.conv_dgrad(dzd, wd, (N, H, H, Cin), s, 0)
+    r_dense = raw.conv_dgrad(dz1, w1, (N, H, H, Cin), 1, 0, out=dense, beta=1.0, bn=bn)
+    dx_sp = torch.full((N, H, H, Cin), float("nan"), device=DEV, dtype=torch.bfloat16)
+    raw.conv_dgrad(dzd, wd, (N, H, H, Cin), s, 0, out=dx_sp, skip_empty=True)
+    even = torch.zeros(H, H, dtype=torch.bool, device=DEV)
+    even[::s, ::s] = True
+    assert torch.isnan(dx_sp[:, ~even]).all() and not torch.isnan(dx_sp[:, even]).any()
+    r_sp = raw.conv_dgrad(dz1, w1, (N, H, H, Cin), 1, 0, out=dx_sp, beta=1.0, bn=bn, beta_stride=s)
+    if with_bn:
+        assert torch.equal(r_sp[0], r_dense[0])
+        torch.testing.assert_close(r_sp[1], r_dense[1], atol=0, rtol=0)
+    else:
+        assert torch.equal(r_sp, r_dense)
+    ref = dz1.float().reshape(-1, C1) @ w1.float().reshape(C1, Cin)
+    ref = ref.reshape(N, H, H, Cin)
+    ref[:, ::s, ::s] += (dzd.float().reshape(-1, Cd) @ wd.float().reshape(Cd, Cin)).reshape(N, OH, OH, Cin)
+    torch.testing.assert_close(dx_sp.float(), ref, atol=3e-2, rtol=3e-2)
