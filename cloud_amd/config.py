@@ -166,7 +166,11 @@ _VARS = [
         "(K = 512 -> N = 128, 8-wave workgroups holding the 512 x 128 dW block)", "ops"),
     Var("CLOUD_AMD_BN_FOLD_WGRAD1", bool, False, "the same one-pass input + weight gradient for stage 1's conv1 with "
         "bn1's backward apply (K = 64 -> N = 256: dz1 never written, four output chunks per tile)", "ops"),
-    Var("CLOUD_AMD_XA_WAVES", int, 8, "128 x 128 transform-A GEMMs (BN folded into the 1x1 convs): 8-wave "
+    Var("CLOUD_AMD_XA_N256", int, 1, "transform-A GEMMs (BN folded into a 1x1 conv) with N a multiple of 256: "
+        "1 = 128 x 256 tiles on 16-wave workgroups (each A tile transformed once), 2 = 128 x 256 on 8 waves, "
+        "0 = 128 x 128 tiles.  Only the fold sites CLOUD_AMD_BN_FOLD_MAX_N admits reach them (none at the "
+        "ResNet-50 default; measured in docs/performance.md, round 6)", "ops"),
+    Var("CLOUD_AMD_XA_WAVES", int, 8,"128 x 128 transform-A GEMMs (BN folded into the 1x1 convs): 8-wave "
         "workgroups (<= 128 registers, two per CU) or 4", "ops"),
     Var("CLOUD_AMD_XA_WAVES_N64", bool, True, "the 128 x 64 transform-A GEMMs (stage 1) on 8-wave workgroups too "
         "(with CLOUD_AMD_XA_WAVES=8)", "ops"),

@@ -69,6 +69,7 @@ int ca_gmp_bwd(const void*, int, const bf16_t*, const bf16_t*, const float*, bf1
 int ca_gemm_bf16(int, const bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float*, float,
                  hipStream_t);
 int ca_gemm_set_core(int);
+int ca_gemm_set_xa_n256(int);
 int ca_gemm_set_streamk(int);
 int ca_gemm_experimental_built();
 int ca_gemm_stat_rows(int, int, int, long, long, long);
@@ -341,6 +342,7 @@ PYBIND11_MODULE(_C, m) {
                                   C, OH, OW, S(s)), "bn_relu_maxpool_s2k3");
   });
   m.def("gemm_set_core", [](int kind) { return ca_gemm_set_core(kind); });
+  m.def("gemm_set_xa_n256", [](int mode) { return ca_gemm_set_xa_n256(mode); });
   m.def("gemm_set_streamk", [](int mode) { return ca_gemm_set_streamk(mode); });
   m.def("experimental_built", []() { return ca_gemm_experimental_built() != 0; });
   m.def("maxpool_bnstats_parts", [](int N, int H, int W, int C) { return ca_maxpool_bnstats_parts(N, H, W, C); });

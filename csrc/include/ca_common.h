@@ -53,6 +53,15 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+// BatchNorm transforms with a FIXED evaluation order (explicit FMAs).  Every kernel that applies
+// one BatchNorm -- the separate passes (bn.hip, pool.hip) and the GEMM operand fetches that fold
+// it (ca_gemm_xa.h) -- must round identically; left to -ffp-contract, `A*d + B*x + D` contracts
+// differently from one template instantiation to the next.
+__device__ __forceinline__ float bn_affine(float x, float scale, float shift) { return __builtin_fmaf(x, scale, shift); }
+__device__ __forceinline__ float bn_bwd_affine(float a, float d, float b, float x, float dd) {
+  return __builtin_fmaf(a, d, __builtin_fmaf(b, x, dd));
+}
+
 // Wave-wide sum / max, every lane gets the result.  DPP within each 16-lane row (row_ror 8 / 4,
 // quad swaps: VALU ops, no LDS permutes), then the four row totals read as scalars in a fixed
 // order -- against six ds_bpermute round trips of the __shfl_xor butterfly.

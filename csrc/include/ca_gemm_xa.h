@@ -177,15 +177,15 @@ __device__ __forceinline__ void mfma_gemm_xa(const CoreParams& P, const XaParams
           float d = bf2f((bf16_t)a0[i][j]);
           if (X.mask_in) d = ((mb[i] >> j) & 1u) ? d : 0.f;
           const float c2 = cf[2][j >> 2][j & 3];
-          v = c0 * d + c1 * bf2f((bf16_t)a1[i][j]) + c2;
+          v = bn_bwd_affine(c0, d, c1, bf2f((bf16_t)a1[i][j]), c2);
         } else {
           // bn_apply_kernel<true, RES>: z*scale + shift (+ r), ReLU, bit = y > 0
-          float z = bf2f((bf16_t)a0[i][j]) * c0 + c1;
+          float z = bn_affine(bf2f((bf16_t)a0[i][j]), c0, c1);
           if constexpr (XM == XA_BN_RES_RELU) z += bf2f((bf16_t)a1[i][j]);
           if constexpr (XM == XA_BN_RESBN_RELU) {
             // the shortcut BN output rounded to bf16 as if stored (bn_apply_resbn_kernel)
-            const float idn = bf2f(f2bf(bf2f((bf16_t)a1[i][j]) * cf[2][j >> 2][j & 3] + cf[3][j >> 2][j & 3]));
-            z = bf2f((bf16_t)a0[i][j]) * c0 + c1 + idn;
+            const float idn = bf2f(f2bf(bn_affine(bf2f((bf16_t)a1[i][j]), cf[2][j >> 2][j & 3], cf[3][j >> 2][j & 3])));
+            z = bn_affine(bf2f((bf16_t)a0[i][j]), c0, c1) + idn;
           }
           z = fmaxf(z, 0.f);
           bits |= (z > 0.f ? 1u : 0u) << j;
@@ -383,8 +383,8 @@ __device__ __forceinline__ void mfma_gemm_xa_dw(const CoreParams& P, const XaPar
         for (int j = 0; j < 8; ++j) {
           float d = bf2f((bf16_t)a0[i][j]);
           if (X.mask_in) d = ((mb[i] >> j) & 1u) ? d : 0.f;
-          o[j] = (short)f2bf(cf[0][j >> 2][j & 3] * d + cf[1][j >> 2][j & 3] * bf2f((bf16_t)a1[i][j]) +
-                             cf[2][j >> 2][j & 3]);
+          o[j] = (short)f2bf(
+              bn_bwd_affine(cf[0][j >> 2][j & 3], d, cf[1][j >> 2][j & 3], bf2f((bf16_t)a1[i][j]), cf[2][j >> 2][j & 3]));
         }
         *reinterpret_cast<s8v*>(As + row * BK + ((c8 ^ (row & 7)) << 3)) = o;
       }
@@ -646,8 +646,8 @@ __device__ __forceinline__ void mfma_gemm_xa_dw_deep(const CoreParams& P, const 
       for (int j = 0; j < 8; ++j) {
         float d = bf2f((bf16_t)a0[p][i][j]);
         if (X.mask_in) d = ((mb[p][i] >> j) & 1u) ? d : 0.f;
-        o[j] = (short)f2bf(cf[0][j >> 2][j & 3] * d + cf[1][j >> 2][j & 3] * bf2f((bf16_t)a1[p][i][j]) +
-                           cf[2][j >> 2][j & 3]);
+        o[j] = (short)f2bf(bn_bwd_affine(cf[0][j >> 2][j & 3], d, cf[1][j >> 2][j & 3], bf2f((bf16_t)a1[p][i][j]),
+                                         cf[2][j >> 2][j & 3]));
       }
       *reinterpret_cast<s8v*>(As + row * BK + ((c8 ^ (row & 7)) << 3)) = o;
     }

@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(BLK) bn_apply_kernel(const bf16_t* __restrict_
     uint32_t bits = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float z = v[j] * sc[j] + sh[j];
+      float z = bn_affine(v[j], sc[j], sh[j]);
       if (RES) z += rv[j];
       if (RELU) {
         z = fmaxf(z, 0.f);
@@ -324,8 +324,8 @@ __global__ void __launch_bounds__(BLK) bn_apply_resbn_kernel(const bf16_t* __res
     for (int j = 0; j < 8; ++j) {
       // the shortcut BN output rounded to bf16 exactly as if it had been stored, so the
       // block stays bit-compatible with the op-by-op path
-      const float idn = bf2f(f2bf(rv[j] * rs[j] + rh[j]));
-      float z = v[j] * sc[j] + sh[j] + idn;
+      const float idn = bf2f(f2bf(bn_affine(rv[j], rs[j], rh[j])));
+      float z = bn_affine(v[j], sc[j], sh[j]) + idn;
       if (RELU) {
         z = fmaxf(z, 0.f);
         bits |= (z > 0.f ? 1u : 0u) << j;
@@ -552,7 +552,7 @@ __global__ void __launch_bounds__(BLK) bn_bwd_apply_kernel(const bf16_t* __restr
     if (RELU) relu_gate(d, y, mask, r, o, t.CT, vc);
     if (DRES) st8bf(dres + o, d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) xv[j] = A[j] * d[j] + B[j] * xv[j] + D[j];
+    for (int j = 0; j < 8; ++j) xv[j] = bn_bwd_affine(A[j], d[j], B[j], xv[j], D[j]);
     st8bf(dx + o, xv);
   }
 }

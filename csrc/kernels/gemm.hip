@@ -634,6 +634,22 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) x
   mfma_gemm_xa<BM, BN, BKC, EPI, XM, 512>(P, X);
 }
 
+// 128 x 256 tiles on 8 waves (2 x 4, wave tile 64 x 64): one workgroup per CU (64 accumulator
+// registers per lane on top of the 128 x 128 form's staging)
+template <int BM, int BN, bool BKC, int EPI, int XM>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) xa_gemm8w_kernel(CoreParams P,
+                                                                                               XaParams X) {
+  mfma_gemm_xa<BM, BN, BKC, EPI, XM, 512>(P, X);
+}
+
+// 128 x 256 tiles on 16 waves (2 x 8, wave tile 64 x 32: the 128 x 128 8-wave form's registers,
+// <= 128 per lane): one workgroup per CU, 16 waves, each A tile transformed once
+template <int BM, int BN, bool BKC, int EPI, int XM>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) xa_gemm16_kernel(CoreParams P,
+                                                                                                XaParams X) {
+  mfma_gemm_xa<BM, BN, BKC, EPI, XM, 1024>(P, X);
+}
+
 // The 128 x 128 transform-A GEMMs on 8-wave workgroups (default; CLOUD_AMD_XA_WAVES=4: the
 // 4-wave form).  ResNet-50 b1024: xa kernels 11.2 -> 10.8 ms/step, 14,614 / 14,617 / 14,560 ->
 // 14,668 / 14,650 / 14,582 img/s interleaved (profiles/r4_s20/).
@@ -646,6 +662,19 @@ static bool xa_waves8_n64() {
     v = (e && e[0] == '0') ? 0 : 1;
   }
   return v != 0;
+}
+// CLOUD_AMD_XA_N256: transform-A GEMMs with N a multiple of 256 (ResNet-50 stages 3-4: bn3 ->
+// conv3 dgrad, bn3 -> next conv1 at N = 256 / 512) on 128 x 256 tiles, so each A tile is read
+// and BN-transformed once per 256 columns instead of once per 128.  1 (default): 16-wave
+// workgroups (wave tile 64 x 32, <= 128 registers: one per CU); 2: 8 waves (64 x 64, ~190
+// registers: one per CU at half the waves); 0: off (128 x 128 tiles)
+int g_xa_n256 = -1;
+static int xa_n256() {
+  if (g_xa_n256 < 0) {
+    const char* e = getenv("CLOUD_AMD_XA_N256");
+    g_xa_n256 = (e && (e[0] == '0' || e[0] == '2')) ? e[0] - '0' : 1;
+  }
+  return g_xa_n256;
 }
 static bool xa_waves8() {
   static int v = -1;
@@ -720,7 +749,18 @@ int xa_launch(const CoreParams& p0, const XaParams& x, hipStream_t s) {
   CoreParams p = p0;
   p.split_xcd = 0;
   const int tm = (p.M + 127) / 128;
-  if (want_small_n(p, 1)) {
+  const int n256 = p.N % 256 == 0 ? xa_n256() : 0;
+  bool w16 = false;
+  if constexpr (EPI != EPI_BF16_BNR2) {  // three 16-wave statistics rows do not fit its LDS image
+    if (n256 == 1) {
+      xa_gemm16_kernel<128, 256, LB, EPI, XM><<<tm * (p.N / 256), 1024, 0, s>>>(p, x);
+      w16 = true;
+    }
+  }
+  if (w16) {
+  } else if (n256) {
+    xa_gemm8w_kernel<128, 256, LB, EPI, XM><<<tm * (p.N / 256), 512, 0, s>>>(p, x);
+  } else if (want_small_n(p, 1)) {
     bool w8 = false;
     if constexpr (EPI != EPI_BF16_BNR2) {  // its three statistics rows do not fit the 8-wave LDS image
       if (xa_waves8() && xa_waves8_n64()) {
@@ -808,6 +848,13 @@ int ca_gemm_set_core(int kind) {
   const int prev = core_kind();
   if (!CA_EXPERIMENTAL && kind >= 2 && kind <= 4) return -1;
   if (kind >= 0 && kind <= 6) g_core_kind = kind;
+  return prev;
+}
+
+// Transform-A tiles for N % 256 == 0 (values as CLOUD_AMD_XA_N256); returns the previous mode.
+int ca_gemm_set_xa_n256(int mode) {
+  const int prev = xa_n256();
+  if (mode >= 0 && mode <= 2) g_xa_n256 = mode;
   return prev;
 }
 

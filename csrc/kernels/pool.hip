@@ -599,7 +599,7 @@ __global__ void __launch_bounds__(256) maxpool_bwd_s2k3_bnapply_kernel(
         const us8 zv = *reinterpret_cast<const us8*>(z + off);
         us8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = f2bf(A[j] * acc[a][b][j] + B[j] * bf2f(zv[j]) + D[j]);
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(bn_bwd_affine(A[j], acc[a][b][j], B[j], bf2f(zv[j]), D[j]));
         *reinterpret_cast<us8*>(dz + off) = o;
       }
     }
