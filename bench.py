@@ -293,6 +293,7 @@ def main():
             "step_stats_rank0": step_stats,
             "gc_frozen_objects": gc_frozen,
             "max_steps_in_flight": pacer.depth if (pacer is not None and pacer.enabled) else None,
+            "pacer_step_ms": round(pacer.step_ms, 3) if (pacer is not None and pacer.step_ms) else None,
             "warnings": step_stats.pop("warnings"),
             "rank_ms_per_step": {"min": round(min(per_rank_ms), 3), "max": round(max(per_rank_ms), 3)},
             "first_step_latency_s": round(first_lat, 3),

@@ -238,6 +238,8 @@ def main():
             "impl": impl, "gc_frozen_objects": gc_frozen, "first_step_latency_s": round(first, 3),
             "run_to_first_step_s": round(run_to_first, 3) if run_to_first is not None else None,
             "startup_phases_rank0": phases, "host_launch_rank0": host_launch,
+            "max_steps_in_flight": pacer.depth if (pacer is not None and pacer.enabled) else None,
+            "pacer_step_ms": round(pacer.step_ms, 3) if (pacer is not None and pacer.step_ms) else None,
             "launched_via": benchlaunch.launched_via(), "comm": comm,
             "backend": dist.get_backend() if world > 1 else None,
             "shared_gpu": bool(config.get("CLOUD_AMD_SHARED_GPU")),

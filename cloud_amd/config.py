@@ -184,6 +184,9 @@ _VARS = [
     Var("CLOUD_AMD_MAX_STEPS_IN_FLIGHT", int, 2, "training loops (benches, Keras fit) let the host enqueue at most this "
         "many steps ahead of the GPU (runtime.step_pacer); bounds the memory in flight so the caching allocator "
         "stops requesting segments after warmup; 0 = unbounded", "runtime"),
+    Var("CLOUD_AMD_RUN_AHEAD_MS", float, 25.0, "the step pacer deepens its bound (up to 4 steps) so the queued steps "
+        "cover at least this much GPU time, measured on the first steps: short steps (BERT-base 8.7 ms -> 3) "
+        "absorb host hiccups, long ones keep CLOUD_AMD_MAX_STEPS_IN_FLIGHT; 0 = fixed depth", "runtime"),
     Var("CLOUD_AMD_GC_FREEZE", bool, True, "training loops (benches, Keras fit) call runtime.gc_control.freeze() after "
         "their first steps: objects alive then are excluded from Python's full collections", "runtime"),
     Var("CLOUD_AMD_WGRAD_STREAM", bool, True, "ResNet block / BERT layer backward: weight-gradient GEMMs on a "
