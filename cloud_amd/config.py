@@ -168,6 +168,7 @@ _VARS = [
         "bn1's backward apply (K = 64 -> N = 256: dz1 never written, four output chunks per tile)", "ops"),
     Var("CLOUD_AMD_XA_N256", int, 1, "transform-A GEMMs (BN folded into a 1x1 conv) with N a multiple of 256: "
         "1 = 128 x 256 tiles on 16-wave workgroups (each A tile transformed once), 2 = 128 x 256 on 8 waves, "
+        "3 = 16 waves with two K tiles' operands in flight (coefficients staged in LDS; K <= 2048), "
         "0 = 128 x 128 tiles.  Only the fold sites CLOUD_AMD_BN_FOLD_MAX_N admits reach them (none at the "
         "ResNet-50 default; measured in docs/performance.md, round 6)", "ops"),
     Var("CLOUD_AMD_XA_WAVES", int, 8,"128 x 128 transform-A GEMMs (BN folded into the 1x1 convs): 8-wave "

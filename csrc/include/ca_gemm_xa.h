@@ -239,6 +239,195 @@ __device__ __forceinline__ void mfma_gemm_xa(const CoreParams& P, const XaParams
 }
 
 // ----------------------------------------------------------------------------------------
+// The same GEMM on 128 x BN tiles with 16 waves and the raw operands of TWO K tiles in flight.
+// One 16-wave workgroup per CU with the one-deep pipeline above keeps only one 32-KB raw K tile
+// per CU on the way from HBM -- the latency-bandwidth product caps that at ~4 TB/s (measured:
+// the stage-3 folded dgrad 3.03 ms vs 2.84 for the passes it replaces, docs/performance.md).
+// Here the BN coefficients of the whole K range are staged in LDS once (K <= XA_DEEP_KMAX),
+// which frees the registers of a second A / B / mask staging set: tile t + 2's loads are issued
+// right after tile t's transform, so tiles t + 1 and t + 2 are in flight during tile t's MFMAs.
+// The loop is unrolled by two so every staging set is a compile-time register set.
+// Arithmetic (transform, K order, epilogue) is mfma_gemm_xa's: the outputs are bit-identical.
+constexpr int XA_DEEP_KMAX = 2048;
+
+template <int BN, bool B_KC, int EPI, int XM>
+__device__ __forceinline__ void mfma_gemm_xa_deep(const CoreParams& P, const XaParams& X) {
+  constexpr int BM = 128, NT = 1024, WM = 2, WN = NT / 128;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  static_assert(FN >= 1, "at least one 16-column fragment per wave");
+  constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK;
+  constexpr int STAGE = A_ELEMS + B_ELEMS;
+  constexpr int EPI_LD = EpiLayout<BN>::LD;
+  constexpr int SRED = 2 * (NT / (BN / 8)) * BN * 2;
+  constexpr int SMEM0 = (STAGE > BM * EPI_LD ? STAGE : BM * EPI_LD);
+  constexpr int SMEM = SMEM0 > SRED ? SMEM0 : SRED;
+  constexpr int CPB = B_ELEMS / 8 / NT;
+  using T = XaTraits<XM>;
+  static_assert(A_ELEMS == 8 * NT, "one A chunk per thread and K step");
+  static_assert(B_ELEMS % (8 * NT) == 0, "B chunks must divide the threads");
+  __shared__ __attribute__((aligned(16))) short smem[SMEM];
+  __shared__ __attribute__((aligned(16))) float coefs[T::NCOEF * XA_DEEP_KMAX];
+  short* const As = smem;
+  short* const Bs = smem + A_ELEMS;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = (P.N + BN - 1) / BN;
+  const BlkPos bp = blk_pos(P);
+  const int tm = bp.tile / tiles_n, tn = bp.tile % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = (P.K + BK - 1) / BK;
+  const int K8 = P.K >> 3;
+
+  {  // the coefficients of every k, once (the host guarantees K <= XA_DEEP_KMAX)
+    const float* cs[4] = {X.c0, X.c1, X.c2, X.c3};
+#pragma unroll
+    for (int q = 0; q < T::NCOEF; ++q)
+      for (int k = tid; k < P.K; k += NT) coefs[q * XA_DEEP_KMAX + k] = cs[q][k];
+  }
+
+  const auto rbw = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(P.B), (short)0,
+                                                     (int)buf_span((long)(B_KC ? P.N : P.K) * P.ldb * 2), 0x00020000);
+  auto b_coord = [&](int i, int& lrow, int& lcol) {
+    const int c = tid + i * NT;
+    if constexpr (B_KC) {
+      lrow = c >> 3;
+      lcol = c & 7;
+    } else {
+      lrow = c / (BN / 8);
+      lcol = c % (BN / 8);
+    }
+  };
+  const int arow = tid >> 3, c8 = tid & 7;
+  const long rows_left = (long)P.M - m0;
+  const uint32_t span = buf_span(rows_left * P.lda * 2);
+  const auto r0s = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(X.src0 + (long)m0 * P.lda), (short)0,
+                                                     (int)span, 0x00020000);
+  const auto r1s = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>((T::TWO ? X.src1 : X.src0) + (long)m0 * P.lda), (short)0, (int)span, 0x00020000);
+  const uint32_t mspan = buf_span(rows_left * K8);
+  const auto rms = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(X.mask_in ? X.mask_in + (long)m0 * K8 : reinterpret_cast<const uint8_t*>(ca_zero16)),
+      (short)0, X.mask_in ? (int)mspan : 0, 0x00020000);
+  const bool write_side = tn == 0;
+  const auto rside = __builtin_amdgcn_make_buffer_rsrc(
+      write_side && X.side ? X.side + (long)m0 * P.lda : const_cast<bf16_t*>(ca_zero16), (short)0,
+      write_side && X.side ? (int)span : 0, 0x00020000);
+  const auto rmout = __builtin_amdgcn_make_buffer_rsrc(
+      write_side && X.mask_out ? X.mask_out + (long)m0 * K8 : reinterpret_cast<uint8_t*>(ca_zero16), (short)0,
+      write_side && X.mask_out ? (int)mspan : 0, 0x00020000);
+
+  // two staging sets, indexed by literal 0 / 1 only (the loop below is unrolled by two)
+  s8v a0[2], a1[2], bw[2][CPB];
+  uint32_t mb[2];
+
+  auto gload = [&](int t, const int S) {
+    const int k = t * BK + 8 * c8;
+    const int kc = k < P.K ? k : P.K - 8;
+    const uint32_t off = (uint32_t)(((long)arow * P.lda + kc) * 2);
+    a0[S] = __builtin_bit_cast(s8v, __builtin_amdgcn_raw_buffer_load_b128(r0s, (int)off, 0, 0));
+    if constexpr (T::TWO) a1[S] = __builtin_bit_cast(s8v, __builtin_amdgcn_raw_buffer_load_b128(r1s, (int)off, 0, 0));
+    if constexpr (T::MASK_IN) mb[S] = __builtin_amdgcn_raw_buffer_load_b8(rms, (int)(arow * K8 + (kc >> 3)), 0, 0);
+#pragma unroll
+    for (int i = 0; i < CPB; ++i) {
+      int lr, lc;
+      b_coord(i, lr, lc);
+      const long boff = B_KC ? (long)(n0 + lr) * P.ldb + t * BK + 8 * lc
+                             : (long)(t * BK + lr) * P.ldb + (n0 + 8 * lc < P.N ? n0 + 8 * lc : P.N - 8);
+      bw[S][i] = __builtin_bit_cast(s8v, __builtin_amdgcn_raw_buffer_load_b128(rbw, (int)(boff * 2), 0, 0));
+    }
+  };
+
+  auto transform_store = [&](int t, const int S) {
+    const int k = t * BK + 8 * c8;
+    const bool kok = k < P.K;
+    const int kc = kok ? k : P.K - 8;
+    f4v cf[T::NCOEF][2];
+#pragma unroll
+    for (int q = 0; q < T::NCOEF; ++q) {
+      cf[q][0] = *reinterpret_cast<const f4v*>(coefs + q * XA_DEEP_KMAX + kc);
+      cf[q][1] = *reinterpret_cast<const f4v*>(coefs + q * XA_DEEP_KMAX + kc + 4);
+    }
+    s8v o;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float c0 = cf[0][j >> 2][j & 3], c1 = cf[1][j >> 2][j & 3];
+      float v;
+      if constexpr (XM == XA_BN_BWD) {
+        float d = bf2f((bf16_t)a0[S][j]);
+        if (X.mask_in) d = ((mb[S] >> j) & 1u) ? d : 0.f;
+        v = bn_bwd_affine(c0, d, c1, bf2f((bf16_t)a1[S][j]), cf[2][j >> 2][j & 3]);
+      } else {
+        float z = bn_affine(bf2f((bf16_t)a0[S][j]), c0, c1);
+        if constexpr (XM == XA_BN_RES_RELU) z += bf2f((bf16_t)a1[S][j]);
+        if constexpr (XM == XA_BN_RESBN_RELU) {
+          const float idn = bf2f(f2bf(bn_affine(bf2f((bf16_t)a1[S][j]), cf[2][j >> 2][j & 3], cf[3][j >> 2][j & 3])));
+          z = bn_affine(bf2f((bf16_t)a0[S][j]), c0, c1) + idn;
+        }
+        z = fmaxf(z, 0.f);
+        bits |= (z > 0.f ? 1u : 0u) << j;
+        v = z;
+      }
+      o[j] = kok ? (short)f2bf(v) : (short)0;
+    }
+    *reinterpret_cast<s8v*>(As + arow * BK + ((c8 ^ (arow & 7)) << 3)) = o;
+    const uint32_t soff = kok ? (uint32_t)(((long)arow * P.lda + k) * 2) : span;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rside, (int)soff, 0, 0);
+    if constexpr (XM != XA_BN_BWD)
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bits, rmout, kok ? (int)(arow * K8 + (k >> 3)) : (int)mspan, 0, 0);
+#pragma unroll
+    for (int i = 0; i < CPB; ++i) {
+      int lr, lc;
+      b_coord(i, lr, lc);
+      short* dst = B_KC ? Bs + lr * BK + ((lc ^ (lr & 7)) << 3) : Bs + lr * BN + ((lc ^ nc_swz<BN>(lr)) << 3);
+      *reinterpret_cast<s8v*>(dst) = bw[S][i];
+    }
+  };
+
+  f4v acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  // Every load is issued unconditionally (past the last tile: the last tile again, never used)
+  // and the loop body has no branch, so the compiler's waitcnt pass sees one static stream of
+  // vector-memory operations and waits for exactly the set it is about to read -- a branch
+  // around a refill merges two counter states and it falls back to vmcnt(0) (checked in the .s).
+  auto step = [&](int t, const int S) {
+    transform_store(t, S);                    // the stage is free: every wave passed t - 1's closing barrier
+    gload(t + 2 < nk ? t + 2 : nk - 1, S);    // refill this set: tiles t + 1 and t + 2 in flight now
+    lgkm_wait0();
+    bar256();
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = read_frag_sw<BM, true>(As, wm * (BM / WM) + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = read_frag_sw<BN, B_KC>(Bs, wn * (BN / WN) + j * 16, kk, lane);
+      mfma_acc<FM, FN>(acc, af, bfr);
+    }
+    lgkm_wait0();
+    bar256();
+  };
+
+  gload(0, 0);  // (the host guarantees K >= 8: nk >= 1)
+  gload(nk > 1 ? 1 : 0, 1);
+  __syncthreads();  // coefficients staged
+  int t = 0;
+#pragma unroll 1
+  for (; t + 1 < nk; t += 2) {
+    step(t, 0);
+    step(t + 1, 1);
+  }
+  if (t < nk) step(t, 0);
+  vm_wait<0>();
+  gemm_epilogue<BM, BN, WM, WN, EPI, SMEM, 1>(P, acc, smem, m0, n0, tm, tid);
+}
+
+// ----------------------------------------------------------------------------------------
 // XA_BN_BWD with the WEIGHT gradient in the same pass (ResNet stage-1 1x1 convolutions:
 // conv3, K = 4c = 256 -> N = c = 64; conv1, K = c = 64 -> N = 4c = 256).  The unfused
 // schedule writes dz (the BN-backward apply, [M][K]) and reads it back in the split-K

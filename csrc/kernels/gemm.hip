@@ -642,6 +642,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) x
   mfma_gemm_xa<BM, BN, BKC, EPI, XM, 512>(P, X);
 }
 
+// the same tiles with two K tiles' raw operands in flight (coefficients staged in LDS)
+template <int BN, bool BKC, int EPI, int XM>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) xa_gemm16d_kernel(CoreParams P,
+                                                                                                 XaParams X) {
+  mfma_gemm_xa_deep<BN, BKC, EPI, XM>(P, X);
+}
+
 // 128 x 256 tiles on 16 waves (2 x 8, wave tile 64 x 32: the 128 x 128 8-wave form's registers,
 // <= 128 per lane): one workgroup per CU, 16 waves, each A tile transformed once
 template <int BM, int BN, bool BKC, int EPI, int XM>
@@ -667,12 +674,13 @@ static bool xa_waves8_n64() {
 // conv3 dgrad, bn3 -> next conv1 at N = 256 / 512) on 128 x 256 tiles, so each A tile is read
 // and BN-transformed once per 256 columns instead of once per 128.  1 (default): 16-wave
 // workgroups (wave tile 64 x 32, <= 128 registers: one per CU); 2: 8 waves (64 x 64, ~190
-// registers: one per CU at half the waves); 0: off (128 x 128 tiles)
+// registers: one per CU at half the waves); 3: 16 waves with two K tiles in flight
+// (mfma_gemm_xa_deep, K <= 2048); 0: off (128 x 128 tiles)
 int g_xa_n256 = -1;
 static int xa_n256() {
   if (g_xa_n256 < 0) {
     const char* e = getenv("CLOUD_AMD_XA_N256");
-    g_xa_n256 = (e && (e[0] == '0' || e[0] == '2')) ? e[0] - '0' : 1;
+    g_xa_n256 = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 1;
   }
   return g_xa_n256;
 }
@@ -752,7 +760,10 @@ int xa_launch(const CoreParams& p0, const XaParams& x, hipStream_t s) {
   const int n256 = p.N % 256 == 0 ? xa_n256() : 0;
   bool w16 = false;
   if constexpr (EPI != EPI_BF16_BNR2) {  // three 16-wave statistics rows do not fit its LDS image
-    if (n256 == 1) {
+    if (n256 == 3 && p.K <= XA_DEEP_KMAX) {
+      xa_gemm16d_kernel<256, LB, EPI, XM><<<tm * (p.N / 256), 1024, 0, s>>>(p, x);
+      w16 = true;
+    } else if (n256 == 1 || n256 == 3) {
       xa_gemm16_kernel<128, 256, LB, EPI, XM><<<tm * (p.N / 256), 1024, 0, s>>>(p, x);
       w16 = true;
     }
@@ -854,7 +865,7 @@ int ca_gemm_set_core(int kind) {
 // Transform-A tiles for N % 256 == 0 (values as CLOUD_AMD_XA_N256); returns the previous mode.
 int ca_gemm_set_xa_n256(int mode) {
   const int prev = xa_n256();
-  if (mode >= 0 && mode <= 2) g_xa_n256 = mode;
+  if (mode >= 0 && mode <= 3) g_xa_n256 = mode;
   return prev;
 }
 

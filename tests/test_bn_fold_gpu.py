@@ -331,7 +331,8 @@ def test_deep_fused_gradient_matches_one_step_form():
 
 @pytest.mark.parametrize("M,K,N", [(3000, 1024, 256), (777, 2048, 512), (1000, 512, 256)])
 def test_wide_tiles_bitwise_vs_128_tiles(M, K, N):
-    """The 128 x 256 transform-A tiles (16-wave and 8-wave forms) against the 128 x 128 ones on
+    """The 128 x 256 transform-A tiles (16-wave, 8-wave and 16-wave two-deep forms) against the
+    128 x 128 ones on
     the same inputs: the BN-backward side output dz, the forward side output y and its ReLU
     bitmask, and the GEMM results (plain, BN-statistics and residual-gated two-BN epilogues) are
     bitwise equal (same per-element K order, fixed-order BN transforms); the BN statistics
@@ -375,7 +376,7 @@ def test_wide_tiles_bitwise_vs_128_tiles(M, K, N):
             ext.gemm_set_xa_n256(prev)
 
     ref = run(0)
-    for mode in (1, 2):
+    for mode in (1, 2, 3):
         got = run(mode)
         for i in (0, 1, 3, 4, 5, 7, 8):
             assert torch.equal(got[i], ref[i]), (mode, i)
