@@ -147,12 +147,11 @@ _VARS = [
     Var("CLOUD_AMD_BN_FOLD_FWD", bool, True, "ResNet block forward: bn2's apply runs in conv3's operand fetch and "
         "bn3's (+ residual) in the next block's conv1 (ca_gemm_xa.h); the applied tensors are written once, by "
         "those GEMMs", "ops"),
-    Var("CLOUD_AMD_BN_FOLD_MAX_N", int, 128, "BN fold sites kept: only GEMMs with K >= 2N and N <= this "
-        "(ResNet-50 default: bn3 -> conv3 dgrad and bn3 -> next conv1 at stages 1-2; 4096 = every stage); the "
-        "transform-A core re-runs the BN transform per N tile and cannot pipeline a one-K-tile GEMM, so the short-K "
-        "sites (bn2 -> conv3, bn1 -> conv1 dgrad) measured slower than the separate pass, and at stages 3-4 (N 256 / "
-        "512: 2-4 N tiles re-transform each A tile) the fold is 0.4 % slower end to end (docs/performance.md, "
-        "round 4)", "ops"),
+    Var("CLOUD_AMD_BN_FOLD_MAX_N", int, 256, "BN fold sites kept: only GEMMs with K >= 2N and N <= this "
+        "(ResNet-50 default: bn3 -> conv3 dgrad and bn3 -> next conv1 at stages 1-3, the stage-3 ones on the two-deep "
+        "128 x 256 transform-A tiles, CLOUD_AMD_XA_N256=3: +0.6 / +1.0 % on two boxes, docs/performance.md round 6; "
+        "4096 = every stage); the short-K sites (bn2 -> conv3, bn1 -> conv1 dgrad) measured slower than the separate "
+        "pass, and stage 4 (N 512) +0.3 % below stages 1-3 only", "ops"),
     Var("CLOUD_AMD_BN_FOLD_WGRAD", bool, True, "bn3 -> conv3 fold at 64 input channels (ResNet stage 1): conv3's weight "
         "gradient runs in the same kernel as its input gradient (ca_gemm_xa.h mfma_gemm_xa_dw), so the BN-backward "
         "output dz3 is never written", "ops"),
@@ -166,11 +165,11 @@ _VARS = [
         "(K = 512 -> N = 128, 8-wave workgroups holding the 512 x 128 dW block)", "ops"),
     Var("CLOUD_AMD_BN_FOLD_WGRAD1", bool, False, "the same one-pass input + weight gradient for stage 1's conv1 with "
         "bn1's backward apply (K = 64 -> N = 256: dz1 never written, four output chunks per tile)", "ops"),
-    Var("CLOUD_AMD_XA_N256", int, 1, "transform-A GEMMs (BN folded into a 1x1 conv) with N a multiple of 256: "
+    Var("CLOUD_AMD_XA_N256", int, 3, "transform-A GEMMs (BN folded into a 1x1 conv) with N a multiple of 256: "
         "1 = 128 x 256 tiles on 16-wave workgroups (each A tile transformed once), 2 = 128 x 256 on 8 waves, "
         "3 = 16 waves with two K tiles' operands in flight (coefficients staged in LDS; K <= 2048), "
-        "0 = 128 x 128 tiles.  Only the fold sites CLOUD_AMD_BN_FOLD_MAX_N admits reach them (none at the "
-        "ResNet-50 default; measured in docs/performance.md, round 6)", "ops"),
+        "0 = 128 x 128 tiles.  Only the fold sites CLOUD_AMD_BN_FOLD_MAX_N admits reach them (ResNet-50 stage 3 "
+        "at the default; measured in docs/performance.md, round 6)", "ops"),
     Var("CLOUD_AMD_XA_WAVES", int, 8,"128 x 128 transform-A GEMMs (BN folded into the 1x1 convs): 8-wave "
         "workgroups (<= 128 registers, two per CU) or 4", "ops"),
     Var("CLOUD_AMD_XA_WAVES_N64", bool, True, "the 128 x 64 transform-A GEMMs (stage 1) on 8-wave workgroups too "

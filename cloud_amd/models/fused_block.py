@@ -118,7 +118,9 @@ def _fold_site(K, N):
     """Whether a BN apply is folded into a 1x1 GEMM of reduction K and N output channels.
     The transform-A core (ca_gemm_xa.h) repeats the BN transform for every N tile and has no
     operand pipeline for a single K tile; measured on MI355X (ResNet-50, b1024) only the long-K,
-    narrow-N sites beat the separate BN pass (docs/performance.md, round 4)."""
+    narrow-N sites beat the separate BN pass (docs/performance.md, round 4); since round 6 stage 3's
+    N = 256 sites run on 128 x 256 tiles with two K tiles in flight (ca_gemm_xa.h mfma_gemm_xa_deep)
+    and pay too."""
     if config.get("CLOUD_AMD_BN_FOLD_ALL"):
         return True
     return K >= 2 * N and N <= config.get("CLOUD_AMD_BN_FOLD_MAX_N")

@@ -672,15 +672,15 @@ static bool xa_waves8_n64() {
 }
 // CLOUD_AMD_XA_N256: transform-A GEMMs with N a multiple of 256 (ResNet-50 stages 3-4: bn3 ->
 // conv3 dgrad, bn3 -> next conv1 at N = 256 / 512) on 128 x 256 tiles, so each A tile is read
-// and BN-transformed once per 256 columns instead of once per 128.  1 (default): 16-wave
-// workgroups (wave tile 64 x 32, <= 128 registers: one per CU); 2: 8 waves (64 x 64, ~190
-// registers: one per CU at half the waves); 3: 16 waves with two K tiles in flight
-// (mfma_gemm_xa_deep, K <= 2048); 0: off (128 x 128 tiles)
+// and BN-transformed once per 256 columns instead of once per 128.  1: 16-wave workgroups (wave
+// tile 64 x 32, <= 128 registers: one per CU); 2: 8 waves (64 x 64, ~190 registers: one per CU
+// at half the waves); 3 (default): 16 waves with two K tiles in flight (mfma_gemm_xa_deep,
+// K <= 2048; else form 1); 0: off (128 x 128 tiles)
 int g_xa_n256 = -1;
 static int xa_n256() {
   if (g_xa_n256 < 0) {
     const char* e = getenv("CLOUD_AMD_XA_N256");
-    g_xa_n256 = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 1;
+    g_xa_n256 = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
   }
   return g_xa_n256;
 }

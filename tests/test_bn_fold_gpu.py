@@ -227,8 +227,8 @@ def test_resnet_bn_fold_bitwise(monkeypatch):
     monkeypatch.setattr(raw, "conv1x1_fwd_bnapply", counting_f)
     ext = _ext_mod().load(required=True)
     # 128-wide transform-A tiles: their per-tile BN statistics happen to sum in an order that
-    # reproduces the separate passes' fp32 coefficients here; the 128 x 256 tiles (default at
-    # N % 256 == 0) regroup those sums, and a 1-ulp coefficient change re-rounds a few bf16
+    # reproduces the separate passes' fp32 coefficients here; the 128 x 256 tiles (the default
+    # at N % 256 == 0) regroup those sums, and a 1-ulp coefficient change re-rounds a few bf16
     # dz values downstream -- checked to a tight tolerance below instead
     prev = ext.gemm_set_xa_n256(0)
     try:
@@ -236,7 +236,7 @@ def test_resnet_bn_fold_bitwise(monkeypatch):
         n_fold = dict(calls)
         g0, l0, _ = _train(False)
         calls_off = dict(calls)
-        ext.gemm_set_xa_n256(1)
+        ext.gemm_set_xa_n256(3)  # the default: two-deep 16-wave tiles
         g2, _, _ = _train(True, steps=1)
     finally:
         ext.gemm_set_xa_n256(prev)
