@@ -166,7 +166,8 @@ _VARS = [
     Var("CLOUD_AMD_BN_FOLD_WGRAD1", bool, False, "the same one-pass input + weight gradient for stage 1's conv1 with "
         "bn1's backward apply (K = 64 -> N = 256: dz1 never written, four output chunks per tile)", "ops"),
     Var("CLOUD_AMD_XA_N256", int, 3, "transform-A GEMMs (BN folded into a 1x1 conv) with N a multiple of 256: "
-        "1 = 128 x 256 tiles on 16-wave workgroups (each A tile transformed once), 2 = 128 x 256 on 8 waves, "
+        "1 = 128 x 256 tiles on 16-wave workgroups (each A tile transformed once), 2 = 128 x 256 on 8 waves "
+        "(CLOUD_AMD_BUILD_EXPERIMENTAL builds only), "
         "3 = 16 waves with two K tiles' operands in flight (coefficients staged in LDS; K <= 2048), "
         "0 = 128 x 128 tiles.  Only the fold sites CLOUD_AMD_BN_FOLD_MAX_N admits reach them (ResNet-50 stage 3 "
         "at the default; measured in docs/performance.md, round 6)", "ops"),

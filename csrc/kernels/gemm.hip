@@ -634,13 +634,16 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) x
   mfma_gemm_xa<BM, BN, BKC, EPI, XM, 512>(P, X);
 }
 
+#if CA_EXPERIMENTAL
 // 128 x 256 tiles on 8 waves (2 x 4, wave tile 64 x 64): one workgroup per CU (64 accumulator
-// registers per lane on top of the 128 x 128 form's staging)
+// registers per lane on top of the 128 x 128 form's staging).  Measured slower than the 16-wave
+// forms (docs/performance.md, round 6): experiment-only (CLOUD_AMD_XA_N256=2)
 template <int BM, int BN, bool BKC, int EPI, int XM>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) xa_gemm8w_kernel(CoreParams P,
                                                                                                XaParams X) {
   mfma_gemm_xa<BM, BN, BKC, EPI, XM, 512>(P, X);
 }
+#endif
 
 // the same tiles with two K tiles' raw operands in flight (coefficients staged in LDS)
 template <int BN, bool BKC, int EPI, int XM>
@@ -674,8 +677,10 @@ static bool xa_waves8_n64() {
 // conv3 dgrad, bn3 -> next conv1 at N = 256 / 512) on 128 x 256 tiles, so each A tile is read
 // and BN-transformed once per 256 columns instead of once per 128.  1: 16-wave workgroups (wave
 // tile 64 x 32, <= 128 registers: one per CU); 2: 8 waves (64 x 64, ~190 registers: one per CU
-// at half the waves); 3 (default): 16 waves with two K tiles in flight (mfma_gemm_xa_deep,
-// K <= 2048; else form 1); 0: off (128 x 128 tiles)
+// at half the waves; CLOUD_AMD_BUILD_EXPERIMENTAL builds only); 3 (default): 16 waves with two K
+// tiles in flight (mfma_gemm_xa_deep, K <= 2048; else form 1); 0: off (128 x 128 tiles).  The
+// two-BN residual epilogue (EPI_BF16_BNR2) keeps the 128-wide tiles: its three statistics rows do
+// not fit the 16-wave LDS image.
 int g_xa_n256 = -1;
 static int xa_n256() {
   if (g_xa_n256 < 0) {
@@ -768,9 +773,14 @@ int xa_launch(const CoreParams& p0, const XaParams& x, hipStream_t s) {
       w16 = true;
     }
   }
-  if (w16) {
-  } else if (n256) {
+  bool w8w = false;
+#if CA_EXPERIMENTAL
+  if (!w16 && n256 == 2) {
     xa_gemm8w_kernel<128, 256, LB, EPI, XM><<<tm * (p.N / 256), 512, 0, s>>>(p, x);
+    w8w = true;
+  }
+#endif
+  if (w16 || w8w) {
   } else if (want_small_n(p, 1)) {
     bool w8 = false;
     if constexpr (EPI != EPI_BF16_BNR2) {  // its three statistics rows do not fit the 8-wave LDS image
@@ -865,6 +875,7 @@ int ca_gemm_set_core(int kind) {
 // Transform-A tiles for N % 256 == 0 (values as CLOUD_AMD_XA_N256); returns the previous mode.
 int ca_gemm_set_xa_n256(int mode) {
   const int prev = xa_n256();
+  if (mode == 2 && !CA_EXPERIMENTAL) return -1;  // the 8-wave form is experiment-only
   if (mode >= 0 && mode <= 3) g_xa_n256 = mode;
   return prev;
 }

@@ -376,7 +376,7 @@ def test_wide_tiles_bitwise_vs_128_tiles(M, K, N):
             ext.gemm_set_xa_n256(prev)
 
     ref = run(0)
-    for mode in (1, 2, 3):
+    for mode in ((1, 2, 3) if ext.experimental_built() else (1, 3)):  # 2: experiment-only build
         got = run(mode)
         for i in (0, 1, 3, 4, 5, 7, 8):
             assert torch.equal(got[i], ref[i]), (mode, i)
