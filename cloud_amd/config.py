@@ -155,6 +155,9 @@ _VARS = [
     Var("CLOUD_AMD_BN_FOLD_WGRAD", bool, True, "bn3 -> conv3 fold at 64 input channels (ResNet stage 1): conv3's weight "
         "gradient runs in the same kernel as its input gradient (ca_gemm_xa.h mfma_gemm_xa_dw), so the BN-backward "
         "output dz3 is never written", "ops"),
+    Var("CLOUD_AMD_BN_FOLD_DS", bool, False, "ResNet projection blocks, stages 2-4: the shortcut BN's backward apply "
+        "runs in the operand fetch of the sparse strided shortcut input-gradient GEMM (ca_gemm_xa_bwd_strided); A/B",
+        "ops"),
     Var("CLOUD_AMD_DS_SPARSE_DGRAD", bool, True, "ResNet projection blocks with a strided 1x1 shortcut: the "
         "shortcut's input gradient is written for its one non-empty output-parity class only, and conv1's input "
         "gradient accumulates into it reading the other pixels as zeros -- no zero-fill of 3/4 of dx and no read "

@@ -341,16 +341,24 @@ class _BottleneckFn(torch.autograd.Function):
                 ddp.notify_grad_ready(c.weight)
                 del dres
             else:
-                if gate_res:
-                    dzd, _ = bn_back(ds["bn"], dout, zd, (sd, None), gate=m3, partials=p_short)
-                else:
-                    dzd, _ = bn_back(ds["bn"], dres, zd, (sd, None))
-                del dres
                 # strided 1x1 shortcut: only its one non-empty parity class is written; conv1's
                 # input gradient below reads the other pixels as zeros (never stored)
                 sparse = (coef1 is None and c.stride > 1 and c.padding == 0 and c.weight.shape[1:3] == (1, 1)
                           and config.get("CLOUD_AMD_DS_SPARSE_DGRAD"))
-                dx = raw.conv_dgrad(dzd, c.weight, x.shape, c.stride, c.padding, skip_empty=sparse)
+                if (sparse and fold and gate_res and p_short is not None and c.cout <= 2048
+                        and config.get("CLOUD_AMD_BN_FOLD_DS")):
+                    # ... and its BN backward (gated by the block output's ReLU) in that GEMM's
+                    # operand fetch: dzd is written once (the weight gradient's operand), never read
+                    coefd = bn_coef(ds["bn"], zd, sd, p_short)
+                    dzd = torch.empty_like(zd)
+                    dx = raw.conv1x1_strided_dgrad_bnbwd(dout, zd, m3, coefd, c.weight, dzd, x.shape, c.stride)
+                else:
+                    if gate_res:
+                        dzd, _ = bn_back(ds["bn"], dout, zd, (sd, None), gate=m3, partials=p_short)
+                    else:
+                        dzd, _ = bn_back(ds["bn"], dres, zd, (sd, None))
+                    dx = raw.conv_dgrad(dzd, c.weight, x.shape, c.stride, c.padding, skip_empty=sparse)
+                del dres
                 dx_stride = c.stride if sparse else 1
                 wgrad(c, dzd, x)
                 del dzd

@@ -274,6 +274,32 @@ def conv1x1_dgrad_bnbwd(dy, z, mask, coef, w, side, out=None, beta=0.0, bn=None,
     return (dx, part, part2) if (len(bn) > 2 and bn[2] is not None) else (dx, part)
 
 
+def conv1x1_strided_dgrad_bnbwd(dy, z, mask, coef, w, side, x_shape, stride):
+    """Input gradient of a stride-``stride`` 1x1 / pad-0 convolution (``w`` [Cout, 1, 1, Cin]; a
+    ResNet projection shortcut) whose output gradient is a BatchNorm backward: ``dz = A*(dy *
+    relu'(mask)) + B*z + D`` is produced in the GEMM's operand fetch and written to ``side`` (the
+    weight gradient's operand); ``dz W`` lands on the one non-empty output-parity class of a new
+    ``x_shape`` tensor, whose other pixels are left UNWRITTEN -- the pair of
+    ``conv_dgrad(..., skip_empty=True)`` after a separate BN backward, in one pass.  The caller's
+    next input-gradient GEMM into it must use ``beta_stride=stride``."""
+    ext = _ext.load(required=True)
+    N, Ho, Wo, Cout = z.shape
+    Nx, H, W, Cin = x_shape
+    assert Nx == N and w.shape == (Cout, 1, 1, Cin) and stride > 1
+    assert Ho == (H - 1) // stride + 1 and Wo == (W - 1) // stride + 1
+    assert dy.shape == z.shape and side.shape == z.shape and dy.is_contiguous() and z.is_contiguous()
+    assert side.is_contiguous() and coef.numel() == 3 * Cout and Cout <= 2048
+    M = N * Ho * Wo
+    assert mask is None or mask.shape == (M, Cout // 8)
+    dx = torch.empty(x_shape, dtype=torch.bfloat16, device=dy.device)
+    cp = coef.data_ptr()
+    ext.gemm_xa_bwd_strided(dy.data_ptr(), z.data_ptr(), _ext.ptr(mask), cp, cp + 4 * Cout, cp + 8 * Cout,
+                            side.data_ptr(), Cout, w.data_ptr(), Cin, dx.data_ptr(), Cin, M, Cin, Cout, N, H, W,
+                            int(stride), _st(dy.device))
+    _log("dgrad1x1s_xa", M, Cin, Cout, _nb(dy, z, mask, side, w) + _nb(dx) // stride ** 2)
+    return dx
+
+
 def dgrad_wgrad_fusable(cout, cin):
     """Shapes the fused input+weight gradient kernel (:func:`conv1x1_dgrad_wgrad_bnbwd`) takes
     (``ca_gemm_xa_dw``): 64 input channels with 64 / 128 / 256 output channels (ResNet stage-1

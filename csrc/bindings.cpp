@@ -45,6 +45,9 @@ int ca_bn_fwd_partials_ex(const bf16_t*, const bf16_t*, const float*, bf16_t*, l
 int ca_gemm_xa(int, int, const bf16_t*, const bf16_t*, const uint8_t*, const float*, const float*, const float*,
                const float*, bf16_t*, uint8_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, float, const bf16_t*,
                const uint8_t*, const bf16_t*, const uint8_t*, float*, const bf16_t*, float*, hipStream_t);
+int ca_gemm_xa_bwd_strided(const bf16_t*, const bf16_t*, const uint8_t*, const float*, const float*, const float*,
+                           bf16_t*, long, const bf16_t*, long, bf16_t*, long, int, int, int, int, int, int, int,
+                           hipStream_t);
 int ca_gemm_xa_dw(const bf16_t*, const bf16_t*, const uint8_t*, const float*, const float*, const float*, long,
                   const bf16_t*, long, bf16_t*, long, int, int, int, float, const bf16_t*, const uint8_t*,
                   const bf16_t*, const uint8_t*, float*, const bf16_t*, float*, const bf16_t*, long, void*, int, float,
@@ -252,6 +255,14 @@ PYBIND11_MODULE(_C, m) {
                      P(const bf16_t*, res), P(const uint8_t*, res_mask), P(const bf16_t*, z), P(const uint8_t*, mask),
                      P(float*, stats), P(const bf16_t*, z2), P(float*, stats2), S(s)),
           "gemm_xa");
+  });
+  m.def("gemm_xa_bwd_strided", [](u64 src0, u64 src1, u64 mask_in, u64 c0, u64 c1, u64 c2, u64 side, long lda, u64 B,
+                                  long ldb, u64 C, long ldc, int M, int N, int K, int Nb, int H, int W, int stride,
+                                  u64 s) {
+    check(ca_gemm_xa_bwd_strided(P(const bf16_t*, src0), P(const bf16_t*, src1), P(const uint8_t*, mask_in),
+                                 P(const float*, c0), P(const float*, c1), P(const float*, c2), P(bf16_t*, side), lda,
+                                 P(const bf16_t*, B), ldb, P(bf16_t*, C), ldc, M, N, K, Nb, H, W, stride, S(s)),
+          "gemm_xa_bwd_strided");
   });
   m.def("gemm_xa_dw", [](u64 src0, u64 src1, u64 mask_in, u64 c0, u64 c1, u64 c2, long lda, u64 B, long ldb, u64 C,
                          long ldc, int M, int N, int K, float beta, u64 res, u64 res_mask, u64 z, u64 mask, u64 stats,

@@ -1050,6 +1050,36 @@ int ca_gemm_xa(int layout, int mode, const bf16_t* src0, const bf16_t* src1, con
   return xa_launch<false, EPI_BF16_BN, XA_BN_BWD>(p, x, s);
 }
 
+// XA_BN_BWD input gradient of a stride-s 1x1 / pad-0 convolution (a ResNet projection shortcut):
+// dz = A*(dy*relu'(mask)) + B*z + D is produced in the operand fetch (and written to `side`, the
+// weight gradient's operand), dX = dz W goes to the one non-empty output-parity class of
+// dx[Nb, H, W, ldc] -- GEMM row (n, qy, qx) to pixel (n, s*qy, s*qx) -- the other pixels are
+// left unwritten (the caller's next input-gradient GEMM reads them as zeros: CoreParams::bpar_s).
+// M must be Nb * ceil(H/s) * ceil(W/s).
+int ca_gemm_xa_bwd_strided(const bf16_t* src0, const bf16_t* src1, const uint8_t* mask_in, const float* c0,
+                           const float* c1, const float* c2, bf16_t* side, long lda, const bf16_t* B, long ldb,
+                           bf16_t* C, long ldc, int M, int N, int K, int Nb, int H, int W, int stride, hipStream_t s) {
+  if (M <= 0 || N < 8 || N % 8 != 0 || K < 8 || K % 8 != 0 || lda % 8 != 0 || !src0 || !src1 || !c0 || !c1 || !c2)
+    return -1;
+  const int Hq = (H + stride - 1) / stride, Wq = (W + stride - 1) / stride;
+  if (stride < 2 || (long)Nb * Hq * Wq != M) return -1;
+  CoreParams p = base_params(src0, lda, B, ldb, C, ldc, M, N, K);
+  p.rowmap = 1;
+  p.dg_py = 0;
+  p.dg_px = 0;
+  p.Nb = Nb;
+  p.H = H;
+  p.W = W;
+  p.sh = stride;
+  p.sw = stride;
+  p.Hq = Hq;
+  p.Wq = Wq;
+  p.div_hq = make_fastdiv(Hq);
+  p.div_wq = make_fastdiv(Wq);
+  XaParams x{src0, src1, mask_in, c0, c1, c2, nullptr, side, nullptr};
+  return xa_launch<false, EPI_BF16, XA_BN_BWD>(p, x, s);
+}
+
 // XA_BN_BWD input gradient with the weight gradient in the same pass (ca_gemm_xa.h
 // mfma_gemm_xa_dw).  Shapes: N == 64 with K in {64, 128, 256} (stage-1 conv3), K == 64 with
 // N == 256 (stage-1 conv1), N == 128 with K == 512 (stage-2 conv3, 8-wave workgroups); the dgrad epilogues of ca_gemm_xa layout 1 (BN statistics bnz/bnmask/

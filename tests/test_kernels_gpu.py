@@ -573,3 +573,33 @@ def test_sparse_shortcut_dgrad_then_sparse_beta_accumulate(H, with_bn):
     ref = ref.reshape(N, H, H, Cin)
     ref[:, ::s, ::s] += (dzd.float().reshape(-1, Cd) @ wd.float().reshape(Cd, Cin)).reshape(N, OH, OH, Cin)
     torch.testing.assert_close(dx_sp.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("H,Cd,Cin", [(16, 512, 256), (15, 1024, 512)])
+def test_strided_shortcut_dgrad_with_folded_bn_backward(H, Cd, Cin):
+    """Projection shortcut input gradient with its BN backward in the operand fetch
+    (raw.conv1x1_strided_dgrad_bnbwd): the written dz equals the stride-1 transform-A kernel's
+    bitwise, dx's even-even pixels equal that kernel's product bitwise (same tiles, same K
+    order), the other pixels stay unwritten, and the result matches an fp32 reference."""
+    from cloud_amd.ops import raw
+
+    torch.manual_seed(31)
+    N, s = 3, 2
+    Ho = (H - 1) // s + 1
+    dy = torch.randn(N, Ho, Ho, Cd, device=DEV).to(torch.bfloat16)
+    z = torch.randn(N, Ho, Ho, Cd, device=DEV).to(torch.bfloat16)
+    keep = torch.rand(N * Ho * Ho, Cd, device=DEV) > 0.4
+    bits = _relu_bits(keep)
+    coef = torch.randn(3 * Cd, device=DEV) * torch.tensor([1.0, 0.1, 0.01], device=DEV).repeat_interleave(Cd)
+    w = (torch.randn(Cd, 1, 1, Cin, device=DEV) / Cd ** 0.5).to(torch.bfloat16)
+    side = torch.empty_like(z)
+    dx = raw.conv1x1_strided_dgrad_bnbwd(dy, z, bits, coef, w, side, (N, H, H, Cin), s)
+    side1 = torch.empty_like(z)
+    dx1 = raw.conv1x1_dgrad_bnbwd(dy, z, bits, coef, w, side1)
+    torch.cuda.synchronize()
+    assert torch.equal(side, side1)
+    assert torch.equal(dx[:, ::s, ::s], dx1)
+    A, B, D = coef[:Cd], coef[Cd:2 * Cd], coef[2 * Cd:]
+    dz = (A * dy.float().reshape(-1, Cd) * keep + B * z.float().reshape(-1, Cd) + D).to(torch.bfloat16).float()
+    ref = (dz @ w.float().reshape(Cd, Cin)).reshape(N, Ho, Ho, Cin)
+    torch.testing.assert_close(dx[:, ::s, ::s].float(), ref, atol=3e-2, rtol=3e-2)
