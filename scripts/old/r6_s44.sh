@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 S=scripts/gpu_step.sh
-tag=r6s44
+tag=${TAG:-r6s44}
 chk() { grep -q " passed" gpurun_out/$1 && ! grep -qE " failed| error" gpurun_out/$1 || { echo "tests failed: $1"; tail -60 gpurun_out/$1; exit 1; }; }
 $S 1000 ${tag}_all.log python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rs || exit 1
 chk ${tag}_all.log
